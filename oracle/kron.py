@@ -1,0 +1,172 @@
+"""Kronecker-structured linear algebra -- CPU oracle (test infrastructure only).
+
+Each function restates one reference routine of
+/root/reference/gp_grief/tensors/kron_matrix.py or gp_grief/linalg.py; the
+citation is in its docstring.  Index convention (kron_matrix.py:19-42, np.kron):
+the flattened vector is a C-order tensor over the factor list, factor 0 the
+slowest axis.  (GridKernel.cov_grid reverses the input dimensions,
+grid_kernel.py:109, so input dimension 0 ends up fastest.)
+"""
+import numpy as np
+
+
+def kron_matvec(factors, x):
+    """y = (K_0 (x) K_1 (x) ... (x) K_{d-1}) x.
+
+    Restates KronMatrix.kronvec_prod (kron_matrix.py:52-97): one GEMM per
+    factor.  Each step contracts the slowest remaining axis against K_k and
+    appends the new axis as the fastest one, so after d steps the axes are back
+    in order (the reference gets the same rotation from its F-order reshapes
+    and transposes).  BLAS3 via numpy.matmul, threads from OpenBLAS.
+    """
+    y = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    ncols = int(np.prod([np.shape(k)[1] for k in factors]))
+    if y.size != ncols:
+        raise ValueError('x is the wrong shape, must be (%d,1), not %s'
+                         % (ncols, repr(np.shape(x))))
+    for K in factors:
+        K = np.asarray(K, dtype=np.float64)
+        p, q = K.shape
+        Y = y.reshape(q, -1)
+        y = np.matmul(Y.T, K.T).reshape(-1)
+    return y
+
+
+def kron_matvec_T(factors, x):
+    """(K_0 (x) ... )^T x -- KronMatrix.transpose (kron_matrix.py:203-213) then *."""
+    return kron_matvec([np.asarray(k).T for k in factors], x)
+
+
+def kron_expand(factors):
+    """Dense expansion, KronMatrix.expand (kron_matrix.py:215-239), 1-D or 2-D."""
+    out = np.ones((1,) * np.ndim(factors[0]))
+    for K in factors:
+        out = np.kron(out, np.asarray(K))
+    return out.reshape(-1) if np.ndim(factors[0]) == 1 else out
+
+
+def log_kron(a, b, a_logged=False, b_logged=False):
+    """log(kron(a, b)) for 1-D a, b -- linalg.log_kron (linalg.py:74-89)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    if a.ndim != 1 or b.ndim != 1:
+        raise AssertionError("currenly only working for 1d arrays")
+    la = a if a_logged else np.log(a)
+    lb = b if b_logged else np.log(b)
+    return np.add.outer(la, lb).reshape(-1)
+
+
+def find_extremum_eigs(eig_factors, n_eigs, mode='largest', log_expand=False,
+                       sort=True, compute_global_loc=False):
+    """Top/bottom-p entries of a 1-D Kronecker vector by sequential pruning.
+
+    Restates KronMatrix.find_extremum_eigs (kron_matrix.py:369-446): after each
+    factor only the n_eigs extreme partial products survive (np.argpartition,
+    the same primitive, so ties break identically), positions are tracked per
+    factor, and the survivors are finally sorted descending with np.argsort.
+    Returns (eig_loc [p x d] int, eig_vals [p], global_loc or None).
+    """
+    if mode not in ('largest', 'smallest'):
+        raise AssertionError("mode must be largest or smallest")
+    p = int(n_eigs)
+
+    def extreme(vec):
+        if vec.size <= p:
+            return np.arange(vec.size), vec
+        if mode == 'largest':
+            ind = np.argpartition(vec, -p)[-p:]
+        else:
+            ind = np.argpartition(vec, p)[:p]
+        return ind, vec[ind]
+
+    f0 = np.asarray(eig_factors[0], dtype=np.float64)
+    loc, vals = extreme(f0)
+    loc = loc.reshape((-1, 1))
+    if log_expand:
+        vals = np.log(vals)
+    for f in eig_factors[1:]:
+        f = np.asarray(f, dtype=np.float64)
+        if log_expand:
+            cand = np.add.outer(vals, np.log(f)).reshape(-1)
+        else:
+            cand = np.multiply.outer(vals, f).reshape(-1)
+        ind, vals = extreme(cand)
+        prev = loc[ind // f.size, :]
+        loc = np.hstack([prev.reshape((ind.size, -1)),
+                         (ind % f.size).astype(prev.dtype).reshape((-1, 1))])
+    gloc = None
+    if compute_global_loc:
+        gloc = np.zeros(loc.shape[0], dtype=np.int64)
+        stride = 1
+        for i in range(len(eig_factors) - 1, -1, -1):
+            gloc = gloc + stride * loc[:, i]
+            stride *= np.size(eig_factors[i])
+    if sort:
+        order = np.argsort(vals)[::-1]
+        vals = vals[order]
+        loc = loc[order]
+        if gloc is not None:
+            gloc = gloc[order]
+    return loc, vals, gloc
+
+
+def factor_eigh(factors):
+    """Per-factor symmetric eigendecomposition (Q_i, lambda_i).
+
+    The reference uses a real Schur form per factor (KronMatrix.schur,
+    kron_matrix.py:161-171; LAPACK gees), whose T is diagonal for symmetric
+    factors; numpy.linalg.eigh gives the same pairs up to ordering, column
+    sign and rounding.  Every quantity the tests compare is invariant to those.
+    """
+    Q, lam = [], []
+    for K in factors:
+        w, v = np.linalg.eigh(np.asarray(K, dtype=np.float64))
+        Q.append(v)
+        lam.append(w)
+    return Q, lam
+
+
+def solve_schur(Q, t, x, shift=0.0):
+    """(K + shift I)^{-1} x = Q ((Q^T x) / (t + shift)) -- kron_matrix.py:328-352."""
+    y = kron_matvec_T(Q, x)
+    y = y / (np.asarray(t).reshape(-1) + shift)
+    return kron_matvec(Q, y)
+
+
+def eig_log_det(eig_factors):
+    """log det of K from per-factor eigenvalues -- KronMatrix.log_det (:466-474)."""
+    sizes = np.array([np.size(e) for e in eig_factors], dtype=np.float64)
+    total = np.prod(sizes)
+    return float(sum((total / sizes[i]) * np.sum(np.log(e))
+                     for i, e in enumerate(eig_factors)))
+
+
+def _partial_products(eig_factors):
+    out = np.ones(1)
+    for e in eig_factors:
+        out = np.multiply.outer(out, np.asarray(e, dtype=np.float64)).reshape(-1)
+    return out
+
+
+def logdet_shifted(eig_factors, shift, chunk_last=True):
+    """log det(K + shift I) = sum_N log(prod_i lambda_i + shift).
+
+    The reference offers only the unshifted log det (kron_matrix.py:466-474);
+    the survey's verified recipe is sum(log(T.diag().expand()+s)).
+    Streamed over the last factor so that N-sized arrays are never formed.
+    """
+    head = _partial_products(eig_factors[:-1])
+    acc = 0.0
+    for lam in np.asarray(eig_factors[-1], dtype=np.float64):
+        acc += float(np.sum(np.log(head * lam + shift)))
+    return acc
+
+
+def grid_latent_var(Q, eig_factors, shift):
+    """diag(K - K (K + s I)^{-1} K) on the grid = (Q o Q)-Kron * (t s / (t + s)).
+
+    Composed from reference primitives (KronMatrix([Q_i**2]) times
+    the expanded eigenvalue vector); the reference has no single routine.
+    """
+    t = _partial_products(eig_factors)
+    return kron_matvec([np.asarray(q) ** 2 for q in Q], t * shift / (t + shift))
