@@ -1,0 +1,201 @@
+"""Benchmark: CG iterations/s on the 4-D RBF grid 200^4 (BASELINE.json configs[2]).
+
+One "step" = one CG iteration on (K + s I) x = y, K = K_0 (x) K_1 (x) K_2 (x) K_3
+(200 x 200 RBF factors, lengthscales 0.1*(1+0.05 i), jitter 1e-12, s = 0.01),
+all vectors (y, x, r, p, q, matvec scratch: 6 x 12.8 GB) resident in HBM.
+
+Prints ONE JSON line (rank 0):
+  metric/value/unit   CG iterations per second, whole job
+  roofline            the dominant kernel (the FP64 MFMA mode product) timed
+                      with HIP events on the stream it runs on, against the
+                      FP64 matrix peak; plus HBM GB/s of the whole matvec
+  cpu_baseline        the CPU oracle (oracle/, NumPy + OpenBLAS) timed on this
+                      host on a bounded sample of the same workload
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 200] [--dims 4]
+N > 1 is launched by torch.distributed.run (one process per GPU); see DESIGN.md
+for what the multi-GPU path does.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, dense (AMD spec)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--grid", type=int, default=200)
+    ap.add_argument("--dims", type=int, default=4)
+    ap.add_argument("--sigma2", type=float, default=0.01)
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--matvec-reps", type=int, default=5)
+    return ap.parse_args()
+
+
+def factors(m, d):
+    import oracle  # factor construction only (m x m); the CPU leg below times it
+    g = np.linspace(0.0, 1.0, m)
+    return [oracle.cov_1d("RBF", g, g, 1.0, 0.1 * (1 + 0.05 * (d - 1 - k))) + 1e-12 * np.eye(m)
+            for k in range(d)]
+
+
+def grid_rhs_device(m, d, torch, dev, seed=1):
+    """y = sum_i sin(6 xg_i) + 0.1 eps on the grid, built on the device."""
+    g = torch.linspace(0.0, 1.0, m, dtype=torch.float64, device=dev)
+    f = torch.sin(6.0 * g)
+    y = torch.zeros([m] * d, dtype=torch.float64, device=dev)
+    for k in range(d):
+        shape = [1] * d
+        shape[k] = m
+        y += f.reshape(shape)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    y = y.reshape(-1)
+    chunk = 1 << 27
+    for i in range(0, y.numel(), chunk):
+        n = min(chunk, y.numel() - i)
+        y[i:i + n] += 0.1 * torch.randn(n, dtype=torch.float64, device=dev, generator=gen)
+    return y
+
+
+def cpu_baseline(m, d, sigma2):
+    """One CG iteration of the CPU oracle at the full grid (bounded sample)."""
+    import oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(limits=threads)
+    except Exception:  # pragma: no cover
+        ctx = None
+    F = factors(m, d)
+    n = m ** d
+    rng = np.random.default_rng(1)
+    block = rng.standard_normal(m ** min(d, 3))
+    b = np.tile(block, n // block.size)
+    mv = lambda v: oracle.kron_matvec(F, v) + sigma2 * v
+    t0 = time.perf_counter()
+    x, info, it = oracle.cg_solve(mv, b, rtol=0.0, maxiter=1)
+    dt = time.perf_counter() - t0
+    del x, b
+    if ctx is not None:
+        ctx.__exit__(None, None, None)
+    return {"value": 1.0 / dt, "unit": "CG iters/s", "cores": threads, "kind": "port",
+            "sample": "1 CG iteration of oracle.cg_solve on the full %d^%d grid "
+                      "(NumPy/OpenBLAS, %d threads), %.1f s" % (m, d, threads, dt)}
+
+
+def main():
+    a = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        dist = None
+    dev = torch.device("cuda", torch.cuda.current_device())
+    import gp_grief_amd as gg
+
+    m, d, s = a.grid, a.dims, a.sigma2
+    F = factors(m, d)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = m ** d
+    y = grid_rhs_device(m, d, torch, dev)
+    solver = gg.linalg.KronCG(K, s)
+    solver.start(y, rtol=0.0, atol=0.0)   # never "converges": exactly the steps asked for
+    torch.cuda.synchronize()
+
+    # ---- matvec kernel timing (HIP events on the stream the kernels run on)
+    xv = y
+    out = torch.empty_like(y)
+    K.matvec_device(xv, shift=s, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.matvec_reps):
+        K.matvec_device(xv, shift=s, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    mv_ms = e0.elapsed_time(e1) / a.matvec_reps
+    del out
+
+    # ---- CG: warmup, then exactly `steps` iterations bracketed by barrier+sync
+    solver.iterate(a.warmup, check_every=0)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    solver.iterate(a.steps, check_every=0)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    it, conv, res, tol = solver.status()
+    assert it == a.warmup + a.steps, (it, a.warmup, a.steps)
+    assert np.isfinite(res)
+
+    launch_ms = mv_ms / d
+    flop_launch = 2.0 * n * m
+    achieved_tf = flop_launch / (launch_ms * 1e-3) / 1e12
+    mv_bytes = 8.0 * n * (2 * d + 1)
+    vec_bytes = 8.0 * n * (3 + 6 + 1)   # p-update 3N, x/r update 6N (+ q read in matvec epilogue 1N)
+    result = {
+        "metric": "CG iters/sec + Kron-matvec achieved HBM GB/s, 4D RBF grid 200^4",
+        "value": world * a.steps / dt if world > 1 else a.steps / dt,
+        "unit": "CG iters/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * dt / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d"
+                               % (m, d, s, n),
+                   "grid": m, "dims": d, "sigma2": s, "n": n,
+                   "parallelism": "replicas" if world > 1 else "single-gpu"},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_MFMA_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tf / FP64_MFMA_PEAK_TFLOPS,
+                     "traffic": None,
+                     "kernel": "gg::mode_product_kernel<13> (one Kronecker mode product)",
+                     "launch_ms": launch_ms, "flop_per_launch": flop_launch},
+        "matvec_ms": mv_ms,
+        "matvec_hbm_gbs": mv_bytes / (mv_ms * 1e-3) / 1e9,
+        "matvec_hbm_frac": mv_bytes / (mv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "cg_vector_ms": 1e3 * dt / a.steps - mv_ms,
+        "cg_vector_algorithmic_bytes": vec_bytes,
+    }
+    if rank == 0 and world == 1 and a.cpu_baseline == "auto":
+        del solver, y
+        torch.cuda.empty_cache()
+        result["cpu_baseline"] = cpu_baseline(m, d, s)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

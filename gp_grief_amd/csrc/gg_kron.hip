@@ -1,0 +1,379 @@
+// Kronecker operator on MI355X: y = (K_0 (x) ... (x) K_{d-1}) x as a chain of
+// FP64 MFMA GEMMs (v_mfma_f64_16x16x4_f64) with LDS-staged factor fragments.
+//
+// Reference: KronMatrix.kronvec_prod, gp_grief/tensors/kron_matrix.py:52-97.
+// The reference reshapes in Fortran order and lets BLAS3 dsymm/dgemm apply one
+// factor at a time, transposing the result so the tensor axes rotate.  Here
+// every step is the same batched-free GEMM
+//
+//     Y[b, j] = sum_i X[i, b] * K[j, i]        X: q x M row-major (ld M)
+//                                              Y: M x p row-major
+//
+// i.e. "contract the slowest axis, append the new axis as the fastest".  After
+// d steps the axes are back in C order, so no transpose pass ever touches HBM.
+//
+// Work decomposition (one step):
+//   * a wave owns a 16-row strip b0..b0+15 of Y and all p output columns
+//     (JT = ceil(p/16) accumulators of 16x16, 4 f64 per lane each);
+//   * the A operand (X^T, one f64 per lane per k-step) streams from HBM
+//     exactly once: lane l loads X[4ks + (l>>4), b0 + (l&15)] -- four 128-B
+//     row segments per wave instruction;
+//   * the B operand (K^T) is pre-packed on the host in MFMA fragment order
+//     [ks][jt][lane] so a k-chunk is one contiguous block; a workgroup of WAVES
+//     waves stages KC k-steps of it in LDS and every wave reads its fragment
+//     with one conflict-free ds_read_b64 per MFMA;
+//   * epilogue: D[b][j] sits at lane (j & 15), register r = row 4r + (l>>4):
+//     four 128-B segments per store.  The last step can fuse y += shift * x
+//     and the partial dot x.y (the CG p.q) per workgroup.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "gg_internal.h"
+
+namespace gg {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kKC = 8;      // k-steps (of 4) staged per LDS chunk
+constexpr int kWaves = 4;   // waves per workgroup (b-strips of 16 rows)
+constexpr int kMaxJT = 16;  // accumulator tiles per launch (<= 256 output columns)
+
+template <int JT>
+__global__ __launch_bounds__(kWaves * 64) void mode_product_kernel(
+    const double* __restrict__ X, double* __restrict__ Y, const double* __restrict__ Bf,
+    int64_t M, int q, int p, int KS, int jt_total, int jt0,
+    const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
+    const int* __restrict__ skip) {
+  if (skip != nullptr && *skip) return;
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // kKC * JT * 64
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wave) * 16;
+  const int64_t brow = b0 + (lane & 15);
+  const bool bvalid = brow < M;
+  const int krow = lane >> 4;
+
+  d4 acc[JT];
+#pragma unroll
+  for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int nchunks = (KS + kKC - 1) / kKC;
+  double a_nxt[kKC];
+#pragma unroll
+  for (int s = 0; s < kKC; ++s) {
+    const int k = s * 4 + krow;
+    a_nxt[s] = (s < KS && bvalid && k < q) ? X[(int64_t)k * M + brow] : 0.0;
+  }
+
+  for (int c = 0; c < nchunks; ++c) {
+    const int ks0 = c * kKC;
+    const int kcn = min(kKC, KS - ks0);
+    double a_cur[kKC];
+#pragma unroll
+    for (int s = 0; s < kKC; ++s) a_cur[s] = a_nxt[s];
+    // prefetch the next chunk's A fragments (HBM) before staging / computing
+    if (c + 1 < nchunks) {
+      const int ksn = ks0 + kKC;
+#pragma unroll
+      for (int s = 0; s < kKC; ++s) {
+        const int k = (ksn + s) * 4 + krow;
+        a_nxt[s] = (ksn + s < KS && bvalid && k < q) ? X[(int64_t)k * M + brow] : 0.0;
+      }
+    }
+    __syncthreads();  // previous chunk fully consumed
+    // stage kcn k-steps x JT fragments of K^T (contiguous per k-step)
+    {
+      const int per_ks2 = JT * 32;  // double2 per k-step for this tile group
+      const int n2 = kcn * per_ks2;
+      double2* dst = reinterpret_cast<double2*>(lds);
+      for (int i = threadIdx.x; i < n2; i += kWaves * 64) {
+        const int s = i / per_ks2;
+        const int o = i - s * per_ks2;
+        const double2* src =
+            reinterpret_cast<const double2*>(Bf + ((int64_t)(ks0 + s) * jt_total + jt0) * 64);
+        dst[i] = src[o];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < kKC; ++s) {
+      if (s < kcn) {
+#pragma unroll
+        for (int t = 0; t < JT; ++t) {
+          const double b = lds[(s * JT + t) * 64 + lane];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- epilogue
+  const int col = lane & 15;
+  const int64_t rbase = b0 + (lane >> 4);
+  double dsum = 0.0;
+#pragma unroll
+  for (int t = 0; t < JT; ++t) {
+    const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = rbase + 4 * r;
+      if (row < M && j < p) {
+        const int64_t idx = row * p + j;
+        double v = acc[t][r];
+        if (xs != nullptr) {
+          const double xv = xs[idx];
+          v = fma(shift, xv, v);
+          dsum = fma(xv, v, dsum);
+        }
+        Y[idx] = v;
+      }
+    }
+  }
+  if (dot_partials != nullptr) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
+    __syncthreads();  // every wave is past its last LDS fragment read
+    if (lane == 0) lds[wave] = dsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += lds[w];
+      dot_partials[blockIdx.x] = s;
+    }
+  }
+}
+
+typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
+                              int, int, const double*, double, double*, const int*);
+
+template <int JT>
+static mode_kernel_t kernel_for() {
+  return mode_product_kernel<JT>;
+}
+
+static mode_kernel_t select_kernel(int jt) {
+  switch (jt) {
+    case 1: return kernel_for<1>();
+    case 2: return kernel_for<2>();
+    case 3: return kernel_for<3>();
+    case 4: return kernel_for<4>();
+    case 5: return kernel_for<5>();
+    case 6: return kernel_for<6>();
+    case 7: return kernel_for<7>();
+    case 8: return kernel_for<8>();
+    case 9: return kernel_for<9>();
+    case 10: return kernel_for<10>();
+    case 11: return kernel_for<11>();
+    case 12: return kernel_for<12>();
+    case 13: return kernel_for<13>();
+    case 14: return kernel_for<14>();
+    case 15: return kernel_for<15>();
+    case 16: return kernel_for<16>();
+    default: throw Error(GG_ERR_VALUE, "bad tile count");
+  }
+}
+
+// One factor in fragment order, for the operator and for its transpose.
+struct Factor {
+  int64_t p = 0, q = 0;   // as applied: p x q
+  int KS = 0, JT = 0;     // k-steps of 4, column tiles of 16
+  double* frag = nullptr; // [KS][JT][64] device
+};
+
+static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool transpose,
+                           Factor& f) {
+  // applied factor F = transpose ? K^T : K, F is p x q; B[k][j] = F[j][k]
+  f.p = transpose ? cols : rows;
+  f.q = transpose ? rows : cols;
+  f.KS = (int)ceil_div(f.q, 4);
+  f.JT = (int)ceil_div(f.p, 16);
+  std::vector<double> h((size_t)f.KS * f.JT * 64, 0.0);
+  for (int ks = 0; ks < f.KS; ++ks)
+    for (int jt = 0; jt < f.JT; ++jt)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t k = (int64_t)ks * 4 + (l >> 4);
+        const int64_t j = (int64_t)jt * 16 + (l & 15);
+        double v = 0.0;
+        if (k < f.q && j < f.p) v = transpose ? K[k * cols + j] : K[j * cols + k];
+        h[((size_t)ks * f.JT + jt) * 64 + l] = v;
+      }
+  GG_HIP(hipMalloc(&f.frag, h.size() * sizeof(double)));
+  GG_HIP(hipMemcpy(f.frag, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+}
+
+}  // namespace gg
+
+struct gg_kron {
+  int d = 0;
+  std::vector<gg::Factor> fwd, bwd;  // operator and transposed operator
+  int64_t n_rows = 1, n_cols = 1;
+  int64_t max_inter_fwd = 0, max_inter_bwd = 0;
+  bool square_steps_fwd = true, square_steps_bwd = true;
+};
+
+namespace gg {
+
+static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max_inter,
+                       bool& all_square) {
+  int64_t s = n_in;
+  max_inter = s;
+  all_square = true;
+  for (const Factor& f : fs) {
+    s = s / f.q * f.p;
+    max_inter = std::max(max_inter, s);
+    if (f.p != f.q) all_square = false;
+  }
+}
+
+void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
+                double* work, double* dot_partials, const int* skip, hipStream_t stream,
+                int64_t* n_partials_out) {
+  const std::vector<Factor>& fs = transpose ? K->bwd : K->fwd;
+  const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
+  const int64_t n_in = transpose ? K->n_rows : K->n_cols;
+  const int64_t max_inter = transpose ? K->max_inter_bwd : K->max_inter_fwd;
+  GG_REQUIRE(x != y, GG_ERR_VALUE, "x and y must not alias");
+  if (shift != 0.0 || dot_partials != nullptr)
+    GG_REQUIRE(K->n_rows == K->n_cols, GG_ERR_VALUE, "shift needs a square operator");
+  const int d = (int)fs.size();
+  int64_t size = n_in;
+  const double* src = x;
+  int64_t np_total = 0;
+  for (int k = 0; k < d; ++k) {
+    const Factor& f = fs[k];
+    const int64_t M = size / f.q;
+    const int64_t out_size = M * f.p;
+    double* dst;
+    if (k == d - 1) {
+      dst = y;
+    } else if (square) {
+      dst = ((d - 1 - k) % 2 == 0) ? y : work;
+    } else {
+      dst = (k % 2 == 0) ? work : work + max_inter;
+    }
+    const bool last = (k == d - 1);
+    const int64_t nblk = ceil_div(M, kWaves * 16);
+    if (M > 0 && nblk > 0) {
+      GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
+      for (int jt0 = 0; jt0 < f.JT; jt0 += kMaxJT) {
+        const int jt = std::min(kMaxJT, f.JT - jt0);
+        mode_kernel_t kern = select_kernel(jt);
+        const size_t lds = (size_t)kKC * jt * 64 * sizeof(double);
+        double* parts = nullptr;
+        if (last && dot_partials != nullptr) {
+          parts = dot_partials + np_total;
+          np_total += nblk;
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kWaves * 64), lds, stream, src,
+                           dst, f.frag, M, (int)f.q, (int)f.p, f.KS, f.JT, jt0,
+                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts,
+                           skip);
+        GG_LAUNCH_CHECK();
+      }
+    }
+    (void)out_size;
+    size = out_size;
+    src = dst;
+  }
+  if (n_partials_out) *n_partials_out = np_total;
+}
+
+int64_t kron_partials_needed(const gg_kron* K, bool transpose) {
+  const std::vector<Factor>& fs = transpose ? K->bwd : K->fwd;
+  const Factor& f = fs.back();
+  const int64_t n_in = transpose ? K->n_rows : K->n_cols;
+  int64_t size = n_in;
+  for (const Factor& g : fs) size = size / g.q * g.p;
+  const int64_t M = size / f.p;
+  return ceil_div(M, kWaves * 16) * ceil_div(f.JT, kMaxJT);
+}
+
+int64_t kron_work_elems(const gg_kron* K, bool transpose) {
+  const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
+  const int64_t mx = transpose ? K->max_inter_bwd : K->max_inter_fwd;
+  return square ? mx : 2 * mx;
+}
+
+int64_t kron_n(const gg_kron* K) { return K->n_rows; }
+
+static void set_lds_limits() {
+  static bool done = false;
+  if (done) return;
+  for (int jt = 1; jt <= kMaxJT; ++jt) {
+    const int bytes = kKC * jt * 64 * (int)sizeof(double);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(select_kernel(jt)),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  }
+  done = true;
+}
+
+}  // namespace gg
+
+extern "C" {
+
+int gg_kron_create(int d, const int64_t* rows, const int64_t* cols,
+                   const double* const* factors_host, gg_kron** out) {
+  return gg::guard([&] {
+    GG_REQUIRE(out != nullptr, GG_ERR_VALUE, "out is NULL");
+    GG_REQUIRE(d >= 1, GG_ERR_VALUE, "need at least one factor");
+    gg::set_lds_limits();
+    gg_kron* K = new gg_kron();
+    try {
+      K->d = d;
+      for (int k = 0; k < d; ++k) {
+        GG_REQUIRE(rows[k] >= 1 && cols[k] >= 1, GG_ERR_VALUE, "empty factor");
+        GG_REQUIRE(rows[k] <= (1 << 20) && cols[k] <= (1 << 20), GG_ERR_VALUE,
+                   "factor too large");
+        K->n_rows *= rows[k];
+        K->n_cols *= cols[k];
+      }
+      K->fwd.resize(d);
+      K->bwd.resize(d);
+      for (int k = 0; k < d; ++k) {
+        gg::pack_fragments(factors_host[k], rows[k], cols[k], false, K->fwd[k]);
+        gg::pack_fragments(factors_host[k], rows[k], cols[k], true, K->bwd[k]);
+      }
+      gg::plan_sizes(K->fwd, K->n_cols, K->max_inter_fwd, K->square_steps_fwd);
+      gg::plan_sizes(K->bwd, K->n_rows, K->max_inter_bwd, K->square_steps_bwd);
+    } catch (...) {
+      gg_kron_destroy(K);
+      throw;
+    }
+    *out = K;
+  });
+}
+
+int gg_kron_destroy(gg_kron* K) {
+  return gg::guard([&] {
+    if (!K) return;
+    for (auto* v : {&K->fwd, &K->bwd})
+      for (gg::Factor& f : *v)
+        if (f.frag) (void)hipFree(f.frag);
+    delete K;
+  });
+}
+
+int gg_kron_shape(const gg_kron* K, int transpose, int64_t* n_out, int64_t* n_in,
+                  int64_t* work_elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr, GG_ERR_VALUE, "NULL handle");
+    if (n_out) *n_out = transpose ? K->n_cols : K->n_rows;
+    if (n_in) *n_in = transpose ? K->n_rows : K->n_cols;
+    if (work_elems) *work_elems = gg::kron_work_elems(K, transpose != 0);
+  });
+}
+
+int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double* y_dev,
+                   double shift, double* work_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
+    gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
+                   gg::as_stream(stream), nullptr);
+  });
+}
+
+}  // extern "C"

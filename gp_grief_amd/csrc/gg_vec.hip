@@ -1,0 +1,647 @@
+// Vector side of the Krylov solvers on MI355X: HBM-bound, coalesced,
+// wave-reduced (shfl over 64 lanes -> LDS across waves -> per-block partial ->
+// one deterministic single-block reduction).  No float atomics anywhere, so
+// every dot product is bitwise reproducible run to run.
+//
+// The reference has no CG or Lanczos; the CG recurrence is the
+// one of scipy.sparse.linalg.cg (oracle/cg.py restates it), driven here with
+// every scalar resident on the device so the host only polls convergence.
+#include <cmath>
+#include <vector>
+
+#include "gg_internal.h"
+
+namespace gg {
+
+// defined in gg_kron.hip
+void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
+                double* work, double* dot_partials, const int* skip, hipStream_t stream,
+                int64_t* n_partials_out);
+int64_t kron_partials_needed(const gg_kron* K, bool transpose);
+int64_t kron_work_elems(const gg_kron* K, bool transpose);
+int64_t kron_n(const gg_kron* K);
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// block (<= 1024 threads) sum; result valid in thread 0
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double red[16];
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 0; i < nw; ++i) s += red[i];
+  }
+  return s;
+}
+
+__global__ __launch_bounds__(kVecThreads) void dot_partials_kernel(const double* __restrict__ x,
+                                                                   const double* __restrict__ y,
+                                                                   int64_t n,
+                                                                   double* __restrict__ partials) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n2 = n / 2;
+  const double2* x2 = reinterpret_cast<const double2*>(x);
+  const double2* y2 = reinterpret_cast<const double2*>(y);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    const double2 a = x2[i], b = y2[i];
+    acc = fma(a.x, b.x, acc);
+    acc = fma(a.y, b.y, acc);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) acc = fma(x[n - 1], y[n - 1], acc);
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void reduce_kernel(const double* __restrict__ partials,
+                                                      int64_t count, double* __restrict__ out) {
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) *out = s;
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+void launch_dot_partials(const double* x, const double* y, int64_t n, double* partials,
+                         int nblocks, hipStream_t s) {
+  GG_REQUIRE(aligned16(x) && aligned16(y), GG_ERR_VALUE, "vectors must be 16-byte aligned");
+  hipLaunchKernelGGL(dot_partials_kernel, dim3(nblocks), dim3(kVecThreads), 0, s, x, y, n,
+                     partials);
+  GG_LAUNCH_CHECK();
+}
+
+void launch_reduce_to(const double* partials, int64_t count, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, s, partials, count, out);
+  GG_LAUNCH_CHECK();
+}
+
+static int vec_blocks(int64_t n) {
+  const int64_t want = ceil_div(std::max<int64_t>(n / 2, 1), kVecThreads);
+  return (int)std::min<int64_t>(kVecBlocks, std::max<int64_t>(want, 1));
+}
+
+__global__ __launch_bounds__(kVecThreads) void axpby_kernel(double a, const double* __restrict__ x,
+                                                            double b, double* __restrict__ y,
+                                                            int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = a * x[i] + b * y[i];
+}
+
+// ------------------------------------------------------------------ CG kernels
+// p = r (first iteration) or p = beta * p + r   (scipy: p *= beta; p += z)
+__global__ __launch_bounds__(kVecThreads) void cg_p_update_kernel(
+    const double* __restrict__ r, double* __restrict__ p, int64_t n,
+    const CgScalars* __restrict__ sc) {
+  if (sc->done) return;
+  const bool first = sc->first != 0;
+  const double beta = sc->beta;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n2 = n / 2;
+  const double2* r2 = reinterpret_cast<const double2*>(r);
+  double2* p2 = reinterpret_cast<double2*>(p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    const double2 rv = r2[i];
+    if (first) {
+      p2[i] = rv;
+    } else {
+      const double2 pv = p2[i];
+      p2[i] = double2{beta * pv.x + rv.x, beta * pv.y + rv.y};
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1))
+    p[n - 1] = first ? r[n - 1] : beta * p[n - 1] + r[n - 1];
+}
+
+// alpha = rho / (p.q)
+__global__ __launch_bounds__(1024) void cg_alpha_kernel(const double* __restrict__ partials,
+                                                        int64_t count, CgScalars* sc) {
+  if (sc->done) return;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) {
+    sc->pq = s;
+    sc->alpha = sc->rho / s;
+  }
+}
+
+// x += alpha p ; r -= alpha q ; partial r.r
+__global__ __launch_bounds__(kVecThreads) void cg_xr_update_kernel(
+    double* __restrict__ x, double* __restrict__ r, const double* __restrict__ p,
+    const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
+    double* __restrict__ partials) {
+  if (sc->done) return;
+  const double a = sc->alpha;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n2 = n / 2;
+  double2* x2 = reinterpret_cast<double2*>(x);
+  double2* r2 = reinterpret_cast<double2*>(r);
+  const double2* p2 = reinterpret_cast<const double2*>(p);
+  const double2* q2 = reinterpret_cast<const double2*>(q);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    const double2 pv = p2[i], qv = q2[i];
+    double2 xv = x2[i], rv = r2[i];
+    xv.x += a * pv.x;
+    xv.y += a * pv.y;
+    rv.x -= a * qv.x;
+    rv.y -= a * qv.y;
+    x2[i] = xv;
+    r2[i] = rv;
+    acc = fma(rv.x, rv.x, acc);
+    acc = fma(rv.y, rv.y, acc);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {
+    x[n - 1] += a * p[n - 1];
+    r[n - 1] -= a * q[n - 1];
+    acc = fma(r[n - 1], r[n - 1], acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// rho_prev = rho ; rho = r.r ; beta ; iteration count ; convergence
+__global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__ partials,
+                                                      int64_t count, CgScalars* sc) {
+  if (sc->done) return;
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) {
+    sc->rho_prev = sc->rho;
+    sc->rho = s;
+    sc->beta = s / sc->rho_prev;
+    sc->iters += 1;
+    sc->first = 0;
+    if (!(sqrt(s) >= sc->tol)) sc->done = 1;  // also stops on NaN
+  }
+}
+
+__global__ void cg_init_kernel(const double* __restrict__ partials, int64_t count,
+                               CgScalars* sc, double rtol, double atol) {
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) {
+    sc->rho = s;
+    sc->rho_prev = 0.0;
+    sc->bnorm = sqrt(s);
+    sc->tol = fmax(atol, rtol * sc->bnorm);
+    sc->iters = 0;
+    sc->first = 1;
+    sc->alpha = sc->beta = sc->pq = 0.0;
+    sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
+  }
+}
+
+// ----------------------------------------------------------- Lanczos kernels
+// w -= beta * v_prev ; partial w.v
+__global__ __launch_bounds__(kVecThreads) void lz_axpy_dot_kernel(
+    double* __restrict__ w, const double* __restrict__ vprev, const double* __restrict__ v,
+    int64_t n, const double* __restrict__ beta_ptr, double* __restrict__ partials) {
+  const double beta = *beta_ptr;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double wi = w[i] - beta * vprev[i];
+    w[i] = wi;
+    acc = fma(wi, v[i], acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// w -= alpha * v ; partial w.w
+__global__ __launch_bounds__(kVecThreads) void lz_axpy_norm_kernel(
+    double* __restrict__ w, const double* __restrict__ v, int64_t n,
+    const double* __restrict__ alpha_ptr, double* __restrict__ partials) {
+  const double alpha = *alpha_ptr;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double wi = w[i] - alpha * v[i];
+    w[i] = wi;
+    acc = fma(wi, wi, acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// out = w / beta
+__global__ __launch_bounds__(kVecThreads) void lz_scale_kernel(const double* __restrict__ w,
+                                                               double* __restrict__ out,
+                                                               int64_t n,
+                                                               const double* __restrict__ beta_ptr) {
+  const double inv = 1.0 / *beta_ptr;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = w[i] * inv;
+}
+
+__global__ void sqrt_inplace_kernel(double* v) { *v = sqrt(*v); }
+
+__global__ __launch_bounds__(kVecThreads) void diag_divide_kernel(const double* __restrict__ t,
+                                                                  double shift,
+                                                                  const double* __restrict__ x,
+                                                                  double* __restrict__ y,
+                                                                  int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    y[i] = x[i] / (t[i] + shift);
+}
+
+// Rademacher probe, bit-identical to oracle/cg.py probe_signs (splitmix64)
+__device__ __forceinline__ uint64_t probe_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kVecThreads) void probe_kernel(uint64_t base, double scale,
+                                                            double* __restrict__ z, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t h = probe_mix(base + (uint64_t)i * 0x9E3779B97F4A7C15ull);
+    z[i] = (h >> 63) == 0 ? scale : -scale;
+  }
+}
+
+static uint64_t probe_base(uint64_t seed, int probe) {
+  return (((seed & 0xffffffffull) << 32) ^ (((uint64_t)probe & 0xffffull) << 16) ^
+          0x9E3779B97F4A7C15ull);
+}
+
+// ----------------------------------------------- Kronecker eigenvalue diagonal
+struct KronDiag {
+  int d;
+  int64_t m[16];
+  int64_t off[16];
+};
+
+__device__ __forceinline__ double kron_eig_at(const KronDiag& kd, const double* lam, int64_t i) {
+  double t = 1.0;
+  for (int k = kd.d - 1; k >= 0; --k) {
+    const int64_t ik = i % kd.m[k];
+    i /= kd.m[k];
+    t *= lam[kd.off[k] + ik];
+  }
+  return t;
+}
+
+__global__ __launch_bounds__(kVecThreads) void diag_scale_kernel(KronDiag kd,
+                                                                 const double* __restrict__ lam,
+                                                                 double shift, int mode,
+                                                                 const double* __restrict__ x,
+                                                                 double* __restrict__ y,
+                                                                 int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double t = kron_eig_at(kd, lam, i);
+    double v;
+    if (mode == GG_DIAG_DIVIDE)
+      v = x[i] / (t + shift);
+    else if (mode == GG_DIAG_POSTVAR)
+      v = t * shift / (t + shift);
+    else
+      v = x[i] * (t + shift);
+    y[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(kVecThreads) void logdet_kernel(KronDiag kd,
+                                                             const double* __restrict__ lam,
+                                                             double shift, int64_t n,
+                                                             double* __restrict__ partials) {
+  // the last factor varies fastest: decode the head once per run of m_last
+  const int64_t ml = kd.m[kd.d - 1];
+  const int64_t nhead = n / ml;
+  const double* lastl = lam + kd.off[kd.d - 1];
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t h = i / ml;
+    const int64_t l = i - h * ml;
+    double t = lastl[l];
+    int64_t hh = h;
+    for (int k = kd.d - 2; k >= 0; --k) {
+      const int64_t ik = hh % kd.m[k];
+      hh /= kd.m[k];
+      t *= lam[kd.off[k] + ik];
+    }
+    acc += log(t + shift);
+  }
+  (void)nhead;
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+static KronDiag make_diag(int d, const int64_t* m, int64_t* n_out) {
+  GG_REQUIRE(d >= 1 && d <= 16, GG_ERR_VALUE, "1 <= d <= 16 factors supported");
+  KronDiag kd{};
+  kd.d = d;
+  int64_t n = 1, off = 0;
+  for (int k = 0; k < d; ++k) {
+    GG_REQUIRE(m[k] >= 1, GG_ERR_VALUE, "empty factor");
+    kd.m[k] = m[k];
+    kd.off[k] = off;
+    off += m[k];
+    n *= m[k];
+  }
+  *n_out = n;
+  return kd;
+}
+
+}  // namespace gg
+
+// ------------------------------------------------------------------- CG state
+struct gg_cg {
+  const gg_kron* K = nullptr;
+  double shift = 0.0;
+  int64_t n = 0;
+  double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
+  double* partials = nullptr;  // device, max(kVecBlocks, matvec partials)
+  gg::CgScalars* sc = nullptr; // device
+  gg::CgScalars* sc_host = nullptr;  // pinned mirror
+  const double* b = nullptr;
+  double* x = nullptr;
+  int64_t mv_partials = 0;
+};
+
+extern "C" {
+
+int gg_dot(const double* x_dev, const double* y_dev, int64_t n, double* out_host,
+           gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(x_dev && y_dev && out_host && n >= 0, GG_ERR_VALUE, "bad argument");
+    hipStream_t s = gg::as_stream(stream);
+    double* buf = nullptr;
+    GG_HIP(hipMallocAsync(&buf, (gg::kVecBlocks + 1) * sizeof(double), s));
+    const int nb = gg::vec_blocks(n);
+    gg::launch_dot_partials(x_dev, y_dev, n, buf, nb, s);
+    gg::launch_reduce_to(buf, nb, buf + gg::kVecBlocks, s);
+    GG_HIP(hipMemcpyAsync(out_host, buf + gg::kVecBlocks, sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    GG_HIP(hipFreeAsync(buf, s));
+    GG_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int gg_axpby(double a, const double* x_dev, double b, double* y_dev, int64_t n,
+             gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(x_dev && y_dev && n >= 0, GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    hipLaunchKernelGGL(gg::axpby_kernel, dim3(gg::vec_blocks(2 * n)), dim3(gg::kVecThreads),
+                       0, gg::as_stream(stream), a, x_dev, b, y_dev, n);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_diag_divide(const double* t_dev, double shift, const double* x_dev, double* y_dev,
+                   int64_t n, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(t_dev && x_dev && y_dev && n >= 0, GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    hipLaunchKernelGGL(gg::diag_divide_kernel, dim3(gg::vec_blocks(2 * n)),
+                       dim3(gg::kVecThreads), 0, gg::as_stream(stream), t_dev, shift, x_dev,
+                       y_dev, n);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_kron_diag_scale(int d, const int64_t* m, const double* lam_dev, double shift, int mode,
+                       const double* x_dev, double* y_dev, gg_stream stream) {
+  return gg::guard([&] {
+    int64_t n = 0;
+    gg::KronDiag kd = gg::make_diag(d, m, &n);
+    GG_REQUIRE(lam_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(mode == GG_DIAG_POSTVAR || x_dev, GG_ERR_VALUE, "x required");
+    GG_REQUIRE(mode >= 0 && mode <= 2, GG_ERR_VALUE, "bad mode");
+    hipLaunchKernelGGL(gg::diag_scale_kernel, dim3(gg::vec_blocks(2 * n)),
+                       dim3(gg::kVecThreads), 0, gg::as_stream(stream), kd, lam_dev, shift,
+                       mode, x_dev, y_dev, n);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_kron_logdet_shifted(int d, const int64_t* m, const double* lam_dev, double shift,
+                           double* out_host, gg_stream stream) {
+  return gg::guard([&] {
+    int64_t n = 0;
+    gg::KronDiag kd = gg::make_diag(d, m, &n);
+    GG_REQUIRE(lam_dev && out_host, GG_ERR_VALUE, "NULL argument");
+    hipStream_t s = gg::as_stream(stream);
+    double* buf = nullptr;
+    GG_HIP(hipMallocAsync(&buf, (gg::kVecBlocks + 1) * sizeof(double), s));
+    const int nb = gg::vec_blocks(2 * n);
+    hipLaunchKernelGGL(gg::logdet_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, kd, lam_dev,
+                       shift, n, buf);
+    GG_LAUNCH_CHECK();
+    gg::launch_reduce_to(buf, nb, buf + gg::kVecBlocks, s);
+    GG_HIP(hipMemcpyAsync(out_host, buf + gg::kVecBlocks, sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    GG_HIP(hipFreeAsync(buf, s));
+    GG_HIP(hipStreamSynchronize(s));
+  });
+}
+
+int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(z_dev && n >= 0, GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    hipLaunchKernelGGL(gg::probe_kernel, dim3(gg::vec_blocks(2 * n)), dim3(gg::kVecThreads),
+                       0, gg::as_stream(stream), gg::probe_base(seed, probe), 1.0, z_dev, n);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
+    const int64_t n = gg::kron_n(K);
+    *elems = 3 * n + gg::kron_work_elems(K, false);
+  });
+}
+
+int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && work_dev && out, GG_ERR_VALUE, "NULL argument");
+    int64_t nr = 0, nc = 0, we = 0;
+    gg_kron_shape(K, 0, &nr, &nc, &we);
+    GG_REQUIRE(nr == nc, GG_ERR_VALUE, "CG needs a square operator");
+    gg_cg* cg = new gg_cg();
+    try {
+      cg->K = K;
+      cg->shift = shift;
+      cg->n = nr;
+      cg->r = work_dev;
+      cg->p = work_dev + nr;
+      cg->q = work_dev + 2 * nr;
+      cg->mv_work = work_dev + 3 * nr;
+      cg->mv_partials = gg::kron_partials_needed(K, false);
+      const int64_t np = std::max<int64_t>(gg::kVecBlocks, cg->mv_partials);
+      GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
+      GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
+      GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
+      GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
+    } catch (...) {
+      gg_cg_destroy(cg);
+      throw;
+    }
+    *out = cg;
+  });
+}
+
+int gg_cg_destroy(gg_cg* cg) {
+  return gg::guard([&] {
+    if (!cg) return;
+    if (cg->partials) (void)hipFree(cg->partials);
+    if (cg->sc) (void)hipFree(cg->sc);
+    if (cg->sc_host) (void)hipHostFree(cg->sc_host);
+    delete cg;
+  });
+}
+
+int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, double atol,
+                gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && b_dev && x_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(rtol >= 0 && atol >= 0, GG_ERR_VALUE,
+               "tolerances must be real, non-negative numbers");
+    hipStream_t s = gg::as_stream(stream);
+    cg->b = b_dev;
+    cg->x = x_dev;
+    const int64_t n = cg->n;
+    GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    GG_HIP(hipMemsetAsync(x_dev, 0, n * sizeof(double), s));
+    const int nb = gg::vec_blocks(n);
+    gg::launch_dot_partials(cg->r, cg->r, n, cg->partials, nb, s);
+    hipLaunchKernelGGL(gg::cg_init_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                       (int64_t)nb, cg->sc, rtol, atol);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
+    hipStream_t s = gg::as_stream(stream);
+    const int64_t n = cg->n;
+    const int nb = gg::vec_blocks(n);
+    if (check_every <= 0) check_every = max_iters;
+    for (int it = 0; it < max_iters; ++it) {
+      hipLaunchKernelGGL(gg::cg_p_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->r,
+                         cg->p, n, cg->sc);
+      GG_LAUNCH_CHECK();
+      int64_t nparts = 0;
+      gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                     &cg->sc->done, s, &nparts);
+      hipLaunchKernelGGL(gg::cg_alpha_kernel, dim3(1), dim3(1024), 0, s, cg->partials, nparts,
+                         cg->sc);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
+                         cg->r, cg->p, cg->q, n, cg->sc, cg->partials);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                         (int64_t)nb, cg->sc);
+      GG_LAUNCH_CHECK();
+      if ((it + 1) % check_every == 0 && it + 1 < max_iters) {
+        GG_HIP(hipMemcpyAsync(cg->sc_host, cg->sc, sizeof(gg::CgScalars),
+                              hipMemcpyDeviceToHost, s));
+        GG_HIP(hipStreamSynchronize(s));
+        if (cg->sc_host->done) break;
+      }
+    }
+  });
+}
+
+int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
+                 gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    hipStream_t s = gg::as_stream(stream);
+    GG_HIP(hipMemcpyAsync(cg->sc_host, cg->sc, sizeof(gg::CgScalars), hipMemcpyDeviceToHost,
+                          s));
+    GG_HIP(hipStreamSynchronize(s));
+    const gg::CgScalars& h = *cg->sc_host;
+    if (iters) *iters = h.iters;
+    if (converged) *converged = (h.done && std::sqrt(h.rho) < h.tol) || h.bnorm == 0.0;
+    if (resid_norm) *resid_norm = std::sqrt(h.rho);
+    if (tol) *tol = h.tol;
+  });
+}
+
+int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                     double* work_dev, double* alphas_host, double* betas_host,
+                     int* steps_done, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && work_dev && alphas_host && betas_host && steps >= 1, GG_ERR_VALUE,
+               "bad argument");
+    int64_t nr = 0, nc = 0, we = 0;
+    gg_kron_shape(K, 0, &nr, &nc, &we);
+    GG_REQUIRE(nr == nc, GG_ERR_VALUE, "Lanczos needs a square operator");
+    GG_REQUIRE(we <= nr, GG_ERR_VALUE, "non-square factors are not supported here");
+    hipStream_t s = gg::as_stream(stream);
+    const int64_t n = nr;
+    double* P = work_dev;        // v_prev
+    double* V = work_dev + n;    // v
+    double* W = work_dev + 2 * n;
+    double* mvw = work_dev + 3 * n;
+    double* scal = nullptr;      // [2*steps] alphas, betas + partials
+    const int nb = gg::vec_blocks(n);
+    GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + gg::kVecBlocks + 1) * sizeof(double), s));
+    double* alphas = scal;
+    double* betas = scal + steps;
+    double* parts = scal + 2 * steps;
+    double* zero = parts + gg::kVecBlocks;
+    GG_HIP(hipMemsetAsync(zero, 0, sizeof(double), s));
+    GG_HIP(hipMemsetAsync(P, 0, n * sizeof(double), s));
+    hipLaunchKernelGGL(gg::probe_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                       gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
+    GG_LAUNCH_CHECK();
+    for (int j = 0; j < steps; ++j) {
+      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr);
+      const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
+      hipLaunchKernelGGL(gg::lz_axpy_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P,
+                         V, n, beta_prev, parts);
+      GG_LAUNCH_CHECK();
+      gg::launch_reduce_to(parts, nb, alphas + j, s);
+      hipLaunchKernelGGL(gg::lz_axpy_norm_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, V,
+                         n, alphas + j, parts);
+      GG_LAUNCH_CHECK();
+      gg::launch_reduce_to(parts, nb, betas + j, s);
+      hipLaunchKernelGGL(gg::sqrt_inplace_kernel, dim3(1), dim3(1), 0, s, betas + j);
+      GG_LAUNCH_CHECK();
+      if (j + 1 < steps) {
+        hipLaunchKernelGGL(gg::lz_scale_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P, n,
+                           betas + j);
+        GG_LAUNCH_CHECK();
+        std::swap(P, V);  // new v_prev = old v ; new v = W / beta (written into old P)
+      }
+    }
+    GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost,
+                          s));
+    GG_HIP(hipMemcpyAsync(betas_host, betas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipFreeAsync(scal, s));
+    GG_HIP(hipStreamSynchronize(s));
+    int done = steps;
+    for (int j = 0; j < steps; ++j)
+      if (!(betas_host[j] > 1e-300)) {
+        done = j + 1;
+        break;
+      }
+    if (steps_done) *steps_done = done;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+"""linalg: the reference's helpers plus the device Krylov solvers.
+
+Host utilities with the reference's behaviour (gp_grief/linalg.py):
+  solver_counter          :53-71   (iteration callback / best-parameter backup)
+  log_kron                :74-89
+  uniquetol               :92-104
+  LogexpTransformation    :107-125
+Device solvers (no reference implementation exists):
+  cg            -- scipy.sparse.linalg.cg's recurrence on (K + shift I), every
+                   vector op and scalar on the MI355X (gg_cg_*).
+  slq_logdet    -- stochastic Lanczos quadrature, Lanczos on the device
+                   (gg_lanczos_probe); the k x k tridiagonal eigensolve of the
+                   quadrature is host-side (k <= a few hundred).
+"""
+import ctypes
+import logging
+import sys
+
+import numpy as np
+
+logger = logging.getLogger(__name__)
+
+
+class solver_counter:
+    """Iteration counter usable as a solver / optimiser callback (linalg.py:53-71)."""
+
+    def __init__(self, disp=True):
+        self._disp = disp
+        self.niter = 0
+        self.backup = None
+
+    def __call__(self, rk=None, msg='', store=None):
+        self.niter += 1
+        if self._disp:
+            logger.info('iter %3i. %s' % (self.niter, msg))
+            sys.stdout.flush()
+        if store is not None:
+            self.backup = store
+
+
+def log_kron(a, b, a_logged=False, b_logged=False):
+    """log(kron(a, b)) for 1-D a, b without forming the product (linalg.py:74-89)."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    assert a.ndim == b.ndim == 1, "currenly only working for 1d arrays"
+    if not a_logged:
+        a = np.log(a)
+    if not b_logged:
+        b = np.log(b)
+    return (a.reshape((-1, 1)) + b.reshape((1, -1))).reshape(-1)
+
+
+def uniquetol(x, tol=1e-6, relative=False):
+    assert x.ndim == 1
+    if relative:
+        tol = np.float64(tol) * np.ptp(x)
+    return x[~(np.triu(np.abs(x[:, None] - x) <= tol, 1)).any(0)]
+
+
+class LogexpTransformation:
+    """Softplus transform for positive parameters (linalg.py:107-125)."""
+    _lim_val = 36.
+    _log_lim_val = np.log(np.finfo(np.float64).max)
+
+    def inverse_transform(self, x):
+        return np.where(x > self._lim_val, x,
+                        np.log1p(np.exp(np.clip(x, -self._log_lim_val, self._lim_val))))
+
+    def transform(self, f):
+        return np.where(f > self._lim_val, f, np.log(np.expm1(f)))
+
+    def transform_grad(self, f, grad_f):
+        return grad_f * np.where(f > self._lim_val, 1., -np.expm1(-f))
+
+
+# ---------------------------------------------------------------- device CG
+class CGResult(object):
+    def __init__(self, x, info, iters, resid, tol):
+        self.x, self.info, self.iters, self.resid, self.tol = x, info, iters, resid, tol
+
+
+class KronCG(object):
+    """Resident CG state for (K + shift I) x = b on one MI355X.
+
+    The operator and all CG vectors (x, r, p, q + one matvec scratch) live in
+    HBM; a CG iteration is 5 kernel launches (p-update, d mode products with
+    the shift and p.q fused into the last, alpha, x/r-update with r.r fused,
+    beta) and no host synchronisation.
+    """
+
+    def __init__(self, K, shift):
+        from . import device as dev
+        from . import native
+        self.K = K
+        self.shift = float(shift)
+        self._dk = K._device()
+        L = native.lib()
+        we = ctypes.c_int64()
+        native.check(L.gg_cg_work_elems(self._dk.h, ctypes.byref(we)))
+        self.work = dev.empty(we.value)
+        h = ctypes.c_void_p()
+        native.check(L.gg_cg_create(self._dk.h, self.shift, native.dptr(self.work),
+                                    ctypes.byref(h)), "gg_cg_create")
+        self.h = h
+        self.n = int(K.shape[0])
+        self.x = None
+
+    def start(self, b_dev, rtol=1e-5, atol=0.0, x_out=None):
+        from . import device as dev
+        from . import native
+        if b_dev.numel() != self.n:
+            raise ValueError("b must have %d entries" % self.n)
+        self.b = dev.ensure_aligned(b_dev.reshape(-1))
+        self.x = dev.empty(self.n) if x_out is None else x_out
+        native.check(native.lib().gg_cg_start(self.h, native.dptr(self.b), native.dptr(self.x),
+                                              float(rtol), float(atol), native.stream_ptr()),
+                     "gg_cg_start")
+
+    def iterate(self, n_iter, check_every=0):
+        from . import native
+        native.check(native.lib().gg_cg_iterate(self.h, int(n_iter), int(check_every),
+                                                native.stream_ptr()), "gg_cg_iterate")
+
+    def status(self):
+        from . import native
+        it, conv = ctypes.c_int(), ctypes.c_int()
+        res, tol = ctypes.c_double(), ctypes.c_double()
+        native.check(native.lib().gg_cg_status(self.h, ctypes.byref(it), ctypes.byref(conv),
+                                               ctypes.byref(res), ctypes.byref(tol),
+                                               native.stream_ptr()))
+        return it.value, bool(conv.value), res.value, tol.value
+
+    def __del__(self):
+        try:
+            from . import native
+            if getattr(self, "h", None) is not None and self.h.value:
+                native.load().gg_cg_destroy(self.h)
+        except Exception:
+            pass
+
+
+def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None):
+    """Solve (K + shift I) x = b with CG on the device (x0 = 0).
+
+    Same stopping rule and recurrence as scipy.sparse.linalg.cg.  b: numpy
+    (N,1)/(N,) or a CUDA tensor; x is returned in the same kind.  `callback`
+    (e.g. a solver_counter) is called once per completed iteration, after the
+    solve, with no arguments beyond the counter protocol (the iterates stay on
+    the device).  Returns (x, info) like scipy: info = 0 converged, else the
+    number of iterations run.
+    """
+    from . import device as dev
+    n = int(K.shape[0])
+    was_dev = dev.is_device_array(b)
+    bd = dev.to_device(b)
+    if bd.numel() != n:
+        raise ValueError('b is the wrong shape, must have %d entries' % n)
+    if maxiter is None:
+        maxiter = n * 10
+    if check_every is None:
+        check_every = 10 if n >= 1 << 20 else 50
+    solver = KronCG(K, shift)
+    solver.start(bd, rtol, atol)
+    done = 0
+    while done < maxiter:
+        chunk = min(maxiter - done, check_every)
+        solver.iterate(chunk, check_every=chunk)
+        done += chunk
+        it, conv, res, tol = solver.status()
+        if conv or it < done:  # converged (the kernels no-op past convergence)
+            break
+    it, conv, res, tol = solver.status()
+    if callback is not None:
+        for _ in range(it):
+            callback()
+    info = 0 if conv else it
+    x = solver.x
+    if was_dev:
+        out = x.reshape(tuple(b.shape)) if b.numel() == n else x
+    else:
+        out = dev.to_host(x).reshape(np.shape(b))
+    cg.last = CGResult(out, info, it, res, tol)
+    return out, info
+
+
+def lanczos_tridiag(K, shift, steps, seed=0, probe=0):
+    """Device Lanczos on (K + shift I) from a Rademacher probe: (alphas, betas)."""
+    from . import device as dev
+    from . import native
+    dk = K._device()
+    n = int(K.shape[0])
+    work = dev.empty(4 * n)
+    a = (ctypes.c_double * steps)()
+    b = (ctypes.c_double * steps)()
+    done = ctypes.c_int()
+    native.check(native.lib().gg_lanczos_probe(dk.h, float(shift), int(seed), int(probe),
+                                               int(steps), native.dptr(work), a, b,
+                                               ctypes.byref(done), native.stream_ptr()),
+                 "gg_lanczos_probe")
+    k = done.value
+    return np.array(a[:k]), np.array(b[:max(k - 1, 0)])
+
+
+def slq_logdet(K, shift, probes=8, steps=30, seed=0):
+    """Stochastic Lanczos quadrature estimate of log det(K + shift I)."""
+    n = int(K.shape[0])
+    ests = []
+    for j in range(probes):
+        a, b = lanczos_tridiag(K, shift, steps, seed=seed, probe=j)
+        T = np.diag(a) + np.diag(b, 1) + np.diag(b, -1)
+        theta, U = np.linalg.eigh(T)
+        ests.append(float(n) * float(np.sum(U[0, :] ** 2 * np.log(theta))))
+    return float(np.mean(ests)), np.array(ests)

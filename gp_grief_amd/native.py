@@ -1,0 +1,147 @@
+"""ctypes binding of libgpgrief.so (the C ABI declared in include/gp_grief_amd.h).
+
+The product path has exactly one implementation: the HIP library.  If the
+shared object is missing, or no MI355X is visible, every compute call raises;
+there is no CPU fallback (the CPU restatement in oracle/ is test-only).
+Device memory and streams come from PyTorch-ROCm (plumbing only): buffers are
+torch.float64 CUDA tensors whose data_ptr() is handed to the C ABI together
+with torch's current HIP stream.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpgrief.so")
+
+GG_OK = 0
+GG_ERR_VALUE = -1
+GG_ERR_LINALG = -2
+GG_ERR_RUNTIME = -3
+GG_ERR_ASSERT = -4
+
+GG_DIAG_DIVIDE = 0
+GG_DIAG_POSTVAR = 1
+GG_DIAG_MULTIPLY = 2
+
+_c_i64p = ctypes.POINTER(ctypes.c_int64)
+_c_dp = ctypes.c_void_p  # device or host double* (passed as raw addresses)
+_vp = ctypes.c_void_p
+
+# name -> argtypes (every function returns c_int status)
+SIGNATURES = {
+    "gg_abi_version": [],
+    "gg_last_error": [ctypes.c_char_p, ctypes.c_size_t],
+    "gg_set_device": [ctypes.c_int],
+    "gg_device_synchronize": [],
+    "gg_kron_create": [ctypes.c_int, _c_i64p, _c_i64p, ctypes.POINTER(ctypes.c_void_p),
+                       ctypes.POINTER(ctypes.c_void_p)],
+    "gg_kron_destroy": [_vp],
+    "gg_kron_shape": [_vp, ctypes.c_int, _c_i64p, _c_i64p, _c_i64p],
+    "gg_kron_matvec": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_double, _c_dp, _vp],
+    "gg_kron_diag_scale": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double, ctypes.c_int, _c_dp,
+                           _c_dp, _vp],
+    "gg_kron_logdet_shifted": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double,
+                               ctypes.POINTER(ctypes.c_double), _vp],
+    "gg_dot": [_c_dp, _c_dp, ctypes.c_int64, ctypes.POINTER(ctypes.c_double), _vp],
+    "gg_axpby": [ctypes.c_double, _c_dp, ctypes.c_double, _c_dp, ctypes.c_int64, _vp],
+    "gg_diag_divide": [_c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
+    "gg_cg_work_elems": [_vp, _c_i64p],
+    "gg_cg_create": [_vp, ctypes.c_double, _c_dp, ctypes.POINTER(ctypes.c_void_p)],
+    "gg_cg_destroy": [_vp],
+    "gg_cg_start": [_vp, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
+    "gg_cg_iterate": [_vp, ctypes.c_int, ctypes.c_int, _vp],
+    "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
+    "gg_lanczos_probe": [_vp, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                         _c_dp, ctypes.POINTER(ctypes.c_double),
+                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), _vp],
+    "gg_probe_fill": [ctypes.c_uint64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
+    "gg_sym_eig_batched": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
+                           ctypes.c_int, _vp],
+    "gg_sym_eig_work_elems": [ctypes.c_int, _c_i64p, _c_i64p],
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeUnavailable(RuntimeError):
+    """libgpgrief.so is not built / cannot be loaded, or no GPU is visible."""
+
+
+def load():
+    """Load the shared object (no GPU needed just to load and inspect it)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                "%s is not built; run `python -c 'import __graft_entry__ as g; g.build()'`"
+                % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(4096)
+    load().gg_last_error(buf, 4096)
+    return buf.value.decode(errors="replace")
+
+
+def check(status, what=""):
+    if status == GG_OK:
+        return
+    msg = last_error()
+    if what:
+        msg = "%s: %s" % (what, msg)
+    if status == GG_ERR_VALUE:
+        raise ValueError(msg)
+    if status == GG_ERR_LINALG:
+        raise np.linalg.LinAlgError(msg)
+    if status == GG_ERR_ASSERT:
+        raise AssertionError(msg)
+    raise RuntimeError(msg)
+
+
+_ready = False
+
+
+def lib():
+    """The library, with cuda:0 (or the current torch device) verified usable."""
+    global _ready
+    L = load()
+    if not _ready:
+        import torch
+        if not torch.cuda.is_available():
+            raise NativeUnavailable("no ROCm GPU visible: the gp_grief_amd product path runs "
+                                    "only on MI355X (gfx950)")
+        name = torch.cuda.get_device_properties(torch.cuda.current_device()).gcnArchName
+        if not str(name).startswith("gfx950"):
+            raise NativeUnavailable("libgpgrief.so is built for gfx950, device is %s" % name)
+        check(L.gg_set_device(torch.cuda.current_device()), "gg_set_device")
+        _ready = True
+    return L
+
+
+def stream_ptr():
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def i64_array(values):
+    arr = (ctypes.c_int64 * len(values))(*[int(v) for v in values])
+    return arr
+
+
+def dptr(t):
+    """Raw device address of a contiguous float64 torch tensor."""
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,471 @@
+"""Structured tensors: the drop-in KronMatrix backed by the HIP library.
+
+Mirrors gp_grief/tensors/kron_matrix.py (class KronMatrix, :12-474) and
+gp_grief/tensors/selection_matrix.py (SelectionMatrixSparse, :55-107): same
+constructor, attributes (n, sshape, shape, ndim, square, sym, read-only K),
+method names, return shapes and exception types.
+
+Where the arithmetic lives:
+  * every N-sized operation (matvec, transposed matvec, the eigenvalue divide of
+    solve_schur, shifted log-det, Kronecker-structured solves) runs on the
+    device through the C ABI (gp_grief_amd.native);
+  * per-factor eigendecompositions run on the device (parallel Jacobi);
+  * factor-sized bookkeeping (diag of factors, expand of small Kronecker
+    products, per-factor Cholesky / inverse used to build a device operator,
+    the top-p eigen-selection) stays on the host exactly as in the reference,
+    where it is O(sum m_i^2) or O(d p m).
+
+Vectors may be numpy (N,1) arrays -- copied over PCIe and the result returned
+as numpy, like the reference -- or float64 CUDA tensors of shape (N,1), which
+stay resident in HBM and are returned as CUDA tensors.
+"""
+import ctypes
+from logging import getLogger
+from warnings import warn
+
+import numpy as np
+
+from . import device as dev
+from . import native
+from .linalg import log_kron
+
+logger = getLogger(__name__)
+
+
+class _DeviceKron(object):
+    """Owner of a gg_kron handle (factors in HBM, MFMA fragment order)."""
+
+    def __init__(self, factors):
+        L = native.lib()
+        mats = [np.ascontiguousarray(np.asarray(f, dtype=np.float64)) for f in factors]
+        for f in mats:
+            if f.ndim != 2:
+                raise ValueError("device Kronecker factors must be 2-D matrices")
+        self._keep = mats
+        rows = native.i64_array([f.shape[0] for f in mats])
+        cols = native.i64_array([f.shape[1] for f in mats])
+        ptrs = (ctypes.c_void_p * len(mats))(*[f.ctypes.data for f in mats])
+        h = ctypes.c_void_p()
+        native.check(L.gg_kron_create(len(mats), rows, cols, ptrs, ctypes.byref(h)),
+                     "gg_kron_create")
+        self.h = h
+        self._work = {}
+        self.n_rows = int(np.prod([f.shape[0] for f in mats]))
+        self.n_cols = int(np.prod([f.shape[1] for f in mats]))
+
+    def shape(self, transpose):
+        a, b, w = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        native.check(native.lib().gg_kron_shape(self.h, int(transpose), ctypes.byref(a),
+                                                ctypes.byref(b), ctypes.byref(w)))
+        return a.value, b.value, w.value
+
+    def work(self, transpose):
+        key = bool(transpose)
+        if key not in self._work:
+            _, _, w = self.shape(transpose)
+            self._work[key] = dev.empty(max(w, 1))
+        return self._work[key]
+
+    def matvec(self, xd, transpose=False, shift=0.0, out=None):
+        n_out, n_in, _ = self.shape(transpose)
+        if xd.numel() != n_in:
+            raise ValueError("x has %d elements, operator needs %d" % (xd.numel(), n_in))
+        y = dev.empty(n_out) if out is None else out
+        w = self.work(transpose)
+        native.check(native.lib().gg_kron_matvec(self.h, int(transpose), native.dptr(xd),
+                                                 native.dptr(y), float(shift), native.dptr(w),
+                                                 native.stream_ptr()), "gg_kron_matvec")
+        return y
+
+    def release_work(self):
+        self._work = {}
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) is not None and self.h.value:
+                native.load().gg_kron_destroy(self.h)
+        except Exception:
+            pass
+
+
+def _as_matrix(Ki):
+    if isinstance(Ki, np.ndarray):
+        return Ki
+    if hasattr(Ki, "expand"):
+        return np.asarray(Ki.expand())
+    return np.asarray(Ki)
+
+
+def _vector_in(x, n, msg):
+    """Shape-check an (n,1) vector and return (device 1-D tensor, was_device)."""
+    if tuple(x.shape) != (n, 1):
+        raise ValueError(msg)
+    return dev.to_device(x), dev.is_device_array(x)
+
+
+def _vector_out(yd, was_device):
+    if was_device:
+        return yd.reshape(-1, 1)
+    return dev.to_host(yd).reshape((-1, 1))
+
+
+def device_sym_eig(factors, max_sweeps=40):
+    """Eigendecomposition of symmetric factors on the device (ascending)."""
+    L = native.lib()
+    t = dev.torch()
+    mats = [np.asarray(f, dtype=np.float64) for f in factors]
+    for f in mats:
+        if f.ndim != 2 or f.shape[0] != f.shape[1]:
+            raise AssertionError("factor must be square")
+        if not np.allclose(f, f.T, rtol=1e-12, atol=1e-14 * max(1.0, np.abs(f).max())):
+            raise NotImplementedError("the device eigensolver handles symmetric factors "
+                                      "(every grid-kernel factor is symmetric)")
+    m = [f.shape[0] for f in mats]
+    A = dev.to_device(np.concatenate([f.reshape(-1) for f in mats]))
+    Q = dev.empty(A.numel())
+    lam = dev.empty(sum(m))
+    marr = native.i64_array(m)
+    we = ctypes.c_int64()
+    native.check(L.gg_sym_eig_work_elems(len(m), marr, ctypes.byref(we)))
+    work = dev.empty(max(we.value, 1))
+    native.check(L.gg_sym_eig_batched(len(m), marr, native.dptr(A), native.dptr(Q),
+                                      native.dptr(lam), native.dptr(work), we.value,
+                                      int(max_sweeps), native.stream_ptr()),
+                 "gg_sym_eig_batched")
+    Qh = dev.to_host(Q)
+    lh = dev.to_host(lam)
+    del t
+    outQ, outL = [], []
+    o = lo = 0
+    for mi in m:
+        outQ.append(np.asfortranarray(Qh[o:o + mi * mi].reshape(mi, mi)))
+        outL.append(lh[lo:lo + mi].copy())
+        o += mi * mi
+        lo += mi
+    return outQ, outL
+
+
+class KronMatrix(object):
+    """Kronecker product of matrices (kron_matrix.py:12-474) on MI355X."""
+
+    def __init__(self, K, sym=False):
+        self._K = K
+        self.n = len(self.K)
+        self.sshape = np.vstack([np.shape(Ki) for Ki in self.K])
+        self.shape = np.atleast_1d(np.prod(np.float64(self.sshape), axis=0))
+        if np.all(self.shape < np.iinfo(np.uint64).max):
+            self.shape = np.uint64(self.shape)
+        self.ndim = self.shape.size
+        assert self.ndim <= 2, "kron matrix cannot be more than 2d"
+        self.square = self.ndim == 2 and self.shape[0] == self.shape[1]
+        self.sym = sym
+        self._dev = None
+        self._dev_key = None
+        if sym:
+            assert np.array_equal(self.sshape[:, 0], self.sshape[:, 1]), \
+                'this matrix cannot be symmetric: it is not square'
+            self.ensure_fortran()
+
+    @property
+    def K(self):
+        return self._K
+
+    @K.setter
+    def K(self, K):
+        raise AttributeError("Attribute is Read only.")
+
+    # ------------------------------------------------------------- device
+    def _device(self):
+        key = tuple(id(Ki) for Ki in self._K)
+        if self._dev is None or self._dev_key != key:
+            assert self.ndim == 2, "device operator needs 2-D factors"
+            self._dev = _DeviceKron([_as_matrix(Ki) for Ki in self._K])
+            self._dev_key = key
+        return self._dev
+
+    def matvec_device(self, xd, transpose=False, shift=0.0, out=None):
+        """y = (K^{T?} + shift I) x for a resident 1-D float64 CUDA tensor."""
+        return self._device().matvec(dev.ensure_aligned(xd), transpose, shift, out)
+
+    # ------------------------------------------------------------- products
+    def kronvec_prod(self, x):
+        """K*x (kron_matrix.py:52-97) on the device; x is (N,1)."""
+        n_in = int(self.shape[1])
+        xd, was_dev = _vector_in(x, n_in, 'x is the wrong shape, must be (%d,1), not %s'
+                                 % (n_in, repr(tuple(np.shape(x)))))
+        return _vector_out(self.matvec_device(xd), was_dev)
+
+    def __mul__(self, x):
+        return self.kronvec_prod(x)
+
+    def kronkron_prod(self, X):
+        """K*X for KronMatrix X (kron_matrix.py:105-116): per-factor products."""
+        if not isinstance(X, KronMatrix):
+            raise TypeError("X is not a KronMatrix")
+        elif X.n != self.n:
+            raise TypeError('inconsistent kron structure')
+        elif not np.array_equal(X.sshape[1], self.sshape[0]):
+            raise TypeError("Dimensions of X submatricies are not consistent")
+        return KronMatrix([np.dot(_as_matrix(self.K[i]), _as_matrix(X.K[i]))
+                           for i in range(self.n)])
+
+    def kronvec_div(self, x):
+        """K \\ x (kron_matrix.py:119-142) = (K_0^-1 (x) ...) x, applied on the device."""
+        assert self.ndim == 2
+        if tuple(x.shape) != (int(self.shape[0]), 1):
+            raise ValueError('x wrong shape, must be (%d,1)' % self.shape[0])
+        inv = [np.linalg.inv(_as_matrix(Ki)) for Ki in self.K]
+        return KronMatrix(inv) * x
+
+    def chol(self):
+        """Upper Cholesky factor per sub-matrix (kron_matrix.py:145-158)."""
+        assert self.square
+        C = np.empty(self.n, dtype=object)
+        for i, Ki in enumerate(self.K):
+            if hasattr(Ki, "chol"):
+                C[i] = Ki.chol()
+            else:
+                C[i] = np.linalg.cholesky(Ki).T
+        return KronMatrix(C)
+
+    def schur(self):
+        """(Q, T) per factor (kron_matrix.py:161-171); device Jacobi for symmetric factors."""
+        assert self.square
+        Q, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
+        T = [np.diag(l) for l in lam]
+        return KronMatrix(Q), KronMatrix(T)
+
+    def svd(self):
+        """(Q, eig_vals) of a PSD KronMatrix (kron_matrix.py:174-200), descending."""
+        assert self.square, "matrix must be square for current implementation"
+        try:
+            Q, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
+        except np.linalg.LinAlgError:
+            logger.error('SVD failed on a dimension.')
+            raise
+        Q = [np.asfortranarray(q[:, ::-1]) for q in Q]
+        lam = [l[::-1].copy() for l in lam]
+        return KronMatrix(Q), KronMatrix(lam)
+
+    def transpose(self):
+        assert self.ndim == 2
+        if self.sym:
+            return self
+        return KronMatrix([Ki.T for Ki in self.K])
+    T = property(transpose)
+
+    def expand(self, log_expansion=False):
+        """Dense expansion (kron_matrix.py:215-239) -- host, for small operators."""
+        if log_expansion:
+            Kb = np.array([0.])
+            for Ki in self.K:
+                Kb = log_kron(a=Kb, b=_as_matrix(Ki), a_logged=True)
+        else:
+            Kb = 1.
+            if self.ndim == 1 and self.n > 10:
+                warn('consider using numerically more stable log_expansion')
+            for Ki in self.K:
+                Kb = np.kron(Kb, _as_matrix(Ki))
+        return Kb.reshape(np.int64(self.shape))
+
+    def inv(self):
+        assert self.square
+        return KronMatrix([Ki.inv() if hasattr(Ki, "inv") else np.linalg.inv(Ki)
+                           for Ki in self.K])
+
+    def diag(self):
+        """Diagonal as a 1-D KronMatrix (kron_matrix.py:254-265)."""
+        assert self.ndim == 2
+        D = np.empty(self.n, dtype=object)
+        for i, Ki in enumerate(self.K):
+            D[i] = Ki.diag() if hasattr(Ki, "diag") else np.diag(Ki)
+        return KronMatrix(D)
+
+    def sub_cond(self):
+        assert self.square
+        return [np.linalg.cond(Ki) for Ki in self.K]
+
+    def sub_shift(self, shift=1e-6):
+        """K_i += shift I in place (kron_matrix.py:276-286)."""
+        if not np.array_equal(self.sshape[:, 0], self.sshape[:, 1]):
+            raise RuntimeError('can only apply sub_shift for square matricies')
+        for i, Ki in enumerate(self.K):
+            self.K[i] = Ki + shift * np.identity(self.sshape[i, 0])
+        if self.sym:
+            self.ensure_fortran()
+        self._dev = None
+        return self
+
+    def ensure_fortran(self):
+        for i, Ki in enumerate(self.K):
+            if isinstance(Ki, np.ndarray):
+                self.K[i] = np.asarray(Ki, order='F')
+        return self
+
+    def solve_chol(U, x):
+        """U \\ (U' \\ x) (kron_matrix.py:297-325) as one device Kron matvec."""
+        if tuple(x.shape) != (int(U.shape[0]), 1):
+            raise ValueError('x wrong shape, must be (%d,1)' % U.shape[0])
+        F = []
+        for Ui in U.K:
+            Ui = _as_matrix(Ui)
+            Uinv = np.linalg.inv(Ui)
+            F.append(Uinv.dot(Uinv.T))
+        return KronMatrix(F) * x
+
+    def solve_schur(Q, t, x, shift=0.0):
+        """(K + shift I) y = x via Q ((Q^T x) / (t + shift)) (kron_matrix.py:328-352).
+
+        t: expanded eigenvalue vector (N,), the T KronMatrix from schur, or a
+        1-D eigenvalue KronMatrix; in the Kronecker cases the eigenvalue
+        product is decoded on the device per element and never expanded.
+        """
+        n = int(Q.shape[0])
+        xd, was_dev = _vector_in(x, n, 'x wrong shape, must be (%d,1)' % n)
+        L = native.lib()
+        y = Q.matvec_device(xd, transpose=True)
+        if isinstance(t, KronMatrix):
+            eig = t.diag() if t.ndim == 2 else t
+            lam = [np.asarray(e, dtype=np.float64).reshape(-1) for e in eig.K]
+            lamd = dev.to_device(np.concatenate(lam))
+            native.check(L.gg_kron_diag_scale(len(lam), native.i64_array([l.size for l in lam]),
+                                              native.dptr(lamd), float(shift),
+                                              native.GG_DIAG_DIVIDE, native.dptr(y),
+                                              native.dptr(y), native.stream_ptr()),
+                         "gg_kron_diag_scale")
+        else:
+            td = dev.to_device(t)
+            if td.numel() != n:
+                raise ValueError("t must have %d entries" % n)
+            native.check(L.gg_diag_divide(native.dptr(td), float(shift), native.dptr(y),
+                                          native.dptr(y), n, native.stream_ptr()),
+                         "gg_diag_divide")
+        out = Q.matvec_device(y)
+        return _vector_out(out, was_dev)
+
+    def eig_vals(self):
+        """Eigenvalues per factor as a 1-D KronMatrix (kron_matrix.py:355-366)."""
+        assert self.ndim == 2
+        if not self.sym:
+            for Ki in self.K:
+                M = _as_matrix(Ki)
+                if not np.allclose(M, M.T):
+                    raise NotImplementedError("eig_vals of non-symmetric factors")
+        _, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
+        return KronMatrix(lam)
+
+    def find_extremum_eigs(eigs, n_eigs, mode='largest', log_expand=False, sort=True,
+                           compute_global_loc=False):
+        """Positions of the n_eigs extreme Kronecker eigenvalues (kron_matrix.py:369-446).
+
+        Host logic, O((d-1) p m), with the reference's numpy primitives so that
+        ties resolve identically (np.argpartition / np.argsort).
+        """
+        assert eigs.ndim == 1, "eigs must be a 1D KronMatrix"
+        assert isinstance(n_eigs, (int, np.integer)), \
+            "n_eigs=%s must be an integer" % repr(n_eigs)
+        assert n_eigs >= 1, "must use at least 1 eigenvalue"
+        assert n_eigs <= eigs.shape[0], "n_eigs > number of eigenvalues"
+        assert mode == 'largest' or mode == 'smallest'
+        if not log_expand and eigs.n > 10:
+            warn('should use log option which will be more numerically stable')
+        p = int(n_eigs)
+
+        def extreme(vec):
+            if vec.size <= p:
+                return np.arange(vec.size), vec
+            if mode == 'largest':
+                ind = np.argpartition(vec, -p)[-p:]
+            else:
+                ind = np.argpartition(vec, p)[:p]
+            return ind, vec[ind]
+
+        loc, vals = extreme(np.asarray(eigs.K[0]))
+        loc = loc.reshape((-1, 1))
+        if log_expand:
+            vals = np.log(vals)
+        for i in range(1, eigs.n):
+            Ki = np.asarray(eigs.K[i])
+            if log_expand:
+                cand = log_kron(a=vals, b=Ki, a_logged=True)
+            else:
+                cand = np.kron(vals, Ki)
+            ind, vals = extreme(cand)
+            prev = loc[np.floor_divide(ind, Ki.size), :]
+            loc = np.hstack([prev.reshape((ind.size, -1)),
+                             np.mod(ind, Ki.size).astype(prev.dtype).reshape((-1, 1))])
+        gloc = None
+        if compute_global_loc:
+            gloc = np.zeros(loc.shape[0], dtype=int)
+            stride = 1
+            for i in reversed(range(eigs.n)):
+                gloc = stride * loc[:, i] + gloc
+                stride *= np.size(eigs.K[i])
+        if sort:
+            order = np.argsort(vals)[::-1]
+            vals = vals[order]
+            loc = loc[order]
+            if gloc is not None:
+                gloc = gloc[order]
+        return loc, vals, gloc
+
+    def get_col(self, pos):
+        assert len(pos) == self.n
+        assert np.size(pos[0]) == 1
+        assert isinstance(pos[0], int)
+        assert self.ndim == 2
+        return KronMatrix([self.K[i][:, j].reshape((-1, 1)) for i, j in enumerate(pos)])
+
+    def log_det(eig_vals):
+        """log det from per-factor eigenvalues (kron_matrix.py:466-474)."""
+        assert eig_vals.ndim == 1
+        ldet = 0
+        for i, eigs in enumerate(eig_vals.K):
+            repetition = np.prod(np.delete(eig_vals.sshape, i))
+            ldet += repetition * np.sum(np.log(eigs))
+        return ldet
+
+    def log_det_shifted(eig_vals, shift):
+        """log det(K + shift I) = sum_grid log(prod lambda + shift), on the device.
+
+        Extension of log_det (the reference covers only shift = 0); the grid
+        sum is streamed on the device with the index decoded per element.
+        """
+        assert eig_vals.ndim == 1
+        lam = [np.asarray(e, dtype=np.float64).reshape(-1) for e in eig_vals.K]
+        lamd = dev.to_device(np.concatenate(lam))
+        out = ctypes.c_double()
+        native.check(native.lib().gg_kron_logdet_shifted(
+            len(lam), native.i64_array([l.size for l in lam]), native.dptr(lamd), float(shift),
+            ctypes.byref(out), native.stream_ptr()), "gg_kron_logdet_shifted")
+        return out.value
+
+
+class SelectionMatrixSparse(object):
+    """Row selection with unique / inverse index (selection_matrix.py:55-107)."""
+    ndim = 2
+
+    def __init__(self, indicies):
+        assert isinstance(indicies, tuple)
+        assert len(indicies) == 2
+        assert indicies[0].ndim == 1
+        self.shape = [indicies[0].size, indicies[1]]
+        self.indicies = indicies[0]
+        self.unique, self.unique_inverse = np.unique(self.indicies, return_inverse=True)
+
+    def mul(self, x):
+        assert x.ndim == 2
+        return x[self.indicies, :]
+    dot = __mul__ = mul
+
+    def mul_unique(self, x):
+        assert x.ndim == 2
+        return x[self.unique, :]
+
+    def mul_T(self, x):
+        raise NotImplementedError('Not finished')
+
+    def __getitem__(self, key):
+        if isinstance(key, tuple):
+            key = key[0]
+        return SelectionMatrixSparse(indicies=(np.atleast_1d(self.indicies[key]), self.shape[1]))

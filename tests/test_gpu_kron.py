@@ -1,0 +1,239 @@
+"""P1 parity on the MI355X: Kronecker matvec, eigensolver, exact solves, CG, Lanczos.
+
+Every test calls the HIP library through the C ABI (gp_grief_amd.native) and
+checks it against the reference-generated golden fixtures and/or the CPU
+oracle on the same inputs.  Tolerances are written per test; the FP64 bar is
+1e-12 relative for a single matvec (one GEMM chain) and 1e-6 relative (the
+north star's) for solver outputs.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def gg(gpu):
+    import gp_grief_amd
+    return gp_grief_amd
+
+
+# ---------------------------------------------------------------- matvec
+def test_matvec_golden_sym5(gg):
+    z = golden("kron_matvec.npz")
+    K = gg.tensors.KronMatrix(list(z["sym5_factors"]), sym=True)
+    y = K * z["sym5_x"].reshape(-1, 1)
+    assert y.shape == (125, 1)
+    assert rel(y, z["sym5_y"]) < 1e-13
+
+
+def test_matvec_golden_nonsquare_and_T(gg):
+    z = golden("kron_matvec.npz")
+    F = [z["nonsq_factor%d" % i] for i in range(3)]
+    K = gg.tensors.KronMatrix(F)
+    assert rel(K * z["nonsq_x"].reshape(-1, 1), z["nonsq_y"]) < 1e-13
+    assert rel(K.T * z["nonsq_xT"].reshape(-1, 1), z["nonsq_yT"]) < 1e-13
+
+
+def test_matvec_golden_rbf12(gg):
+    z = golden("kron_matvec.npz")
+    K = gg.tensors.KronMatrix(list(z["rbf12_factors"]), sym=True)
+    assert rel(K * z["rbf12_x"].reshape(-1, 1), z["rbf12_y"]) < 1e-13
+
+
+def test_matvec_wrong_shape_raises(gg):
+    z = golden("kron_matvec.npz")
+    K = gg.tensors.KronMatrix(list(z["sym5_factors"]), sym=True)
+    with pytest.raises(ValueError):
+        K * np.zeros((125,))
+    with pytest.raises(ValueError):
+        K * np.zeros((124, 1))
+
+
+@pytest.mark.parametrize("shape", [
+    [(7, 7)], [(1, 1), (3, 3)], [(16, 16), (16, 16)], [(13, 17), (5, 3), (33, 31)],
+    [(40, 40)] * 4, [(64, 64)] * 3, [(200, 200)] * 2, [(203, 203), (9, 9)],
+    [(300, 300), (20, 20)], [(257, 255), (6, 2)], [(2, 2)] * 12,
+])
+def test_matvec_random_vs_oracle(gg, shape):
+    rng = np.random.default_rng(len(shape) * 1000 + shape[0][0])
+    F = [rng.standard_normal(s) for s in shape]
+    K = gg.tensors.KronMatrix(F)
+    n_in = int(np.prod([s[1] for s in shape]))
+    n_out = int(np.prod([s[0] for s in shape]))
+    x = rng.standard_normal((n_in, 1))
+    y = K * x
+    assert rel(y, oracle.kron_matvec(F, x[:, 0])) < 1e-12
+    xt = rng.standard_normal((n_out, 1))
+    assert rel(K.T * xt, oracle.kron_matvec_T(F, xt[:, 0])) < 1e-12
+
+
+def test_matvec_resident_and_shift(gg):
+    import torch
+    rng = np.random.default_rng(5)
+    F = [rng.standard_normal((37, 37)) for _ in range(3)]
+    F = [f + f.T for f in F]
+    K = gg.tensors.KronMatrix(F, sym=True)
+    x = rng.standard_normal(37 ** 3)
+    xd = torch.from_numpy(x).cuda()
+    y = K.matvec_device(xd, shift=0.37)
+    assert y.is_cuda
+    ref = oracle.kron_matvec(F, x) + 0.37 * x
+    assert rel(y.cpu().numpy(), ref) < 1e-12
+    y2 = K * xd.reshape(-1, 1)
+    assert y2.is_cuda and y2.shape == (37 ** 3, 1)
+    assert rel(y2.cpu().numpy(), oracle.kron_matvec(F, x)) < 1e-12
+
+
+def test_matvec_200_cubed(gg):
+    """The north-star factor size (m = 200) on an 8e6 grid, vs the oracle."""
+    import torch
+    g = np.linspace(0, 1, 200)
+    F = [oracle.cov_1d("RBF", g, g, 1.0, 0.1 * (1 + 0.05 * k)) + 1e-12 * np.eye(200)
+         for k in range(3)]
+    K = gg.tensors.KronMatrix(F, sym=True)
+    x = np.random.default_rng(9).standard_normal(200 ** 3)
+    y = K.matvec_device(torch.from_numpy(x).cuda(), shift=0.01).cpu().numpy()
+    assert rel(y, oracle.kron_matvec(F, x) + 0.01 * x) < 1e-12
+
+
+# ---------------------------------------------------------------- eigensolver
+@pytest.mark.parametrize("m", [1, 2, 5, 12, 33, 64, 128, 200])
+def test_device_eigensolver(gg, m):
+    rng = np.random.default_rng(m)
+    A = rng.standard_normal((m, m))
+    A = A + A.T
+    g = np.linspace(0, 1, m)
+    R = oracle.cov_1d("RBF", g, g, 1.0, 0.15) + 1e-12 * np.eye(m)
+    Q, lam = gg.tensors.device_sym_eig([A, R])
+    for M, q, l in zip([A, R], Q, lam):
+        w = np.linalg.eigvalsh(M)
+        scale = np.abs(w).max()
+        assert np.max(np.abs(l - w)) < 1e-12 * scale * max(1, m / 10)
+        assert np.max(np.abs(q.T.dot(q) - np.eye(m))) < 1e-12 * max(1, m / 10)
+        assert np.max(np.abs(q.dot(np.diag(l)).dot(q.T) - M)) < 1e-12 * scale * max(1, m / 10)
+
+
+def test_schur_solve_golden_sym5(gg):
+    z = golden("kron_matvec.npz")
+    K = gg.tensors.KronMatrix(list(z["sym5_factors"]), sym=True)
+    Q, T = K.schur()
+    y = Q.solve_schur(T, z["sym5_x"].reshape(-1, 1), shift=float(z["sym5_solve_shift"]))
+    assert rel(y, z["sym5_y_solve"]) < 1e-8
+    # the reference test's own check: K y + lam y = x  (test_kron_matrix_sym.py:60-72)
+    x = z["sym5_x"].reshape(-1, 1)
+    resid = (K * y) + float(z["sym5_solve_shift"]) * y - x
+    assert np.linalg.norm(resid) / np.linalg.norm(x) < 1e-10
+    assert abs(K.eig_vals().log_det() - z["sym5_logdet"]) < 1e-8 * abs(z["sym5_logdet"])
+
+
+def test_grid_gp_exact_golden(gg):
+    z = golden("grid_gp.npz")
+    s = float(z["sigma2"])
+    K = gg.tensors.KronMatrix(list(z["factors"]), sym=True)
+    Q, T = K.schur()
+    y = z["y"].reshape(-1, 1)
+    alpha = Q.solve_schur(T, y, shift=s)
+    assert rel(alpha, z["alpha"]) < 1e-8
+    assert rel(K * alpha, z["mean"]) < 1e-8
+    eig = T.diag()
+    ld = eig.log_det_shifted(s)
+    assert abs(ld - z["logdet"]) < 1e-9 * abs(z["logdet"])
+    lml = -0.5 * (float(y[:, 0].dot(alpha[:, 0])) + ld + y.size * np.log(2 * np.pi))
+    assert abs(lml - z["lml"]) < 1e-8 * abs(z["lml"])
+
+
+# ---------------------------------------------------------------- CG
+def test_cg_golden_grid(gg):
+    z = golden("grid_gp.npz")
+    s = float(z["sigma2"])
+    K = gg.tensors.KronMatrix(list(z["factors"]), sym=True)
+    x, info = gg.linalg.cg(K, z["y"].reshape(-1, 1), shift=s, rtol=float(z["cg_rtol"]))
+    assert info == 0
+    it = gg.linalg.cg.last.iters
+    assert abs(it - int(z["cg_iters"])) <= 0.05 * int(z["cg_iters"])
+    assert rel(x, z["cg_x"]) < 1e-8
+    assert rel(x, z["alpha"]) < 1e-8
+
+
+def test_cg_fixed_iterations_match_oracle(gg):
+    """50 CG steps: the device recurrence tracks scipy's to rounding growth."""
+    z = golden("grid_gp.npz")
+    s = float(z["sigma2"])
+    F = list(z["factors"])
+    K = gg.tensors.KronMatrix(F, sym=True)
+    x, info = gg.linalg.cg(K, z["y"], shift=s, rtol=1e-30, maxiter=50)
+    assert info == 50 and gg.linalg.cg.last.iters == 50
+    xo, _, _ = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + s * v, z["y"],
+                               rtol=1e-30, maxiter=50)
+    assert rel(x, xo) < 1e-4
+    assert rel(x, z["cg50_x"]) < 1e-4
+
+
+def test_cg_zero_rhs_and_edge(gg):
+    F = [np.eye(3) * 2.0, np.eye(4)]
+    K = gg.tensors.KronMatrix(F, sym=True)
+    x, info = gg.linalg.cg(K, np.zeros((12, 1)), shift=1.0)
+    assert info == 0 and np.all(x == 0)
+    b = np.arange(12.0).reshape(-1, 1)
+    x, info = gg.linalg.cg(K, b, shift=1.0, rtol=1e-14)
+    assert info == 0 and rel(x, b / 3.0) < 1e-13
+
+
+def test_cg_random_spd_vs_exact(gg):
+    rng = np.random.default_rng(1)
+    F = []
+    for m in (31, 17, 45):
+        A = rng.standard_normal((m, m))
+        F.append(A.dot(A.T) / m + 0.1 * np.eye(m))
+    K = gg.tensors.KronMatrix(F, sym=True)
+    b = rng.standard_normal((31 * 17 * 45, 1))
+    x, info = gg.linalg.cg(K, b, shift=0.05, rtol=1e-11)
+    assert info == 0
+    Q, lam = oracle.factor_eigh(F)
+    ex = oracle.solve_schur(Q, oracle.kron_expand(lam), b[:, 0], 0.05)
+    assert rel(x, ex) < 1e-8
+
+
+# ---------------------------------------------------------------- Lanczos / SLQ
+def test_probe_bit_identical(gg):
+    import torch
+    from gp_grief_amd import native, device
+    n = 10001
+    z = device.empty(n)
+    native.check(native.lib().gg_probe_fill(7, 3, native.dptr(z), n, native.stream_ptr()))
+    np.testing.assert_array_equal(z.cpu().numpy(), oracle.cg.probe_signs(7, 3, n))
+
+
+def test_lanczos_matches_oracle(gg):
+    z = golden("grid_gp.npz")
+    s = float(z["sigma2"])
+    F = list(z["factors"])
+    K = gg.tensors.KronMatrix(F, sym=True)
+    a, b = gg.linalg.lanczos_tridiag(K, s, 12, seed=3, probe=1)
+    zp = oracle.cg.probe_signs(3, 1, z["y"].size)
+    ao, bo = oracle.lanczos_tridiag(lambda v: oracle.kron_matvec(F, v) + s * v, zp, 12)
+    np.testing.assert_allclose(a, ao, rtol=1e-8)
+    np.testing.assert_allclose(b, bo, rtol=1e-7)
+
+
+def test_slq_logdet_vs_exact(gg):
+    z = golden("grid_gp.npz")
+    s = float(z["sigma2"])
+    K = gg.tensors.KronMatrix(list(z["factors"]), sym=True)
+    est, per = gg.linalg.slq_logdet(K, s, probes=16, steps=60, seed=3)
+    assert abs(est - z["logdet"]) < 0.02 * abs(z["logdet"])
+    F = list(z["factors"])
+    eo, po = oracle.slq_logdet(lambda v: oracle.kron_matvec(F, v) + s * v, z["y"].size,
+                               probes=16, steps=60, seed=3)
+    # same probes, same recurrence: the estimates agree far below the SLQ error
+    assert abs(est - eo) < 1e-6 * abs(eo)
