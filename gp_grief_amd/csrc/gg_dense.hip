@@ -1,0 +1,481 @@
+// Dense FP64 building blocks of the GRIEF solve on MI355X: an MFMA GEMM
+// (v_mfma_f64_16x16x4_f64, 128x128 block tile, LDS double buffer), GEMV, and a
+// blocked Cholesky / triangular-solve suite built on them.
+//
+// Reference arithmetic replaced (gp_grief/models/gp_grief_model.py):
+//   A = Phi^T Phi                       :149   (numpy -> dsyrk)       -> gg_gemm
+//   P = A + diag(s / w); cho_factor(P)  :152-153 (LAPACK potrf)       -> gg_potrf
+//   cho_solve(P, .)                     :175, 234 (LAPACK potrs)       -> gg_potrs
+//   Phi.T.dot(y), Phi.dot(v)            :97, 173, 224, 234            -> gg_gemv
+// Layout: every matrix is row-major with an explicit leading dimension.
+#include <cmath>
+#include <vector>
+
+#include "gg_internal.h"
+
+namespace gg {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBM = 128, kBN = 128, kBK = 16, kPad = 16;
+constexpr int kLdT = kBM + kPad;  // LDS row stride (doubles): 144*8 B = 36*32 -> +32 banks per k-row
+constexpr int kGemmThreads = 256;
+constexpr int kLoadPerT = kBM * kBK / kGemmThreads;  // 8 doubles of A and of B per thread
+
+// C = alpha op(A) op(B) + beta C.   op(A): M x K, op(B): K x N.
+// TA: A stored K x M (lda) ; else M x K.   TB: B stored N x K (ldb) ; else K x N.
+// uplo 1: only C[i][j] with i >= j is written (lower), 2: i <= j (upper).
+// partial != nullptr: split-K; block z writes its raw sum to partial + z*M*N.
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) double sA[2][kBK * kLdT];
+  __shared__ __attribute__((aligned(16))) double sB[2][kBK * kLdT];
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+  if (uplo == 1 && n0 > m0 + kBM - 1) return;
+  if (uplo == 2 && m0 > n0 + kBN - 1) return;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  double ra[kLoadPerT], rb[kLoadPerT];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kLoadPerT; ++u) {
+      const int e = tid + u * kGemmThreads;
+      int mi, ki;
+      if (TA) { ki = e / kBM; mi = e % kBM; } else { mi = e / kBK; ki = e % kBK; }
+      const int gm = m0 + mi, gk = k0 + ki;
+      double v = 0.0;
+      if (gm < M && gk < kend) v = TA ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
+      ra[u] = v;
+      int ni, kj;
+      if (TB) { ni = e / kBK; kj = e % kBK; } else { kj = e / kBN; ni = e % kBN; }
+      const int gn = n0 + ni, gk2 = k0 + kj;
+      double w = 0.0;
+      if (gn < N && gk2 < kend) w = TB ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn];
+      rb[u] = w;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < kLoadPerT; ++u) {
+      const int e = tid + u * kGemmThreads;
+      int mi, ki;
+      if (TA) { ki = e / kBM; mi = e % kBM; } else { mi = e / kBK; ki = e % kBK; }
+      sA[buf][ki * kLdT + mi] = ra[u];
+      int ni, kj;
+      if (TB) { ni = e / kBK; kj = e % kBK; } else { kj = e / kBN; ni = e % kBN; }
+      sB[buf][kj * kLdT + ni] = rb[u];
+    }
+  };
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  const int nk = (kend - kbeg + kBK - 1) / kBK;
+  if (nk > 0) {
+    load(kbeg);
+    store(0);
+    __syncthreads();
+    for (int c = 0; c < nk; ++c) {
+      const bool more = c + 1 < nk;
+      if (more) load(kbeg + (c + 1) * kBK);
+      const double* a_s = sA[c & 1];
+      const double* b_s = sB[c & 1];
+#pragma unroll
+      for (int s = 0; s < kBK / 4; ++s) {
+        const int kr = (4 * s + (lane >> 4)) * kLdT + (lane & 15);
+        double af[4], bf[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = a_s[kr + wm + 16 * i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = b_s[kr + wn + 16 * j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) store((c + 1) & 1);
+      __syncthreads();
+    }
+  }
+
+  // f64 C/D layout: lane holds D[(lane>>4) + 4r][lane & 15]
+  double* P = partial ? partial + (int64_t)blockIdx.z * M * N : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + (lane >> 4) + 4 * r;
+        const int col = n0 + wn + 16 * j + (lane & 15);
+        if (row >= M || col >= N) continue;
+        if (uplo == 1 && col > row) continue;
+        if (uplo == 2 && row > col) continue;
+        const double v = acc[i][j][r];
+        if (P) {
+          P[(int64_t)row * N + col] = v;
+        } else {
+          double* c = C + (int64_t)row * ldc + col;
+          *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
+        }
+      }
+}
+
+__global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restrict__ partial,
+                                     double alpha, double beta, double* C, int64_t ldc,
+                                     int uplo) {
+  const int64_t total = (int64_t)M * N;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(e / N), col = (int)(e % N);
+    if (uplo == 1 && col > row) continue;
+    if (uplo == 2 && row > col) continue;
+    double s = 0.0;
+    for (int z = 0; z < S; ++z) s += partial[(int64_t)z * total + e];
+    double* c = C + (int64_t)row * ldc + col;
+    *c = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * *c);
+  }
+}
+
+void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, int64_t lda,
+          const double* B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+          hipStream_t s, double* splitk_buf = nullptr, int64_t splitk_elems = 0) {
+  if (M <= 0 || N <= 0) return;
+  const int gm = (int)ceil_div(M, kBM), gn = (int)ceil_div(N, kBN);
+  int S = 1;
+  if (splitk_buf != nullptr && K > 4 * kBK) {
+    const int64_t tiles = (int64_t)gm * gn;
+    const int64_t want = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+    const int64_t cap_mem = std::max<int64_t>(1, splitk_elems / ((int64_t)M * N));
+    const int64_t cap_k = std::max<int64_t>(1, K / (4 * kBK));
+    S = (int)std::min(std::min(want, cap_mem), std::min<int64_t>(cap_k, 64));
+  }
+  const int kchunk = (int)(ceil_div(ceil_div(std::max(K, 1), S), kBK) * kBK);
+  S = (int)ceil_div(std::max(K, 1), kchunk);
+  dim3 grid(gn, gm, S);
+  double* part = (S > 1) ? splitk_buf : nullptr;
+#define GG_GEMM_LAUNCH(TA_, TB_)                                                              \
+  hipLaunchKernelGGL((gemm_kernel<TA_, TB_>), grid, dim3(kGemmThreads), 0, s, M, N, K, alpha, \
+                     A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part)
+  if (ta && tb) GG_GEMM_LAUNCH(true, true);
+  else if (ta) GG_GEMM_LAUNCH(true, false);
+  else if (tb) GG_GEMM_LAUNCH(false, true);
+  else GG_GEMM_LAUNCH(false, false);
+#undef GG_GEMM_LAUNCH
+  GG_LAUNCH_CHECK();
+  if (part) {
+    const int64_t total = (int64_t)M * N;
+    const int nb = (int)std::min<int64_t>(4096, ceil_div(total, 256));
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nb), dim3(256), 0, s, M, N, S, part, alpha,
+                       beta, C, ldc, uplo);
+    GG_LAUNCH_CHECK();
+  }
+}
+
+// ------------------------------------------------------------------ GEMV
+// y[j] = alpha * sum_r A[r][j] x[r] + beta y[j]   (A: R x Cn row-major), split over rows
+__global__ __launch_bounds__(256) void gemv_t_partial_kernel(int64_t R, int Cn,
+                                                             const double* __restrict__ A,
+                                                             int64_t lda,
+                                                             const double* __restrict__ x,
+                                                             int64_t rows_per,
+                                                             double* __restrict__ part) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = min(R, r0 + rows_per);
+  if (j >= Cn) return;
+  double s = 0.0;
+  for (int64_t r = r0; r < r1; ++r) s = fma(A[r * lda + j], x[r], s);
+  part[(int64_t)blockIdx.y * Cn + j] = s;
+}
+
+__global__ void gemv_t_reduce_kernel(int Cn, int S, const double* __restrict__ part,
+                                     double alpha, double beta, double* y) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= Cn) return;
+  double s = 0.0;
+  for (int z = 0; z < S; ++z) s += part[(int64_t)z * Cn + j];
+  y[j] = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * y[j]);
+}
+
+// y[r] = alpha * sum_j A[r][j] x[j] + beta y[r] : one wave per row
+__global__ __launch_bounds__(256) void gemv_n_kernel(int64_t R, int Cn,
+                                                     const double* __restrict__ A, int64_t lda,
+                                                     const double* __restrict__ x, double alpha,
+                                                     double beta, double* y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const double* row = A + r * lda;
+  double s = 0.0;
+  for (int j = lane; j < Cn; j += 64) s = fma(row[j], x[j], s);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) y[r] = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * y[r]);
+}
+
+void gemv(bool trans, int64_t R, int Cn, double alpha, const double* A, int64_t lda,
+          const double* x, double beta, double* y, double* work, int64_t work_elems,
+          hipStream_t s) {
+  if (R <= 0 || Cn <= 0) return;
+  if (!trans) {
+    hipLaunchKernelGGL(gemv_n_kernel, dim3((unsigned)ceil_div(R, 4)), dim3(256), 0, s, R, Cn,
+                       A, lda, x, alpha, beta, y);
+    GG_LAUNCH_CHECK();
+    return;
+  }
+  const int gx = (int)ceil_div(Cn, 256);
+  int64_t S = std::max<int64_t>(1, 2048 / gx);
+  S = std::min<int64_t>(S, std::max<int64_t>(1, work_elems / Cn));
+  S = std::min<int64_t>(S, std::max<int64_t>(1, R / 64));
+  const int64_t rows_per = ceil_div(R, S);
+  S = ceil_div(R, rows_per);
+  GG_REQUIRE(work != nullptr && work_elems >= S * Cn, GG_ERR_VALUE, "gemv work too small");
+  hipLaunchKernelGGL(gemv_t_partial_kernel, dim3(gx, (unsigned)S), dim3(256), 0, s, R, Cn, A,
+                     lda, x, rows_per, work);
+  GG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(gemv_t_reduce_kernel, dim3(gx), dim3(256), 0, s, Cn, (int)S, work, alpha,
+                     beta, y);
+  GG_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------ Cholesky
+constexpr int kNB = 64;
+
+// Factor the nb x nb diagonal block at A (lda) in place (lower) and write its
+// inverse (lower) to W (ld kNB).  status <- 1 if a pivot is not positive/finite.
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* A, int64_t lda, int nb,
+                                                         double* W, int* status) {
+  __shared__ double L[kNB][kNB + 1];
+  __shared__ double Wi[kNB][kNB + 1];
+  __shared__ int bad;
+  const int tid = threadIdx.x;
+  if (tid == 0) bad = 0;
+  for (int e = tid; e < nb * nb; e += blockDim.x) {
+    const int i = e / nb, j = e % nb;
+    L[i][j] = (j <= i) ? A[(int64_t)i * lda + j] : 0.0;
+  }
+  __syncthreads();
+  for (int k = 0; k < nb; ++k) {
+    if (tid == 0) {
+      const double d = L[k][k];
+      if (!(d > 0.0) || !isfinite(d)) bad = 1;
+      L[k][k] = sqrt(fmax(d, 0.0));
+    }
+    __syncthreads();
+    const double dk = L[k][k];
+    for (int i = k + 1 + tid; i < nb; i += blockDim.x) L[i][k] = L[i][k] / dk;
+    __syncthreads();
+    const int rem = nb - k - 1;
+    for (int e = tid; e < rem * rem; e += blockDim.x) {
+      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+      if (j <= i) L[i][j] -= L[i][k] * L[j][k];
+    }
+    __syncthreads();
+  }
+  // inverse of the lower-triangular factor, one column per thread
+  for (int j = tid; j < nb; j += blockDim.x) {
+    for (int i = 0; i < nb; ++i) Wi[i][j] = 0.0;
+    Wi[j][j] = 1.0 / L[j][j];
+    for (int i = j + 1; i < nb; ++i) {
+      double s = 0.0;
+      for (int k = j; k < i; ++k) s = fma(L[i][k], Wi[k][j], s);
+      Wi[i][j] = -s / L[i][i];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * nb; e += blockDim.x) {
+    const int i = e / nb, j = e % nb;
+    if (j <= i) A[(int64_t)i * lda + j] = L[i][j];
+    W[(int64_t)i * kNB + j] = Wi[i][j];
+  }
+  if (tid == 0 && bad) *status = 1;
+}
+
+__global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += log(A[(int64_t)i * lda + i]);
+  __shared__ double red[16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w];
+    *out = t;
+  }
+}
+
+// P = A + diag(s / w)  (w may be null -> s)
+__global__ void add_diag_kernel(int n, const double* __restrict__ A, int64_t lda, double s,
+                                const double* __restrict__ w, double* P, int64_t ldp) {
+  const int64_t total = (int64_t)n * n;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(e / n), j = (int)(e % n);
+    double v = A[(int64_t)i * lda + j];
+    if (i == j) v += w ? s / w[i] : s;
+    P[(int64_t)i * ldp + j] = v;
+  }
+}
+
+// out[j] = sum_i M[i][j]^2 (column sums of squares; lower-triangular M uses i >= j)
+__global__ void colsumsq_kernel(int n, const double* __restrict__ Mx, int64_t ld, double* out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  double s = 0.0;
+  for (int i = j; i < n; ++i) {
+    const double v = Mx[(int64_t)i * ld + j];
+    s = fma(v, v, s);
+  }
+  out[j] = s;
+}
+
+}  // namespace gg
+
+extern "C" {
+
+int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const double* A_dev,
+            int64_t lda, const double* B_dev, int64_t ldb, double beta, double* C_dev,
+            int64_t ldc, int uplo, double* splitk_dev, int64_t splitk_elems, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(M >= 0 && N >= 0 && K >= 0, GG_ERR_VALUE, "negative dimension");
+    GG_REQUIRE(C_dev && (K == 0 || (A_dev && B_dev)), GG_ERR_VALUE, "NULL matrix");
+    GG_REQUIRE(uplo >= 0 && uplo <= 2, GG_ERR_VALUE, "bad uplo");
+    gg::gemm(trans_a != 0, trans_b != 0, M, N, K, alpha, A_dev, lda, B_dev, ldb, beta, C_dev,
+             ldc, uplo, gg::as_stream(stream), splitk_dev, splitk_elems);
+  });
+}
+
+int gg_gemv(int trans, int64_t rows, int cols, double alpha, const double* A_dev, int64_t lda,
+            const double* x_dev, double beta, double* y_dev, double* work_dev,
+            int64_t work_elems, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(rows >= 0 && cols >= 0 && A_dev && x_dev && y_dev, GG_ERR_VALUE, "bad argument");
+    gg::gemv(trans != 0, rows, cols, alpha, A_dev, lda, x_dev, beta, y_dev, work_dev,
+             work_elems, gg::as_stream(stream));
+  });
+}
+
+int gg_add_diag(int n, const double* A_dev, int64_t lda, double s, const double* w_dev,
+                double* P_dev, int64_t ldp, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 0 && A_dev && P_dev, GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    const int nb = (int)std::min<int64_t>(4096, gg::ceil_div((int64_t)n * n, 256));
+    hipLaunchKernelGGL(gg::add_diag_kernel, dim3(nb), dim3(256), 0, gg::as_stream(stream), n,
+                       A_dev, lda, s, w_dev, P_dev, ldp);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_potrf_work_elems(int n, int64_t* elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 0 && elems, GG_ERR_VALUE, "bad argument");
+    *elems = gg::ceil_div(n, gg::kNB) * gg::kNB * gg::kNB + 16;
+  });
+}
+
+int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet_host,
+             gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 1 && A_dev && winv_dev, GG_ERR_VALUE, "bad argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nblk = (int)gg::ceil_div(n, gg::kNB);
+    int* status = reinterpret_cast<int*>(winv_dev + (int64_t)nblk * gg::kNB * gg::kNB);
+    double* ld = winv_dev + (int64_t)nblk * gg::kNB * gg::kNB + 8;
+    GG_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+    for (int b = 0; b < nblk; ++b) {
+      const int k0 = b * gg::kNB;
+      const int nb = std::min(gg::kNB, n - k0);
+      double* Akk = A_dev + (int64_t)k0 * lda + k0;
+      double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
+      hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(256), 0, s, Akk, lda, nb, Wk,
+                         status);
+      GG_LAUNCH_CHECK();
+      const int rest = n - k0 - nb;
+      if (rest > 0) {
+        double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
+        // L21 = A21 W^T (in place: one column tile, each block owns its rows)
+        gg::gemm(false, true, rest, nb, nb, 1.0, A21, lda, Wk, gg::kNB, 0.0, A21, lda, 0, s);
+        double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
+        gg::gemm(false, true, rest, rest, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
+      }
+    }
+    hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
+    GG_LAUNCH_CHECK();
+    int st = 0;
+    double lds = 0.0;
+    GG_HIP(hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipMemcpyAsync(&lds, ld, sizeof(double), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    GG_REQUIRE(st == 0, GG_ERR_LINALG, "Matrix is not positive definite (device Cholesky)");
+    if (logdet_host) *logdet_host = 2.0 * lds;
+  });
+}
+
+// Solve (L L^T) X = B in place for B: n x r (ldb), using the factor and the
+// diagonal-block inverses from gg_potrf.  which: 1 = forward only (L^-1 B),
+// 2 = backward only (L^-T B), 3 = both (P^-1 B).
+int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_dev,
+             double* B_dev, int64_t ldb, int which, double* tmp_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 1 && r >= 0 && L_dev && winv_dev && B_dev && tmp_dev, GG_ERR_VALUE,
+               "bad argument");
+    if (r == 0) return;
+    hipStream_t s = gg::as_stream(stream);
+    const int nblk = (int)gg::ceil_div(n, gg::kNB);
+    if (which & 1) {
+      for (int b = 0; b < nblk; ++b) {
+        const int k0 = b * gg::kNB, nb = std::min(gg::kNB, n - k0);
+        double* Bk = B_dev + (int64_t)k0 * ldb;
+        if (k0 > 0)  // B_k -= L[k0:k0+nb, 0:k0] Y[0:k0]
+          gg::gemm(false, false, nb, r, k0, -1.0, L_dev + (int64_t)k0 * lda, lda, B_dev, ldb,
+                   1.0, Bk, ldb, 0, s);
+        // Y_k = W_k B_k  (through tmp: W_k reads all nb rows of B_k)
+        gg::gemm(false, false, nb, r, nb, 1.0, winv_dev + (int64_t)b * gg::kNB * gg::kNB,
+                 gg::kNB, Bk, ldb, 0.0, tmp_dev, r, 0, s);
+        GG_HIP(hipMemcpy2DAsync(Bk, ldb * sizeof(double), tmp_dev, r * sizeof(double),
+                                r * sizeof(double), nb, hipMemcpyDeviceToDevice, s));
+      }
+    }
+    if (which & 2) {
+      for (int b = nblk - 1; b >= 0; --b) {
+        const int k0 = b * gg::kNB, nb = std::min(gg::kNB, n - k0);
+        const int below = n - k0 - nb;
+        double* Bk = B_dev + (int64_t)k0 * ldb;
+        if (below > 0)  // Y_k -= L[k0+nb:n, k0:k0+nb]^T X[k0+nb:n]
+          gg::gemm(true, false, nb, r, below, -1.0, L_dev + (int64_t)(k0 + nb) * lda + k0, lda,
+                   B_dev + (int64_t)(k0 + nb) * ldb, ldb, 1.0, Bk, ldb, 0, s);
+        gg::gemm(true, false, nb, r, nb, 1.0, winv_dev + (int64_t)b * gg::kNB * gg::kNB,
+                 gg::kNB, Bk, ldb, 0.0, tmp_dev, r, 0, s);
+        GG_HIP(hipMemcpy2DAsync(Bk, ldb * sizeof(double), tmp_dev, r * sizeof(double),
+                                r * sizeof(double), nb, hipMemcpyDeviceToDevice, s));
+      }
+    }
+  });
+}
+
+int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
+                      gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 0 && M_dev && out_dev, GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    hipLaunchKernelGGL(gg::colsumsq_kernel, dim3((unsigned)gg::ceil_div(n, 256)), dim3(256), 0,
+                       gg::as_stream(stream), n, M_dev, ld, out_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+}  // extern "C"

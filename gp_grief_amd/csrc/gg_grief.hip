@@ -1,0 +1,210 @@
+// GRIEF eigenfunction matrix Phi on MI355X.
+//
+// Reference (gp_grief/kern/grief_kernel.py:68-111 with tensors/tensors.py:97-128):
+//   Kux_f   = k_f(xg_f, x[:, dim_f])                              (m_f x n)
+//   X_f     = (Q_f^T)[unique_f, :] . Kux_f                        (u_f x n)
+//   sign    = prod_f sign(X_f)[inv_f]        (taken before zeros -> 1)
+//   log     = sum_f log|X_f|[inv_f]
+//   Phi     = sign^T * exp(log^T - 0.5 log_lam)                    (n x p)
+// Two kernels:
+//   grief_tables_kernel: one thread per data point computes the m_f kernel
+//     values on the fly (never storing Kux) and contracts them with the u_f
+//     selected eigenvector rows; writes log|X| and sign(X) as an n x U table
+//     (U = sum_f u_f), i.e. exactly the reference's x_unique, per point.
+//   grief_phi_kernel: HBM-bound writer of Phi (n x p row-major, or p x n):
+//     one block owns 16 data points (their table rows in LDS) and a 256-wide
+//     range of eigenfunctions j (their table columns c_{j,f} in LDS); every
+//     Phi element is d LDS adds, d sign multiplies and one exp.
+// Also the dense stationary covariance used for the grid factors K_f.
+#include <cmath>
+#include <vector>
+
+#include "gg_internal.h"
+
+namespace gg {
+
+enum KernKind { kRBF = 0, kExponential = 1, kMatern32 = 2, kMatern52 = 3 };
+
+// k(r^2) for the reference's 1-D stationary kernels (stationary.py:108-258)
+__device__ __forceinline__ double stationary(int kind, double d2, double var, double ls) {
+  switch (kind) {
+    case kRBF:
+      if (ls < 1e-6) return d2 == 0.0 ? var : 0.0;
+      return var * exp(-0.5 * d2 / (ls * ls));
+    case kExponential: {
+      const double r = sqrt(d2) / ls;
+      return var * exp(-r);
+    }
+    case kMatern32: {
+      const double r = sqrt(d2) / ls;
+      const double s3 = 1.7320508075688772;
+      return var * (1.0 + s3 * r) * exp(-s3 * r);
+    }
+    default: {
+      const double r2 = d2 / (ls * ls);
+      const double r = sqrt(r2);
+      const double s5 = 2.23606797749979;
+      return var * (1.0 + s5 * r + (5.0 / 3) * r2) * exp(-s5 * r);
+    }
+  }
+}
+
+// out[i][j] (mode 0 = write, 1 = *=, 2 = +=) for x: N x D, z: M x D row-major
+__global__ __launch_bounds__(256) void cov_kernel(int kind, double var, double ls, int D,
+                                                  const double* __restrict__ x, int64_t N,
+                                                  const double* __restrict__ z, int64_t M,
+                                                  int mode, double* __restrict__ out) {
+  const int64_t total = N * M;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / M, j = e - i * M;
+    double d2 = 0.0;
+    for (int k = 0; k < D; ++k) {
+      const double t = x[i * D + k] - z[j * D + k];
+      d2 = fma(t, t, d2);
+    }
+    const double v = stationary(kind, d2, var, ls);
+    out[e] = mode == 0 ? v : (mode == 1 ? out[e] * v : out[e] + v);
+  }
+}
+
+constexpr int kUG = 16;  // selected eigenvector rows per thread
+
+// For dim f: X[u][a] = sum_k Qsel[u][k] * k_f(xg[k], x[a]) for u in a group of
+// kUG rows; writes table L[a][col0+u] = log|X| (X == 0 -> 0), S = sign(X).
+__global__ __launch_bounds__(256) void grief_tables_kernel(
+    int kind, double var, double ls, const double* __restrict__ x, int64_t x_stride,
+    int64_t n, const double* __restrict__ xg, int m, const double* __restrict__ Qsel, int u,
+    double* __restrict__ Ltab, double* __restrict__ Stab, int U, int col0) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int ug = blockIdx.y * kUG;
+  if (a >= n) return;
+  const double xa = x[a * x_stride];
+  double acc[kUG];
+#pragma unroll
+  for (int t = 0; t < kUG; ++t) acc[t] = 0.0;
+  for (int k = 0; k < m; ++k) {
+    const double d = xg[k] - xa;
+    const double kv = stationary(kind, d * d, var, ls);
+#pragma unroll
+    for (int t = 0; t < kUG; ++t)
+      if (ug + t < u) acc[t] = fma(Qsel[(int64_t)(ug + t) * m + k], kv, acc[t]);
+  }
+#pragma unroll
+  for (int t = 0; t < kUG; ++t) {
+    if (ug + t < u) {
+      const double v = acc[t];
+      const int64_t o = a * U + col0 + ug + t;
+      Stab[o] = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
+      Ltab[o] = log(fabs(v == 0.0 ? 1.0 : v));
+    }
+  }
+}
+
+constexpr int kPhiRows = 16;
+constexpr int kPhiCols = 256;
+constexpr int kMaxDim = 64;
+
+// Phi[a][j] = prod_f S[a][c_jf] * exp(sum_f L[a][c_jf] - 0.5 log_lam[j])
+// cidx: p x d column index into the tables (c_jf = col0_f + inverse_f[j]).
+__global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
+    const double* __restrict__ Ltab, const double* __restrict__ Stab, int U, int64_t n,
+    const int* __restrict__ cidx, int d, const double* __restrict__ log_lam, int p,
+    int transposed, double* __restrict__ Phi) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* sL = sm;                          // kPhiRows x U
+  double* sS = sm + kPhiRows * U;           // kPhiRows x U
+  int* sC = reinterpret_cast<int*>(sm + 2 * kPhiRows * U);  // d x kPhiCols
+  const int64_t a0 = (int64_t)blockIdx.x * kPhiRows;
+  const int j = blockIdx.y * kPhiCols + threadIdx.x;
+  const int rows = (int)min<int64_t>(kPhiRows, n - a0);
+  for (int e = threadIdx.x; e < rows * U; e += blockDim.x) {
+    sL[e] = Ltab[a0 * U + e];
+    sS[e] = Stab[a0 * U + e];
+  }
+  if (j < p)
+    for (int f = 0; f < d; ++f) sC[f * kPhiCols + threadIdx.x] = cidx[(int64_t)j * d + f];
+  __syncthreads();
+  if (j >= p) return;
+  const double hl = 0.5 * log_lam[j];
+  for (int r = 0; r < rows; ++r) {
+    double lg = 0.0, sg = 1.0;
+    for (int f = 0; f < d; ++f) {
+      const int c = sC[f * kPhiCols + threadIdx.x];
+      lg += sL[r * U + c];
+      sg *= sS[r * U + c];
+    }
+    const double v = sg * exp(lg - hl);
+    const int64_t a = a0 + r;
+    if (transposed)
+      Phi[(int64_t)j * n + a] = v;
+    else
+      Phi[a * p + j] = v;
+  }
+}
+
+}  // namespace gg
+
+extern "C" {
+
+int gg_cov(int kind, double variance, double lengthscale, int dims, const double* x_dev,
+           int64_t nx, const double* z_dev, int64_t nz, int mode, double* out_dev,
+           gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(kind >= 0 && kind <= 3, GG_ERR_VALUE, "unknown kernel kind");
+    GG_REQUIRE(mode >= 0 && mode <= 2, GG_ERR_VALUE, "bad mode");
+    GG_REQUIRE(dims >= 1 && x_dev && z_dev && out_dev && nx >= 0 && nz >= 0, GG_ERR_VALUE,
+               "bad argument");
+    const int64_t total = nx * nz;
+    if (total == 0) return;
+    const int nb = (int)std::min<int64_t>(8192, gg::ceil_div(total, 256));
+    hipLaunchKernelGGL(gg::cov_kernel, dim3(nb), dim3(256), 0, gg::as_stream(stream), kind,
+                       variance, lengthscale, dims, x_dev, nx, z_dev, nz, mode, out_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_grief_tables(int kind, double variance, double lengthscale, const double* x_dev,
+                    int64_t x_stride, int64_t n, const double* xg_dev, int m,
+                    const double* qsel_dev, int u, double* ltab_dev, double* stab_dev, int U,
+                    int col0, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(kind >= 0 && kind <= 3, GG_ERR_VALUE, "unknown kernel kind");
+    GG_REQUIRE(x_dev && xg_dev && qsel_dev && ltab_dev && stab_dev, GG_ERR_VALUE, "NULL");
+    GG_REQUIRE(m >= 1 && u >= 1 && col0 >= 0 && col0 + u <= U && n >= 0, GG_ERR_VALUE,
+               "bad table geometry");
+    if (n == 0) return;
+    dim3 grid((unsigned)gg::ceil_div(n, 256), (unsigned)gg::ceil_div(u, gg::kUG));
+    hipLaunchKernelGGL(gg::grief_tables_kernel, grid, dim3(256), 0, gg::as_stream(stream),
+                       kind, variance, lengthscale, x_dev, x_stride, n, xg_dev, m, qsel_dev, u,
+                       ltab_dev, stab_dev, U, col0);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t n,
+                 const int* cidx_dev, int d, const double* log_lam_dev, int p, int transposed,
+                 double* phi_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(ltab_dev && stab_dev && cidx_dev && log_lam_dev && phi_dev, GG_ERR_VALUE, "NULL");
+    GG_REQUIRE(d >= 1 && d <= gg::kMaxDim && U >= 1 && p >= 1 && n >= 0, GG_ERR_VALUE,
+               "bad Phi geometry");
+    if (n == 0) return;
+    const size_t lds = (size_t)2 * gg::kPhiRows * U * sizeof(double) +
+                       (size_t)d * gg::kPhiCols * sizeof(int);
+    GG_REQUIRE(lds <= 160 * 1024, GG_ERR_VALUE, "too many selected eigenvector rows");
+    static bool attr = false;
+    if (!attr) {
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gg::grief_phi_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    dim3 grid((unsigned)gg::ceil_div(n, gg::kPhiRows), (unsigned)gg::ceil_div(p, gg::kPhiCols));
+    hipLaunchKernelGGL(gg::grief_phi_kernel, grid, dim3(gg::kPhiCols), lds,
+                       gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
+                       log_lam_dev, p, transposed, phi_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+}  // extern "C"

@@ -26,6 +26,7 @@
 //     four 128-B segments per store.  The last step can fuse y += shift * x
 //     and the partial dot x.y (the CG p.q) per workgroup.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -35,106 +36,172 @@ namespace gg {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int kKC = 8;      // k-steps (of 4) staged per LDS chunk
-constexpr int kWaves = 4;   // waves per workgroup (b-strips of 16 rows)
 constexpr int kMaxJT = 16;  // accumulator tiles per launch (<= 256 output columns)
+constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued together
 
-template <int JT>
-__global__ __launch_bounds__(kWaves * 64) void mode_product_kernel(
+// Double-buffered chunk pipeline, one barrier per chunk:
+//   issue global loads of chunk c+1 (K^T fragments -> registers, X -> A regs)
+//   MFMA over chunk c from LDS buffer c&1
+//   write the staged registers into LDS buffer (c+1)&1 ; barrier
+// so the L2 latency of the factor fragments and the HBM latency of X hide
+// under 8*JT MFMAs (64 cycles each) per wave.
+template <int JT, int kWaves, int kKC>
+__global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
     const double* __restrict__ X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
     const int* __restrict__ skip) {
   if (skip != nullptr && *skip) return;
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // kKC * JT * 64
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JT * 64
+  constexpr int kThreads = kWaves * 64;
+  constexpr int kChunk2 = kKC * JT * 32;                  // double2 per full chunk
+  constexpr int kPerT = (kChunk2 + kThreads - 1) / kThreads;
+  constexpr int kBuf = kKC * JT * 64;                     // doubles per LDS buffer
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wave) * 16;
   const int64_t brow = b0 + (lane & 15);
   const bool bvalid = brow < M;
+  const int64_t bclamp = bvalid ? brow : M - 1;
   const int krow = lane >> 4;
+  const int nchunks = (KS + kKC - 1) / kKC;
+
+  // staging: element i of chunk c lives at Bf[((ks0 + s) * jt_total + jt0) * 64 + 2 o]
+#define GG_STAGE_LOAD(c, st)                                                          \
+  do {                                                                                \
+    const int ks0_ = (c) * kKC;                                                       \
+    const int n2_ = min(kKC, KS - ks0_) * JT * 32;                                    \
+    _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                               \
+      int i_ = threadIdx.x + u * kThreads;                                            \
+      i_ = i_ < n2_ ? i_ : n2_ - 1;                                                   \
+      const int s_ = i_ / (JT * 32);                                                  \
+      const int o_ = i_ - s_ * (JT * 32);                                             \
+      const double2 v_ = reinterpret_cast<const double2*>(                            \
+          Bf + ((int64_t)(ks0_ + s_) * jt_total + jt0) * 64)[o_];                     \
+      st##x[u] = v_.x; st##y[u] = v_.y;                                               \
+    }                                                                                 \
+  } while (0)
+#define GG_STAGE_STORE(c, st)                                                         \
+  do {                                                                                \
+    const int n2_ = min(kKC, KS - (c) * kKC) * JT * 32;                               \
+    double2* dst_ = reinterpret_cast<double2*>(lds + ((c) & 1) * kBuf);               \
+    _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                               \
+      const int i_ = threadIdx.x + u * kThreads;                                      \
+      if (i_ < n2_) dst_[i_] = double2{st##x[u], st##y[u]};                           \
+    }                                                                                 \
+  } while (0)
+// A fragments: unconditional loads from a clamped (always valid) address; the
+// mask (rows past q, strips past M) is applied when the registers are consumed,
+// so no load is followed by a wait.
+#define GG_A_LOAD(c, a)                                                               \
+  do {                                                                                \
+    const int ks0_ = (c) * kKC;                                                       \
+    _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
+      const int k_ = min((ks0_ + s_) * 4 + krow, q - 1);                              \
+      a[s_] = X[(int64_t)k_ * M + bclamp];                                            \
+    }                                                                                 \
+  } while (0)
+#define GG_A_MASK(c, a)                                                               \
+  do {                                                                                \
+    const int ks0_ = (c) * kKC;                                                       \
+    _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
+      const int k_ = (ks0_ + s_) * 4 + krow;                                          \
+      a[s_] = (bvalid && k_ < q) ? a[s_] : 0.0;                                       \
+    }                                                                                 \
+  } while (0)
 
   d4 acc[JT];
 #pragma unroll
   for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 
-  const int nchunks = (KS + kKC - 1) / kKC;
-  double a_nxt[kKC];
-#pragma unroll
-  for (int s = 0; s < kKC; ++s) {
-    const int k = s * 4 + krow;
-    a_nxt[s] = (s < KS && bvalid && k < q) ? X[(int64_t)k * M + brow] : 0.0;
-  }
+  double a_cur[kKC], a_nxt[kKC];
+  double stx[kPerT], sty[kPerT];
+  GG_STAGE_LOAD(0, st);
+  GG_A_LOAD(0, a_cur);
+  GG_STAGE_STORE(0, st);
+  GG_A_MASK(0, a_cur);
+  __syncthreads();
 
   for (int c = 0; c < nchunks; ++c) {
-    const int ks0 = c * kKC;
-    const int kcn = min(kKC, KS - ks0);
-    double a_cur[kKC];
-#pragma unroll
-    for (int s = 0; s < kKC; ++s) a_cur[s] = a_nxt[s];
-    // prefetch the next chunk's A fragments (HBM) before staging / computing
-    if (c + 1 < nchunks) {
-      const int ksn = ks0 + kKC;
-#pragma unroll
-      for (int s = 0; s < kKC; ++s) {
-        const int k = (ksn + s) * 4 + krow;
-        a_nxt[s] = (ksn + s < KS && bvalid && k < q) ? X[(int64_t)k * M + brow] : 0.0;
-      }
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      GG_STAGE_LOAD(c + 1, st);
+      GG_A_LOAD(c + 1, a_nxt);
     }
-    __syncthreads();  // previous chunk fully consumed
-    // stage kcn k-steps x JT fragments of K^T (contiguous per k-step)
-    {
-      const int per_ks2 = JT * 32;  // double2 per k-step for this tile group
-      const int n2 = kcn * per_ks2;
-      double2* dst = reinterpret_cast<double2*>(lds);
-      for (int i = threadIdx.x; i < n2; i += kWaves * 64) {
-        const int s = i / per_ks2;
-        const int o = i - s * per_ks2;
-        const double2* src =
-            reinterpret_cast<const double2*>(Bf + ((int64_t)(ks0 + s) * jt_total + jt0) * 64);
-        dst[i] = src[o];
-      }
-    }
-    __syncthreads();
+    const int kcn = min(kKC, KS - c * kKC);
+    const double* buf = lds + (c & 1) * kBuf;
 #pragma unroll
     for (int s = 0; s < kKC; ++s) {
       if (s < kcn) {
 #pragma unroll
         for (int t = 0; t < JT; ++t) {
-          const double b = lds[(s * JT + t) * 64 + lane];
+          const double b = buf[(s * JT + t) * 64 + lane];
           acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
         }
       }
     }
+    if (more) {
+      GG_STAGE_STORE(c + 1, st);
+#pragma unroll
+      for (int s = 0; s < kKC; ++s) a_cur[s] = a_nxt[s];
+      GG_A_MASK(c + 1, a_cur);
+    }
+    __syncthreads();
   }
 
-  // ---- epilogue
+  // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4)
   const int col = lane & 15;
   const int64_t rbase = b0 + (lane >> 4);
   double dsum = 0.0;
+  if (xs == nullptr) {
 #pragma unroll
-  for (int t = 0; t < JT; ++t) {
-    const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+    for (int t = 0; t < JT; ++t) {
+      const int64_t j = (int64_t)(jt0 + t) * 16 + col;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = rbase + 4 * r;
-      if (row < M && j < p) {
-        const int64_t idx = row * p + j;
-        double v = acc[t][r];
-        if (xs != nullptr) {
-          const double xv = xs[idx];
-          v = fma(shift, xv, v);
-          dsum = fma(xv, v, dsum);
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = rbase + 4 * r;
+        if (row < M && j < p) Y[row * p + j] = acc[t][r];
+      }
+    }
+  } else {
+    // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
+    // does not serialise one load round trip per output element
+#pragma unroll
+    for (int t0 = 0; t0 < JT; t0 += kEpiBatch) {
+      double xv[kEpiBatch][4];
+#pragma unroll
+      for (int tb = 0; tb < kEpiBatch; ++tb) {
+        const int t = t0 + tb;
+        const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = rbase + 4 * r;
+          xv[tb][r] = (t < JT && row < M && j < p) ? xs[row * p + j] : 0.0;
         }
-        Y[idx] = v;
+      }
+#pragma unroll
+      for (int tb = 0; tb < kEpiBatch; ++tb) {
+        const int t = t0 + tb;
+        if (t < JT) {
+          const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t row = rbase + 4 * r;
+            if (row < M && j < p) {
+              const double v = fma(shift, xv[tb][r], acc[t][r]);
+              dsum = fma(xv[tb][r], v, dsum);
+              Y[row * p + j] = v;
+            }
+          }
+        }
       }
     }
   }
   if (dot_partials != nullptr) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-    __syncthreads();  // every wave is past its last LDS fragment read
+    // the k-loop ended with a barrier: LDS is free
     if (lane == 0) lds[wave] = dsum;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -149,31 +216,59 @@ __global__ __launch_bounds__(kWaves * 64) void mode_product_kernel(
 typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
                               int, int, const double*, double, double*, const int*);
 
-template <int JT>
-static mode_kernel_t kernel_for() {
-  return mode_product_kernel<JT>;
+// Launch configuration of one mode product: waves per workgroup, k-steps per
+// LDS chunk.  The default (8 waves, KC 8, one workgroup per CU) was chosen by
+// A/B on MI355X (profiles/); GG_MP_VARIANT selects another for tuning runs.
+struct ModeConfig {
+  mode_kernel_t fn;
+  int waves, kc;
+};
+
+template <int JT, int W, int KC>
+static ModeConfig cfg() {
+  return ModeConfig{mode_product_kernel<JT, W, KC>, W, KC};
 }
 
-static mode_kernel_t select_kernel(int jt) {
+template <int JT>
+static ModeConfig config_for(int variant) {
+  switch (variant) {
+    case 1: return cfg<JT, 4, 4>();
+    case 2: return cfg<JT, 4, 8>();
+    case 3: return cfg<JT, 8, 4>();
+    case 4: return cfg<JT, 8, 10>();
+    default: return cfg<JT, 8, 8>();
+  }
+}
+
+static int mode_variant() {
+  const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
+  return e ? atoi(e) : 0;
+}
+
+static ModeConfig select_kernel(int jt, int variant) {
   switch (jt) {
-    case 1: return kernel_for<1>();
-    case 2: return kernel_for<2>();
-    case 3: return kernel_for<3>();
-    case 4: return kernel_for<4>();
-    case 5: return kernel_for<5>();
-    case 6: return kernel_for<6>();
-    case 7: return kernel_for<7>();
-    case 8: return kernel_for<8>();
-    case 9: return kernel_for<9>();
-    case 10: return kernel_for<10>();
-    case 11: return kernel_for<11>();
-    case 12: return kernel_for<12>();
-    case 13: return kernel_for<13>();
-    case 14: return kernel_for<14>();
-    case 15: return kernel_for<15>();
-    case 16: return kernel_for<16>();
+    case 1: return config_for<1>(variant);
+    case 2: return config_for<2>(variant);
+    case 3: return config_for<3>(variant);
+    case 4: return config_for<4>(variant);
+    case 5: return config_for<5>(variant);
+    case 6: return config_for<6>(variant);
+    case 7: return config_for<7>(variant);
+    case 8: return config_for<8>(variant);
+    case 9: return config_for<9>(variant);
+    case 10: return config_for<10>(variant);
+    case 11: return config_for<11>(variant);
+    case 12: return config_for<12>(variant);
+    case 13: return config_for<13>(variant);
+    case 14: return config_for<14>(variant);
+    case 15: return config_for<15>(variant);
+    case 16: return config_for<16>(variant);
     default: throw Error(GG_ERR_VALUE, "bad tile count");
   }
+}
+
+static size_t mode_lds_bytes(int jt, const ModeConfig& c) {
+  return 2 * (size_t)c.kc * jt * 64 * sizeof(double);
 }
 
 // One factor in fragment order, for the operator and for its transpose.
@@ -255,22 +350,22 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
       dst = (k % 2 == 0) ? work : work + max_inter;
     }
     const bool last = (k == d - 1);
-    const int64_t nblk = ceil_div(M, kWaves * 16);
-    if (M > 0 && nblk > 0) {
-      GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
+    const int variant = mode_variant();
+    if (M > 0) {
       for (int jt0 = 0; jt0 < f.JT; jt0 += kMaxJT) {
         const int jt = std::min(kMaxJT, f.JT - jt0);
-        mode_kernel_t kern = select_kernel(jt);
-        const size_t lds = (size_t)kKC * jt * 64 * sizeof(double);
+        const ModeConfig mc = select_kernel(jt, variant);
+        const int64_t nblk = ceil_div(M, (int64_t)mc.waves * 16);
+        GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         double* parts = nullptr;
         if (last && dot_partials != nullptr) {
           parts = dot_partials + np_total;
           np_total += nblk;
         }
-        hipLaunchKernelGGL(kern, dim3((unsigned)nblk), dim3(kWaves * 64), lds, stream, src,
-                           dst, f.frag, M, (int)f.q, (int)f.p, f.KS, f.JT, jt0,
-                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts,
-                           skip);
+        hipLaunchKernelGGL(mc.fn, dim3((unsigned)nblk), dim3(mc.waves * 64),
+                           mode_lds_bytes(jt, mc), stream, src, dst, f.frag, M, (int)f.q,
+                           (int)f.p, f.KS, f.JT, jt0,
+                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip);
         GG_LAUNCH_CHECK();
       }
     }
@@ -288,7 +383,8 @@ int64_t kron_partials_needed(const gg_kron* K, bool transpose) {
   int64_t size = n_in;
   for (const Factor& g : fs) size = size / g.q * g.p;
   const int64_t M = size / f.p;
-  return ceil_div(M, kWaves * 16) * ceil_div(f.JT, kMaxJT);
+  // upper bound over the launch variants (the smallest workgroup has 4 waves)
+  return ceil_div(M, 4 * 16) * ceil_div(f.JT, kMaxJT);
 }
 
 int64_t kron_work_elems(const gg_kron* K, bool transpose) {
@@ -302,11 +398,13 @@ int64_t kron_n(const gg_kron* K) { return K->n_rows; }
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
-  for (int jt = 1; jt <= kMaxJT; ++jt) {
-    const int bytes = kKC * jt * 64 * (int)sizeof(double);
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(select_kernel(jt)),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  }
+  for (int v = 0; v <= 4; ++v)
+    for (int jt = 1; jt <= kMaxJT; ++jt) {
+      const ModeConfig mc = select_kernel(jt, v);
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)mode_lds_bytes(jt, mc)));
+    }
   done = true;
 }
 

@@ -250,6 +250,24 @@ __global__ __launch_bounds__(kVecThreads) void lz_scale_kernel(const double* __r
 
 __global__ void sqrt_inplace_kernel(double* v) { *v = sqrt(*v); }
 
+// A[i][j] *= w[i] (mode 0) or /= w[i] (mode 1); square (mode 2): A = A * A
+__global__ __launch_bounds__(kVecThreads) void scale_rows_kernel(double* __restrict__ A,
+                                                                 int64_t rows, int64_t cols,
+                                                                 const double* __restrict__ w,
+                                                                 int mode) {
+  const int64_t total = rows * cols;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const double a = A[e];
+    if (mode == 2) {
+      A[e] = a * a;
+    } else {
+      const double s = w[e / cols];
+      A[e] = mode == 0 ? a * s : a / s;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kVecThreads) void diag_divide_kernel(const double* __restrict__ t,
                                                                   double shift,
                                                                   const double* __restrict__ x,
@@ -415,6 +433,20 @@ int gg_diag_divide(const double* t_dev, double shift, const double* x_dev, doubl
     hipLaunchKernelGGL(gg::diag_divide_kernel, dim3(gg::vec_blocks(2 * n)),
                        dim3(gg::kVecThreads), 0, gg::as_stream(stream), t_dev, shift, x_dev,
                        y_dev, n);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_scale_rows(double* A_dev, int64_t rows, int64_t cols, const double* w_dev, int mode,
+                  gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(A_dev && rows >= 0 && cols >= 0 && mode >= 0 && mode <= 2, GG_ERR_VALUE,
+               "bad argument");
+    GG_REQUIRE(mode == 2 || w_dev, GG_ERR_VALUE, "w required");
+    if (rows * cols == 0) return;
+    hipLaunchKernelGGL(gg::scale_rows_kernel, dim3(gg::vec_blocks(2 * rows * cols)),
+                       dim3(gg::kVecThreads), 0, gg::as_stream(stream), A_dev, rows, cols, w_dev,
+                       mode);
     GG_LAUNCH_CHECK();
   });
 }

@@ -1,0 +1,461 @@
+"""Kernels: drop-in mirror of gp_grief.kern with device evaluation.
+
+  BaseKernel           gp_grief/kern/basekernel.py:8-204   (parameters, constraints,
+                                                           * / + composition, copy)
+  RBF, Exponential,
+  Matern32, Matern52   gp_grief/kern/stationary.py:79-258  (cov on the device, gg_cov)
+  GridKernel           gp_grief/kern/grid_kernel.py:11-259 (cov_grid -> KronMatrix,
+                                                           cov, cov_kr, parameters)
+  GriefKernel          gp_grief/kern/grief_kernel.py:12-190 (device eigensolve of the
+                                                           grid factors, top-p selection,
+                                                           Phi built on the device)
+Parameter / constraint bookkeeping is host logic identical in behaviour to the
+reference (including the shared-kernel-object quirk of GridKernel's setter,
+grid_kernel.py:233-239).  Every covariance evaluation and the eigenfunction
+matrix Phi run on the MI355X.  GPyKernel is not provided: GPy is not part of
+this stack.
+"""
+import ctypes
+import logging
+from copy import deepcopy
+
+import numpy as np
+
+from . import device as dev
+from . import native
+from .grid import InducingGrid
+from .tensors import KronMatrix, SelectionMatrixSparse, device_sym_eig
+
+logger = logging.getLogger(__name__)
+
+
+class BaseKernel(object):
+    """Base of all kernels (basekernel.py:8-204)."""
+
+    def __init__(self, n_dims, active_dims, name):
+        self.n_dims = n_dims
+        if active_dims is None:
+            active_dims = np.arange(self.n_dims)
+        else:
+            active_dims = np.ravel(active_dims)
+            assert 'int' in active_dims.dtype.type.__name__
+            assert active_dims.min() >= 0
+            assert active_dims.max() < self.n_dims
+        self.active_dims = active_dims
+        self.name = self.__class__.__name__ if name is None else name
+        self.parameter_list = None
+        self.constraint_map = None
+        self._children = []
+
+    def cov(self, x, z=None):
+        x, z = self._process_cov_inputs(x, z)
+        raise NotImplementedError('Not implemented')
+
+    @property
+    def parameters(self):
+        if self.parameter_list is None:
+            raise NotImplementedError('Need to specify kern.parameter_list')
+        parts = [np.ravel(getattr(self, nm)) for nm in self.parameter_list]
+        parts += [child.parameters for _, child in self._children]
+        return np.concatenate(parts, axis=0) if parts else np.array([])
+
+    @parameters.setter
+    def parameters(self, value):
+        assert isinstance(value, np.ndarray)
+        assert value.ndim == 1
+        i0 = 0
+        for nm in self.parameter_list:
+            old = getattr(self, nm)
+            setattr(self, nm, value[i0:i0 + np.size(old)].reshape(np.shape(old)))
+            i0 += np.size(old)
+        for _, child in self._children:
+            old = child.parameters
+            child.parameters = value[i0:i0 + np.size(old)].reshape(np.shape(old))
+            i0 += np.size(old)
+
+    @property
+    def constraints(self):
+        if self.constraint_map is None:
+            raise NotImplementedError('Need to specify kern.constraint_map')
+        parts = [np.ravel(self.constraint_map[nm]) for nm in self.parameter_list]
+        parts += [child.constraints for _, child in self._children]
+        return np.concatenate(parts, axis=0) if parts else np.array([])
+
+    def is_stationary(self):
+        return isinstance(self, Stationary)
+
+    def _process_cov_inputs(self, x, z):
+        assert x.ndim == 2
+        assert x.shape[1] == self.n_dims
+        if z is None:
+            z = x
+        else:
+            assert z.ndim == 2
+            assert z.shape[1] == self.n_dims, "should be %d dims, not %d" % (self.n_dims,
+                                                                             z.shape[1])
+        return x, z
+
+    def __mul__(k1, k2):
+        assert isinstance(k2, BaseKernel)
+        assert k2.n_dims == k1.n_dims
+        parent, child = k1.copy(), k2.copy()
+        if np.size(child.constraint_map['variance']) > 1:
+            child.constraint_map['variance'][0] = 'fixed'
+        else:
+            child.constraint_map['variance'] = 'fixed'
+        parent._children.append(('mul', child))
+        return parent
+
+    def __add__(k1, k2):
+        assert isinstance(k2, BaseKernel), 'k2 must be a kernel'
+        parent, child = k1.copy(), k2.copy()
+        parent._children.append(('add', child))
+        return parent
+
+    def copy(self):
+        c = deepcopy(self)
+        c._children = [(deepcopy(op), ch.copy()) for op, ch in c._children]
+        return c
+
+
+class Stationary(BaseKernel):
+    """Stationary kernels evaluated on the device (stationary.py:9-76)."""
+    _kind = None
+
+    def _device_cov(self, x, z, mode, out, lengthscale=None):
+        """Evaluate into the device matrix `out` (N x M); mode 0/1/2 = set/mul/add."""
+        x = np.asarray(x, dtype=np.float64)[:, self.active_dims] if not dev.is_device_array(x) \
+            else x[:, self.active_dims.tolist()]
+        z = np.asarray(z, dtype=np.float64)[:, self.active_dims] if not dev.is_device_array(z) \
+            else z[:, self.active_dims.tolist()]
+        ls = float(np.asarray(self.lengthscale).reshape(-1)[0])
+        if lengthscale is not None:
+            lsv = np.asarray(lengthscale, dtype=np.float64).reshape(-1)
+            assert len(lsv) == self.active_dims.size
+            x = x / lsv
+            z = z / lsv
+            ls = 1.0
+        xd = dev.to_device(x)
+        zd = dev.to_device(z)
+        D = int(self.active_dims.size)
+        native.check(native.lib().gg_cov(native.GG_KERN[self._kind],
+                                         float(np.asarray(self.variance).reshape(-1)[0]), ls, D,
+                                         native.dptr(xd), xd.numel() // D, native.dptr(zd),
+                                         zd.numel() // D, int(mode), native.dptr(out),
+                                         native.stream_ptr()), "gg_cov")
+
+    def _cov_into(self, x, z, out, mode=0, lengthscale=None):
+        self._device_cov(x, z, mode, out, lengthscale)
+        for op, child in self._children:
+            if not isinstance(child, Stationary):
+                raise NotImplementedError("device composition needs stationary children")
+            child._cov_into(x, z, out, mode=1 if op == 'mul' else 2)
+
+    def cov(self, x, z=None, lengthscale=None):
+        """Covariance matrix (N, M); numpy in, numpy out (CUDA tensors stay on device)."""
+        on_dev = dev.is_device_array(x)
+        x, z = self._process_cov_inputs(x, z)
+        out = dev.empty(int(x.shape[0]) * int(z.shape[0]))
+        if lengthscale is not None and self._kind != "RBF":
+            raise TypeError("per-dimension lengthscales are an RBF option")
+        self._cov_into(x, z, out, lengthscale=lengthscale)
+        out = out.reshape(int(x.shape[0]), int(z.shape[0]))
+        return out if on_dev else dev.to_host(out)
+
+
+def _stationary_init(self, n_dims, variance, lengthscale, active_dims, name, check_size):
+    Stationary.__init__(self, n_dims=n_dims, active_dims=active_dims, name=name)
+    logger.debug('Initializing %s kernel.' % self.name)
+    if check_size:
+        assert np.size(variance) == 1
+        assert np.size(lengthscale) == 1
+    self.variance = np.float64(variance)
+    self.lengthscale = np.float64(lengthscale)
+    self.parameter_list = ['variance', 'lengthscale']
+    self.constraint_map = {'variance': '+ve', 'lengthscale': '+ve'}
+
+
+class RBF(Stationary):
+    """Squared exponential (stationary.py:79-134)."""
+    _kind = "RBF"
+
+    def __init__(self, n_dims, variance=1., lengthscale=1., active_dims=None, name=None):
+        _stationary_init(self, n_dims, variance, lengthscale, active_dims, name, True)
+
+
+class Exponential(Stationary):
+    """stationary.py:137-175."""
+    _kind = "Exponential"
+
+    def __init__(self, n_dims, variance=1., lengthscale=1., active_dims=None, name=None):
+        _stationary_init(self, n_dims, variance, lengthscale, active_dims, name, False)
+
+
+class Matern32(Stationary):
+    """stationary.py:178-216."""
+    _kind = "Matern32"
+
+    def __init__(self, n_dims, variance=1., lengthscale=1., active_dims=None, name=None):
+        _stationary_init(self, n_dims, variance, lengthscale, active_dims, name, False)
+
+
+class Matern52(Stationary):
+    """stationary.py:219-258."""
+    _kind = "Matern52"
+
+    def __init__(self, n_dims, variance=1., lengthscale=1., active_dims=None, name=None):
+        _stationary_init(self, n_dims, variance, lengthscale, active_dims, name, False)
+
+
+class GridKernel(object):
+    """Product of 1-D kernels on a grid (grid_kernel.py:11-259)."""
+
+    def __init__(self, kern_list, radial_kernel=False):
+        self.kern_list = kern_list
+        self.grid_dim = len(kern_list)
+        assert isinstance(radial_kernel, bool)
+        self.radial_kernel = radial_kernel
+        if self.radial_kernel:
+            for kern in self.kern_list:
+                assert kern.n_dims == self.kern_list[0].n_dims, \
+                    "number of grid dims must be equal for all slices"
+            self.kern_list = [self.kern_list[0], ] * np.size(kern_list)
+        else:
+            for i in range(1, self.grid_dim):
+                if hasattr(self.kern_list[i], 'fix_variance'):
+                    self.kern_list[i].fix_variance()
+                elif np.size(self.kern_list[i].constraint_map['variance']) > 1:
+                    logger.info("Multiple variance parameters found in the kernel, "
+                                "will only fix the first")
+                    self.kern_list[i].constraint_map['variance'][0] = 'fixed'
+                else:
+                    self.kern_list[i].constraint_map['variance'] = 'fixed'
+        self.n_dims = np.sum([kern.n_dims for kern in self.kern_list])
+
+    def cov_grid(self, x, z=None, dim_noise_var=None, use_toeplitz=False):
+        """Per-dimension covariances as a KronMatrix, input dims reversed (:56-115)."""
+        assert dim_noise_var is not None, "dim_noise_var must be specified"
+        if isinstance(use_toeplitz, bool):
+            use_toeplitz = [use_toeplitz, ] * self.grid_dim
+        else:
+            assert np.size(use_toeplitz) == self.grid_dim
+        if np.any(use_toeplitz):
+            raise NotImplementedError("no kernel implements cov_toeplitz (reference neither)")
+        assert len(x) == self.grid_dim
+        cross = z is not None
+        if not cross:
+            z = [None, ] * self.grid_dim
+        else:
+            assert len(z) == self.grid_dim
+        K = [kern.cov(x=x[i], z=z[i]) for i, kern in enumerate(self.kern_list)]
+        K = KronMatrix(K[::-1], sym=(z[0] is None))
+        if dim_noise_var != 0.:
+            assert not cross, "not implemented for cross covariances yet"
+            K = K.sub_shift(shift=dim_noise_var)
+        return K
+
+    def cov(self, x, z=None, dim_noise_var=None):
+        """Dense Hadamard product over dimensions (:118-145), on the device."""
+        assert dim_noise_var is None, "currenly no way to add dim_noise_var"
+        on_dev = dev.is_device_array(x)
+        zz = x if z is None else z
+        out = dev.empty(int(x.shape[0]) * int(zz.shape[0]))
+        i_cur = 0
+        for i, kern in enumerate(self.kern_list):
+            sl = slice(i_cur, i_cur + kern.n_dims)
+            i_cur += kern.n_dims
+            xi = x[:, sl]
+            zi = zz[:, sl]
+            if not isinstance(kern, Stationary):
+                raise NotImplementedError("device GridKernel.cov needs stationary kernels")
+            kern._cov_into(xi, zi, out, mode=0 if i == 0 else 1)
+        out = out.reshape(int(x.shape[0]), int(zz.shape[0]))
+        return out if on_dev else dev.to_host(out)
+
+    def cov_kr(self, x, z, dim_noise_var=None, form_kr=True):
+        """Row-partitioned Khatri-Rao cross covariance (:148-179), factors reversed."""
+        assert dim_noise_var is None, "currenly no way to add dim_noise_var"
+        (N, d) = x.shape
+        assert self.grid_dim == d, "currently only works for 1-dimensional grids"
+        Kxz = [kern.cov(x=x[:, (i,)], z=z[i]) for i, kern in enumerate(self.kern_list)]
+        Kxz = Kxz[::-1]
+        if form_kr:
+            raise NotImplementedError("KhatriRaoMatrix is outside the ported hot path; "
+                                      "use form_kr=False")
+        return Kxz
+
+    def cov_kr_grad(self, x, z, grad_dim):
+        raise NotImplementedError  # needs GPyKernel in the reference (grid_kernel.py:196-199)
+
+    @property
+    def parameters(self):
+        if self.radial_kernel:
+            return np.ravel(self.kern_list[0].parameters)
+        return np.concatenate([np.ravel(k.parameters) for k in self.kern_list], axis=0)
+
+    @parameters.setter
+    def parameters(self, value):
+        assert isinstance(value, np.ndarray)
+        assert value.ndim == 1
+        if self.radial_kernel:
+            self.kern_list[0].parameters = value
+            self.kern_list = [self.kern_list[0], ] * np.size(self.kern_list)
+        else:
+            i0 = 0
+            for kern in self.kern_list:
+                old = kern.parameters
+                kern.parameters = value[i0:i0 + np.size(old)].reshape(np.shape(old))
+                i0 += np.size(old)
+
+    @property
+    def constraints(self):
+        if self.radial_kernel:
+            return np.ravel(self.kern_list[0].constraints)
+        return np.concatenate([np.ravel(k.constraints) for k in self.kern_list], axis=0)
+
+    @property
+    def diag_val(self):
+        return self.cov(np.zeros((1, self.n_dims))).squeeze()
+
+
+class GriefKernel(GridKernel):
+    """GRId-structured EIgenFunctions kernel (grief_kernel.py:12-190).
+
+    cov(x) returns (Phi, w, Phi) with Phi = (n x p) numpy; the models keep Phi
+    on the device through phi_device().
+    """
+
+    def __init__(self, kern_list, grid, n_eigs=1000, reweight_eig_funs=True,
+                 opt_kernel_params=False, w=1., dim_noise_var=1e-12, log_KRrowcol=True,
+                 **kwargs):
+        self.reweight_eig_funs = bool(reweight_eig_funs)
+        self.opt_kernel_params = bool(opt_kernel_params)
+        super(GriefKernel, self).__init__(kern_list=kern_list, **kwargs)
+        assert isinstance(grid, InducingGrid), "must be an InducingGrid"
+        assert grid.input_dim == self.n_dims, "number of dimensions do not match"
+        self.grid = grid
+        self.dim_noise_var = float(dim_noise_var)
+        self.n_eigs = int(min(n_eigs, self.grid.num_data))
+        if not self.opt_kernel_params:
+            for i, kern in enumerate(self.kern_list):
+                for key in kern.constraint_map:
+                    self.kern_list[i].constraint_map[key] = \
+                        np.tile('fixed', np.shape(kern.constraint_map[key]))
+        label = '+ve' if self.reweight_eig_funs else 'fixed'
+        self.w_constraints = np.array([label, ] * self.n_eigs, dtype='|S10')
+        if np.isscalar(w) and w == 1.:
+            self.w = np.ones(self.n_eigs)
+        else:
+            w = np.asarray(w, dtype=np.float64)
+            assert w.shape == (self.n_eigs,)
+            assert np.all(w > 0.), "w's must be positive"
+            self.w = w
+        self._old_base_kern_params = None
+        self.log_KRrowcol = log_KRrowcol
+        self._dev_basis = None
+
+    # ------------------------------------------------------------------ Phi
+    def cov(self, x, z=None):
+        assert x.shape[1] == self.n_dims
+        if z is not None:
+            Phi_L = self.cov(x=x)[0]
+            Phi_R = self.cov(x=z)[0]
+            return Phi_L, self.w, Phi_R
+        Phi = dev.to_host(self.phi_device(x))
+        return Phi, self.w, Phi
+
+    def phi_device(self, x, transposed=False):
+        """Phi (n x p) row-major -- or Phi^T (p x n) -- as a CUDA tensor."""
+        self._setup_inducing_cov()
+        B = self._dev_basis
+        xd = dev.to_device(x)
+        n = xd.numel() // self.grid_dim
+        d = self.grid_dim
+        L = native.lib()
+        ltab = dev.empty(max(n * B["U"], 1))
+        stab = dev.empty(max(n * B["U"], 1))
+        for f in range(d):
+            i = d - 1 - f
+            kern = self.kern_list[i]
+            if not isinstance(kern, Stationary) or kern._children:
+                raise NotImplementedError("GRIEF device basis needs plain stationary kernels")
+            native.check(L.gg_grief_tables(
+                native.GG_KERN[kern._kind], float(np.asarray(kern.variance).reshape(-1)[0]),
+                float(np.asarray(kern.lengthscale).reshape(-1)[0]),
+                ctypes.c_void_p(xd.data_ptr() + 8 * i), d, n, native.dptr(B["xg"][f]),
+                B["m"][f], native.dptr(B["qsel"][f]), B["u"][f], native.dptr(ltab),
+                native.dptr(stab), B["U"], B["col0"][f], native.stream_ptr()), "gg_grief_tables")
+        p = self.n_eigs
+        phi = dev.empty(n * p)
+        native.check(L.gg_grief_phi(native.dptr(ltab), native.dptr(stab), B["U"], n,
+                                    native.dptr(B["cidx"]), d, native.dptr(B["log_lam"]), p,
+                                    int(bool(transposed)), native.dptr(phi),
+                                    native.stream_ptr()), "gg_grief_phi")
+        return phi.reshape(p, n) if transposed else phi.reshape(n, p)
+
+    def cov_grad(self, x, grad_dim):
+        raise NotImplementedError  # needs GPyKernel gradients (grid_kernel.py:196-199)
+
+    # ------------------------------------------------------------ parameters
+    @property
+    def parameters(self):
+        return np.concatenate([super(GriefKernel, self).parameters, self.w], axis=0)
+
+    @parameters.setter
+    def parameters(self, value):
+        n_theta = value.size - self.n_eigs
+        GridKernel.parameters.fset(self, value[:n_theta])
+        self.w = value[n_theta:]
+
+    @property
+    def constraints(self):
+        return np.concatenate([super(GriefKernel, self).constraints, self.w_constraints],
+                              axis=0)
+
+    @property
+    def diag_val(self):
+        raise NotImplementedError('')
+
+    # ------------------------------------------------- inducing eigen-basis
+    def _setup_inducing_cov(self):
+        """Factors, device eigendecomposition, top-p selection (:168-190).
+
+        Cached on the base-kernel parameters like the reference.
+        """
+        base = super(GriefKernel, self).parameters
+        if self._old_base_kern_params is not None and \
+                np.array_equal(self._old_base_kern_params, base):
+            return
+        Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
+        Q, lam = device_sym_eig([np.asarray(k) for k in Kuu.K])
+        self._Quu = KronMatrix(Q)
+        all_eig_vals = KronMatrix(lam)
+        n_eigs = int(min(self.n_eigs, all_eig_vals.shape[0]))
+        eig_pos, self._log_lam = all_eig_vals.find_extremum_eigs(
+            n_eigs=n_eigs, mode='largest', log_expand=True)[:2]
+        self._Sp = [SelectionMatrixSparse((col, Kuu.K[i].shape[0]))
+                    for i, col in enumerate(eig_pos.T)]
+        self._old_base_kern_params = base
+        self._build_device_basis()
+
+    def _build_device_basis(self):
+        d = self.grid_dim
+        qsel, xg, us, ms, col0 = [], [], [], [], []
+        cidx = np.zeros((self.n_eigs, d), dtype=np.int32)
+        c = 0
+        for f in range(d):
+            i = d - 1 - f
+            S = self._Sp[f]
+            Qf = np.asarray(self._Quu.K[f])
+            qsel.append(dev.to_device(np.ascontiguousarray(Qf.T[S.unique, :])))
+            xg.append(dev.to_device(np.asarray(self.grid.xg[i], dtype=np.float64).reshape(-1)))
+            us.append(int(S.unique.size))
+            ms.append(int(Qf.shape[0]))
+            col0.append(c)
+            cidx[:, f] = c + np.asarray(S.unique_inverse).reshape(-1)
+            c += int(S.unique.size)
+        t = dev.torch()
+        self._dev_basis = dict(
+            qsel=qsel, xg=xg, u=us, m=ms, col0=col0, U=c,
+            cidx=t.from_numpy(cidx.reshape(-1)).to(dev.device()),
+            log_lam=dev.to_device(self._log_lam))

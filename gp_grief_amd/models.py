@@ -1,0 +1,411 @@
+"""Models: drop-in mirror of gp_grief.models on the MI355X.
+
+  BaseModel      gp_grief/models/basemodel.py:14-379 -- parameter vector, softplus
+                 transforms, L-BFGS optimize, finite-difference gradient,
+                 checkgrad, cache invalidation (host logic, same behaviour)
+  GPGriefModel   gp_grief/models/gp_grief_model.py:15-245 -- Phi, the p x p
+                 Gram, Cholesky, Woodbury solve, log det, LML, adjoint gradient,
+                 predict: every O(n p) / O(p^3) step on the device
+  GPGridModel    (new, the north star's P1 model) exact or CG grid GP on a full
+                 Kronecker-structured grid: KronMatrix operator, device CG /
+                 exact eigen-solve, exact or Lanczos (SLQ) log det, posterior
+                 mean and latent variance on the grid.
+
+Device state keeps the reference's attribute names (_Phi, _A, _P, _Pchol,
+_alpha, _alpha_p) holding CUDA tensors (or small host arrays where the
+reference keeps scalars/vectors).
+"""
+import logging
+from traceback import format_exc
+
+import numpy as np
+from numpy.linalg import LinAlgError
+from numpy.testing import assert_array_almost_equal
+from scipy.optimize import fmin_l_bfgs_b
+
+from . import dense
+from . import device as dev
+from .kern import GriefKernel, BaseKernel
+from .linalg import solver_counter, LogexpTransformation
+
+logger = logging.getLogger(__name__)
+
+
+class BaseModel(object):
+    """Parameter plumbing and optimisation (basemodel.py:14-379)."""
+    param_shift = {'+ve': 1e-200, '-ve': -1e-200}
+    _transformations = {'+ve': LogexpTransformation()}
+
+    def __init__(self):
+        logger.debug('Initializing %s model.' % self.__class__.__name__)
+        self.dependent_attributes = ['_alpha', '_log_like', '_gradient', '_K', '_log_det']
+        self._previous_parameters = None
+        self.grad_method = None
+        self.noise_var_constraint = '+ve'
+
+    def log_likelihood(self, return_gradient=False):
+        p = self.parameters
+        if return_gradient and (self._gradient is None):
+            if 'adjoint' in self.grad_method:
+                (self._log_like, self._gradient) = self._adjoint_gradient(p)
+            elif 'finite_difference' in self.grad_method:
+                (self._log_like, self._gradient) = self._finite_diff_gradient(p)
+            else:
+                raise RuntimeError('unknown grad_method %s' % repr(self.grad_method))
+        elif self._log_like is None:
+            self._log_like = self._compute_log_likelihood(p)
+        if return_gradient:
+            return self._log_like, self._gradient
+        return self._log_like
+
+    def optimize(self, max_iters=1e3, messages=False, use_counter=False, factr=1e7,
+                 pgtol=1e-05):
+        logger.debug('Beginning MLE to optimize hyperparams. grad_method=%s' % self.grad_method)
+        try:
+            x0 = self._transform_parameters(self.parameters)
+            assert np.all(np.isfinite(x0))
+        except Exception:
+            logger.error('Transformation failed for initial values. '
+                         'Ensure constraints are met or the value is not too small.')
+            raise
+        free = np.logical_not(self._fixed_indicies)
+        x0 = x0[free]
+        self._counter = solver_counter(disp=True) if use_counter else None
+        try:
+            x_opt, f_opt, opt = fmin_l_bfgs_b(func=self._objective_grad, x0=x0, factr=factr,
+                                              pgtol=pgtol, maxiter=max_iters, disp=messages)
+        except (KeyboardInterrupt, IndexError):
+            logger.info('Keyboard interrupt raised. Cleaning up...')
+            if self._counter is not None and self._counter.backup is not None:
+                self.parameters = self._counter.backup[1]
+                logger.info('will return best parameter set with log-likelihood = %.4g'
+                            % self._counter.backup[0])
+            opt = None
+        else:
+            logger.info('Function Evals: %d. Exit status: %s' % (f_opt, opt['warnflag']))
+            transformed = self._previous_parameters
+            transformed[free] = x_opt
+            self.parameters = self._untransform_parameters(transformed)
+        return opt
+
+    def checkgrad(self, decimal=3, raise_if_fails=True):
+        grad_exact = self._finite_diff_gradient(self.parameters)[1]
+        grad_exact[self._fixed_indicies] = 1
+        grad_analytic = self.log_likelihood(return_gradient=True)[1].copy()
+        grad_analytic[self._fixed_indicies] = 1
+        protected_nan = np.logical_and(np.abs(grad_exact) < 1e-8, np.abs(grad_analytic) < 1e-8)
+        protected_div0 = np.abs(grad_exact - grad_analytic) < 1e-5
+        prot = np.logical_or(protected_nan, protected_div0)
+        grad_exact[prot] = 1.
+        grad_analytic[prot] = 1.
+        try:
+            assert_array_almost_equal(grad_exact / grad_analytic, np.ones(grad_exact.shape),
+                                      decimal=decimal)
+        except AssertionError:
+            logger.info('Gradient check failed.')
+            logger.debug('[[Finite-Diff Gradient], [Analytic Gradient]]:\n%s\n'
+                         % repr(np.asarray([grad_exact, grad_analytic])))
+            if raise_if_fails:
+                raise
+            logger.info(format_exc())
+            return False
+        logger.info('Gradient check passed.')
+        return True
+
+    @property
+    def parameters(self):
+        parameters = np.concatenate((np.ravel(self.noise_var), self.kern.parameters), axis=0)
+        if not np.array_equal(parameters, self._previous_parameters):
+            for attr in self.dependent_attributes:
+                setattr(self, attr, None)
+            self._previous_parameters = parameters.copy()
+        return parameters.copy()
+
+    @parameters.setter
+    def parameters(self, parameters):
+        self.noise_var = parameters[0]
+        self.kern.parameters = parameters[1:]
+        if not np.array_equal(parameters, self._previous_parameters):
+            for attr in self.dependent_attributes:
+                setattr(self, attr, None)
+            self._previous_parameters = parameters.copy()
+
+    @property
+    def constraints(self):
+        return np.concatenate((np.ravel(self.noise_var_constraint), self.kern.constraints),
+                              axis=0)
+
+    def predict(self, Xnew, compute_var=None):
+        raise NotImplementedError('')
+
+    def fit(self):
+        raise NotImplementedError('')
+
+    def _objective_grad(self, transformed_free_parameters):
+        free = np.logical_not(self._fixed_indicies)
+        transformed = self._previous_parameters
+        transformed[free] = transformed_free_parameters
+        try:
+            self.parameters = self._untransform_parameters(transformed)
+            (objective, gradient) = self.log_likelihood(return_gradient=True)
+            objective = -objective
+            gradient = -gradient
+            if not np.isfinite(objective):
+                logger.debug('objective is not finite')
+            if not np.all(np.isfinite(gradient[free])):
+                logger.debug('some derivatives are non-finite')
+            gradient = self._transform_gradient(self.parameters, gradient)
+        except (LinAlgError, ZeroDivisionError, ValueError):
+            logger.error('numerical issue computing log-likelihood or gradient')
+            raise
+        free_gradient = gradient[free]
+        if self._counter is not None:
+            msg = 'log-likelihood=%.4g, gradient_norm=%.2g' % (-objective,
+                                                              np.linalg.norm(gradient))
+            if self._counter.backup is None or self._counter.backup[0] < -objective:
+                self._counter(msg=msg, store=(-objective, self.parameters.copy()))
+            else:
+                self._counter(msg=msg)
+        return objective, free_gradient
+
+    @property
+    def _fixed_indicies(self):
+        return self.constraints == 'fixed'
+
+    @property
+    def _free_indicies(self):
+        return np.logical_not(self._fixed_indicies)
+
+    def _transform_parameters(self, parameters):
+        constraints = self.constraints
+        assert parameters.size == np.size(constraints)
+        out = np.zeros(parameters.size)
+        for i, (param, c) in enumerate(zip(parameters, constraints)):
+            if c is None or c == 'fixed' or c == '':
+                out[i] = param
+            else:
+                out[i] = self._transformations[c].transform(param - self.param_shift[c])
+        if not np.all(np.isfinite(out)):
+            logger.debug('transformation led to non-finite value')
+        return out
+
+    def _transform_gradient(self, parameters, gradients):
+        constraints = self.constraints
+        assert parameters.size == gradients.size == np.size(constraints)
+        out = np.zeros(parameters.size)
+        for i, (param, grad, c) in enumerate(zip(parameters, gradients, constraints)):
+            if c is None or c == '':
+                out[i] = grad
+            elif c != 'fixed':
+                out[i] = self._transformations[c].transform_grad(param - self.param_shift[c],
+                                                                grad)
+        if not np.all(np.isfinite(out)):
+            logger.debug('transformation led to non-finite value')
+        return out
+
+    def _untransform_parameters(self, transformed_parameters):
+        assert transformed_parameters.size == np.size(self.constraints)
+        out = np.zeros(transformed_parameters.size)
+        for i, (t, c) in enumerate(zip(transformed_parameters, self.constraints)):
+            if c is None or c == 'fixed' or c == '':
+                out[i] = t
+            else:
+                out[i] = self._transformations[c].inverse_transform(t) + self.param_shift[c]
+        if not np.all(np.isfinite(out)):
+            logger.debug('transformation led to non-finite value')
+        return out
+
+    def _finite_diff_gradient(self, parameters):
+        """Forward differences, step 1e-6 (basemodel.py:328-361)."""
+        assert isinstance(parameters, np.ndarray)
+        free_inds = np.nonzero(np.logical_not(self._fixed_indicies))[0]
+        step = 1e-6
+        ll_fs = np.zeros(free_inds.size)
+        for i, idx in enumerate(free_inds):
+            p_fs = parameters.copy()
+            p_fs[idx] += step
+            ll_fs[i] = np.squeeze(self._compute_log_likelihood(p_fs))
+        log_like = self._compute_log_likelihood(parameters)
+        gradient = np.zeros(parameters.shape)
+        gradient[free_inds] = (ll_fs - np.squeeze(log_like)) / step
+        return log_like, gradient
+
+    def _compute_log_likelihood(self, parameters):
+        raise NotImplementedError('')
+
+    def _adjoint_gradient(self, parameters):
+        raise NotImplementedError('')
+
+
+def _dev_2d(x):
+    xd = dev.to_device(x)
+    shape = tuple(x.shape)
+    return xd.reshape(shape[0], shape[1] if len(shape) > 1 else 1)
+
+
+class GPGriefModel(BaseModel):
+    """GP-GRIEF (gp_grief_model.py:15-245) with every O(np), O(np^2), O(p^3)
+    step on the MI355X (Phi build, SYRK Gram on FP64 MFMA, blocked Cholesky,
+    Woodbury solves, GEMV / GEMM predictions)."""
+
+    def __init__(self, X, Y, kern, noise_var=1.):
+        super(GPGriefModel, self).__init__()
+        assert X.ndim == 2
+        assert Y.ndim == 2
+        self.X = np.asarray(X)
+        self.Y = np.asarray(Y)
+        assert not np.any(np.isnan(Y))
+        self.num_data, self.input_dim = self.X.shape
+        if Y.shape[0] != self.num_data:
+            raise ValueError('X and Y sizes are inconsistent')
+        self.output_dim = self.Y.shape[1]
+        if self.output_dim != 1:
+            raise RuntimeError('this only deals with 1 response for now')
+        assert isinstance(kern, GriefKernel)
+        assert np.ndim(kern.kern_list) == 1
+        for ki in kern.kern_list:
+            assert isinstance(ki, BaseKernel)
+            assert ki.n_dims == 1, "currently only 1-dimensional grids allowed"
+        self.kern = kern
+        self.noise_var = np.float64(noise_var)
+        self.dependent_attributes = np.unique(np.concatenate(
+            (self.dependent_attributes, ['_P', '_Pchol', '_alpha_p'])))
+        if self.kern.opt_kernel_params:
+            self.dependent_attributes = np.unique(np.concatenate(
+                (self.dependent_attributes, ['_A', '_Phi', '_X_last_pred', '_Phi_last_pred'])))
+        else:
+            self._A = None
+            self._Phi = None
+            self._Phi_last_pred = None
+            self._X_last_pred = None
+        if self.kern.opt_kernel_params:
+            self.grad_method = 'finite_difference'
+        else:
+            self.grad_method = ['adjoint', 'finite_difference'][0]
+        self._Yd = None
+
+    def _y_dev(self):
+        if self._Yd is None:
+            self._Yd = dev.to_device(self.Y[:, 0])
+        return self._Yd
+
+    def fit(self, **kwargs):
+        self.parameters
+        if self._alpha is not None:
+            return
+        self._cov_setup()
+        self._alpha = self._mv_cov_inv_dev(self._y_dev())
+
+    def predict_precompute(self, Xnew):
+        assert Xnew.ndim == 2
+        assert Xnew.shape[1] == self.input_dim
+        self.parameters
+        if self._alpha is None:
+            self.fit()
+        if self._alpha_p is None:
+            t = dense.matvec(self._Phi, self._alpha, trans=True)
+            self._alpha_p = dense.scale_rows(t, dev.to_device(self.kern.w), 0)
+
+    def predict(self, Xnew):
+        """(Yhat (M,1), Yhatvar (M,M)) with Var = s Phi* P^-1 Phi*^T + s I (:99-125)."""
+        self.predict_precompute(Xnew)
+        if self._Phi_last_pred is None or not np.array_equal(Xnew, self._X_last_pred):
+            self._Phi_last_pred = self.kern.phi_device(Xnew, transposed=True)  # p x M
+            self._X_last_pred = Xnew
+        PhiT = self._Phi_last_pred
+        yhat = dense.matvec(PhiT, self._alpha_p, trans=True)
+        V = self._Pchol.solve(PhiT, which=1)                  # L^-1 Phi*^T  (p x M)
+        var = dense.matmul(V, V, ta=True, alpha=float(self.noise_var))
+        var = dense.add_diag(var, float(self.noise_var))
+        return dense.host(yhat).reshape((-1, 1)), dense.host(var)
+
+    def d_Yhat_d_x(self, Xnew, dim):
+        raise NotImplementedError  # needs GriefKernel.cov_grad (GPyKernel only)
+
+    def _cov_setup(self):
+        if self._P is not None:
+            return
+        self._w = self.kern.w
+        if self._A is None:
+            self._Phi = self.kern.phi_device(self.X)          # n x p
+            self._A = dense.matmul(self._Phi, self._Phi, ta=True)  # Phi^T Phi
+        wd = dev.to_device(np.asarray(self._w, dtype=np.float64))
+        self._P = dense.add_diag(self._A, float(self.noise_var), wd)
+        self._Pchol = dense.Cholesky(self._P)
+
+    def _adjoint_gradient(self, parameters):
+        """dL/dw and dL/dsigma^2 (:156-200) via diag(P^-1): with P = A + D,
+        sum_i A_ij (P^-1 A)_ij = A_jj - d_j + d_j^2 (P^-1)_jj and
+        tr(P^-1 A) = p - sum_j d_j (P^-1)_jj  (exact algebra, one triangular
+        inverse instead of the reference's p x p cho_solve)."""
+        assert isinstance(parameters, np.ndarray)
+        free_inds = np.nonzero(np.logical_not(self._fixed_indicies))[0]
+        gradient = np.zeros(parameters.shape) + np.nan
+        log_like = self._compute_log_likelihood(parameters)
+        s = float(self.noise_var)
+        w = np.asarray(self._w, dtype=np.float64)
+        dvec = s / w
+        pinv_diag = None
+        if self.kern.reweight_eig_funs or self.noise_var_constraint != 'fixed':
+            pinv_diag = dense.host(self._Pchol.inverse_diag())
+        if self.kern.reweight_eig_funs:
+            phia = dense.host(dense.matvec(self._Phi, self._alpha, trans=True))
+            data_fit_grad = 0.5 * phia ** 2
+            complexity_grad = -0.5 * dvec * (1.0 - dvec * pinv_diag) / s
+            gradient[-self.kern.n_eigs:] = data_fit_grad + complexity_grad
+        if self.noise_var_constraint != 'fixed':
+            data_fit = 0.5 * dense.dot(self._alpha, self._alpha)
+            tr = float(self.kern.n_eigs) - float(np.sum(dvec * pinv_diag))
+            gradient[0] = data_fit - 0.5 * (float(self.num_data) - tr) / s
+        if self.kern.opt_kernel_params:
+            raise NotImplementedError("adjoint method not implemented for"
+                                      "kernel parameter optimiszation, just weights")
+        assert not np.any(np.isnan(gradient[free_inds])), "gradient missed!"
+        return log_like, gradient
+
+    def _compute_log_likelihood(self, parameters):
+        self.parameters = parameters
+        self.fit()
+        yd = self._y_dev()
+        ll = -0.5 * (dense.dot(yd, self._alpha) + self._cov_log_det()
+                     + self.num_data * np.log(np.pi * 2))
+        return np.array([[ll]])
+
+    def _mv_cov(self, x):
+        """(Phi W Phi^T + s I) x (:217-225)."""
+        assert x.shape[0] == self.num_data
+        assert self._Phi is not None, "cov has not been setup"
+        xd = _dev_2d(x)
+        t = dense.matmul(self._Phi, xd, ta=True)
+        dense.scale_rows(t, dev.to_device(np.asarray(self._w, dtype=np.float64)), 0)
+        out = xd.clone()
+        dense.matmul(self._Phi, t, alpha=1.0, beta=float(self.noise_var), C=out)
+        return dense.host(out).reshape(np.shape(x))
+
+    def _mv_cov_inv_dev(self, xd):
+        """(x - Phi P^-1 Phi^T x) / s for a 1-D device vector."""
+        t = dense.matvec(self._Phi, xd, trans=True)
+        t = self._Pchol.solve(t, which=3)
+        out = xd.clone()
+        dense.matvec(self._Phi, t, alpha=-1.0, beta=1.0, y=out)
+        dense.axpby(0.0, out, 1.0 / float(self.noise_var), out)
+        return out
+
+    def _mv_cov_inv(self, x):
+        """(x - Phi cho_solve(P, Phi^T x)) / s (:228-235)."""
+        assert x.shape[0] == self.num_data
+        assert self._Pchol is not None, "cov has not been setup"
+        xd = _dev_2d(x)
+        t = dense.matmul(self._Phi, xd, ta=True)
+        t = self._Pchol.solve(t, which=3)
+        out = xd.clone()
+        dense.matmul(self._Phi, t, alpha=-1.0, beta=1.0, C=out)
+        flat = out.reshape(-1)
+        dense.axpby(0.0, flat, 1.0 / float(self.noise_var), flat)
+        return dense.host(out).reshape(np.shape(x))
+
+    def _cov_log_det(self):
+        """2 sum log diag chol(P) + sum log w + (n - p) log s (:238-245)."""
+        assert self._Pchol is not None, "cov has not been setup"
+        return (self._Pchol.logdet + np.sum(np.log(self._w))
+                + float(self.num_data - self.kern.n_eigs) * np.log(self.noise_var))

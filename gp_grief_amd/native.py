@@ -47,6 +47,7 @@ SIGNATURES = {
                                ctypes.POINTER(ctypes.c_double), _vp],
     "gg_dot": [_c_dp, _c_dp, ctypes.c_int64, ctypes.POINTER(ctypes.c_double), _vp],
     "gg_axpby": [ctypes.c_double, _c_dp, ctypes.c_double, _c_dp, ctypes.c_int64, _vp],
+    "gg_scale_rows": [_c_dp, ctypes.c_int64, ctypes.c_int64, _c_dp, ctypes.c_int, _vp],
     "gg_diag_divide": [_c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
     "gg_cg_work_elems": [_vp, _c_i64p],
     "gg_cg_create": [_vp, ctypes.c_double, _c_dp, ctypes.POINTER(ctypes.c_void_p)],
@@ -62,7 +63,29 @@ SIGNATURES = {
     "gg_sym_eig_batched": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
                            ctypes.c_int, _vp],
     "gg_sym_eig_work_elems": [ctypes.c_int, _c_i64p, _c_i64p],
+    "gg_cov": [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_dp,
+               ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
+    "gg_grief_tables": [ctypes.c_int, ctypes.c_double, ctypes.c_double, _c_dp, ctypes.c_int64,
+                        ctypes.c_int64, _c_dp, ctypes.c_int, _c_dp, ctypes.c_int, _c_dp, _c_dp,
+                        ctypes.c_int, ctypes.c_int, _vp],
+    "gg_grief_phi": [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int64, _c_dp, ctypes.c_int, _c_dp,
+                     ctypes.c_int, ctypes.c_int, _c_dp, _vp],
+    "gg_gemm": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                ctypes.c_double, _c_dp, ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_double,
+                _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
+    "gg_gemv": [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _c_dp,
+                ctypes.c_int64, _c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
+    "gg_add_diag": [ctypes.c_int, _c_dp, ctypes.c_int64, ctypes.c_double, _c_dp, _c_dp,
+                    ctypes.c_int64, _vp],
+    "gg_potrf_work_elems": [ctypes.c_int, _c_i64p],
+    "gg_potrf": [ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, ctypes.POINTER(ctypes.c_double),
+                 _vp],
+    "gg_potrs": [ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _c_dp,
+                 ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
+    "gg_colsumsq_lower": [ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _vp],
 }
+
+GG_KERN = {"RBF": 0, "Exponential": 1, "Matern32": 2, "Matern52": 3}
 
 _lock = threading.Lock()
 _lib = None
@@ -78,6 +101,10 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
+        # PyTorch-ROCm bundles its own libamdhip64; load it FIRST so that the
+        # library resolves its HIP dependency to that same runtime instead of
+        # bringing a second runtime into the process.
+        import torch  # noqa: F401
         if not os.path.exists(LIB_PATH):
             raise NativeUnavailable(
                 "%s is not built; run `python -c 'import __graft_entry__ as g; g.build()'`"

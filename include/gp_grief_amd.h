@@ -82,6 +82,9 @@ int gg_dot(const double* x_dev, const double* y_dev, int64_t n, double* out_host
            gg_stream stream); /* synchronising */
 int gg_axpby(double a, const double* x_dev, double b, double* y_dev, int64_t n,
              gg_stream stream); /* y = a x + b y */
+/* A[i][:] *= w[i] (mode 0), /= w[i] (mode 1), or A = A*A elementwise (mode 2). */
+int gg_scale_rows(double* A_dev, int64_t rows, int64_t cols, const double* w_dev, int mode,
+                  gg_stream stream);
 /* y = x / (t + shift) for an explicit eigenvalue vector t (solve_schur with an
  * expanded t, kron_matrix.py:349-350).                                        */
 int gg_diag_divide(const double* t_dev, double shift, const double* x_dev, double* y_dev,
@@ -120,6 +123,62 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
                        double* lam_dev, double* work_dev, int64_t work_elems,
                        int max_sweeps, gg_stream stream);
 int gg_sym_eig_work_elems(int count, const int64_t* m, int64_t* elems);
+
+
+/* ------------------------------------------------------- GRIEF basis (P2)
+ * Stationary covariance k(x_i, z_j) for x: nx x dims, z: nz x dims row-major
+ * (RBF / Exponential / Matern32 / Matern52, gp_grief/kern/stationary.py:108-258).
+ * mode: 0 out = k, 1 out *= k, 2 out += k (kernel products / sums,
+ * basekernel.py:139-155).                                                   */
+#define GG_KERN_RBF 0
+#define GG_KERN_EXPONENTIAL 1
+#define GG_KERN_MATERN32 2
+#define GG_KERN_MATERN52 3
+int gg_cov(int kind, double variance, double lengthscale, int dims, const double* x_dev,
+           int64_t nx, const double* z_dev, int64_t nz, int mode, double* out_dev,
+           gg_stream stream);
+/* Per-dimension tables of expand_SKC (gp_grief/tensors/tensors.py:97-128):
+ * X[u][a] = sum_k qsel[u][k] k(xg[k], x[a * x_stride]); writes
+ * ltab[a*U + col0 + u] = log|X| (0 where X == 0) and stab = sign(X).        */
+int gg_grief_tables(int kind, double variance, double lengthscale, const double* x_dev,
+                    int64_t x_stride, int64_t n, const double* xg_dev, int m,
+                    const double* qsel_dev, int u, double* ltab_dev, double* stab_dev, int U,
+                    int col0, gg_stream stream);
+/* Phi[a][j] = prod_f stab[a][c_jf] * exp(sum_f ltab[a][c_jf] - log_lam[j] / 2)
+ * (GriefKernel.cov, gp_grief/kern/grief_kernel.py:96-104); cidx: p x d int32.
+ * transposed != 0 writes Phi^T (p x n).                                      */
+int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t n,
+                 const int* cidx_dev, int d, const double* log_lam_dev, int p, int transposed,
+                 double* phi_dev, gg_stream stream);
+
+/* ----------------------------------------- dense FP64 (GRIEF p x p system)
+ * C = alpha op(A) op(B) + beta C on FP64 MFMA, row-major with leading dims.
+ * uplo 1/2 writes only the lower/upper triangle.  splitk_dev (optional,
+ * splitk_elems doubles) enables split-K for tall-skinny products such as
+ * A = Phi^T Phi (gp_grief_model.py:149).                                      */
+int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const double* A_dev,
+            int64_t lda, const double* B_dev, int64_t ldb, double beta, double* C_dev,
+            int64_t ldc, int uplo, double* splitk_dev, int64_t splitk_elems, gg_stream stream);
+/* y = alpha op(A) x + beta y, A: rows x cols row-major (Phi^T y, Phi v).    */
+int gg_gemv(int trans, int64_t rows, int cols, double alpha, const double* A_dev, int64_t lda,
+            const double* x_dev, double beta, double* y_dev, double* work_dev,
+            int64_t work_elems, gg_stream stream);
+/* P = A + diag(s / w)  (w NULL -> s), gp_grief_model.py:152                  */
+int gg_add_diag(int n, const double* A_dev, int64_t lda, double s, const double* w_dev,
+                double* P_dev, int64_t ldp, gg_stream stream);
+/* Blocked Cholesky P = L L^T in place (lower), cho_factor, :153.  winv_dev
+ * (gg_potrf_work_elems) receives the inverted diagonal blocks used by
+ * gg_potrs; logdet_host = log det P.  Non-SPD -> GG_ERR_LINALG (synchronising). */
+int gg_potrf_work_elems(int n, int64_t* elems);
+int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet_host,
+             gg_stream stream);
+/* B <- L^-1 B (which=1), L^-T B (2) or P^-1 B (3), B: n x r (cho_solve).
+ * tmp_dev: 64 * r doubles.                                                   */
+int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_dev,
+             double* B_dev, int64_t ldb, int which, double* tmp_dev, gg_stream stream);
+/* out[j] = sum_{i >= j} M[i][j]^2 (diag of P^-1 from M = L^-1).              */
+int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
+                      gg_stream stream);
 
 #ifdef __cplusplus
 }

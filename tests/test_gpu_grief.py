@@ -1,0 +1,213 @@
+"""P2 (GRIEF) parity on the MI355X: covariances, MFMA GEMM, Cholesky, Phi, and
+the GPGriefModel API against the reference-generated fixtures and the oracle."""
+import numpy as np
+import pytest
+
+import oracle
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def gg(gpu):
+    import gp_grief_amd
+    import gp_grief_amd.kern  # noqa: F401
+    import gp_grief_amd.models  # noqa: F401
+    import gp_grief_amd.grid  # noqa: F401
+    return gp_grief_amd
+
+
+# ------------------------------------------------------------------ kernels
+@pytest.mark.parametrize("kind", ["RBF", "Exponential", "Matern32", "Matern52"])
+def test_cov_1d_vs_oracle(gg, kind):
+    rng = np.random.default_rng(0)
+    x = rng.random((37, 1))
+    z = rng.random((23, 1))
+    k = getattr(gg.kern, kind)(1, variance=1.7, lengthscale=0.31)
+    K = k.cov(x, z)
+    assert K.shape == (37, 23)
+    assert rel(K, oracle.cov_1d(kind, x[:, 0], z[:, 0], 1.7, 0.31)) < 1e-14
+    Kxx = k.cov(x)
+    assert np.allclose(Kxx, Kxx.T)
+
+
+def test_cov_multidim_product_and_sum(gg):
+    rng = np.random.default_rng(1)
+    x = rng.random((11, 2))
+    k = gg.kern.RBF(2, variance=2.0, lengthscale=0.5) * gg.kern.Matern52(2, lengthscale=0.7)
+    d2 = ((x[:, None, :] - x[None, :, :]) ** 2).sum(-1)
+    r = np.sqrt(d2) / 0.7
+    ref = 2.0 * np.exp(-0.5 * d2 / 0.25) * (1 + np.sqrt(5) * r + 5.0 / 3 * r ** 2) * \
+        np.exp(-np.sqrt(5) * r)
+    assert rel(k.cov(x), ref) < 1e-13
+    k2 = gg.kern.RBF(2) + gg.kern.Exponential(2)
+    ref2 = np.exp(-0.5 * d2) + np.exp(-np.sqrt(d2))
+    assert rel(k2.cov(x), ref2) < 1e-13
+
+
+# ------------------------------------------------------------------ GEMM / GEMV
+@pytest.mark.parametrize("shape", [(1, 1, 1), (7, 5, 3), (128, 128, 16), (130, 257, 33),
+                                   (300, 40, 5000), (64, 64, 100000)])
+@pytest.mark.parametrize("ta", [False, True])
+@pytest.mark.parametrize("tb", [False, True])
+def test_gemm_vs_numpy(gg, shape, ta, tb):
+    import torch
+    from gp_grief_amd import dense
+    M, N, K = shape
+    rng = np.random.default_rng(M + N + K)
+    A = rng.standard_normal((K, M) if ta else (M, K))
+    B = rng.standard_normal((N, K) if tb else (K, N))
+    C0 = rng.standard_normal((M, N))
+    opA = A.T if ta else A
+    opB = B.T if tb else B
+    Ad, Bd = torch.from_numpy(A).cuda(), torch.from_numpy(B).cuda()
+    C = dense.matmul(Ad, Bd, ta=ta, tb=tb, alpha=0.5, beta=-2.0,
+                     C=torch.from_numpy(C0.copy()).cuda())
+    ref = 0.5 * opA.dot(opB) - 2.0 * C0
+    assert rel(C.cpu().numpy(), ref) < 1e-13
+
+
+def test_gemm_triangle(gg):
+    import torch
+    from gp_grief_amd import dense
+    rng = np.random.default_rng(3)
+    R = rng.standard_normal((500, 300))
+    Rd = torch.from_numpy(R).cuda()
+    C = torch.zeros((300, 300), dtype=torch.float64, device="cuda")
+    dense.matmul(Rd, Rd, ta=True, C=C, beta=0.0, uplo=1)
+    ref = R.T.dot(R)
+    Ch = C.cpu().numpy()
+    assert rel(np.tril(Ch), np.tril(ref)) < 1e-13
+    assert np.all(np.triu(Ch, 1) == 0)
+
+
+@pytest.mark.parametrize("R,C", [(1, 1), (1000, 37), (100000, 300), (33, 5000)])
+def test_gemv(gg, R, C):
+    import torch
+    from gp_grief_amd import dense
+    rng = np.random.default_rng(R + C)
+    A = rng.standard_normal((R, C))
+    x = rng.standard_normal(R)
+    v = rng.standard_normal(C)
+    Ad = torch.from_numpy(A).cuda()
+    yt = dense.matvec(Ad, torch.from_numpy(x).cuda(), trans=True).cpu().numpy()
+    assert rel(yt, A.T.dot(x)) < 1e-13
+    yn = dense.matvec(Ad, torch.from_numpy(v).cuda()).cpu().numpy()
+    assert rel(yn, A.dot(v)) < 1e-13
+
+
+# ------------------------------------------------------------------ Cholesky
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 300, 1000])
+def test_cholesky_solve_logdet(gg, n):
+    import torch
+    from gp_grief_amd import dense
+    rng = np.random.default_rng(n)
+    G = rng.standard_normal((n, n + 10))
+    P = G.dot(G.T) / n + 0.1 * np.eye(n)
+    ch = dense.Cholesky(torch.from_numpy(P).cuda())
+    assert abs(ch.logdet - np.linalg.slogdet(P)[1]) < 1e-10 * max(1, abs(ch.logdet))
+    L = np.tril(ch.L.cpu().numpy())
+    assert rel(L.dot(L.T), P) < 1e-13
+    B = rng.standard_normal((n, 3))
+    X = ch.solve(torch.from_numpy(B).cuda(), which=3).cpu().numpy()
+    assert rel(X, np.linalg.solve(P, B)) < 1e-10
+    b = rng.standard_normal(n)
+    x = ch.solve(torch.from_numpy(b).cuda(), which=3).cpu().numpy()
+    assert rel(x, np.linalg.solve(P, b)) < 1e-10
+    dinv = ch.inverse_diag().cpu().numpy()
+    assert rel(dinv, np.diag(np.linalg.inv(P))) < 1e-10
+
+
+def test_cholesky_not_spd_raises(gg):
+    import torch
+    from gp_grief_amd import dense
+    P = np.eye(70)
+    P[40, 40] = -1.0
+    with pytest.raises(np.linalg.LinAlgError):
+        dense.Cholesky(torch.from_numpy(P).cuda())
+
+
+# ------------------------------------------------------------------ GRIEF model
+def _grief_test_model(gg, z):
+    d = z["x"].shape[1]
+    grid = gg.grid.InducingGrid(z["x"])
+    np.testing.assert_allclose(np.stack([g[:, 0] for g in grid.xg]), z["xg"])
+    kern = gg.kern.RBF(1, lengthscale=0.5)
+    kern = gg.kern.GriefKernel(kern_list=[kern] * d, grid=grid, n_eigs=50)
+    return gg.models.GPGriefModel(z["x"], z["y"].reshape(-1, 1), kern, noise_var=0.1)
+
+
+def test_grief_test_fixture_model(gg):
+    """The reference's own test (test_gp_grief_model.py) with the in-house RBF."""
+    z = golden("grief_test.npz")
+    m = _grief_test_model(gg, z)
+    np.testing.assert_allclose(m.parameters, z["params"])
+    lml = m._compute_log_likelihood(m.parameters)
+    assert lml.shape == (1, 1)
+    assert abs(lml[0, 0] - z["lml"]) < 1e-8 * abs(z["lml"])
+    np.testing.assert_allclose(m.kern._log_lam, z["log_lam"], rtol=1e-10, atol=1e-12)
+    Kd = m._mv_cov(np.identity(z["x"].shape[0]))
+    assert rel(Kd, z["cov_dense"]) < 1e-10
+    alp = m._mv_cov_inv(z["y"].reshape(-1, 1))
+    assert rel(alp, z["alpha"]) < 1e-8
+    assert rel(alp, np.linalg.solve(Kd, z["y"])) < 1e-6
+    assert abs(m._cov_log_det() - z["logdet"]) < 1e-8 * abs(z["logdet"])
+    ll, grad = m.log_likelihood(return_gradient=True)
+    g = z["grad"]
+    free = ~np.isnan(g)
+    np.testing.assert_array_equal(np.isnan(grad), np.isnan(g))
+    np.testing.assert_allclose(grad[free], g[free], rtol=1e-6, atol=1e-9)
+    mean, var = m.predict(z["x"][:7])
+    assert rel(mean[:, 0], z["pred_mean"]) < 1e-8
+    assert rel(var, z["pred_var"]) < 1e-8
+    Phi = m.kern.cov(z["x"])[0]
+    assert rel(np.abs(Phi), np.abs(z["phi_signnorm"])) < 1e-9
+
+
+@pytest.mark.parametrize("case", ["3d", "6d", "8d"])
+def test_grief_small_fixtures_model(gg, case):
+    z = golden("grief_small_%s.npz" % case)
+    d = z["x"].shape[1]
+    kind = str(z["kind"])
+    kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=float(l)) for l in z["lengthscales"]]
+    grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, int(z["m"])).reshape(-1, 1)
+                                    for _ in range(d)])
+    kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=int(z["p"]))
+    m = gg.models.GPGriefModel(z["x"], z["y"].reshape(-1, 1), kern, noise_var=float(z["sigma2"]))
+    ll, grad = m.log_likelihood(return_gradient=True)
+    # north-star bar: LML, posterior mean and variance to 1e-6 relative
+    assert abs(ll[0, 0] - z["lml"]) < 1e-6 * abs(z["lml"])
+    np.testing.assert_allclose(m.kern._log_lam, z["log_lam"], rtol=1e-9, atol=1e-10)
+    mean, var = m.predict(z["xtest"])
+    assert rel(mean[:, 0], z["pred_mean"]) < 1e-6
+    assert rel(var, z["pred_var"]) < 1e-6
+    assert rel(grad[-int(z["p"]):], z["grad"][-int(z["p"]):]) < 1e-6
+    assert abs(grad[0] - z["grad"][0]) < 1e-6 * abs(z["grad"][0])
+
+
+def test_automobile_optimize(gg):
+    """Type-II tutorial case: L-BFGS with finite-difference gradients over the
+    device LML; parameters, LML and test RMSE after 5 iterations."""
+    z = golden("automobile.npz")
+    x, y, itr = z["x"], z["y"].reshape(-1, 1), z["i_train"]
+    grid = gg.grid.InducingGrid(x=x)
+    np.testing.assert_allclose(np.concatenate([g[:, 0] for g in grid.xg]), z["xg_cat"])
+    kern = gg.kern.GriefKernel(kern_list=[gg.kern.RBF(1, lengthscale=1.0)] * x.shape[1],
+                               grid=grid, n_eigs=100, reweight_eig_funs=False,
+                               opt_kernel_params=True)
+    m = gg.models.GPGriefModel(X=x[itr], Y=y[itr], kern=kern, noise_var=1.0)
+    np.testing.assert_allclose(m.parameters, z["params0"])
+    assert abs(float(np.squeeze(m.log_likelihood())) - z["lml0"]) < 1e-8 * abs(z["lml0"])
+    m.optimize(max_iters=5)
+    np.testing.assert_allclose(m.parameters, z["params_opt"], rtol=1e-4)
+    assert abs(float(np.squeeze(m.log_likelihood())) - z["lml_opt"]) < 1e-5 * abs(z["lml_opt"])
+    mean, var = m.predict(Xnew=x[~itr])
+    rmse = np.linalg.norm((mean[:, 0] - y[~itr, 0]) * z["y_scale"]) / np.sqrt(mean.size)
+    assert abs(rmse - z["rmse"]) < 1e-4 * z["rmse"]
