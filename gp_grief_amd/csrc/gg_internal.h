@@ -79,6 +79,12 @@ struct CgScalars {
   int pad;
 };
 
+// Fused CG direction update for the first mode product (gg_kron.hip).
+struct CgPrologue {
+  const double* r;
+  const CgScalars* sc;
+};
+
 // Reduction partial-buffer length used by grid-stride vector kernels.
 constexpr int kVecBlocks = 2048;
 constexpr int kVecThreads = 256;

@@ -45,12 +45,18 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 //   write the staged registers into LDS buffer (c+1)&1 ; barrier
 // so the L2 latency of the factor fragments and the HBM latency of X hide
 // under 8*JT MFMAs (64 cycles each) per wave.
-template <int JT, int kWaves, int kKC>
-__global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
-    const double* __restrict__ X, double* __restrict__ Y, const double* __restrict__ Bf,
+//
+// CGP = true fuses CG's direction update into the first mode product: the A
+// operand is p_new = beta * p + r (p_new = r on the first iteration, selected,
+// so an uninitialised p never leaks in), written back in place; each element
+// is read and written by exactly one lane.
+template <int JT, int kWaves, int kKC, bool CGP, int kMinW>
+__global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
+    const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
-    const int* __restrict__ skip) {
+    const int* __restrict__ skip, const double* __restrict__ R,
+    const CgScalars* __restrict__ sc, double* Pout) {
   if (skip != nullptr && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JT * 64
   constexpr int kThreads = kWaves * 64;
@@ -94,20 +100,27 @@ __global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
 // A fragments: unconditional loads from a clamped (always valid) address; the
 // mask (rows past q, strips past M) is applied when the registers are consumed,
 // so no load is followed by a wait.
-#define GG_A_LOAD(c, a)                                                               \
+#define GG_A_LOAD(c, a, rr)                                                           \
   do {                                                                                \
     const int ks0_ = (c) * kKC;                                                       \
     _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
       const int k_ = min((ks0_ + s_) * 4 + krow, q - 1);                              \
       a[s_] = X[(int64_t)k_ * M + bclamp];                                            \
+      if (CGP) rr[s_] = R[(int64_t)k_ * M + bclamp];                                  \
     }                                                                                 \
   } while (0)
-#define GG_A_MASK(c, a)                                                               \
+#define GG_A_MASK(c, a, rr)                                                           \
   do {                                                                                \
     const int ks0_ = (c) * kKC;                                                       \
     _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
       const int k_ = (ks0_ + s_) * 4 + krow;                                          \
-      a[s_] = (bvalid && k_ < q) ? a[s_] : 0.0;                                       \
+      const bool ok_ = bvalid && k_ < q;                                              \
+      double v_ = a[s_];                                                              \
+      if (CGP) {                                                                      \
+        v_ = cg_first ? rr[s_] : fma(cg_beta, v_, rr[s_]);                            \
+        if (ok_) Pout[(int64_t)k_ * M + brow] = v_;                                   \
+      }                                                                               \
+      a[s_] = ok_ ? v_ : 0.0;                                                         \
     }                                                                                 \
   } while (0)
 
@@ -115,19 +128,25 @@ __global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
 #pragma unroll
   for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 
-  double a_cur[kKC], a_nxt[kKC];
+  double a_cur[kKC], a_nxt[kKC], r_cur[kKC], r_nxt[kKC];
   double stx[kPerT], sty[kPerT];
+  bool cg_first = false;
+  double cg_beta = 0.0;
+  if (CGP) {
+    cg_first = sc->first != 0;
+    cg_beta = sc->beta;
+  }
   GG_STAGE_LOAD(0, st);
-  GG_A_LOAD(0, a_cur);
+  GG_A_LOAD(0, a_cur, r_cur);
   GG_STAGE_STORE(0, st);
-  GG_A_MASK(0, a_cur);
+  GG_A_MASK(0, a_cur, r_cur);
   __syncthreads();
 
   for (int c = 0; c < nchunks; ++c) {
     const bool more = c + 1 < nchunks;
     if (more) {
       GG_STAGE_LOAD(c + 1, st);
-      GG_A_LOAD(c + 1, a_nxt);
+      GG_A_LOAD(c + 1, a_nxt, r_nxt);
     }
     const int kcn = min(kKC, KS - c * kKC);
     const double* buf = lds + (c & 1) * kBuf;
@@ -144,8 +163,11 @@ __global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
     if (more) {
       GG_STAGE_STORE(c + 1, st);
 #pragma unroll
-      for (int s = 0; s < kKC; ++s) a_cur[s] = a_nxt[s];
-      GG_A_MASK(c + 1, a_cur);
+      for (int s = 0; s < kKC; ++s) {
+        a_cur[s] = a_nxt[s];
+        if (CGP) r_cur[s] = r_nxt[s];
+      }
+      GG_A_MASK(c + 1, a_cur, r_cur);
     }
     __syncthreads();
   }
@@ -214,7 +236,8 @@ __global__ __launch_bounds__(kWaves * 64, 2) void mode_product_kernel(
 }
 
 typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
-                              int, int, const double*, double, double*, const int*);
+                              int, int, const double*, double, double*, const int*,
+                              const double*, const CgScalars*, double*);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
 // LDS chunk.  The default (8 waves, KC 8, one workgroup per CU) was chosen by
@@ -224,45 +247,48 @@ struct ModeConfig {
   int waves, kc;
 };
 
-template <int JT, int W, int KC>
+template <int JT, int W, int KC, bool CGP, int MINW>
 static ModeConfig cfg() {
-  return ModeConfig{mode_product_kernel<JT, W, KC>, W, KC};
+  return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW>, W, KC};
 }
 
-template <int JT>
+// variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
+template <int JT, bool CGP>
 static ModeConfig config_for(int variant) {
   switch (variant) {
-    case 1: return cfg<JT, 4, 4>();
-    case 2: return cfg<JT, 4, 8>();
-    case 3: return cfg<JT, 8, 4>();
-    case 4: return cfg<JT, 8, 10>();
-    default: return cfg<JT, 8, 8>();
+    case 1: return cfg<JT, 8, 4, CGP, 2>();
+    case 2: return cfg<JT, 6, 4, CGP, 3>();
+    case 3: return cfg<JT, 4, 4, CGP, 3>();
+    case 4: return cfg<JT, 12, 2, CGP, 3>();
+    case 5: return cfg<JT, 12, 6, CGP, 3>();
+    default: return cfg<JT, 12, 4, CGP, 3>();
   }
 }
+constexpr int kNumVariants = 6;
 
 static int mode_variant() {
   const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
   return e ? atoi(e) : 0;
 }
 
-static ModeConfig select_kernel(int jt, int variant) {
+static ModeConfig select_kernel(int jt, int variant, bool cgp) {
   switch (jt) {
-    case 1: return config_for<1>(variant);
-    case 2: return config_for<2>(variant);
-    case 3: return config_for<3>(variant);
-    case 4: return config_for<4>(variant);
-    case 5: return config_for<5>(variant);
-    case 6: return config_for<6>(variant);
-    case 7: return config_for<7>(variant);
-    case 8: return config_for<8>(variant);
-    case 9: return config_for<9>(variant);
-    case 10: return config_for<10>(variant);
-    case 11: return config_for<11>(variant);
-    case 12: return config_for<12>(variant);
-    case 13: return config_for<13>(variant);
-    case 14: return config_for<14>(variant);
-    case 15: return config_for<15>(variant);
-    case 16: return config_for<16>(variant);
+    case 1: return cgp ? config_for<1, true>(variant) : config_for<1, false>(variant);
+    case 2: return cgp ? config_for<2, true>(variant) : config_for<2, false>(variant);
+    case 3: return cgp ? config_for<3, true>(variant) : config_for<3, false>(variant);
+    case 4: return cgp ? config_for<4, true>(variant) : config_for<4, false>(variant);
+    case 5: return cgp ? config_for<5, true>(variant) : config_for<5, false>(variant);
+    case 6: return cgp ? config_for<6, true>(variant) : config_for<6, false>(variant);
+    case 7: return cgp ? config_for<7, true>(variant) : config_for<7, false>(variant);
+    case 8: return cgp ? config_for<8, true>(variant) : config_for<8, false>(variant);
+    case 9: return cgp ? config_for<9, true>(variant) : config_for<9, false>(variant);
+    case 10: return cgp ? config_for<10, true>(variant) : config_for<10, false>(variant);
+    case 11: return cgp ? config_for<11, true>(variant) : config_for<11, false>(variant);
+    case 12: return cgp ? config_for<12, true>(variant) : config_for<12, false>(variant);
+    case 13: return cgp ? config_for<13, true>(variant) : config_for<13, false>(variant);
+    case 14: return cgp ? config_for<14, true>(variant) : config_for<14, false>(variant);
+    case 15: return cgp ? config_for<15, true>(variant) : config_for<15, false>(variant);
+    case 16: return cgp ? config_for<16, true>(variant) : config_for<16, false>(variant);
     default: throw Error(GG_ERR_VALUE, "bad tile count");
   }
 }
@@ -325,7 +351,7 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
 
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out) {
+                int64_t* n_partials_out, const CgPrologue* pro) {
   const std::vector<Factor>& fs = transpose ? K->bwd : K->fwd;
   const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
   const int64_t n_in = transpose ? K->n_rows : K->n_cols;
@@ -354,7 +380,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
     if (M > 0) {
       for (int jt0 = 0; jt0 < f.JT; jt0 += kMaxJT) {
         const int jt = std::min(kMaxJT, f.JT - jt0);
-        const ModeConfig mc = select_kernel(jt, variant);
+        // the fused CG direction update runs once, in the first launch of step 0
+        const bool cgp = pro != nullptr && k == 0 && jt0 == 0;
+        const ModeConfig mc = select_kernel(jt, variant, cgp);
         const int64_t nblk = ceil_div(M, (int64_t)mc.waves * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         double* parts = nullptr;
@@ -365,7 +393,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)nblk), dim3(mc.waves * 64),
                            mode_lds_bytes(jt, mc), stream, src, dst, f.frag, M, (int)f.q,
                            (int)f.p, f.KS, f.JT, jt0,
-                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip);
+                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip,
+                           cgp ? pro->r : nullptr, cgp ? pro->sc : nullptr,
+                           cgp ? const_cast<double*>(x) : nullptr);
         GG_LAUNCH_CHECK();
       }
     }
@@ -398,13 +428,14 @@ int64_t kron_n(const gg_kron* K) { return K->n_rows; }
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
-  for (int v = 0; v <= 4; ++v)
-    for (int jt = 1; jt <= kMaxJT; ++jt) {
-      const ModeConfig mc = select_kernel(jt, v);
-      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)mode_lds_bytes(jt, mc)));
-    }
+  for (int v = 0; v < kNumVariants; ++v)
+    for (int jt = 1; jt <= kMaxJT; ++jt)
+      for (int cgp = 0; cgp < 2; ++cgp) {
+        const ModeConfig mc = select_kernel(jt, v, cgp != 0);
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)mode_lds_bytes(jt, mc)));
+      }
   done = true;
 }
 
@@ -470,7 +501,7 @@ int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double*
     GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
     GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
     gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
-                   gg::as_stream(stream), nullptr);
+                   gg::as_stream(stream), nullptr, nullptr);
   });
 }
 

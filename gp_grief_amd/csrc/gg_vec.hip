@@ -16,7 +16,7 @@ namespace gg {
 // defined in gg_kron.hip
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out);
+                int64_t* n_partials_out, const CgPrologue* pro);
 int64_t kron_partials_needed(const gg_kron* K, bool transpose);
 int64_t kron_work_elems(const gg_kron* K, bool transpose);
 int64_t kron_n(const gg_kron* K);
@@ -98,29 +98,7 @@ __global__ __launch_bounds__(kVecThreads) void axpby_kernel(double a, const doub
 }
 
 // ------------------------------------------------------------------ CG kernels
-// p = r (first iteration) or p = beta * p + r   (scipy: p *= beta; p += z)
-__global__ __launch_bounds__(kVecThreads) void cg_p_update_kernel(
-    const double* __restrict__ r, double* __restrict__ p, int64_t n,
-    const CgScalars* __restrict__ sc) {
-  if (sc->done) return;
-  const bool first = sc->first != 0;
-  const double beta = sc->beta;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t n2 = n / 2;
-  const double2* r2 = reinterpret_cast<const double2*>(r);
-  double2* p2 = reinterpret_cast<double2*>(p);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
-    const double2 rv = r2[i];
-    if (first) {
-      p2[i] = rv;
-    } else {
-      const double2 pv = p2[i];
-      p2[i] = double2{beta * pv.x + rv.x, beta * pv.y + rv.y};
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1))
-    p[n - 1] = first ? r[n - 1] : beta * p[n - 1] + r[n - 1];
-}
+// (p = beta p + r is fused into the first mode product, gg_kron.hip)
 
 // alpha = rho / (p.q)
 __global__ __launch_bounds__(1024) void cg_alpha_kernel(const double* __restrict__ partials,
@@ -571,13 +549,12 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
     const int64_t n = cg->n;
     const int nb = gg::vec_blocks(n);
     if (check_every <= 0) check_every = max_iters;
+    const gg::CgPrologue pro{cg->r, cg->sc};
     for (int it = 0; it < max_iters; ++it) {
-      hipLaunchKernelGGL(gg::cg_p_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->r,
-                         cg->p, n, cg->sc);
-      GG_LAUNCH_CHECK();
+      // p = r + beta p is fused into the first mode product of q = (K + s I) p
       int64_t nparts = 0;
       gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
-                     &cg->sc->done, s, &nparts);
+                     &cg->sc->done, s, &nparts, &pro);
       hipLaunchKernelGGL(gg::cg_alpha_kernel, dim3(1), dim3(1024), 0, s, cg->partials, nparts,
                          cg->sc);
       GG_LAUNCH_CHECK();
@@ -642,7 +619,7 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
     for (int j = 0; j < steps; ++j) {
-      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr);
+      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr);
       const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
       hipLaunchKernelGGL(gg::lz_axpy_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P,
                          V, n, beta_prev, parts);
