@@ -85,6 +85,15 @@ struct CgPrologue {
   const CgScalars* sc;
 };
 
+// Output address map of a mode product (see gg_kron.hip epilogue):
+//   addr = (j / cg) * gs + (j % cg) + h * hs + a * as + br * cg,
+//   a = row / mi, h = (row % mi) / cr, br = (row % mi) % cr.
+struct OutMap {
+  int identity;
+  int64_t cg, gs, mi, cr, hs, as;
+  static OutMap ident() { return OutMap{1, 1, 0, 1, 1, 0, 0}; }
+};
+
 // Reduction partial-buffer length used by grid-stride vector kernels.
 constexpr int kVecBlocks = 2048;
 constexpr int kVecThreads = 256;

@@ -50,13 +50,13 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 // operand is p_new = beta * p + r (p_new = r on the first iteration, selected,
 // so an uninitialised p never leaks in), written back in place; each element
 // is read and written by exactly one lane.
-template <int JT, int kWaves, int kKC, bool CGP, int kMinW>
+template <int JT, int kWaves, int kKC, bool CGP, int kMinW, bool kIdent>
 __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
     const int* __restrict__ skip, const double* __restrict__ R,
-    const CgScalars* __restrict__ sc, double* Pout) {
+    const CgScalars* __restrict__ sc, double* Pout, OutMap om) {
   if (skip != nullptr && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JT * 64
   constexpr int kThreads = kWaves * 64;
@@ -172,19 +172,42 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     __syncthreads();
   }
 
-  // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4)
+  // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
+  // Output address = rowoff(row) + coloff(j): the identity map is row * p + j;
+  // the distributed matvec permutes rows / columns into all-to-all order
+  // (OutMap, gg_dist.hip).  Offsets are decomposed once per row and column.
   const int col = lane & 15;
   const int64_t rbase = b0 + (lane >> 4);
+  int64_t rowoff[4];
+  bool rowok[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = rbase + 4 * r;
+    rowok[r] = row < M;
+    if (kIdent) {
+      rowoff[r] = row * p;
+    } else {
+      const int64_t a_ = row / om.mi, bi = row - a_ * om.mi;
+      const int64_t h = bi / om.cr, br = bi - h * om.cr;
+      rowoff[r] = h * om.hs + a_ * om.as + br * om.cg;
+    }
+  }
+  auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + t) * 16 + col; };
+  auto coloff = [&](int t) -> int64_t {
+    const int64_t j = colj(t);
+    if (kIdent) return j;
+    const int64_t jg = j / om.cg;
+    return jg * om.gs + (j - jg * om.cg);
+  };
   double dsum = 0.0;
   if (xs == nullptr) {
 #pragma unroll
     for (int t = 0; t < JT; ++t) {
-      const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+      const bool cok = colj(t) < p;
+      const int64_t co = coloff(t);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = rbase + 4 * r;
-        if (row < M && j < p) Y[row * p + j] = acc[t][r];
-      }
+      for (int r = 0; r < 4; ++r)
+        if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
     }
   } else {
     // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
@@ -194,26 +217,24 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       double xv[kEpiBatch][4];
 #pragma unroll
       for (int tb = 0; tb < kEpiBatch; ++tb) {
-        const int t = t0 + tb;
-        const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+        const int t = t0 + tb < JT ? t0 + tb : JT - 1;
+        const bool cok = t0 + tb < JT && colj(t) < p;
+        const int64_t co = coloff(t);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = rbase + 4 * r;
-          xv[tb][r] = (t < JT && row < M && j < p) ? xs[row * p + j] : 0.0;
-        }
+        for (int r = 0; r < 4; ++r) xv[tb][r] = (rowok[r] && cok) ? xs[rowoff[r] + co] : 0.0;
       }
 #pragma unroll
       for (int tb = 0; tb < kEpiBatch; ++tb) {
         const int t = t0 + tb;
         if (t < JT) {
-          const int64_t j = (int64_t)(jt0 + t) * 16 + col;
+          const bool cok = colj(t) < p;
+          const int64_t co = coloff(t);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int64_t row = rbase + 4 * r;
-            if (row < M && j < p) {
+            if (rowok[r] && cok) {
               const double v = fma(shift, xv[tb][r], acc[t][r]);
               dsum = fma(xv[tb][r], v, dsum);
-              Y[row * p + j] = v;
+              Y[rowoff[r] + co] = v;
             }
           }
         }
@@ -237,7 +258,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 
 typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
                               int, int, const double*, double, double*, const int*,
-                              const double*, const CgScalars*, double*);
+                              const double*, const CgScalars*, double*, OutMap);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
 // LDS chunk.  The default (8 waves, KC 8, one workgroup per CU) was chosen by
@@ -249,7 +270,7 @@ struct ModeConfig {
 
 template <int JT, int W, int KC, bool CGP, int MINW>
 static ModeConfig cfg() {
-  return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW>, W, KC};
+  return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW, true>, W, KC};
 }
 
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
@@ -395,7 +416,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
                            (int)f.p, f.KS, f.JT, jt0,
                            last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip,
                            cgp ? pro->r : nullptr, cgp ? pro->sc : nullptr,
-                           cgp ? const_cast<double*>(x) : nullptr);
+                           cgp ? const_cast<double*>(x) : nullptr, OutMap::ident());
         GG_LAUNCH_CHECK();
       }
     }
@@ -502,6 +523,187 @@ int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double*
     GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
     gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
                    gg::as_stream(stream), nullptr, nullptr);
+  });
+}
+
+}  // extern "C"
+
+// ===================================================================== P1 sharded
+// The Kronecker operator sharded over G ranks along factor 0 (the slowest
+// axis), one process per GPU; the exchange steps are the caller's RCCL
+// all-to-alls (gp_grief_amd/distributed.py).  Local layout of a sharded
+// vector: (m_1, ..., m_{d-1}, a) C-order with a = i_0 - rank * s0 fastest,
+// s0 = m_0 / G.  A matvec is
+//   phase 1  local mode products for factors 1..d-1 (the slab axis rides along
+//            in M); the first one may fuse CG's p = r + beta p; the last one
+//            writes its rows in all-to-all chunk order;
+//   exchange #1 (N/G^2 per peer)  -> recv = (m_0, R/G) row-major, R = N/m_0;
+//   phase 2  mode product for factor 0, columns grouped by destination rank;
+//   exchange #2                    -> the result in the input layout.
+// Every mode product is the same MFMA kernel as the single-GPU path.
+
+struct gg_kron_dist {
+  int d = 0, world = 1, rank = 0;
+  std::vector<int64_t> m;
+  std::vector<gg::Factor> f;
+  int64_t n = 1, n_local = 1, s0 = 1;
+};
+
+namespace gg {
+
+template <int JT>
+static mode_kernel_t dist_kernel(bool cgp, bool ident) {
+  if (cgp) return mode_product_kernel<JT, 12, 4, true, 3, true>;
+  if (ident) return mode_product_kernel<JT, 12, 4, false, 3, true>;
+  return mode_product_kernel<JT, 12, 4, false, 3, false>;
+}
+
+static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {
+  switch (jt) {
+    case 1: return dist_kernel<1>(cgp, ident);
+    case 2: return dist_kernel<2>(cgp, ident);
+    case 3: return dist_kernel<3>(cgp, ident);
+    case 4: return dist_kernel<4>(cgp, ident);
+    case 5: return dist_kernel<5>(cgp, ident);
+    case 6: return dist_kernel<6>(cgp, ident);
+    case 7: return dist_kernel<7>(cgp, ident);
+    case 8: return dist_kernel<8>(cgp, ident);
+    case 9: return dist_kernel<9>(cgp, ident);
+    case 10: return dist_kernel<10>(cgp, ident);
+    case 11: return dist_kernel<11>(cgp, ident);
+    case 12: return dist_kernel<12>(cgp, ident);
+    case 13: return dist_kernel<13>(cgp, ident);
+    case 14: return dist_kernel<14>(cgp, ident);
+    case 15: return dist_kernel<15>(cgp, ident);
+    case 16: return dist_kernel<16>(cgp, ident);
+    default: throw Error(GG_ERR_VALUE, "bad tile count");
+  }
+}
+
+constexpr int kDistWaves = 12, kDistKC = 4;
+
+static void dist_step(const Factor& f, const double* X, double* Y, int64_t M, OutMap om,
+                      const CgPrologue* pro, double* pin, hipStream_t s) {
+  if (M <= 0) return;
+  GG_REQUIRE(f.JT <= kMaxJT, GG_ERR_VALUE, "sharded operator supports factors up to 256");
+  const bool cgp = pro != nullptr;
+  mode_kernel_t fn = select_dist(f.JT, cgp, om.identity != 0);
+  static bool attr[2][2][kMaxJT + 1] = {};
+  bool& done = attr[cgp][om.identity != 0][f.JT];
+  const size_t lds = 2 * (size_t)kDistKC * f.JT * 64 * sizeof(double);
+  if (!done) {
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    done = true;
+  }
+  const int64_t nblk = ceil_div(M, (int64_t)kDistWaves * 16);
+  hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kDistWaves * 64), lds, s, X, Y, f.frag, M,
+                     (int)f.q, (int)f.p, f.KS, f.JT, 0, nullptr, 0.0, nullptr,
+                     cgp ? &pro->sc->done : nullptr, cgp ? pro->r : nullptr,
+                     cgp ? pro->sc : nullptr, cgp ? pin : nullptr, om);
+  GG_LAUNCH_CHECK();
+}
+
+}  // namespace gg
+
+extern "C" {
+
+int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_host, int world,
+                        int rank, gg_kron_dist** out) {
+  return gg::guard([&] {
+    GG_REQUIRE(out && m && factors_host, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(d >= 2, GG_ERR_VALUE, "the sharded operator needs d >= 2 factors");
+    GG_REQUIRE(world >= 1 && rank >= 0 && rank < world, GG_ERR_VALUE, "bad rank / world");
+    GG_REQUIRE(m[0] % world == 0, GG_ERR_VALUE, "world size must divide the factor-0 size");
+    GG_REQUIRE(m[1] % world == 0, GG_ERR_VALUE, "world size must divide the factor-1 size");
+    gg::set_lds_limits();
+    gg_kron_dist* D = new gg_kron_dist();
+    try {
+      D->d = d;
+      D->world = world;
+      D->rank = rank;
+      D->m.assign(m, m + d);
+      D->f.resize(d);
+      for (int k = 0; k < d; ++k) {
+        GG_REQUIRE(m[k] >= 1 && m[k] <= 256, GG_ERR_VALUE, "factor size must be in [1, 256]");
+        gg::pack_fragments(factors_host[k], m[k], m[k], false, D->f[k]);
+        D->n *= m[k];
+      }
+      D->n_local = D->n / world;
+      D->s0 = m[0] / world;
+    } catch (...) {
+      gg_kron_dist_destroy(D);
+      throw;
+    }
+    *out = D;
+  });
+}
+
+int gg_kron_dist_destroy(gg_kron_dist* D) {
+  return gg::guard([&] {
+    if (!D) return;
+    for (gg::Factor& f : D->f)
+      if (f.frag) (void)hipFree(f.frag);
+    delete D;
+  });
+}
+
+int gg_kron_dist_sizes(const gg_kron_dist* D, int64_t* n_local, int64_t* work_elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(D, GG_ERR_VALUE, "NULL handle");
+    if (n_local) *n_local = D->n_local;
+    if (work_elems) *work_elems = D->n_local;
+  });
+}
+
+int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
+                        double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
+                        gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && x_local_dev && send_dev && work_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE((cg_r_dev == nullptr) == (cg_scalars_dev == nullptr), GG_ERR_VALUE,
+               "CG fusion needs both r and the scalars");
+    hipStream_t s = gg::as_stream(stream);
+    const int d = D->d;
+    const int G = D->world;
+    const gg::CgPrologue pro{cg_r_dev, reinterpret_cast<const gg::CgScalars*>(cg_scalars_dev)};
+    const int64_t nl = D->n_local;
+    const double* src = x_local_dev;
+    for (int k = 1; k < d; ++k) {
+      const gg::Factor& f = D->f[k];
+      const int64_t M = nl / f.q;
+      const bool last = (k == d - 1);
+      gg::OutMap om = gg::OutMap::ident();
+      double* dst;
+      if (last) {
+        dst = send_dev;
+        if (d == 2) {  // rows = slab index, columns j1 grouped by destination
+          const int64_t cg = f.p / G;
+          om = gg::OutMap{0, cg, D->s0 * cg, 1, 1, 0, cg};
+        } else {       // rows = (a, j1..j_{d-2}); chunk by j1
+          const int64_t mi = M / D->s0;
+          const int64_t cr = mi / G;
+          om = gg::OutMap{0, f.p, 0, mi, cr, D->s0 * cr * f.p, cr * f.p};
+        }
+      } else {
+        // alternate work / send so that the last local step lands in send
+        dst = ((d - 1 - k) % 2 == 0) ? send_dev : work_dev;
+      }
+      const bool fuse = (k == 1) && cg_r_dev != nullptr;
+      gg::dist_step(f, src, dst, M, om, fuse ? &pro : nullptr, x_local_dev, s);
+      src = dst;
+    }
+  });
+}
+
+int gg_kron_dist_phase2(const gg_kron_dist* D, const double* recv_dev, double* send_dev,
+                        gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && recv_dev && send_dev && recv_dev != send_dev, GG_ERR_VALUE, "bad argument");
+    const gg::Factor& f = D->f[0];
+    const int64_t C = D->n_local / f.q;  // = R / G
+    const gg::OutMap om{0, D->s0, C * D->s0, C, C, 0, 0};
+    gg::dist_step(f, recv_dev, send_dev, C, om, nullptr, nullptr, gg::as_stream(stream));
   });
 }
 

@@ -654,3 +654,180 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
 }
 
 }  // extern "C"
+
+// ============================================ CG scalars for a host-driven (sharded) CG
+// The sharded solve (gp_grief_amd/distributed.py) runs the same recurrence as
+// gg_cg_*: local partial dots land in device doubles, the caller all-reduces
+// them with RCCL, and these kernels consume the global values.
+namespace gg {
+
+__global__ __launch_bounds__(kVecThreads) void shift_dot_kernel(double* __restrict__ q,
+                                                                const double* __restrict__ p,
+                                                                int64_t n, double shift,
+                                                                const CgScalars* __restrict__ sc,
+                                                                double* __restrict__ partials) {
+  if (sc->done) return;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double pv = p[i];
+    const double v = fma(shift, pv, q[i]);
+    q[i] = v;
+    acc = fma(pv, v, acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ void cgs_init_kernel(CgScalars* sc, const double* rr, double rtol, double atol) {
+  const double s = *rr;
+  sc->rho = s;
+  sc->rho_prev = 0.0;
+  sc->bnorm = sqrt(s);
+  sc->tol = fmax(atol, rtol * sc->bnorm);
+  sc->iters = 0;
+  sc->first = 1;
+  sc->alpha = sc->beta = sc->pq = 0.0;
+  sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
+}
+
+__global__ void cgs_alpha_kernel(CgScalars* sc, const double* pq) {
+  if (sc->done) return;
+  sc->pq = *pq;
+  sc->alpha = sc->rho / *pq;
+}
+
+__global__ void cgs_rho_kernel(CgScalars* sc, const double* rr) {
+  if (sc->done) return;
+  const double s = *rr;
+  sc->rho_prev = sc->rho;
+  sc->rho = s;
+  sc->beta = s / sc->rho_prev;
+  sc->iters += 1;
+  sc->first = 0;
+  if (!(sqrt(s) >= sc->tol)) sc->done = 1;
+}
+
+}  // namespace gg
+
+struct gg_cgs {
+  gg::CgScalars* sc = nullptr;
+  gg::CgScalars* host = nullptr;
+  double* partials = nullptr;
+};
+
+extern "C" {
+
+int gg_cgs_create(gg_cgs** out) {
+  return gg::guard([&] {
+    GG_REQUIRE(out, GG_ERR_VALUE, "NULL argument");
+    gg_cgs* c = new gg_cgs();
+    try {
+      GG_HIP(hipMalloc(&c->sc, sizeof(gg::CgScalars)));
+      GG_HIP(hipMemset(c->sc, 0, sizeof(gg::CgScalars)));
+      GG_HIP(hipHostMalloc(&c->host, sizeof(gg::CgScalars), hipHostMallocDefault));
+      GG_HIP(hipMalloc(&c->partials, gg::kVecBlocks * sizeof(double)));
+    } catch (...) {
+      gg_cgs_destroy(c);
+      throw;
+    }
+    *out = c;
+  });
+}
+
+int gg_cgs_destroy(gg_cgs* c) {
+  return gg::guard([&] {
+    if (!c) return;
+    if (c->sc) (void)hipFree(c->sc);
+    if (c->host) (void)hipHostFree(c->host);
+    if (c->partials) (void)hipFree(c->partials);
+    delete c;
+  });
+}
+
+int gg_cgs_scalars(gg_cgs* c, void** scalars_dev) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && scalars_dev, GG_ERR_VALUE, "NULL argument");
+    *scalars_dev = c->sc;
+  });
+}
+
+int gg_cgs_local_dot(gg_cgs* c, const double* x_dev, const double* y_dev, int64_t n,
+                     double* out_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && x_dev && y_dev && out_dev, GG_ERR_VALUE, "NULL argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nb = gg::vec_blocks(n);
+    gg::launch_dot_partials(x_dev, y_dev, n, c->partials, nb, s);
+    gg::launch_reduce_to(c->partials, nb, out_dev, s);
+  });
+}
+
+int gg_cgs_init(gg_cgs* c, const double* rr_dev, double rtol, double atol, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && rr_dev && rtol >= 0 && atol >= 0, GG_ERR_VALUE, "bad argument");
+    hipLaunchKernelGGL(gg::cgs_init_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream), c->sc,
+                       rr_dev, rtol, atol);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_shift_dot(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, double shift,
+                     double* out_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && q_dev && p_dev && out_dev, GG_ERR_VALUE, "NULL argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nb = gg::vec_blocks(n);
+    hipLaunchKernelGGL(gg::shift_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, q_dev,
+                       p_dev, n, shift, c->sc, c->partials);
+    GG_LAUNCH_CHECK();
+    gg::launch_reduce_to(c->partials, nb, out_dev, s);
+  });
+}
+
+int gg_cgs_alpha(gg_cgs* c, const double* pq_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && pq_dev, GG_ERR_VALUE, "NULL argument");
+    hipLaunchKernelGGL(gg::cgs_alpha_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream), c->sc,
+                       pq_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_update(gg_cgs* c, double* x_dev, double* r_dev, const double* p_dev,
+                  const double* q_dev, int64_t n, double* out_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && x_dev && r_dev && p_dev && q_dev && out_dev, GG_ERR_VALUE, "NULL argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nb = gg::vec_blocks(n);
+    hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, x_dev,
+                       r_dev, p_dev, q_dev, n, c->sc, c->partials);
+    GG_LAUNCH_CHECK();
+    gg::launch_reduce_to(c->partials, nb, out_dev, s);
+  });
+}
+
+int gg_cgs_rho(gg_cgs* c, const double* rr_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && rr_dev, GG_ERR_VALUE, "NULL argument");
+    hipLaunchKernelGGL(gg::cgs_rho_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream), c->sc,
+                       rr_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_status(gg_cgs* c, int* iters, int* done, double* rho, double* tol,
+                  gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c, GG_ERR_VALUE, "NULL handle");
+    hipStream_t s = gg::as_stream(stream);
+    GG_HIP(hipMemcpyAsync(c->host, c->sc, sizeof(gg::CgScalars), hipMemcpyDeviceToHost, s));
+    GG_HIP(hipStreamSynchronize(s));
+    if (iters) *iters = c->host->iters;
+    if (done) *done = c->host->done;
+    if (rho) *rho = c->host->rho;
+    if (tol) *tol = c->host->tol;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,226 @@
+"""P1 across GPUs: the Kronecker CG with factor 0 sharded over ranks.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
+Vectors are sharded along factor 0 (the slowest axis of the reference's
+flattening); every rank holds N/G elements in the local layout
+(m_1, ..., m_{d-1}, a), a = i_0 - rank * m_0/G fastest.  A matvec is two
+local MFMA phases around two all-to-alls (include/gp_grief_amd.h,
+gg_kron_dist_*); each CG dot product is one scalar all-reduce.  The CG
+recurrence and its stopping rule are the single-GPU ones (scipy's), so a
+sharded solve converges in the same number of iterations up to rounding.
+
+The arithmetic lives in the "engine" (HipEngine: the C ABI on this rank's
+GPU).  The exchange is injected: `TorchExchange` (RCCL / gloo collectives) in
+production; the tests also drive the same orchestration with virtual ranks.
+"""
+import ctypes
+
+import numpy as np
+
+from . import device as dev
+from . import native
+
+
+def local_index_map(m, world, rank):
+    """Global flat indices (C order over the factors) of this rank's local
+    elements, in local order.  Host helper for scatter / gather and tests."""
+    m = [int(v) for v in m]
+    s0 = m[0] // world
+    rest = int(np.prod(m[1:]))
+    a = np.arange(s0)
+    r = np.arange(rest)
+    # local (r, a) -> global (i0 = rank*s0 + a, r)
+    return ((rank * s0 + a)[None, :] * rest + r[:, None]).reshape(-1)
+
+
+def scatter_global(vec, m, world, rank):
+    return np.asarray(vec).reshape(-1)[local_index_map(m, world, rank)]
+
+
+def gather_global(locals_, m):
+    world = len(locals_)
+    n = int(np.prod(m))
+    out = np.empty(n)
+    for g, loc in enumerate(locals_):
+        out[local_index_map(m, world, g)] = np.asarray(loc).reshape(-1)
+    return out
+
+
+class TorchExchange(object):
+    """All-to-all and all-reduce over a torch.distributed process group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+
+    def all_to_all(self, out, inp):
+        self.dist.all_to_all_single(out, inp, group=self.group)
+
+    def all_reduce(self, t):
+        self.dist.all_reduce(t, group=self.group)
+
+
+class HipEngine(object):
+    """This rank's share of the sharded operator and CG scalars on its GPU."""
+
+    def __init__(self, factors, world, rank):
+        L = native.lib()
+        mats = [np.ascontiguousarray(np.asarray(f, dtype=np.float64)) for f in factors]
+        for f in mats:
+            if f.ndim != 2 or f.shape[0] != f.shape[1]:
+                raise ValueError("the sharded operator needs square factors")
+        self._keep = mats
+        self.m = [f.shape[0] for f in mats]
+        ptrs = (ctypes.c_void_p * len(mats))(*[f.ctypes.data for f in mats])
+        h = ctypes.c_void_p()
+        native.check(L.gg_kron_dist_create(len(mats), native.i64_array(self.m), ptrs, int(world),
+                                           int(rank), ctypes.byref(h)), "gg_kron_dist_create")
+        self.h = h
+        nl, we = ctypes.c_int64(), ctypes.c_int64()
+        native.check(L.gg_kron_dist_sizes(self.h, ctypes.byref(nl), ctypes.byref(we)))
+        self.n_local = nl.value
+        self.work = dev.empty(we.value)
+        c = ctypes.c_void_p()
+        native.check(L.gg_cgs_create(ctypes.byref(c)), "gg_cgs_create")
+        self.cgs = c
+        sc = ctypes.c_void_p()
+        native.check(L.gg_cgs_scalars(self.cgs, ctypes.byref(sc)))
+        self.sc = sc
+        self.red = dev.zeros(2)  # [0]: the scalar being all-reduced
+
+    def empty(self):
+        return dev.empty(self.n_local)
+
+    def zeros(self):
+        return dev.zeros(self.n_local)
+
+    def phase1(self, x, send, r=None):
+        native.check(native.lib().gg_kron_dist_phase1(
+            self.h, native.dptr(x), native.dptr(send), native.dptr(self.work),
+            native.dptr(r) if r is not None else None, self.sc if r is not None else None,
+            native.stream_ptr()), "gg_kron_dist_phase1")
+
+    def phase2(self, recv, send):
+        native.check(native.lib().gg_kron_dist_phase2(self.h, native.dptr(recv),
+                                                      native.dptr(send), native.stream_ptr()),
+                     "gg_kron_dist_phase2")
+
+    # ---- CG scalar steps; each writes / reads self.red[0]
+    def local_dot(self, x, y):
+        native.check(native.lib().gg_cgs_local_dot(self.cgs, native.dptr(x), native.dptr(y),
+                                                   self.n_local, native.dptr(self.red),
+                                                   native.stream_ptr()))
+
+    def cg_init(self, rtol, atol):
+        native.check(native.lib().gg_cgs_init(self.cgs, native.dptr(self.red), float(rtol),
+                                              float(atol), native.stream_ptr()))
+
+    def shift_dot(self, q, p, shift):
+        native.check(native.lib().gg_cgs_shift_dot(self.cgs, native.dptr(q), native.dptr(p),
+                                                   self.n_local, float(shift),
+                                                   native.dptr(self.red), native.stream_ptr()))
+
+    def cg_alpha(self):
+        native.check(native.lib().gg_cgs_alpha(self.cgs, native.dptr(self.red),
+                                               native.stream_ptr()))
+
+    def cg_update(self, x, r, p, q):
+        native.check(native.lib().gg_cgs_update(self.cgs, native.dptr(x), native.dptr(r),
+                                                native.dptr(p), native.dptr(q), self.n_local,
+                                                native.dptr(self.red), native.stream_ptr()))
+
+    def cg_rho(self):
+        native.check(native.lib().gg_cgs_rho(self.cgs, native.dptr(self.red),
+                                             native.stream_ptr()))
+
+    def cg_status(self):
+        it, done = ctypes.c_int(), ctypes.c_int()
+        rho, tol = ctypes.c_double(), ctypes.c_double()
+        native.check(native.lib().gg_cgs_status(self.cgs, ctypes.byref(it), ctypes.byref(done),
+                                                ctypes.byref(rho), ctypes.byref(tol),
+                                                native.stream_ptr()))
+        return it.value, bool(done.value), rho.value, tol.value
+
+    def reduce_buffer(self):
+        return self.red[:1]
+
+    def copy(self, dst, src):
+        dst.copy_(src)
+
+    def zero(self, x):
+        x.zero_()
+
+    def __del__(self):
+        try:
+            L = native.load()
+            if getattr(self, "h", None) is not None and self.h.value:
+                L.gg_kron_dist_destroy(self.h)
+            if getattr(self, "cgs", None) is not None and self.cgs.value:
+                L.gg_cgs_destroy(self.cgs)
+        except Exception:
+            pass
+
+
+class DistKronCG(object):
+    """CG on (K + shift I) x = b with K sharded over the ranks of `exchange`.
+
+    engine: HipEngine (or a test engine with the same methods); all vectors
+    are this rank's local shards.
+    """
+
+    def __init__(self, engine, exchange, shift):
+        self.e = engine
+        self.x_ex = exchange
+        self.shift = float(shift)
+        n = engine.n_local
+        self.n_local = n
+        self.r, self.p, self.q = engine.empty(), engine.zeros(), engine.empty()
+        self.send, self.recv = engine.empty(), engine.empty()
+        self.x = None
+
+    def _allreduce(self):
+        self.x_ex.all_reduce(self.e.reduce_buffer())
+
+    def apply(self, x, y, fuse_cg=False):
+        """y = K x (no shift) for local shards; fuse_cg: x <- beta x + r first."""
+        self.e.phase1(x, self.send, r=self.r if fuse_cg else None)
+        self.x_ex.all_to_all(self.recv, self.send)
+        self.e.phase2(self.recv, self.send)
+        self.x_ex.all_to_all(y, self.send)
+
+    def start(self, b, rtol=1e-5, atol=0.0, x_out=None):
+        self.x = self.e.zeros() if x_out is None else x_out
+        self.e.zero(self.x)
+        self.e.copy(self.r, b)
+        self.e.local_dot(self.r, self.r)
+        self._allreduce()
+        self.e.cg_init(rtol, atol)
+
+    def iterate(self, n_iter):
+        for _ in range(int(n_iter)):
+            self.apply(self.p, self.q, fuse_cg=True)        # p = r + beta p ; q = K p
+            self.e.shift_dot(self.q, self.p, self.shift)     # q += s p ; local p.q
+            self._allreduce()
+            self.e.cg_alpha()
+            self.e.cg_update(self.x, self.r, self.p, self.q)  # x, r ; local r.r
+            self._allreduce()
+            self.e.cg_rho()
+
+    def status(self):
+        return self.e.cg_status()
+
+    def solve(self, b, rtol=1e-5, atol=0.0, maxiter=None, check_every=20):
+        self.start(b, rtol, atol)
+        n_global = self.n_local  # caller may pass maxiter; default like scipy uses n
+        maxiter = 10 * n_global if maxiter is None else maxiter
+        done_iters = 0
+        while done_iters < maxiter:
+            k = min(check_every, maxiter - done_iters)
+            self.iterate(k)
+            done_iters += k
+            it, done, rho, tol = self.status()
+            if done:
+                break
+        it, done, rho, tol = self.status()
+        return self.x, (0 if done and np.sqrt(max(rho, 0.0)) < tol else it)

@@ -83,6 +83,23 @@ SIGNATURES = {
     "gg_potrs": [ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _c_dp,
                  ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
     "gg_colsumsq_lower": [ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _vp],
+    "gg_kron_dist_create": [ctypes.c_int, _c_i64p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                            ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
+    "gg_kron_dist_destroy": [_vp],
+    "gg_kron_dist_sizes": [_vp, _c_i64p, _c_i64p],
+    "gg_kron_dist_phase1": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, _vp, _vp],
+    "gg_kron_dist_phase2": [_vp, _c_dp, _c_dp, _vp],
+    "gg_cgs_create": [ctypes.POINTER(ctypes.c_void_p)],
+    "gg_cgs_destroy": [_vp],
+    "gg_cgs_scalars": [_vp, ctypes.POINTER(ctypes.c_void_p)],
+    "gg_cgs_local_dot": [_vp, _c_dp, _c_dp, ctypes.c_int64, _c_dp, _vp],
+    "gg_cgs_init": [_vp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
+    "gg_cgs_shift_dot": [_vp, _c_dp, _c_dp, ctypes.c_int64, ctypes.c_double, _c_dp, _vp],
+    "gg_cgs_alpha": [_vp, _c_dp, _vp],
+    "gg_cgs_update": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64, _c_dp, _vp],
+    "gg_cgs_rho": [_vp, _c_dp, _vp],
+    "gg_cgs_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
 }
 
 GG_KERN = {"RBF": 0, "Exponential": 1, "Matern32": 2, "Matern52": 3}

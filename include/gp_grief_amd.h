@@ -180,6 +180,43 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
 int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
                       gg_stream stream);
 
+/* --------------------------------------------- P1 sharded over G ranks (RCCL)
+ * The Kronecker operator with factor 0 split over `world` ranks (one per GPU).
+ * Local vector layout: (m_1, ..., m_{d-1}, a) with a = i_0 - rank * m_0 / G the
+ * fastest index.  One matvec = phase1 -> all-to-all(send -> recv, N/G^2 per
+ * peer) -> phase2 -> all-to-all(send -> y_local); the exchanges are the
+ * caller's (torch.distributed / RCCL).  phase1 can fuse CG's p = r + beta p
+ * (cg_r_dev / cg_scalars_dev from gg_cgs, else NULL).  All buffers n_local.  */
+typedef struct gg_kron_dist gg_kron_dist;
+int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_host, int world,
+                        int rank, gg_kron_dist** out);
+int gg_kron_dist_destroy(gg_kron_dist* D);
+int gg_kron_dist_sizes(const gg_kron_dist* D, int64_t* n_local, int64_t* work_elems);
+int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
+                        double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
+                        gg_stream stream);
+int gg_kron_dist_phase2(const gg_kron_dist* D, const double* recv_dev, double* send_dev,
+                        gg_stream stream);
+
+/* Device CG scalars for a host-driven (sharded) CG: the same recurrence as
+ * gg_cg_*, with each global dot product all-reduced by the caller between the
+ * kernels that produce the local value (out_dev) and consume it.             */
+typedef struct gg_cgs gg_cgs;
+int gg_cgs_create(gg_cgs** out);
+int gg_cgs_destroy(gg_cgs* c);
+int gg_cgs_scalars(gg_cgs* c, void** scalars_dev);
+int gg_cgs_local_dot(gg_cgs* c, const double* x_dev, const double* y_dev, int64_t n,
+                     double* out_dev, gg_stream stream);
+int gg_cgs_init(gg_cgs* c, const double* rr_dev, double rtol, double atol, gg_stream stream);
+int gg_cgs_shift_dot(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, double shift,
+                     double* out_dev, gg_stream stream);
+int gg_cgs_alpha(gg_cgs* c, const double* pq_dev, gg_stream stream);
+int gg_cgs_update(gg_cgs* c, double* x_dev, double* r_dev, const double* p_dev,
+                  const double* q_dev, int64_t n, double* out_dev, gg_stream stream);
+int gg_cgs_rho(gg_cgs* c, const double* rr_dev, gg_stream stream);
+int gg_cgs_status(gg_cgs* c, int* iters, int* done, double* rho, double* tol,
+                  gg_stream stream); /* synchronising */
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,162 @@
+"""Test-only helpers for the sharded Kronecker CG (gp_grief_amd/distributed.py).
+
+NumpyEngine: the engine interface of distributed.HipEngine restated with NumPy
+on torch CPU tensors (so gloo collectives work on them).  Its layout logic is
+written independently of the HIP kernels' address maps (reshape / transpose
+here, integer address arithmetic there), so agreement checks both.
+
+ThreadExchange: all-to-all / all-reduce between virtual ranks that run as
+Python threads in one process (used to drive G HipEngines on one GPU).
+"""
+import threading
+
+import numpy as np
+import torch
+
+import oracle
+
+
+class NumpyEngine(object):
+    def __init__(self, factors, world, rank):
+        self.F = [np.asarray(f, dtype=np.float64) for f in factors]
+        self.m = [f.shape[0] for f in self.F]
+        self.G, self.rank = world, rank
+        self.s0 = self.m[0] // world
+        self.n_local = int(np.prod(self.m)) // world
+        self.red = torch.zeros(2, dtype=torch.float64)
+        self.sc = dict(rho=0.0, rho_prev=0.0, alpha=0.0, beta=0.0, tol=0.0, iters=0, done=False,
+                       first=True)
+
+    def empty(self):
+        return torch.empty(self.n_local, dtype=torch.float64)
+
+    def zeros(self):
+        return torch.zeros(self.n_local, dtype=torch.float64)
+
+    def phase1(self, x, send, r=None):
+        xv = x.numpy()
+        if r is not None and not self.sc["done"]:
+            xv[:] = r.numpy() if self.sc["first"] else self.sc["beta"] * xv + r.numpy()
+        d, G, s0 = len(self.m), self.G, self.s0
+        X = xv.reshape(self.m[1:] + [s0])
+        X = np.moveaxis(X, -1, 0)                      # (s0, m1, ..., m_{d-1})
+        for k in range(1, d):
+            X = np.moveaxis(np.tensordot(self.F[k], X, axes=([1], [k])), 0, k)
+        p1 = self.m[1]
+        Y = X.reshape(s0, G, p1 // G, -1).transpose(1, 0, 2, 3)
+        send.numpy()[:] = Y.reshape(-1)
+
+    def phase2(self, recv, send):
+        m0 = self.m[0]
+        Z = self.F[0].dot(recv.numpy().reshape(m0, -1))   # (p0, C)
+        C = Z.shape[1]
+        send.numpy()[:] = Z.T.reshape(C, self.G, self.s0).transpose(1, 0, 2).reshape(-1)
+
+    def local_dot(self, x, y):
+        self.red[0] = float(np.dot(x.numpy(), y.numpy()))
+
+    def cg_init(self, rtol, atol):
+        s = float(self.red[0])
+        self.sc.update(rho=s, tol=max(atol, rtol * np.sqrt(s)), iters=0, first=True)
+        self.sc["done"] = s == 0.0 or not np.sqrt(s) >= self.sc["tol"]
+
+    def shift_dot(self, q, p, shift):
+        if self.sc["done"]:
+            return
+        qv = q.numpy()
+        qv += shift * p.numpy()
+        self.red[0] = float(np.dot(p.numpy(), qv))
+
+    def cg_alpha(self):
+        if not self.sc["done"]:
+            self.sc["alpha"] = self.sc["rho"] / float(self.red[0])
+
+    def cg_update(self, x, r, p, q):
+        if self.sc["done"]:
+            return
+        a = self.sc["alpha"]
+        x.numpy()[:] += a * p.numpy()
+        r.numpy()[:] -= a * q.numpy()
+        self.red[0] = float(np.dot(r.numpy(), r.numpy()))
+
+    def cg_rho(self):
+        if self.sc["done"]:
+            return
+        s = float(self.red[0])
+        self.sc.update(rho_prev=self.sc["rho"], rho=s, iters=self.sc["iters"] + 1, first=False)
+        self.sc["beta"] = s / self.sc["rho_prev"]
+        if not np.sqrt(s) >= self.sc["tol"]:
+            self.sc["done"] = True
+
+    def cg_status(self):
+        return self.sc["iters"], self.sc["done"], self.sc["rho"], self.sc["tol"]
+
+    def reduce_buffer(self):
+        return self.red[:1]
+
+    def copy(self, dst, src):
+        dst.copy_(src)
+
+    def zero(self, x):
+        x.zero_()
+
+
+class ThreadExchange(object):
+    """Collectives between `world` threads of one process (virtual ranks)."""
+
+    def __init__(self, world):
+        self.G = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+        self.local = threading.local()
+
+    def bind(self, rank):
+        self.local.rank = rank
+
+    def all_to_all(self, out, inp):
+        g = self.local.rank
+        self.slots[g] = inp
+        self.bar.wait()
+        c = out.numel() // self.G
+        for h in range(self.G):
+            out[h * c:(h + 1) * c].copy_(self.slots[h][g * c:(g + 1) * c])
+        self.bar.wait()
+
+    def all_reduce(self, t):
+        g = self.local.rank
+        self.slots[g] = t.clone()
+        self.bar.wait()
+        acc = self.slots[0].clone()
+        for h in range(1, self.G):
+            acc += self.slots[h]
+        self.bar.wait()
+        t.copy_(acc)
+        self.bar.wait()
+
+
+def run_threads(world, fn):
+    """Run fn(rank) in `world` threads; re-raise the first failure."""
+    errs = [None] * world
+    out = [None] * world
+
+    def body(g):
+        try:
+            out[g] = fn(g)
+        except BaseException as e:  # pragma: no cover - surfaced below
+            errs[g] = e
+
+    ts = [threading.Thread(target=body, args=(g,)) for g in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+def reference_factors(m, d, seed=0):
+    g = np.linspace(0, 1, m)
+    return [oracle.cov_1d("RBF", g, g, 1.0, 0.15 * (1 + 0.1 * k)) + 1e-12 * np.eye(m)
+            for k in range(d)]
