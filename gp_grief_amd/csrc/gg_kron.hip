@@ -261,7 +261,7 @@ typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, in
                               const double*, const CgScalars*, double*, OutMap);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
-// LDS chunk.  The default (8 waves, KC 8, one workgroup per CU) was chosen by
+// LDS chunk.  The default (12 waves, KC 4, 3 workgroups per CU) was chosen by
 // A/B on MI355X (profiles/); GG_MP_VARIANT selects another for tuning runs.
 struct ModeConfig {
   mode_kernel_t fn;
