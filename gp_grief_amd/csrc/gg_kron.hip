@@ -50,7 +50,11 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 // operand is p_new = beta * p + r (p_new = r on the first iteration, selected,
 // so an uninitialised p never leaks in), written back in place; each element
 // is read and written by exactly one lane.
-template <int JT, int kWaves, int kKC, bool CGP, int kMinW, bool kIdent>
+//
+// kSplit = 2 splits the output columns of a strip over two waves (JT tiles
+// each): half the accumulators per wave, so two workgroups fit a CU and one
+// workgroup's prologue / epilogue overlaps the other's MFMAs.
+template <int JT, int kWaves, int kKC, bool CGP, int kMinW, bool kIdent, int kSplit, int kOpt>
 __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
@@ -58,55 +62,99 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const int* __restrict__ skip, const double* __restrict__ R,
     const CgScalars* __restrict__ sc, double* Pout, OutMap om) {
   if (skip != nullptr && *skip) return;
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JT * 64
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JTL * 64
+  constexpr int JTL = JT * kSplit;                        // tiles staged per launch
   constexpr int kThreads = kWaves * 64;
-  constexpr int kChunk2 = kKC * JT * 32;                  // double2 per full chunk
+  constexpr int kChunk2 = kKC * JTL * 32;                 // double2 per full chunk
   constexpr int kPerT = (kChunk2 + kThreads - 1) / kThreads;
-  constexpr int kBuf = kKC * JT * 64;                     // doubles per LDS buffer
+  constexpr int kBuf = kKC * JTL * 64;                    // doubles per LDS buffer
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wave) * 16;
+  const int hp = kSplit == 1 ? 0 : wave % kSplit;         // column part of this wave
+  const int strip = kSplit == 1 ? wave : wave / kSplit;
+  const int nt = min(JTL, jt_total - jt0);                // real tiles in this launch
+  const int64_t b0 = ((int64_t)blockIdx.x * (kWaves / kSplit) + strip) * 16;
   const int64_t brow = b0 + (lane & 15);
   const bool bvalid = brow < M;
   const int64_t bclamp = bvalid ? brow : M - 1;
   const int krow = lane >> 4;
   const int nchunks = (KS + kKC - 1) / kKC;
 
-  // staging: element i of chunk c lives at Bf[((ks0 + s) * jt_total + jt0) * 64 + 2 o]
+  // ---- per-thread addressing, computed once (the k-loop only adds strides)
+  // staging: element i of a chunk is double2 o of k-step s, i.e.
+  // Bf[((ks0 + s) * jt_total + jt0) * 64 + 2 o].  The packed factor carries 8
+  // zero k-steps of padding, so a partial last chunk needs no clamp; tiles
+  // past nt (kSplit > 1 only) re-read the last real tile and are never used.
+  const double* __restrict__ bbase = Bf + (int64_t)jt0 * 64;
+  const int64_t bchunk = (int64_t)kKC * jt_total * 64;          // doubles per chunk
+  int boff[kPerT];
+  bool bfull[kPerT];
+#pragma unroll
+  for (int u = 0; u < kPerT; ++u) {
+    int i = threadIdx.x + u * kThreads;
+    bfull[u] = i < kChunk2;
+    i = i < kChunk2 ? i : kChunk2 - 1;
+    const int s_ = i / (JTL * 32);
+    int o_ = i - s_ * (JTL * 32);
+    if (kSplit > 1) o_ = min(o_, nt * 32 - 1);
+    boff[u] = s_ * jt_total * 64 + 2 * o_;
+  }
+  // A operand: lane l reads X[4 ks + (l >> 4)][b0 + (l & 15)]
+  const int64_t m4 = 4 * M;
+  const int64_t aoff0 = (int64_t)krow * M + bclamp;
+  const int64_t alast = (int64_t)(q - 1) * M + bclamp;
+  const int64_t achunk = (int64_t)kKC * m4;
+
+  // kOpt & 2: the factor chunk goes global -> LDS directly (global_load_lds,
+  // lane-linear 1 KiB per wave instruction), no staging registers
 #define GG_STAGE_LOAD(c, st)                                                          \
   do {                                                                                \
-    const int ks0_ = (c) * kKC;                                                       \
-    const int n2_ = min(kKC, KS - ks0_) * JT * 32;                                    \
-    _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                               \
-      int i_ = threadIdx.x + u * kThreads;                                            \
-      i_ = i_ < n2_ ? i_ : n2_ - 1;                                                   \
-      const int s_ = i_ / (JT * 32);                                                  \
-      const int o_ = i_ - s_ * (JT * 32);                                             \
-      const double2 v_ = reinterpret_cast<const double2*>(                            \
-          Bf + ((int64_t)(ks0_ + s_) * jt_total + jt0) * 64)[o_];                     \
-      st##x[u] = v_.x; st##y[u] = v_.y;                                               \
+    const double* cb_ = bbase + (int64_t)(c) * bchunk;                                \
+    if (kOpt & 2) {                                                                   \
+      double* dstb_ = lds + ((c) & 1) * kBuf + wave * 128;                            \
+      _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                             \
+        if (bfull[u])                                                                 \
+          __builtin_amdgcn_global_load_lds(                                           \
+              (const __attribute__((address_space(1))) void*)(cb_ + boff[u]),         \
+              (__attribute__((address_space(3))) void*)(dstb_ + u * kThreads * 2),    \
+              16, 0, 0);                                                              \
+      }                                                                               \
+    } else {                                                                          \
+      _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                             \
+        const double2 v_ = *reinterpret_cast<const double2*>(cb_ + boff[u]);          \
+        st##x[u] = v_.x; st##y[u] = v_.y;                                             \
+      }                                                                               \
     }                                                                                 \
   } while (0)
 #define GG_STAGE_STORE(c, st)                                                         \
   do {                                                                                \
-    const int n2_ = min(kKC, KS - (c) * kKC) * JT * 32;                               \
-    double2* dst_ = reinterpret_cast<double2*>(lds + ((c) & 1) * kBuf);               \
-    _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                               \
-      const int i_ = threadIdx.x + u * kThreads;                                      \
-      if (i_ < n2_) dst_[i_] = double2{st##x[u], st##y[u]};                           \
+    if (!(kOpt & 2)) {                                                                \
+      double2* dst_ = reinterpret_cast<double2*>(lds + ((c) & 1) * kBuf);             \
+      _Pragma("unroll") for (int u = 0; u < kPerT; ++u) {                             \
+        if (bfull[u]) dst_[threadIdx.x + u * kThreads] = double2{st##x[u], st##y[u]}; \
+      }                                                                               \
     }                                                                                 \
   } while (0)
-// A fragments: unconditional loads from a clamped (always valid) address; the
-// mask (rows past q, strips past M) is applied when the registers are consumed,
-// so no load is followed by a wait.
+// A fragments: unconditional loads; only the last chunk clamps the row to
+// q - 1.  The mask (rows past q, strips past M) is applied when the
+// registers are consumed, so no load is followed by a wait.
 #define GG_A_LOAD(c, a, rr)                                                           \
   do {                                                                                \
-    const int ks0_ = (c) * kKC;                                                       \
-    _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
-      const int k_ = min((ks0_ + s_) * 4 + krow, q - 1);                              \
-      a[s_] = X[(int64_t)k_ * M + bclamp];                                            \
-      if (CGP) rr[s_] = R[(int64_t)k_ * M + bclamp];                                  \
+    int64_t o_ = aoff0 + (int64_t)(c) * achunk;                                       \
+    if ((c) == nchunks - 1) {                                                         \
+      _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                            \
+        const int64_t oc_ = o_ < alast ? o_ : alast;                                  \
+        a[s_] = X[oc_];                                                               \
+        if (CGP) rr[s_] = R[oc_];                                                     \
+        o_ += m4;                                                                     \
+      }                                                                               \
+    } else {                                                                          \
+      _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                            \
+        a[s_] = X[o_];                                                                \
+        if (CGP) rr[s_] = R[o_];                                                      \
+        o_ += m4;                                                                     \
+      }                                                                               \
     }                                                                                 \
   } while (0)
 #define GG_A_MASK(c, a, rr)                                                           \
@@ -118,7 +166,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       double v_ = a[s_];                                                              \
       if (CGP) {                                                                      \
         v_ = cg_first ? rr[s_] : fma(cg_beta, v_, rr[s_]);                            \
-        if (ok_) Pout[(int64_t)k_ * M + brow] = v_;                                   \
+        if (ok_ && hp == 0) Pout[(int64_t)k_ * M + brow] = v_;                        \
       }                                                                               \
       a[s_] = ok_ ? v_ : 0.0;                                                         \
     }                                                                                 \
@@ -142,21 +190,30 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   GG_A_MASK(0, a_cur, r_cur);
   __syncthreads();
 
+  // Per chunk: the first k-step's MFMAs are placed before the next chunk's
+  // global loads in the source (kOpt & 1 pins that order with sched_barrier),
+  // so the waves of a SIMD restart their MFMAs right after the barrier.
   for (int c = 0; c < nchunks; ++c) {
     const bool more = c + 1 < nchunks;
-    if (more) {
-      GG_STAGE_LOAD(c + 1, st);
-      GG_A_LOAD(c + 1, a_nxt, r_nxt);
-    }
     const int kcn = min(kKC, KS - c * kKC);
     const double* buf = lds + (c & 1) * kBuf;
 #pragma unroll
     for (int s = 0; s < kKC; ++s) {
+      if (s == 1 || (kKC == 1 && s == 0)) {
+        if (kOpt & 1) __builtin_amdgcn_sched_barrier(0);
+        if (more) {
+          GG_STAGE_LOAD(c + 1, st);
+          GG_A_LOAD(c + 1, a_nxt, r_nxt);
+        }
+        if (kOpt & 1) __builtin_amdgcn_sched_barrier(0);
+      }
       if (s < kcn) {
 #pragma unroll
         for (int t = 0; t < JT; ++t) {
-          const double b = buf[(s * JT + t) * 64 + lane];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
+          if (kSplit == 1 || hp * JT + t < nt) {
+            const double b = buf[(s * JTL + hp * JT + t) * 64 + lane];
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
+          }
         }
       }
     }
@@ -192,7 +249,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       rowoff[r] = h * om.hs + a_ * om.as + br * om.cg;
     }
   }
-  auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + t) * 16 + col; };
+  auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + hp * JT + t) * 16 + col; };
   auto coloff = [&](int t) -> int64_t {
     const int64_t j = colj(t);
     if (kIdent) return j;
@@ -261,28 +318,32 @@ typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, in
                               const double*, const CgScalars*, double*, OutMap);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
-// LDS chunk.  The default (12 waves, KC 4, 3 workgroups per CU) was chosen by
+// LDS chunk.  The default (12 waves, KC 4, one workgroup per CU, factor chunks
+// staged by global_load_lds) was chosen by
 // A/B on MI355X (profiles/); GG_MP_VARIANT selects another for tuning runs.
 struct ModeConfig {
   mode_kernel_t fn;
-  int waves, kc;
+  int waves, kc, split, jtl;  // jtl: tiles staged per launch (LDS size)
 };
 
-template <int JT, int W, int KC, bool CGP, int MINW>
+// JT = output tiles of the launch; a split config gives each wave ceil(JT/2)
+template <int JT, int W, int KC, bool CGP, int MINW, int SPLIT, int OPT>
 static ModeConfig cfg() {
-  return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW, true>, W, KC};
+  constexpr int JW = (JT + SPLIT - 1) / SPLIT;
+  return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT>, W, KC, SPLIT,
+                    JW * SPLIT};
 }
 
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
 template <int JT, bool CGP>
 static ModeConfig config_for(int variant) {
   switch (variant) {
-    case 1: return cfg<JT, 8, 4, CGP, 2>();
-    case 2: return cfg<JT, 6, 4, CGP, 3>();
-    case 3: return cfg<JT, 4, 4, CGP, 3>();
-    case 4: return cfg<JT, 12, 2, CGP, 3>();
-    case 5: return cfg<JT, 12, 6, CGP, 3>();
-    default: return cfg<JT, 12, 4, CGP, 3>();
+    case 1: return cfg<JT, 12, 4, CGP, 3, 1, 0>();  // register-staged factor chunks
+    case 2: return cfg<JT, 12, 4, CGP, 3, 1, 3>();
+    case 3: return cfg<JT, 12, 4, CGP, 3, 1, 1>();
+    case 4: return cfg<JT, 12, 2, CGP, 3, 1, 2>();
+    case 5: return cfg<JT, 8, 4, CGP, 4, 2, 2>();
+    default: return cfg<JT, 12, 4, CGP, 3, 1, 2>();  // factor chunks by global_load_lds
   }
 }
 constexpr int kNumVariants = 6;
@@ -314,8 +375,8 @@ static ModeConfig select_kernel(int jt, int variant, bool cgp) {
   }
 }
 
-static size_t mode_lds_bytes(int jt, const ModeConfig& c) {
-  return 2 * (size_t)c.kc * jt * 64 * sizeof(double);
+static size_t mode_lds_bytes(const ModeConfig& c) {
+  return 2 * (size_t)c.kc * c.jtl * 64 * sizeof(double);
 }
 
 // One factor in fragment order, for the operator and for its transpose.
@@ -332,7 +393,8 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
   f.q = transpose ? rows : cols;
   f.KS = (int)ceil_div(f.q, 4);
   f.JT = (int)ceil_div(f.p, 16);
-  std::vector<double> h((size_t)f.KS * f.JT * 64, 0.0);
+  // 8 zero k-steps of padding: a partial last LDS chunk (kKC <= 8) stays in bounds
+  std::vector<double> h(((size_t)f.KS + 8) * f.JT * 64, 0.0);
   for (int ks = 0; ks < f.KS; ++ks)
     for (int jt = 0; jt < f.JT; ++jt)
       for (int l = 0; l < 64; ++l) {
@@ -404,7 +466,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // the fused CG direction update runs once, in the first launch of step 0
         const bool cgp = pro != nullptr && k == 0 && jt0 == 0;
         const ModeConfig mc = select_kernel(jt, variant, cgp);
-        const int64_t nblk = ceil_div(M, (int64_t)mc.waves * 16);
+        const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         double* parts = nullptr;
         if (last && dot_partials != nullptr) {
@@ -412,7 +474,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           np_total += nblk;
         }
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)nblk), dim3(mc.waves * 64),
-                           mode_lds_bytes(jt, mc), stream, src, dst, f.frag, M, (int)f.q,
+                           mode_lds_bytes(mc), stream, src, dst, f.frag, M, (int)f.q,
                            (int)f.p, f.KS, f.JT, jt0,
                            last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip,
                            cgp ? pro->r : nullptr, cgp ? pro->sc : nullptr,
@@ -434,8 +496,8 @@ int64_t kron_partials_needed(const gg_kron* K, bool transpose) {
   int64_t size = n_in;
   for (const Factor& g : fs) size = size / g.q * g.p;
   const int64_t M = size / f.p;
-  // upper bound over the launch variants (the smallest workgroup has 4 waves)
-  return ceil_div(M, 4 * 16) * ceil_div(f.JT, kMaxJT);
+  // upper bound over the launch variants (the smallest workgroup has 2 strips)
+  return ceil_div(M, 2 * 16) * ceil_div(f.JT, kMaxJT);
 }
 
 int64_t kron_work_elems(const gg_kron* K, bool transpose) {
@@ -455,7 +517,7 @@ static void set_lds_limits() {
         const ModeConfig mc = select_kernel(jt, v, cgp != 0);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)mode_lds_bytes(jt, mc)));
+                                   (int)mode_lds_bytes(mc)));
       }
   done = true;
 }
@@ -553,9 +615,10 @@ namespace gg {
 
 template <int JT>
 static mode_kernel_t dist_kernel(bool cgp, bool ident) {
-  if (cgp) return mode_product_kernel<JT, 12, 4, true, 3, true>;
-  if (ident) return mode_product_kernel<JT, 12, 4, false, 3, true>;
-  return mode_product_kernel<JT, 12, 4, false, 3, false>;
+  if (cgp && ident) return mode_product_kernel<JT, 12, 4, true, 3, true, 1, 2>;
+  if (cgp) return mode_product_kernel<JT, 12, 4, true, 3, false, 1, 2>;  // d == 2: fused + mapped
+  if (ident) return mode_product_kernel<JT, 12, 4, false, 3, true, 1, 2>;
+  return mode_product_kernel<JT, 12, 4, false, 3, false, 1, 2>;
 }
 
 static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {

@@ -45,6 +45,17 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / 3
                 res.setdefault((v, name), []).append(ms)
+    # every variant must give the same product (bitwise up to summation order)
+    ref = None
+    for v in variants:
+        os.environ["GG_MP_VARIANT"] = v
+        K.matvec_device(inputs["randn"], shift=0.01, out=y)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = y.clone()
+        err = float((y - ref).abs().max() / ref.abs().max())
+        print(json.dumps({"variant": v, "max_rel_diff_vs_first": err}), flush=True)
+        assert err < 1e-12, (v, err)
     for (v, name), ts in sorted(res.items()):
         ms = min(ts)
         print(json.dumps({"variant": v, "input": name, "matvec_ms_min": ms,
