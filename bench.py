@@ -41,7 +41,6 @@ def parse():
     ap.add_argument("--dims", type=int, default=4)
     ap.add_argument("--sigma2", type=float, default=0.01)
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
-    ap.add_argument("--matvec-reps", type=int, default=5)
     return ap.parse_args()
 
 
@@ -141,6 +140,22 @@ def run_sharded(a, world, rank, torch, dev, dist):
     }
 
 
+KERNEL_NAME = "gg::mode_product_kernel<13, 4, 3, false, 3, true, 1, 2>"
+
+
+def pmc_traffic(m, d):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    passes (tools/pmc_traffic.py), if they were taken on this kernel and
+    workload; else None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_mode_product.json")
+    if (m, d) != (200, 4) or not os.path.exists(path):
+        return None, None
+    rec = json.load(open(path))
+    if KERNEL_NAME.replace("gg::", "") not in str(rec.get("kernel")):
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(path, ROOT)
+
+
 def cpu_baseline(m, d, sigma2):
     """One CG iteration of the CPU oracle at the full grid (bounded sample)."""
     import oracle
@@ -197,25 +212,14 @@ def main():
     solver.start(y, rtol=0.0, atol=0.0)   # never "converges": exactly the steps asked for
     torch.cuda.synchronize()
 
-    # ---- matvec kernel timing (HIP events on the stream the kernels run on)
-    xv = y
-    out = torch.empty_like(y)
-    K.matvec_device(xv, shift=s, out=out)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(a.matvec_reps):
-        K.matvec_device(xv, shift=s, out=out)
-    e1.record()
-    torch.cuda.synchronize()
-    mv_ms = e0.elapsed_time(e1) / a.matvec_reps
-    del out
-
     # ---- CG: warmup, then exactly `steps` iterations bracketed by barrier+sync
     solver.iterate(a.warmup, check_every=0)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    # live kernel timing: HIP events around every mode product of the timed
+    # iterations, recorded by the library on the stream the kernels run on
+    solver.profile(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     solver.iterate(a.steps, check_every=0)
@@ -223,6 +227,9 @@ def main():
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    n_mv, mode_ms = solver.profile_read()
+    solver.profile(False)
+    assert n_mv == a.steps, (n_mv, a.steps)
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -231,9 +238,14 @@ def main():
     assert it == a.warmup + a.steps, (it, a.warmup, a.steps)
     assert np.isfinite(res)
 
-    launch_ms = mv_ms / d
+    # dominant kernel: the plain mode product (positions 2..d of each matvec;
+    # position 1 is the CG-fused instantiation, reported separately)
+    mv_ms = sum(mode_ms) / n_mv
+    launch_ms = sum(mode_ms[1:]) / (n_mv * (d - 1))
+    fused_ms = mode_ms[0] / n_mv
     flop_launch = 2.0 * n * m
     achieved_tf = flop_launch / (launch_ms * 1e-3) / 1e12
+    traffic, traffic_src = pmc_traffic(m, d)
     mv_bytes = 8.0 * n * (2 * d + 1)
     vec_bytes = 8.0 * n * (3 + 6 + 1)   # p-update 3N, x/r update 6N (+ q read in matvec epilogue 1N)
     result = {
@@ -245,7 +257,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
@@ -255,9 +267,13 @@ def main():
                    "parallelism": "single-gpu"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_MFMA_PEAK_TFLOPS,
-                     "traffic": None,
-                     "kernel": "gg::mode_product_kernel<13> (one Kronecker mode product)",
-                     "launch_ms": launch_ms, "flop_per_launch": flop_launch},
+                     "traffic": traffic, "traffic_unit": "bytes per launch",
+                     "traffic_source": traffic_src,
+                     "kernel": KERNEL_NAME, "launch_ms": launch_ms,
+                     "launch_ms_source": "HIP events around each launch in the timed region",
+                     "algorithmic_bytes_per_launch": 16.0 * n,
+                     "flop_per_launch": flop_launch},
+        "cg_fused_mode_product_ms": fused_ms,
         "matvec_ms": mv_ms,
         "matvec_hbm_gbs": mv_bytes / (mv_ms * 1e-3) / 1e9,
         "matvec_hbm_frac": mv_bytes / (mv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

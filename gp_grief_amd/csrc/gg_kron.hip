@@ -318,9 +318,11 @@ typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, in
                               const double*, const CgScalars*, double*, OutMap);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
-// LDS chunk.  The default (12 waves, KC 4, one workgroup per CU, factor chunks
-// staged by global_load_lds) was chosen by
-// A/B on MI355X (profiles/); GG_MP_VARIANT selects another for tuning runs.
+// LDS chunk.  The default -- 4-wave workgroups (one wave per SIMD), 3 k-steps
+// per chunk, three independent workgroups per CU, factor chunks staged by
+// global_load_lds -- was chosen by A/B on MI355X (profiles/r01_*_mode_variants):
+// three workgroups drift apart, so one's barrier or epilogue overlaps the
+// others' MFMAs.  GG_MP_VARIANT selects another for tuning runs.
 struct ModeConfig {
   mode_kernel_t fn;
   int waves, kc, split, jtl;  // jtl: tiles staged per launch (LDS size)
@@ -338,15 +340,17 @@ static ModeConfig cfg() {
 template <int JT, bool CGP>
 static ModeConfig config_for(int variant) {
   switch (variant) {
-    case 1: return cfg<JT, 12, 4, CGP, 3, 1, 0>();  // register-staged factor chunks
-    case 2: return cfg<JT, 12, 4, CGP, 3, 1, 3>();
-    case 3: return cfg<JT, 12, 4, CGP, 3, 1, 1>();
-    case 4: return cfg<JT, 12, 2, CGP, 3, 1, 2>();
-    case 5: return cfg<JT, 8, 4, CGP, 4, 2, 2>();
-    default: return cfg<JT, 12, 4, CGP, 3, 1, 2>();  // factor chunks by global_load_lds
+    case 1: return cfg<JT, 12, 4, CGP, 3, 1, 2>();
+    case 2: return cfg<JT, 12, 4, CGP, 3, 1, 0>();  // register-staged factor chunks
+    case 3: return cfg<JT, 4, 4, CGP, 3, 1, 2>();
+    case 4: return cfg<JT, 4, 2, CGP, 3, 1, 2>();
+    case 5: return cfg<JT, 2, 2, CGP, 3, 1, 2>();
+    case 6: return cfg<JT, 8, 4, CGP, 4, 2, 2>();   // columns split over two waves
+    case 7: return cfg<JT, 12, 4, CGP, 3, 1, 3>();  // + sched_barrier around the prefetch
+    default: return cfg<JT, 4, 3, CGP, 3, 1, 2>();
   }
 }
-constexpr int kNumVariants = 6;
+constexpr int kNumVariants = 8;
 
 static int mode_variant() {
   const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
@@ -434,7 +438,9 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
 
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out, const CgPrologue* pro) {
+                int64_t* n_partials_out, const CgPrologue* pro, hipEvent_t* ev) {
+  // ev (optional, d + 1 events): recorded before the first mode product and
+  // after each one, for live per-launch timing (gg_cg_profile)
   const std::vector<Factor>& fs = transpose ? K->bwd : K->fwd;
   const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
   const int64_t n_in = transpose ? K->n_rows : K->n_cols;
@@ -446,6 +452,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   int64_t size = n_in;
   const double* src = x;
   int64_t np_total = 0;
+  if (ev) GG_HIP(hipEventRecord(ev[0], stream));
   for (int k = 0; k < d; ++k) {
     const Factor& f = fs[k];
     const int64_t M = size / f.q;
@@ -483,6 +490,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
       }
     }
     (void)out_size;
+    if (ev) GG_HIP(hipEventRecord(ev[k + 1], stream));
     size = out_size;
     src = dst;
   }
@@ -507,6 +515,7 @@ int64_t kron_work_elems(const gg_kron* K, bool transpose) {
 }
 
 int64_t kron_n(const gg_kron* K) { return K->n_rows; }
+int kron_d(const gg_kron* K) { return K->d; }
 
 static void set_lds_limits() {
   static bool done = false;
@@ -584,7 +593,7 @@ int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double*
     GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
     GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
     gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
-                   gg::as_stream(stream), nullptr, nullptr);
+                   gg::as_stream(stream), nullptr, nullptr, nullptr);
   });
 }
 
@@ -613,12 +622,14 @@ struct gg_kron_dist {
 
 namespace gg {
 
+constexpr int kDistWaves = 4, kDistKC = 3;  // the single-GPU default
+
 template <int JT>
 static mode_kernel_t dist_kernel(bool cgp, bool ident) {
-  if (cgp && ident) return mode_product_kernel<JT, 12, 4, true, 3, true, 1, 2>;
-  if (cgp) return mode_product_kernel<JT, 12, 4, true, 3, false, 1, 2>;  // d == 2: fused + mapped
-  if (ident) return mode_product_kernel<JT, 12, 4, false, 3, true, 1, 2>;
-  return mode_product_kernel<JT, 12, 4, false, 3, false, 1, 2>;
+  if (cgp && ident) return mode_product_kernel<JT, kDistWaves, kDistKC, true, 3, true, 1, 2>;
+  if (cgp) return mode_product_kernel<JT, kDistWaves, kDistKC, true, 3, false, 1, 2>;  // d == 2: fused + mapped
+  if (ident) return mode_product_kernel<JT, kDistWaves, kDistKC, false, 3, true, 1, 2>;
+  return mode_product_kernel<JT, kDistWaves, kDistKC, false, 3, false, 1, 2>;
 }
 
 static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {
@@ -643,7 +654,6 @@ static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {
   }
 }
 
-constexpr int kDistWaves = 12, kDistKC = 4;
 
 static void dist_step(const Factor& f, const double* X, double* Y, int64_t M, OutMap om,
                       const CgPrologue* pro, double* pin, hipStream_t s) {

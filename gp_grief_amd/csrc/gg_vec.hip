@@ -16,10 +16,11 @@ namespace gg {
 // defined in gg_kron.hip
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out, const CgPrologue* pro);
+                int64_t* n_partials_out, const CgPrologue* pro, hipEvent_t* ev);
 int64_t kron_partials_needed(const gg_kron* K, bool transpose);
 int64_t kron_work_elems(const gg_kron* K, bool transpose);
 int64_t kron_n(const gg_kron* K);
+int kron_d(const gg_kron* K);
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -371,6 +372,11 @@ struct gg_cg {
   const double* b = nullptr;
   double* x = nullptr;
   int64_t mv_partials = 0;
+  // live timing of the mode products (gg_cg_profile): d + 1 events per
+  // profiled iteration, recorded on the CG stream, read back on demand
+  bool profiling = false;
+  std::vector<hipEvent_t> events;
+  size_t events_used = 0;
 };
 
 extern "C" {
@@ -518,7 +524,38 @@ int gg_cg_destroy(gg_cg* cg) {
     if (cg->partials) (void)hipFree(cg->partials);
     if (cg->sc) (void)hipFree(cg->sc);
     if (cg->sc_host) (void)hipHostFree(cg->sc_host);
+    for (hipEvent_t e : cg->events) (void)hipEventDestroy(e);
     delete cg;
+  });
+}
+
+int gg_cg_profile(gg_cg* cg, int enable) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    cg->profiling = enable != 0;
+    cg->events_used = 0;
+  });
+}
+
+int gg_cg_profile_read(gg_cg* cg, int* n_matvecs, double* mode_ms, int mode_ms_len) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && n_matvecs, GG_ERR_VALUE, "NULL argument");
+    const int d = gg::kron_d(cg->K);
+    GG_REQUIRE(mode_ms == nullptr || mode_ms_len >= d, GG_ERR_VALUE, "mode_ms too short");
+    const size_t per = (size_t)d + 1;
+    const int nm = (int)(cg->events_used / per);
+    if (mode_ms)
+      for (int k = 0; k < d; ++k) mode_ms[k] = 0.0;
+    for (int it = 0; it < nm; ++it) {
+      hipEvent_t* ev = cg->events.data() + it * per;
+      GG_HIP(hipEventSynchronize(ev[d]));
+      for (int k = 0; k < d && mode_ms; ++k) {
+        float ms = 0.0f;
+        GG_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+        mode_ms[k] += ms;
+      }
+    }
+    *n_matvecs = nm;
   });
 }
 
@@ -553,8 +590,19 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
     for (int it = 0; it < max_iters; ++it) {
       // p = r + beta p is fused into the first mode product of q = (K + s I) p
       int64_t nparts = 0;
+      hipEvent_t* ev = nullptr;
+      if (cg->profiling) {
+        const size_t need = cg->events_used + (size_t)gg::kron_d(cg->K) + 1;
+        while (cg->events.size() < need) {
+          hipEvent_t e;
+          GG_HIP(hipEventCreate(&e));
+          cg->events.push_back(e);
+        }
+        ev = cg->events.data() + cg->events_used;
+        cg->events_used = need;
+      }
       gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
-                     &cg->sc->done, s, &nparts, &pro);
+                     &cg->sc->done, s, &nparts, &pro, ev);
       hipLaunchKernelGGL(gg::cg_alpha_kernel, dim3(1), dim3(1024), 0, s, cg->partials, nparts,
                          cg->sc);
       GG_LAUNCH_CHECK();
@@ -619,7 +667,7 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
     for (int j = 0; j < steps; ++j) {
-      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr);
+      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr, nullptr);
       const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
       hipLaunchKernelGGL(gg::lz_axpy_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P,
                          V, n, beta_prev, parts);

@@ -130,6 +130,21 @@ class KronCG(object):
                                                native.stream_ptr()))
         return it.value, bool(conv.value), res.value, tol.value
 
+    def profile(self, enable=True):
+        """Record HIP events around every mode product of later iterations."""
+        from . import native
+        native.check(native.lib().gg_cg_profile(self.h, int(bool(enable))), "gg_cg_profile")
+
+    def profile_read(self):
+        """(profiled matvecs, [summed ms per mode-product position]) (synchronising)."""
+        from . import native
+        d = len(self._dk._keep)
+        nm = ctypes.c_int()
+        buf = (ctypes.c_double * 16)()
+        native.check(native.lib().gg_cg_profile_read(self.h, ctypes.byref(nm), buf, 16),
+                     "gg_cg_profile_read")
+        return nm.value, [buf[k] for k in range(d)]
+
     def __del__(self):
         try:
             from . import native

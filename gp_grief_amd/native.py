@@ -56,6 +56,9 @@ SIGNATURES = {
     "gg_cg_iterate": [_vp, ctypes.c_int, ctypes.c_int, _vp],
     "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
+    "gg_cg_profile": [_vp, ctypes.c_int],
+    "gg_cg_profile_read": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double),
+                           ctypes.c_int],
     "gg_lanczos_probe": [_vp, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                          _c_dp, ctypes.POINTER(ctypes.c_double),
                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), _vp],

@@ -103,6 +103,12 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
+/* Live timing: while enabled, every gg_cg_iterate matvec records HIP events
+ * around each of its d mode products on the CG stream.  profile_read
+ * (synchronising) returns the number of profiled matvecs and, per mode
+ * product position k, the summed duration in ms.  Enabling resets.        */
+int gg_cg_profile(gg_cg* cg, int enable);
+int gg_cg_profile_read(gg_cg* cg, int* n_matvecs, double* mode_ms, int mode_ms_len);
 
 /* ----------------------------------------------- Lanczos (SLQ log-det, P1)
  * k steps of three-term Lanczos on (K + shift I) from z / ||z|| where z is the

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 tag=${1:-pmc}
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
-args="--steps 2 --warmup 1 --cpu-baseline off --matvec-reps 1"
+args="--steps 2 --warmup 1 --cpu-baseline off"
 scripts/gpu_step.sh ${tag}_pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_${tag}_fetch -o run --output-format csv -- python bench.py $args; rc=$?
 ok $rc || exit $rc
 scripts/gpu_step.sh ${tag}_pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_${tag}_write -o run --output-format csv -- python bench.py $args; rc=$?
