@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--dims", type=int, default=4)
     ap.add_argument("--sigma2", type=float, default=0.01)
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--recurrence", default="fused", choices=["fused", "textbook"])
     return ap.parse_args()
 
 
@@ -140,7 +141,7 @@ def run_sharded(a, world, rank, torch, dev, dist):
     }
 
 
-KERNEL_NAME = "gg::mode_product_kernel<13, 4, 3, false, 3, true, 1, 2>"
+KERNEL_NAME = "gg::mode_product_kernel<13, 4, 3, 0, 3, true, 1, 2, 0>"
 
 
 def pmc_traffic(m, d):
@@ -208,7 +209,7 @@ def main():
     K = gg.tensors.KronMatrix(F, sym=True)
     n = m ** d
     y = grid_rhs_device(m, d, torch, dev)
-    solver = gg.linalg.KronCG(K, s)
+    solver = gg.linalg.KronCG(K, s, recurrence=a.recurrence)
     solver.start(y, rtol=0.0, atol=0.0)   # never "converges": exactly the steps asked for
     torch.cuda.synchronize()
 
@@ -238,16 +239,25 @@ def main():
     assert it == a.warmup + a.steps, (it, a.warmup, a.steps)
     assert np.isfinite(res)
 
-    # dominant kernel: the plain mode product (positions 2..d of each matvec;
-    # position 1 is the CG-fused instantiation, reported separately)
-    mv_ms = sum(mode_ms) / n_mv
-    launch_ms = sum(mode_ms[1:]) / (n_mv * (d - 1))
-    fused_ms = mode_ms[0] / n_mv
+    # dominant kernel: the plain mode product.  Positions of a matvec: 0 is the
+    # CG-fused first product (prologue), 1 carries the fused x-update side
+    # job, d-1 the fused epilogue (shift, p.q / r.q / q.q); the plain ones are
+    # 1..d-2 (textbook) or 2..d-2 (fused).
+    per_pos = [t / n_mv for t in mode_ms]
+    plain = list(range(2 if solver.recurrence == "fused" else 1, d - 1)) or [d - 1]
+    launch_ms = sum(per_pos[k] for k in plain) / len(plain)
+    mv_ms = sum(per_pos)
     flop_launch = 2.0 * n * m
     achieved_tf = flop_launch / (launch_ms * 1e-3) / 1e12
     traffic, traffic_src = pmc_traffic(m, d)
+    # algorithmic HBM bytes of one iteration (8 B per element per pass):
+    # d mode products read + write 2N each; CG vectors (textbook) p-update
+    # r, p -> p 3N; +s p / p.q read p 1N; x/r update 6N.  Fused: the same
+    # vector passes ride on the mode products (first: r, q, p -> r, p; second:
+    # x, p -> x; last: p, r): 10N either way (+ one closing update per
+    # iterate() call in the fused case).
     mv_bytes = 8.0 * n * (2 * d + 1)
-    vec_bytes = 8.0 * n * (3 + 6 + 1)   # p-update 3N, x/r update 6N (+ q read in matvec epilogue 1N)
+    it_bytes = 8.0 * n * (2 * d + 10)
     result = {
         "metric": "CG iters/sec + Kron-matvec achieved HBM GB/s, 4D RBF grid 200^4",
         "value": a.steps / dt,
@@ -264,6 +274,7 @@ def main():
         "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d"
                                % (m, d, s, n),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
+                   "cg_recurrence": solver.recurrence,
                    "parallelism": "single-gpu"},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_MFMA_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_MFMA_PEAK_TFLOPS,
@@ -273,12 +284,14 @@ def main():
                      "launch_ms_source": "HIP events around each launch in the timed region",
                      "algorithmic_bytes_per_launch": 16.0 * n,
                      "flop_per_launch": flop_launch},
-        "cg_fused_mode_product_ms": fused_ms,
+        "mode_product_ms_by_position": per_pos,
         "matvec_ms": mv_ms,
+        "matvec_tflops": 2.0 * n * m * d / (mv_ms * 1e-3) / 1e12,
         "matvec_hbm_gbs": mv_bytes / (mv_ms * 1e-3) / 1e9,
         "matvec_hbm_frac": mv_bytes / (mv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        "cg_vector_ms": 1e3 * dt / a.steps - mv_ms,
-        "cg_vector_algorithmic_bytes": vec_bytes,
+        "iteration_algorithmic_bytes": it_bytes,
+        "iteration_hbm_gbs": it_bytes / (dt / a.steps) / 1e9,
+        "outside_mode_products_ms": 1e3 * dt / a.steps - mv_ms,
     }
     if rank == 0 and world == 1 and a.cpu_baseline == "auto":
         del solver, y

@@ -76,13 +76,33 @@ struct CgScalars {
   int iters;        // completed iterations
   int done;         // 1 = converged / stopped: every kernel becomes a no-op
   int first;        // 1 = next p-update is p = r
-  int pad;
+  int pending;      // fused CG: x += alpha p, r -= alpha q not yet applied
+  double rq, qq;    // fused CG: r.q and q.q of the last matvec
 };
 
-// Fused CG direction update for the first mode product (gg_kron.hip).
-struct CgPrologue {
-  const double* r;
-  const CgScalars* sc;
+// Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
+// optional (nullptr = off); kron_apply hands each field to the launch it
+// belongs to.
+struct MpFuse {
+  // CG prologue of the first mode product: X holds p_old, the MFMA A operand
+  // is p_new = r + beta p_old (r = b on the first iteration), written to
+  // p_out (== X in place for the textbook recurrence).  Fused recurrence
+  // (q_old != nullptr): when sc->pending, first r -= alpha q_old (written
+  // back) and the block's partial r.r goes to rr_part.
+  double* r = nullptr;
+  const double* q_old = nullptr;
+  double* p_out = nullptr;
+  const CgScalars* sc = nullptr;
+  double* rr_part = nullptr;
+  // side job of the second mode product (fused CG): x += alpha p_side over
+  // this workgroup's slice [blk * schunk, (blk + 1) * schunk) of sn elements
+  double* sx = nullptr;
+  const double* sp = nullptr;
+  int64_t sn = 0, schunk = 0;
+  // last mode product: partial r.q and q.q next to p.q (fused CG); the three
+  // partial arrays are pstride apart
+  const double* er = nullptr;
+  int64_t pstride = 0;
 };
 
 // Output address map of a mode product (see gg_kron.hip epilogue):

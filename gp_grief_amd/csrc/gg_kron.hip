@@ -46,21 +46,31 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 // so the L2 latency of the factor fragments and the HBM latency of X hide
 // under 8*JT MFMAs (64 cycles each) per wave.
 //
-// CGP = true fuses CG's direction update into the first mode product: the A
-// operand is p_new = beta * p + r (p_new = r on the first iteration, selected,
-// so an uninitialised p never leaks in), written back in place; each element
-// is read and written by exactly one lane.
+// CGP fuses CG's direction update into the first mode product (MpFuse):
+//   CGP = 1 (textbook recurrence): the A operand is p_new = beta * p + r
+//           (p_new = r on the first iteration, selected, so an uninitialised p
+//           never leaks in), written back in place;
+//   CGP = 2 (fused recurrence, see gg_vec.hip): when the previous iteration's
+//           updates are pending, r -= alpha q_old first (written back, r.r
+//           partial per workgroup), then p_new = r + beta p_old goes to a
+//           second p buffer.
+// Each element is read and written by exactly one lane (kSplit = 1).
 //
 // kSplit = 2 splits the output columns of a strip over two waves (JT tiles
 // each): half the accumulators per wave, so two workgroups fit a CU and one
 // workgroup's prologue / epilogue overlaps the other's MFMAs.
-template <int JT, int kWaves, int kKC, bool CGP, int kMinW, bool kIdent, int kSplit, int kOpt>
+//
+// kEpi = 2 (fused CG, last mode product): the epilogue also reads r and
+// accumulates r.q and q.q next to p.q (MpFuse::er); a smaller load batch
+// keeps the extra loads within the register budget.
+template <int JT, int kWaves, int kKC, int CGP, int kMinW, bool kIdent, int kSplit, int kOpt,
+          int kEpi = 0>
 __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
-    const int* __restrict__ skip, const double* __restrict__ R,
-    const CgScalars* __restrict__ sc, double* Pout, OutMap om) {
+    const int* __restrict__ skip, OutMap om, MpFuse fz) {
+  static_assert(CGP == 0 || kSplit == 1, "the CG prologue needs one wave per element");
   if (skip != nullptr && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JTL * 64
   constexpr int JTL = JT * kSplit;                        // tiles staged per launch
@@ -105,6 +115,9 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   const int64_t aoff0 = (int64_t)krow * M + bclamp;
   const int64_t alast = (int64_t)(q - 1) * M + bclamp;
   const int64_t achunk = (int64_t)kKC * m4;
+  double* __restrict__ Rg = fz.r;
+  const double* __restrict__ Qg = fz.q_old;
+  double* Pout = fz.p_out;
 
   // kOpt & 2: the factor chunk goes global -> LDS directly (global_load_lds,
   // lane-linear 1 KiB per wave instruction), no staging registers
@@ -139,25 +152,27 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 // A fragments: unconditional loads; only the last chunk clamps the row to
 // q - 1.  The mask (rows past q, strips past M) is applied when the
 // registers are consumed, so no load is followed by a wait.
-#define GG_A_LOAD(c, a, rr)                                                           \
+#define GG_A_LOAD(c, a, rr, qq)                                                       \
   do {                                                                                \
     int64_t o_ = aoff0 + (int64_t)(c) * achunk;                                       \
     if ((c) == nchunks - 1) {                                                         \
       _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                            \
         const int64_t oc_ = o_ < alast ? o_ : alast;                                  \
         a[s_] = X[oc_];                                                               \
-        if (CGP) rr[s_] = R[oc_];                                                     \
+        if (CGP) rr[s_] = Rg[oc_];                                                    \
+        if (CGP == 2) qq[s_] = Qg[oc_];                                               \
         o_ += m4;                                                                     \
       }                                                                               \
     } else {                                                                          \
       _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                            \
         a[s_] = X[o_];                                                                \
-        if (CGP) rr[s_] = R[o_];                                                      \
+        if (CGP) rr[s_] = Rg[o_];                                                     \
+        if (CGP == 2) qq[s_] = Qg[o_];                                                \
         o_ += m4;                                                                     \
       }                                                                               \
     }                                                                                 \
   } while (0)
-#define GG_A_MASK(c, a, rr)                                                           \
+#define GG_A_MASK(c, a, rr, qq)                                                       \
   do {                                                                                \
     const int ks0_ = (c) * kKC;                                                       \
     _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                              \
@@ -165,8 +180,17 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       const bool ok_ = bvalid && k_ < q;                                              \
       double v_ = a[s_];                                                              \
       if (CGP) {                                                                      \
-        v_ = cg_first ? rr[s_] : fma(cg_beta, v_, rr[s_]);                            \
-        if (ok_ && hp == 0) Pout[(int64_t)k_ * M + brow] = v_;                        \
+        double r_ = rr[s_];                                                           \
+        const int64_t e_ = (int64_t)k_ * M + brow;                                    \
+        if (CGP == 2 && cg_pending) {                                                 \
+          r_ = r_ - cg_alpha * qq[s_];                                                \
+          if (ok_) {                                                                  \
+            Rg[e_] = r_;                                                              \
+            rr_acc = fma(r_, r_, rr_acc);                                             \
+          }                                                                           \
+        }                                                                             \
+        v_ = cg_first ? r_ : fma(cg_beta, v_, r_);                                    \
+        if (ok_ && hp == 0) Pout[e_] = v_;                                            \
       }                                                                               \
       a[s_] = ok_ ? v_ : 0.0;                                                         \
     }                                                                                 \
@@ -176,18 +200,22 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 #pragma unroll
   for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 
-  double a_cur[kKC], a_nxt[kKC], r_cur[kKC], r_nxt[kKC];
+  double a_cur[kKC], a_nxt[kKC], r_cur[kKC], r_nxt[kKC], q_cur[kKC], q_nxt[kKC];
   double stx[kPerT], sty[kPerT];
-  bool cg_first = false;
-  double cg_beta = 0.0;
+  bool cg_first = false, cg_pending = false;
+  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0;
   if (CGP) {
-    cg_first = sc->first != 0;
-    cg_beta = sc->beta;
+    cg_first = fz.sc->first != 0;
+    cg_beta = fz.sc->beta;
+    if (CGP == 2) {
+      cg_pending = fz.sc->pending != 0;
+      cg_alpha = fz.sc->alpha;
+    }
   }
   GG_STAGE_LOAD(0, st);
-  GG_A_LOAD(0, a_cur, r_cur);
+  GG_A_LOAD(0, a_cur, r_cur, q_cur);
   GG_STAGE_STORE(0, st);
-  GG_A_MASK(0, a_cur, r_cur);
+  GG_A_MASK(0, a_cur, r_cur, q_cur);
   __syncthreads();
 
   // Per chunk: the first k-step's MFMAs are placed before the next chunk's
@@ -203,7 +231,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
         if (kOpt & 1) __builtin_amdgcn_sched_barrier(0);
         if (more) {
           GG_STAGE_LOAD(c + 1, st);
-          GG_A_LOAD(c + 1, a_nxt, r_nxt);
+          GG_A_LOAD(c + 1, a_nxt, r_nxt, q_nxt);
         }
         if (kOpt & 1) __builtin_amdgcn_sched_barrier(0);
       }
@@ -223,11 +251,16 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       for (int s = 0; s < kKC; ++s) {
         a_cur[s] = a_nxt[s];
         if (CGP) r_cur[s] = r_nxt[s];
+        if (CGP == 2) q_cur[s] = q_nxt[s];
       }
-      GG_A_MASK(c + 1, a_cur, r_cur);
+      GG_A_MASK(c + 1, a_cur, r_cur, q_cur);
     }
     __syncthreads();
   }
+#undef GG_STAGE_LOAD
+#undef GG_STAGE_STORE
+#undef GG_A_LOAD
+#undef GG_A_MASK
 
   // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
   // Output address = rowoff(row) + coloff(j): the identity map is row * p + j;
@@ -256,7 +289,10 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const int64_t jg = j / om.cg;
     return jg * om.gs + (j - jg * om.cg);
   };
-  double dsum = 0.0;
+  double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
+  const double* __restrict__ er = fz.er;
+  constexpr bool edots = kEpi == 2;
+  constexpr int kEB = edots ? 2 : kEpiBatch;
   if (xs == nullptr) {
 #pragma unroll
     for (int t = 0; t < JT; ++t) {
@@ -270,18 +306,22 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
     // does not serialise one load round trip per output element
 #pragma unroll
-    for (int t0 = 0; t0 < JT; t0 += kEpiBatch) {
-      double xv[kEpiBatch][4];
+    for (int t0 = 0; t0 < JT; t0 += kEB) {
+      double xv[kEB][4], ev[kEB][4];
 #pragma unroll
-      for (int tb = 0; tb < kEpiBatch; ++tb) {
+      for (int tb = 0; tb < kEB; ++tb) {
         const int t = t0 + tb < JT ? t0 + tb : JT - 1;
         const bool cok = t0 + tb < JT && colj(t) < p;
         const int64_t co = coloff(t);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xv[tb][r] = (rowok[r] && cok) ? xs[rowoff[r] + co] : 0.0;
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = rowok[r] && cok;
+          xv[tb][r] = ok ? xs[rowoff[r] + co] : 0.0;
+          ev[tb][r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+        }
       }
 #pragma unroll
-      for (int tb = 0; tb < kEpiBatch; ++tb) {
+      for (int tb = 0; tb < kEB; ++tb) {
         const int t = t0 + tb;
         if (t < JT) {
           const bool cok = colj(t) < p;
@@ -291,6 +331,10 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
             if (rowok[r] && cok) {
               const double v = fma(shift, xv[tb][r], acc[t][r]);
               dsum = fma(xv[tb][r], v, dsum);
+              if (edots) {
+                rqsum = fma(ev[tb][r], v, rqsum);
+                qqsum = fma(v, v, qqsum);
+              }
               Y[rowoff[r] + co] = v;
             }
           }
@@ -298,56 +342,103 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       }
     }
   }
-  if (dot_partials != nullptr) {
+  // ---- per-workgroup partial sums: p.q (+ r.q, q.q) of the epilogue, r.r of
+  // the fused prologue.  The k-loop ended with a barrier: LDS is free.
+  const bool want_dot = dot_partials != nullptr;
+  const bool want_rr = CGP == 2 && fz.rr_part != nullptr;
+  if (want_dot || want_rr) {
+    double v4[4] = {dsum, rqsum, qqsum, rr_acc};
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off, 64);
-    // the k-loop ended with a barrier: LDS is free
-    if (lane == 0) lds[wave] = dsum;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v4[i] += __shfl_xor(v4[i], off, 64);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lds[4 * wave + i] = v4[i];
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 4) {
+      const int i = threadIdx.x;
       double s = 0.0;
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) s += lds[w];
-      dot_partials[blockIdx.x] = s;
+      for (int w = 0; w < kWaves; ++w) s += lds[4 * w + i];
+      if (i == 0 && want_dot) dot_partials[blockIdx.x] = s;
+      if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blockIdx.x] = s;
+      if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blockIdx.x] = s;
+      if (i == 3 && want_rr) fz.rr_part[blockIdx.x] = s;
+    }
+  }
+  // ---- side job (fused CG, second mode product): x += alpha p_old over this
+  // workgroup's slice.  The MFMA-bound kernel has HBM headroom; the other
+  // workgroups of the CU keep the matrix cores busy meanwhile.
+  if (fz.sx != nullptr && fz.sc->pending) {
+    const double al = fz.sc->alpha;
+    const int64_t lo = (int64_t)blockIdx.x * fz.schunk;
+    const int64_t hi = min(fz.sn, lo + fz.schunk);
+    double* __restrict__ sx = fz.sx;
+    const double* __restrict__ sp = fz.sp;
+    constexpr int kB = 4;
+    int64_t i = lo + 2 * threadIdx.x;
+    for (; i + 2 * kThreads * (kB - 1) + 1 < hi; i += 2 * kThreads * kB) {
+      double2 xv2[kB], pv2[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        xv2[u] = *reinterpret_cast<const double2*>(sx + i + 2 * kThreads * u);
+        pv2[u] = *reinterpret_cast<const double2*>(sp + i + 2 * kThreads * u);
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        xv2[u].x += al * pv2[u].x;
+        xv2[u].y += al * pv2[u].y;
+        *reinterpret_cast<double2*>(sx + i + 2 * kThreads * u) = xv2[u];
+      }
+    }
+    for (; i < hi; i += 2 * kThreads) {
+      sx[i] += al * sp[i];
+      if (i + 1 < hi) sx[i + 1] += al * sp[i + 1];
     }
   }
 }
 
 typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
-                              int, int, const double*, double, double*, const int*,
-                              const double*, const CgScalars*, double*, OutMap);
+                              int, int, const double*, double, double*, const int*, OutMap,
+                              MpFuse);
 
 // Launch configuration of one mode product: waves per workgroup, k-steps per
 // LDS chunk.  The default -- 4-wave workgroups (one wave per SIMD), 3 k-steps
 // per chunk, three independent workgroups per CU, factor chunks staged by
 // global_load_lds -- was chosen by A/B on MI355X (profiles/r01_*_mode_variants):
 // three workgroups drift apart, so one's barrier or epilogue overlaps the
-// others' MFMAs.  GG_MP_VARIANT selects another for tuning runs.
+// others' MFMAs.  GG_MP_VARIANT selects another for tuning runs (plain mode
+// products only; the CG-fused ones always use the default).
 struct ModeConfig {
   mode_kernel_t fn;
   int waves, kc, split, jtl;  // jtl: tiles staged per launch (LDS size)
 };
 
 // JT = output tiles of the launch; a split config gives each wave ceil(JT/2)
-template <int JT, int W, int KC, bool CGP, int MINW, int SPLIT, int OPT>
+template <int JT, int W, int KC, int CGP, int MINW, int SPLIT, int OPT, int EPI = 0>
 static ModeConfig cfg() {
   constexpr int JW = (JT + SPLIT - 1) / SPLIT;
-  return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT>, W, KC, SPLIT,
-                    JW * SPLIT};
+  return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT, EPI>, W, KC,
+                    SPLIT, JW * SPLIT};
 }
 
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
-template <int JT, bool CGP>
-static ModeConfig config_for(int variant) {
+// cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG epilogue
+template <int JT>
+static ModeConfig config_for(int variant, int cgp) {
+  if (cgp == 1) return cfg<JT, 4, 3, 1, 3, 1, 2>();
+  if (cgp == 2) return cfg<JT, 4, 3, 2, 3, 1, 2>();
+  if (cgp == 3) return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
   switch (variant) {
-    case 1: return cfg<JT, 12, 4, CGP, 3, 1, 2>();
-    case 2: return cfg<JT, 12, 4, CGP, 3, 1, 0>();  // register-staged factor chunks
-    case 3: return cfg<JT, 4, 4, CGP, 3, 1, 2>();
-    case 4: return cfg<JT, 4, 2, CGP, 3, 1, 2>();
-    case 5: return cfg<JT, 2, 2, CGP, 3, 1, 2>();
-    case 6: return cfg<JT, 8, 4, CGP, 4, 2, 2>();   // columns split over two waves
-    case 7: return cfg<JT, 12, 4, CGP, 3, 1, 3>();  // + sched_barrier around the prefetch
-    default: return cfg<JT, 4, 3, CGP, 3, 1, 2>();
+    case 1: return cfg<JT, 12, 4, 0, 3, 1, 2>();
+    case 2: return cfg<JT, 12, 4, 0, 3, 1, 0>();  // register-staged factor chunks
+    case 3: return cfg<JT, 4, 4, 0, 3, 1, 2>();
+    case 4: return cfg<JT, 4, 2, 0, 3, 1, 2>();
+    case 5: return cfg<JT, 2, 2, 0, 3, 1, 2>();
+    case 6: return cfg<JT, 8, 4, 0, 4, 2, 2>();   // columns split over two waves
+    case 7: return cfg<JT, 12, 4, 0, 3, 1, 3>();  // + sched_barrier around the prefetch
+    default: return cfg<JT, 4, 3, 0, 3, 1, 2>();
   }
 }
 constexpr int kNumVariants = 8;
@@ -357,24 +448,24 @@ static int mode_variant() {
   return e ? atoi(e) : 0;
 }
 
-static ModeConfig select_kernel(int jt, int variant, bool cgp) {
+static ModeConfig select_kernel(int jt, int variant, int cgp) {
   switch (jt) {
-    case 1: return cgp ? config_for<1, true>(variant) : config_for<1, false>(variant);
-    case 2: return cgp ? config_for<2, true>(variant) : config_for<2, false>(variant);
-    case 3: return cgp ? config_for<3, true>(variant) : config_for<3, false>(variant);
-    case 4: return cgp ? config_for<4, true>(variant) : config_for<4, false>(variant);
-    case 5: return cgp ? config_for<5, true>(variant) : config_for<5, false>(variant);
-    case 6: return cgp ? config_for<6, true>(variant) : config_for<6, false>(variant);
-    case 7: return cgp ? config_for<7, true>(variant) : config_for<7, false>(variant);
-    case 8: return cgp ? config_for<8, true>(variant) : config_for<8, false>(variant);
-    case 9: return cgp ? config_for<9, true>(variant) : config_for<9, false>(variant);
-    case 10: return cgp ? config_for<10, true>(variant) : config_for<10, false>(variant);
-    case 11: return cgp ? config_for<11, true>(variant) : config_for<11, false>(variant);
-    case 12: return cgp ? config_for<12, true>(variant) : config_for<12, false>(variant);
-    case 13: return cgp ? config_for<13, true>(variant) : config_for<13, false>(variant);
-    case 14: return cgp ? config_for<14, true>(variant) : config_for<14, false>(variant);
-    case 15: return cgp ? config_for<15, true>(variant) : config_for<15, false>(variant);
-    case 16: return cgp ? config_for<16, true>(variant) : config_for<16, false>(variant);
+    case 1: return config_for<1>(variant, cgp);
+    case 2: return config_for<2>(variant, cgp);
+    case 3: return config_for<3>(variant, cgp);
+    case 4: return config_for<4>(variant, cgp);
+    case 5: return config_for<5>(variant, cgp);
+    case 6: return config_for<6>(variant, cgp);
+    case 7: return config_for<7>(variant, cgp);
+    case 8: return config_for<8>(variant, cgp);
+    case 9: return config_for<9>(variant, cgp);
+    case 10: return config_for<10>(variant, cgp);
+    case 11: return config_for<11>(variant, cgp);
+    case 12: return config_for<12>(variant, cgp);
+    case 13: return config_for<13>(variant, cgp);
+    case 14: return config_for<14>(variant, cgp);
+    case 15: return config_for<15>(variant, cgp);
+    case 16: return config_for<16>(variant, cgp);
     default: throw Error(GG_ERR_VALUE, "bad tile count");
   }
 }
@@ -438,7 +529,11 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
 
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out, const CgPrologue* pro, hipEvent_t* ev) {
+                int64_t* n_partials_out, const MpFuse* cg, int cgp, hipEvent_t* ev) {
+  // cg / cgp (optional): CG fusions (MpFuse).  cgp = 1: textbook prologue on
+  // the first mode product (p updated in place in x); cgp = 2: the fused
+  // recurrence -- prologue (p_new -> cg->p_out), side job on the second mode
+  // product, r.q / q.q partials on the last.
   // ev (optional, d + 1 events): recorded before the first mode product and
   // after each one, for live per-launch timing (gg_cg_profile)
   const std::vector<Factor>& fs = transpose ? K->bwd : K->fwd;
@@ -448,7 +543,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   GG_REQUIRE(x != y, GG_ERR_VALUE, "x and y must not alias");
   if (shift != 0.0 || dot_partials != nullptr)
     GG_REQUIRE(K->n_rows == K->n_cols, GG_ERR_VALUE, "shift needs a square operator");
+  if (cg == nullptr) cgp = 0;
   const int d = (int)fs.size();
+  GG_REQUIRE(cgp != 2 || d >= 2, GG_ERR_VALUE, "the fused CG recurrence needs d >= 2");
   int64_t size = n_in;
   const double* src = x;
   int64_t np_total = 0;
@@ -468,25 +565,50 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
     const bool last = (k == d - 1);
     const int variant = mode_variant();
     if (M > 0) {
+      const double* step_src = src;
       for (int jt0 = 0; jt0 < f.JT; jt0 += kMaxJT) {
         const int jt = std::min(kMaxJT, f.JT - jt0);
-        // the fused CG direction update runs once, in the first launch of step 0
-        const bool cgp = pro != nullptr && k == 0 && jt0 == 0;
-        const ModeConfig mc = select_kernel(jt, variant, cgp);
+        MpFuse fz;
+        // the fused CG direction update runs once, in the first launch of
+        // step 0; the later launches of that step read the updated p
+        const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? cgp : 0;
+        const bool epi = cgp == 2 && last && dot_partials != nullptr;
+        const ModeConfig mc = select_kernel(jt, variant, epi ? 3 : pro);
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
+        if (pro) {
+          fz.r = cg->r;
+          fz.sc = cg->sc;
+          fz.p_out = pro == 1 ? const_cast<double*>(x) : cg->p_out;
+          if (pro == 2) {
+            fz.q_old = cg->q_old;
+            fz.rr_part = cg->rr_part;
+          }
+        }
+        if (cgp == 2 && k == 1 && jt0 == 0) {
+          fz.sc = cg->sc;
+          fz.sx = cg->sx;
+          fz.sp = cg->sp;
+          fz.sn = cg->sn;
+          fz.schunk = 2 * ceil_div(cg->sn, 2 * nblk);
+        }
         double* parts = nullptr;
         if (last && dot_partials != nullptr) {
           parts = dot_partials + np_total;
           np_total += nblk;
+          if (cgp == 2) {
+            fz.er = cg->er;
+            fz.pstride = cg->pstride;
+          }
         }
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)nblk), dim3(mc.waves * 64),
-                           mode_lds_bytes(mc), stream, src, dst, f.frag, M, (int)f.q,
+                           mode_lds_bytes(mc), stream, step_src, dst, f.frag, M, (int)f.q,
                            (int)f.p, f.KS, f.JT, jt0,
-                           last && (shift != 0.0 || parts) ? x : nullptr, shift, parts, skip,
-                           cgp ? pro->r : nullptr, cgp ? pro->sc : nullptr,
-                           cgp ? const_cast<double*>(x) : nullptr, OutMap::ident());
+                           last && (shift != 0.0 || parts) ? (cgp == 2 ? cg->p_out : x)
+                                                           : nullptr,
+                           shift, parts, skip, OutMap::ident(), fz);
         GG_LAUNCH_CHECK();
+        if (pro) step_src = fz.p_out;
       }
     }
     (void)out_size;
@@ -508,6 +630,14 @@ int64_t kron_partials_needed(const gg_kron* K, bool transpose) {
   return ceil_div(M, 2 * 16) * ceil_div(f.JT, kMaxJT);
 }
 
+// workgroups of the (forward) first mode product's first launch with the
+// fused CG prologue: the length of its r.r partial array
+int64_t kron_prologue_blocks(const gg_kron* K) {
+  const Factor& f = K->fwd[0];
+  const ModeConfig mc = select_kernel(std::min(kMaxJT, f.JT), 0, 2);
+  return ceil_div(K->n_cols / f.q, (int64_t)(mc.waves / mc.split) * 16);
+}
+
 int64_t kron_work_elems(const gg_kron* K, bool transpose) {
   const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
   const int64_t mx = transpose ? K->max_inter_bwd : K->max_inter_fwd;
@@ -522,8 +652,8 @@ static void set_lds_limits() {
   if (done) return;
   for (int v = 0; v < kNumVariants; ++v)
     for (int jt = 1; jt <= kMaxJT; ++jt)
-      for (int cgp = 0; cgp < 2; ++cgp) {
-        const ModeConfig mc = select_kernel(jt, v, cgp != 0);
+      for (int cgp = 0; cgp < 4; ++cgp) {
+        const ModeConfig mc = select_kernel(jt, v, cgp);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)mode_lds_bytes(mc)));
@@ -593,7 +723,7 @@ int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double*
     GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
     GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
     gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
-                   gg::as_stream(stream), nullptr, nullptr, nullptr);
+                   gg::as_stream(stream), nullptr, nullptr, 0, nullptr);
   });
 }
 
@@ -626,10 +756,10 @@ constexpr int kDistWaves = 4, kDistKC = 3;  // the single-GPU default
 
 template <int JT>
 static mode_kernel_t dist_kernel(bool cgp, bool ident) {
-  if (cgp && ident) return mode_product_kernel<JT, kDistWaves, kDistKC, true, 3, true, 1, 2>;
-  if (cgp) return mode_product_kernel<JT, kDistWaves, kDistKC, true, 3, false, 1, 2>;  // d == 2: fused + mapped
-  if (ident) return mode_product_kernel<JT, kDistWaves, kDistKC, false, 3, true, 1, 2>;
-  return mode_product_kernel<JT, kDistWaves, kDistKC, false, 3, false, 1, 2>;
+  if (cgp && ident) return mode_product_kernel<JT, kDistWaves, kDistKC, 1, 3, true, 1, 2>;
+  if (cgp) return mode_product_kernel<JT, kDistWaves, kDistKC, 1, 3, false, 1, 2>;  // d == 2: fused + mapped
+  if (ident) return mode_product_kernel<JT, kDistWaves, kDistKC, 0, 3, true, 1, 2>;
+  return mode_product_kernel<JT, kDistWaves, kDistKC, 0, 3, false, 1, 2>;
 }
 
 static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {
@@ -656,7 +786,7 @@ static mode_kernel_t select_dist(int jt, bool cgp, bool ident) {
 
 
 static void dist_step(const Factor& f, const double* X, double* Y, int64_t M, OutMap om,
-                      const CgPrologue* pro, double* pin, hipStream_t s) {
+                      const MpFuse* pro, hipStream_t s) {
   if (M <= 0) return;
   GG_REQUIRE(f.JT <= kMaxJT, GG_ERR_VALUE, "sharded operator supports factors up to 256");
   const bool cgp = pro != nullptr;
@@ -672,8 +802,7 @@ static void dist_step(const Factor& f, const double* X, double* Y, int64_t M, Ou
   const int64_t nblk = ceil_div(M, (int64_t)kDistWaves * 16);
   hipLaunchKernelGGL(fn, dim3((unsigned)nblk), dim3(kDistWaves * 64), lds, s, X, Y, f.frag, M,
                      (int)f.q, (int)f.p, f.KS, f.JT, 0, nullptr, 0.0, nullptr,
-                     cgp ? &pro->sc->done : nullptr, cgp ? pro->r : nullptr,
-                     cgp ? pro->sc : nullptr, cgp ? pin : nullptr, om);
+                     cgp ? &pro->sc->done : nullptr, om, cgp ? *pro : MpFuse());
   GG_LAUNCH_CHECK();
 }
 
@@ -739,7 +868,10 @@ int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send
     hipStream_t s = gg::as_stream(stream);
     const int d = D->d;
     const int G = D->world;
-    const gg::CgPrologue pro{cg_r_dev, reinterpret_cast<const gg::CgScalars*>(cg_scalars_dev)};
+    gg::MpFuse pro;
+    pro.r = const_cast<double*>(cg_r_dev);  // read only (textbook prologue)
+    pro.sc = reinterpret_cast<const gg::CgScalars*>(cg_scalars_dev);
+    pro.p_out = x_local_dev;                // p updated in place
     const int64_t nl = D->n_local;
     const double* src = x_local_dev;
     for (int k = 1; k < d; ++k) {
@@ -763,7 +895,7 @@ int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send
         dst = ((d - 1 - k) % 2 == 0) ? send_dev : work_dev;
       }
       const bool fuse = (k == 1) && cg_r_dev != nullptr;
-      gg::dist_step(f, src, dst, M, om, fuse ? &pro : nullptr, x_local_dev, s);
+      gg::dist_step(f, src, dst, M, om, fuse ? &pro : nullptr, s);
       src = dst;
     }
   });
@@ -776,7 +908,7 @@ int gg_kron_dist_phase2(const gg_kron_dist* D, const double* recv_dev, double* s
     const gg::Factor& f = D->f[0];
     const int64_t C = D->n_local / f.q;  // = R / G
     const gg::OutMap om{0, D->s0, C * D->s0, C, C, 0, 0};
-    gg::dist_step(f, recv_dev, send_dev, C, om, nullptr, nullptr, gg::as_stream(stream));
+    gg::dist_step(f, recv_dev, send_dev, C, om, nullptr, gg::as_stream(stream));
   });
 }
 

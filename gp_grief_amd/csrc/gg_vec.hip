@@ -16,8 +16,9 @@ namespace gg {
 // defined in gg_kron.hip
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
-                int64_t* n_partials_out, const CgPrologue* pro, hipEvent_t* ev);
+                int64_t* n_partials_out, const MpFuse* cg, int cgp, hipEvent_t* ev);
 int64_t kron_partials_needed(const gg_kron* K, bool transpose);
+int64_t kron_prologue_blocks(const gg_kron* K);
 int64_t kron_work_elems(const gg_kron* K, bool transpose);
 int64_t kron_n(const gg_kron* K);
 int kron_d(const gg_kron* K);
@@ -118,8 +119,8 @@ __global__ __launch_bounds__(1024) void cg_alpha_kernel(const double* __restrict
 __global__ __launch_bounds__(kVecThreads) void cg_xr_update_kernel(
     double* __restrict__ x, double* __restrict__ r, const double* __restrict__ p,
     const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
-    double* __restrict__ partials) {
-  if (sc->done) return;
+    double* __restrict__ partials, int need_pending) {
+  if (sc->done || (need_pending && !sc->pending)) return;
   const double a = sc->alpha;
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -151,8 +152,9 @@ __global__ __launch_bounds__(kVecThreads) void cg_xr_update_kernel(
 
 // rho_prev = rho ; rho = r.r ; beta ; iteration count ; convergence
 __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__ partials,
-                                                      int64_t count, CgScalars* sc) {
-  if (sc->done) return;
+                                                      int64_t count, CgScalars* sc,
+                                                      int need_pending) {
+  if (sc->done || (need_pending && !sc->pending)) return;
   double acc = 0.0;
   for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
   const double s = block_sum(acc);
@@ -162,7 +164,61 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
     sc->beta = s / sc->rho_prev;
     sc->iters += 1;
     sc->first = 0;
+    sc->pending = 0;
     if (!(sqrt(s) >= sc->tol)) sc->done = 1;  // also stops on NaN
+  }
+}
+
+// Fused recurrence, end of iteration j (after the last mode product):
+//   rho_j = r_j.r_j (partials of the first mode product's prologue, which
+//   applied r_j = r_{j-1} - alpha q_{j-1}), stopping test on it;
+//   alpha_j = rho_j / (p_j.q_j);
+//   beta_j = |r_{j+1}|^2 / rho_j with |r_{j+1}|^2 = rho_j - 2 alpha (r.q) +
+//   alpha^2 (q.q), the exact expansion of |r_j - alpha_j q_j|^2.  The true
+//   r_{j+1}.r_{j+1} replaces it in the next iteration (stopping test, alpha).
+// The x / r updates of iteration j stay pending until the next iteration's
+// first two mode products (or gg_cg_iterate's closing update).
+__global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
+    const double* __restrict__ rr_part, int64_t nrr, const double* __restrict__ mv_part,
+    int64_t nmv, int64_t pstride, CgScalars* sc) {
+  if (sc->done) return;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
+    a0 += mv_part[i];
+    a1 += mv_part[pstride + i];
+    a2 += mv_part[2 * pstride + i];
+  }
+  const bool pend = sc->pending != 0;
+  if (pend)
+    for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a3 += rr_part[i];
+  const double pq = block_sum(a0);
+  __syncthreads();
+  const double rq = block_sum(a1);
+  __syncthreads();
+  const double qq = block_sum(a2);
+  __syncthreads();
+  const double rr = block_sum(a3);
+  if (threadIdx.x == 0) {
+    if (pend) {
+      sc->rho_prev = sc->rho;
+      sc->rho = rr;
+      sc->iters += 1;
+      if (!(sqrt(rr) >= sc->tol)) {  // converged (or NaN): x_j, r_j are final
+        sc->done = 1;
+        sc->pending = 0;
+        return;
+      }
+    }
+    const double rho = sc->rho;
+    const double alpha = rho / pq;
+    double rt = rho - 2.0 * alpha * rq + alpha * alpha * qq;
+    sc->pq = pq;
+    sc->rq = rq;
+    sc->qq = qq;
+    sc->alpha = alpha;
+    sc->beta = rt > 0.0 ? rt / rho : 0.0;  // cancellation guard: restart direction
+    sc->first = 0;
+    sc->pending = 1;
   }
 }
 
@@ -178,7 +234,8 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->tol = fmax(atol, rtol * sc->bnorm);
     sc->iters = 0;
     sc->first = 1;
-    sc->alpha = sc->beta = sc->pq = 0.0;
+    sc->pending = 0;
+    sc->alpha = sc->beta = sc->pq = sc->rq = sc->qq = 0.0;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -366,7 +423,11 @@ struct gg_cg {
   double shift = 0.0;
   int64_t n = 0;
   double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
-  double* partials = nullptr;  // device, max(kVecBlocks, matvec partials)
+  double* p2 = nullptr;        // second direction buffer (fused recurrence)
+  bool fused = true;           // recurrence: fused (default) or textbook
+  double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
+  double* rr_part = nullptr;   // device, prologue r.r partials (fused)
+  int64_t rr_count = 0;
   gg::CgScalars* sc = nullptr; // device
   gg::CgScalars* sc_host = nullptr;  // pinned mirror
   const double* b = nullptr;
@@ -485,7 +546,7 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
-    *elems = 3 * n + gg::kron_work_elems(K, false);
+    *elems = 4 * n + gg::kron_work_elems(K, false);
   });
 }
 
@@ -503,10 +564,19 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->r = work_dev;
       cg->p = work_dev + nr;
       cg->q = work_dev + 2 * nr;
-      cg->mv_work = work_dev + 3 * nr;
+      cg->p2 = work_dev + 3 * nr;
+      cg->mv_work = work_dev + 4 * nr;
       cg->mv_partials = gg::kron_partials_needed(K, false);
-      const int64_t np = std::max<int64_t>(gg::kVecBlocks, cg->mv_partials);
+      const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
       GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
+      // the fused recurrence needs d >= 2 and 16-byte aligned vectors (its
+      // side job moves double2); otherwise the textbook recurrence runs
+      cg->fused = gg::kron_d(K) >= 2 && (nr % 2) == 0 &&
+                  (reinterpret_cast<uintptr_t>(work_dev) & 15) == 0;
+      if (cg->fused) {
+        cg->rr_count = gg::kron_prologue_blocks(K);
+        GG_HIP(hipMalloc(&cg->rr_part, cg->rr_count * sizeof(double)));
+      }
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
       GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
@@ -522,6 +592,7 @@ int gg_cg_destroy(gg_cg* cg) {
   return gg::guard([&] {
     if (!cg) return;
     if (cg->partials) (void)hipFree(cg->partials);
+    if (cg->rr_part) (void)hipFree(cg->rr_part);
     if (cg->sc) (void)hipFree(cg->sc);
     if (cg->sc_host) (void)hipHostFree(cg->sc_host);
     for (hipEvent_t e : cg->events) (void)hipEventDestroy(e);
@@ -579,6 +650,39 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
   });
 }
 
+int gg_cg_set_recurrence(gg_cg* cg, int fused) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set the recurrence before gg_cg_start");
+    if (!fused) {
+      cg->fused = false;
+    } else {
+      GG_REQUIRE(cg->rr_part != nullptr, GG_ERR_VALUE,
+                 "the fused recurrence needs d >= 2, an even n and 16-byte aligned work");
+      cg->fused = true;
+    }
+  });
+}
+
+int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && fused, GG_ERR_VALUE, "NULL argument");
+    *fused = cg->fused ? 1 : 0;
+  });
+}
+
+// Textbook recurrence, one iteration:
+//   q = (K + s I) p with p = r + beta p fused into the first mode product
+//   and p.q into the last; alpha; x += alpha p, r -= alpha q, r.r; beta.
+// Fused recurrence, one iteration j (every vector pass rides on a mode
+// product; the matrix cores bound the kernels and HBM has room):
+//   mode product 1: r_j = r_{j-1} - alpha q_{j-1} (in place, r.r partials),
+//                   p_j = r_j + beta p_{j-1} (into the other p buffer);
+//   mode product 2: side job x_j = x_{j-1} + alpha p_{j-1};
+//   mode product d: q_j = K p_j + s p_j, partials p.q, r.q, q.q;
+//   scalars: rho_j, stopping test, alpha_j, beta_j (cg_fused_scalars_kernel).
+// Leaving gg_cg_iterate applies the pending x / r update with the textbook
+// kernels, so the state it leaves (x, r, iteration count) is the textbook's.
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
@@ -586,9 +690,7 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
     const int64_t n = cg->n;
     const int nb = gg::vec_blocks(n);
     if (check_every <= 0) check_every = max_iters;
-    const gg::CgPrologue pro{cg->r, cg->sc};
     for (int it = 0; it < max_iters; ++it) {
-      // p = r + beta p is fused into the first mode product of q = (K + s I) p
       int64_t nparts = 0;
       hipEvent_t* ev = nullptr;
       if (cg->profiling) {
@@ -601,23 +703,56 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         ev = cg->events.data() + cg->events_used;
         cg->events_used = need;
       }
-      gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
-                     &cg->sc->done, s, &nparts, &pro, ev);
-      hipLaunchKernelGGL(gg::cg_alpha_kernel, dim3(1), dim3(1024), 0, s, cg->partials, nparts,
-                         cg->sc);
-      GG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
-                         cg->r, cg->p, cg->q, n, cg->sc, cg->partials);
-      GG_LAUNCH_CHECK();
-      hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
-                         (int64_t)nb, cg->sc);
-      GG_LAUNCH_CHECK();
+      if (cg->fused) {
+        gg::MpFuse fz;
+        fz.r = cg->r;
+        fz.q_old = cg->q;
+        fz.p_out = cg->p2;
+        fz.sc = cg->sc;
+        fz.rr_part = cg->rr_part;
+        fz.sx = cg->x;
+        fz.sp = cg->p;
+        fz.sn = n;
+        fz.er = cg->r;
+        fz.pstride = cg->mv_partials;
+        gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                       &cg->sc->done, s, &nparts, &fz, 2, ev);
+        hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
+                           cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc);
+        GG_LAUNCH_CHECK();
+        std::swap(cg->p, cg->p2);
+      } else {
+        gg::MpFuse fz;
+        fz.r = cg->r;
+        fz.sc = cg->sc;
+        gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                       &cg->sc->done, s, &nparts, &fz, 1, ev);
+        hipLaunchKernelGGL(gg::cg_alpha_kernel, dim3(1), dim3(1024), 0, s, cg->partials, nparts,
+                           cg->sc);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           cg->x, cg->r, cg->p, cg->q, n, cg->sc, cg->partials, 0);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                           (int64_t)nb, cg->sc, 0);
+        GG_LAUNCH_CHECK();
+      }
       if ((it + 1) % check_every == 0 && it + 1 < max_iters) {
         GG_HIP(hipMemcpyAsync(cg->sc_host, cg->sc, sizeof(gg::CgScalars),
                               hipMemcpyDeviceToHost, s));
         GG_HIP(hipStreamSynchronize(s));
         if (cg->sc_host->done) break;
       }
+    }
+    if (cg->fused) {
+      // closing update (no-op unless pending): x += alpha p, r -= alpha q,
+      // rho = r.r, beta, iteration count -- the textbook state
+      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
+                         cg->r, cg->p, cg->q, n, cg->sc, cg->partials, 1);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                         (int64_t)nb, cg->sc, 1);
+      GG_LAUNCH_CHECK();
     }
   });
 }
@@ -667,7 +802,8 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
     for (int j = 0; j < steps; ++j) {
-      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr, nullptr);
+      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr, 0,
+                     nullptr);
       const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
       hipLaunchKernelGGL(gg::lz_axpy_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P,
                          V, n, beta_prev, parts);
@@ -735,6 +871,7 @@ __global__ void cgs_init_kernel(CgScalars* sc, const double* rr, double rtol, do
   sc->tol = fmax(atol, rtol * sc->bnorm);
   sc->iters = 0;
   sc->first = 1;
+  sc->pending = 0;
   sc->alpha = sc->beta = sc->pq = 0.0;
   sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
 }
@@ -849,7 +986,7 @@ int gg_cgs_update(gg_cgs* c, double* x_dev, double* r_dev, const double* p_dev,
     hipStream_t s = gg::as_stream(stream);
     const int nb = gg::vec_blocks(n);
     hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, x_dev,
-                       r_dev, p_dev, q_dev, n, c->sc, c->partials);
+                       r_dev, p_dev, q_dev, n, c->sc, c->partials, 0);
     GG_LAUNCH_CHECK();
     gg::launch_reduce_to(c->partials, nb, out_dev, s);
   });

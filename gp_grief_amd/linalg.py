@@ -82,13 +82,18 @@ class CGResult(object):
 class KronCG(object):
     """Resident CG state for (K + shift I) x = b on one MI355X.
 
-    The operator and all CG vectors (x, r, p, q + one matvec scratch) live in
-    HBM; a CG iteration is 5 kernel launches (p-update, d mode products with
-    the shift and p.q fused into the last, alpha, x/r-update with r.r fused,
-    beta) and no host synchronisation.
+    The operator and all CG vectors (x, r, two p buffers, q + one matvec
+    scratch) live in HBM; no host synchronisation inside an iteration.
+
+    recurrence="fused" (default for d >= 2): an iteration is the d mode
+    products plus one scalar kernel -- r -= alpha q, p = r + beta p (and r.r)
+    ride on the first mode product, x += alpha p on the second, p.q / r.q /
+    q.q on the last; beta comes from |r - alpha q|^2 expanded (gg_vec.hip).
+    recurrence="textbook": scipy's operation order, with a separate
+    x / r update pass.  Both leave iterate() in the textbook state.
     """
 
-    def __init__(self, K, shift):
+    def __init__(self, K, shift, recurrence="fused"):
         from . import device as dev
         from . import native
         self.K = K
@@ -102,6 +107,13 @@ class KronCG(object):
         native.check(L.gg_cg_create(self._dk.h, self.shift, native.dptr(self.work),
                                     ctypes.byref(h)), "gg_cg_create")
         self.h = h
+        if recurrence not in ("fused", "textbook"):
+            raise ValueError("recurrence must be 'fused' or 'textbook'")
+        if recurrence == "textbook":
+            native.check(L.gg_cg_set_recurrence(h, 0), "gg_cg_set_recurrence")
+        f = ctypes.c_int()
+        native.check(L.gg_cg_get_recurrence(h, ctypes.byref(f)))
+        self.recurrence = "fused" if f.value else "textbook"
         self.n = int(K.shape[0])
         self.x = None
 
@@ -118,7 +130,8 @@ class KronCG(object):
 
     def iterate(self, n_iter, check_every=0):
         from . import native
-        native.check(native.lib().gg_cg_iterate(self.h, int(n_iter), int(check_every),
+        n_iter = min(int(n_iter), 2 ** 31 - 1)
+        native.check(native.lib().gg_cg_iterate(self.h, n_iter, min(int(check_every), n_iter),
                                                 native.stream_ptr()), "gg_cg_iterate")
 
     def status(self):
@@ -154,10 +167,12 @@ class KronCG(object):
             pass
 
 
-def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None):
+def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None,
+       recurrence="fused"):
     """Solve (K + shift I) x = b with CG on the device (x0 = 0).
 
-    Same stopping rule and recurrence as scipy.sparse.linalg.cg.  b: numpy
+    Same stopping rule and iterates as scipy.sparse.linalg.cg (recurrence:
+    see KronCG).  b: numpy
     (N,1)/(N,) or a CUDA tensor; x is returned in the same kind.  `callback`
     (e.g. a solver_counter) is called once per completed iteration, after the
     solve, with no arguments beyond the counter protocol (the iterates stay on
@@ -174,16 +189,11 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         maxiter = n * 10
     if check_every is None:
         check_every = 10 if n >= 1 << 20 else 50
-    solver = KronCG(K, shift)
+    solver = KronCG(K, shift, recurrence)
     solver.start(bd, rtol, atol)
-    done = 0
-    while done < maxiter:
-        chunk = min(maxiter - done, check_every)
-        solver.iterate(chunk, check_every=chunk)
-        done += chunk
-        it, conv, res, tol = solver.status()
-        if conv or it < done:  # converged (the kernels no-op past convergence)
-            break
+    # one call: the library polls the device's done flag every check_every
+    # iterations and stops issuing work once converged
+    solver.iterate(maxiter, check_every=check_every)
     it, conv, res, tol = solver.status()
     if callback is not None:
         for _ in range(it):

@@ -94,12 +94,21 @@ int gg_diag_divide(const double* t_dev, double shift, const double* x_dev, doubl
  * Unpreconditioned CG on (K + shift I) x = b, x0 = 0, the recurrence of
  * scipy.sparse.linalg.cg (the reference's solver_counter, linalg.py:53-71, is
  * its iteration callback).  All scalars stay on the device; the host polls
- * convergence every `check_every` iterations.  work_dev: gg_cg_work_elems. */
+ * convergence every `check_every` iterations.  work_dev: gg_cg_work_elems.
+ * Two recurrences (gg_cg_set_recurrence, before gg_cg_start):
+ *   fused (1, the default when d >= 2): every vector update rides on a mode
+ *     product; beta from the exact expansion of |r - alpha q|^2 (the true r.r
+ *     drives the stopping test and alpha) -- same iterates as scipy's up to
+ *     rounding;
+ *   textbook (0): scipy's operation order (separate x / r update pass).
+ * Either way gg_cg_iterate returns in the textbook state (x_k, r_k, k).     */
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems);
 int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out);
 int gg_cg_destroy(gg_cg* cg);
 int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, double atol,
                 gg_stream stream);
+int gg_cg_set_recurrence(gg_cg* cg, int fused);
+int gg_cg_get_recurrence(const gg_cg* cg, int* fused);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
