@@ -39,6 +39,165 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kMaxJT = 16;  // accumulator tiles per launch (<= 256 output columns)
 constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued together
 
+// Epilogue shared by the mode-product kernels: store D (+ shift * x, CG dot
+// partials), per-workgroup partial sums, and the fused-CG side job.  Called
+// after the k-loop's last barrier (LDS is free).
+// blk: the output block (strip group) index of the partial sums and the side
+// job slice.  kRaw: the reduction barrier is a raw s_barrier (LDS DMAs of the
+// next strip may be in flight, cdna_hip_programming.md "Pipelining across
+// barriers"); red: 4 * kWaves doubles of LDS scratch outside any DMA target.
+template <int JT, int kWaves, int kSplit, bool kIdent, int kEpi, int CGP, bool kRaw = false,
+          int kBatch = kEpiBatch>
+__device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restrict__ Y, int64_t M,
+                                          int p, int jt0, const double* __restrict__ xs,
+                                          double shift, double* __restrict__ dot_partials,
+                                          const OutMap& om, const MpFuse& fz, double rr_acc,
+                                          int64_t b0, int hp, double* red, int64_t blk) {
+  constexpr int kThreads = kWaves * 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
+  // Output address = rowoff(row) + coloff(j): the identity map is row * p + j;
+  // the distributed matvec permutes rows / columns into all-to-all order
+  // (OutMap, gg_dist.hip).  Offsets are decomposed once per row and column.
+  const int col = lane & 15;
+  const int64_t rbase = b0 + (lane >> 4);
+  int64_t rowoff[4];
+  bool rowok[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t row = rbase + 4 * r;
+    rowok[r] = row < M;
+    if (kIdent) {
+      rowoff[r] = row * p;
+    } else {
+      const int64_t a_ = row / om.mi, bi = row - a_ * om.mi;
+      const int64_t h = bi / om.cr, br = bi - h * om.cr;
+      rowoff[r] = h * om.hs + a_ * om.as + br * om.cg;
+    }
+  }
+  auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + hp * JT + t) * 16 + col; };
+  auto coloff = [&](int t) -> int64_t {
+    const int64_t j = colj(t);
+    if (kIdent) return j;
+    const int64_t jg = j / om.cg;
+    return jg * om.gs + (j - jg * om.cg);
+  };
+  double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
+  const double* __restrict__ er = fz.er;
+  constexpr bool edots = kEpi == 2;
+  constexpr int kEB = edots ? (kBatch < 2 ? kBatch : 2) : kBatch;
+  if (xs == nullptr) {
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const bool cok = colj(t) < p;
+      const int64_t co = coloff(t);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
+    }
+  } else {
+    // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
+    // does not serialise one load round trip per output element
+#pragma unroll
+    for (int t0 = 0; t0 < JT; t0 += kEB) {
+      double xv[kEB][4], ev[kEB][4];
+#pragma unroll
+      for (int tb = 0; tb < kEB; ++tb) {
+        const int t = t0 + tb < JT ? t0 + tb : JT - 1;
+        const bool cok = t0 + tb < JT && colj(t) < p;
+        const int64_t co = coloff(t);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = rowok[r] && cok;
+          xv[tb][r] = ok ? xs[rowoff[r] + co] : 0.0;
+          ev[tb][r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int tb = 0; tb < kEB; ++tb) {
+        const int t = t0 + tb;
+        if (t < JT) {
+          const bool cok = colj(t) < p;
+          const int64_t co = coloff(t);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (rowok[r] && cok) {
+              const double v = fma(shift, xv[tb][r], acc[t][r]);
+              dsum = fma(xv[tb][r], v, dsum);
+              if (edots) {
+                rqsum = fma(ev[tb][r], v, rqsum);
+                qqsum = fma(v, v, qqsum);
+              }
+              Y[rowoff[r] + co] = v;
+            }
+          }
+        }
+      }
+    }
+  }
+  // ---- per-workgroup partial sums: p.q (+ r.q, q.q) of the epilogue, r.r of
+  // the fused prologue.  The k-loop ended with a barrier: LDS is free.
+  const bool want_dot = dot_partials != nullptr;
+  const bool want_rr = CGP == 2 && fz.rr_part != nullptr;
+  if (want_dot || want_rr) {
+    double v4[4] = {dsum, rqsum, qqsum, rr_acc};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v4[i] += __shfl_xor(v4[i], off, 64);
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[4 * wave + i] = v4[i];
+    if (kRaw) {
+      __builtin_amdgcn_s_waitcnt((7 << 4) | 0xC00F);  // lgkmcnt(0) only
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
+    if (threadIdx.x < 4) {
+      const int i = threadIdx.x;
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) s += red[4 * w + i];
+      if (i == 0 && want_dot) dot_partials[blk] = s;
+      if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blk] = s;
+      if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blk] = s;
+      if (i == 3 && want_rr) fz.rr_part[blk] = s;
+    }
+  }
+  // ---- side job (fused CG, second mode product): x += alpha p_old over this
+  // workgroup's slice.  The MFMA-bound kernel has HBM headroom; the other
+  // workgroups of the CU keep the matrix cores busy meanwhile.
+  if (kEpi >= 1 && fz.sx != nullptr && fz.sc->pending) {
+    const double al = fz.sc->alpha;
+    const int64_t lo = blk * fz.schunk;
+    const int64_t hi = min(fz.sn, lo + fz.schunk);
+    double* __restrict__ sx = fz.sx;
+    const double* __restrict__ sp = fz.sp;
+    constexpr int kB = 4;
+    int64_t i = lo + 2 * threadIdx.x;
+    for (; i + 2 * kThreads * (kB - 1) + 1 < hi; i += 2 * kThreads * kB) {
+      double2 xv2[kB], pv2[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        xv2[u] = *reinterpret_cast<const double2*>(sx + i + 2 * kThreads * u);
+        pv2[u] = *reinterpret_cast<const double2*>(sp + i + 2 * kThreads * u);
+      }
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        xv2[u].x += al * pv2[u].x;
+        xv2[u].y += al * pv2[u].y;
+        *reinterpret_cast<double2*>(sx + i + 2 * kThreads * u) = xv2[u];
+      }
+    }
+    for (; i < hi; i += 2 * kThreads) {
+      sx[i] += al * sp[i];
+      if (i + 1 < hi) sx[i + 1] += al * sp[i + 1];
+    }
+  }
+}
+
 // Double-buffered chunk pipeline, one barrier per chunk:
 //   issue global loads of chunk c+1 (K^T fragments -> registers, X -> A regs)
 //   MFMA over chunk c from LDS buffer c&1
@@ -60,9 +219,10 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 // each): half the accumulators per wave, so two workgroups fit a CU and one
 // workgroup's prologue / epilogue overlaps the other's MFMAs.
 //
-// kEpi = 2 (fused CG, last mode product): the epilogue also reads r and
-// accumulates r.q and q.q next to p.q (MpFuse::er); a smaller load batch
-// keeps the extra loads within the register budget.
+// kEpi = 1 (fused CG, second mode product): the x-update side job after the
+// epilogue.  kEpi = 2 (fused CG, last mode product): the epilogue also reads r
+// and accumulates r.q and q.q next to p.q (MpFuse::er), a smaller load batch
+// keeping the extra loads within the register budget; side job too (d = 2).
 template <int JT, int kWaves, int kKC, int CGP, int kMinW, bool kIdent, int kSplit, int kOpt,
           int kEpi = 0>
 __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
@@ -262,141 +422,181 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 #undef GG_A_LOAD
 #undef GG_A_MASK
 
-  // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
-  // Output address = rowoff(row) + coloff(j): the identity map is row * p + j;
-  // the distributed matvec permutes rows / columns into all-to-all order
-  // (OutMap, gg_dist.hip).  Offsets are decomposed once per row and column.
-  const int col = lane & 15;
-  const int64_t rbase = b0 + (lane >> 4);
-  int64_t rowoff[4];
-  bool rowok[4];
+  mp_finish<JT, kWaves, kSplit, kIdent, kEpi, CGP>(acc, Y, M, p, jt0, xs, shift, dot_partials, om,
+                                                   fz, rr_acc, b0, hp, lds, blockIdx.x);
+}
+
+// All-LDS-DMA pipeline (plain / side-job / fused-epilogue roles, CGP = 0):
+// both operands go global -> LDS with global_load_lds (16 B per lane), kNS
+// stages in flight, one raw s_barrier per chunk preceded by a counted
+// s_waitcnt vmcnt(N) that retires only the oldest stage -- so the HBM stream
+// of X runs kNS - 1 chunks ahead of the MFMAs instead of being drained at
+// every barrier (an ordinary global load or __syncthreads() while an LDS DMA
+// is in flight makes hipcc wait vmcnt(0); cdna_hip_programming.md
+// "Pipelining across barriers").  Stage layout (doubles):
+//   B: [k-step][tile][lane]  kKC * JT * 64       (factor fragments, as packed)
+//   A: [wave][row][16]       4 * kKC * 4 * 16    (X rows of the wave's strip)
+// The A operand of lane l at k-step s is A[wave][4 s + (l >> 4)][l & 15]: one
+// conflict-free ds_read_b64 of 512 contiguous bytes.  Needs M even and X
+// 16-byte aligned (16-byte row segments); kron_apply checks.
+//
+// A launch grid smaller than the strip count makes it persistent: workgroup b
+// runs strips b, b + grid, ... as one flat chunk sequence.
+template <int JT, int kKC, int kNS, int kMinW, int kEpi>
+__global__ __launch_bounds__(256, kMinW) void mode_product_glds_kernel(
+    const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
+    int64_t M, int q, int p, int KS, int jt_total, int jt0,
+    const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
+    const int* __restrict__ skip, OutMap om, MpFuse fz) {
+  constexpr int kWaves = 4;
+  constexpr int kThreads = 256;
+  constexpr int kBChunk2 = kKC * JT * 32;                  // double2 of B per stage
+  constexpr int kPerT = (kBChunk2 + kThreads - 1) / kThreads;
+  constexpr int kARows = kKC * 4;                          // X rows per wave per stage
+  static_assert(kARows % 8 == 0, "whole 1 KiB A instructions per wave");
+  constexpr int kAInstr = kARows / 8;
+  constexpr int kBD = kKC * JT * 64;                       // B doubles per stage
+  constexpr int kStage = kBD + kWaves * kARows * 16;       // doubles per stage
+  // B instructions the last wave issues per stage (the fewest of any wave);
+  // vmcnt(N) with the minimum only ever waits a little longer in other waves
+  constexpr int kBLast = (kBChunk2 - 3 * 64 + kThreads - 1) / kThreads;
+  constexpr int kN = kBLast + kAInstr;
+  constexpr int kWaitN = (kN & 15) | (((kN >> 4) & 3) << 14) | (7 << 4) | (15 << 8);
+  constexpr int kWait0 = (7 << 4) | (15 << 8);
+  if (skip != nullptr && *skip) return;
+  extern __shared__ __attribute__((aligned(16))) double lds[];  // kNS * kStage + red
+  double* red = lds + kNS * kStage;                             // 4 * kWaves doubles
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int krow = lane >> 4;
+  const int nchunks = (KS + kKC - 1) / kKC;
+  // persistent: this workgroup runs strips blockIdx.x + i * gridDim.x (64 rows
+  // of Y each) as one flat chunk sequence, so the stage ring never drains
+  // between strips and no workgroup is ever relaunched
+  const int64_t nstrips = (M + kWaves * 16 - 1) / (kWaves * 16);
+  if ((int64_t)blockIdx.x >= nstrips) return;
+  const int64_t my_strips = (nstrips - 1 - blockIdx.x) / gridDim.x + 1;
+  const int64_t G = my_strips * nchunks;
+
+  // B staging addresses (lane-linear in LDS), recomputed per issue (cheap
+  // integer work; keeping them live across the strip epilogue would spill)
+  const double* __restrict__ bbase = Bf + (int64_t)jt0 * 64;
+  const int64_t bchunk = (int64_t)kKC * jt_total * 64;
+  // A staging: instruction j of this wave loads rows 8 j + (lane >> 3),
+  // columns b0 + 2 (lane & 7) .. +1 of the chunk; rows past q clamp to q - 1,
+  // columns past M to M - 2 (those output rows are never stored)
+  const int arow = lane >> 3;
+  const int acol = 2 * (lane & 7);
+
+  // the next chunk to issue: strip ii (its first row b0i), chunk ic, stage is
+  int64_t b0i = ((int64_t)blockIdx.x * kWaves + wave) * 16;
+  const int64_t b0step = (int64_t)gridDim.x * kWaves * 16;
+  int ic = 0, is = 0;
+  auto issue = [&]() {
+    const int c = ic;
+    double* st = lds + is * kStage;
+    const double* cb = bbase + (int64_t)c * bchunk;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t row = rbase + 4 * r;
-    rowok[r] = row < M;
-    if (kIdent) {
-      rowoff[r] = row * p;
-    } else {
-      const int64_t a_ = row / om.mi, bi = row - a_ * om.mi;
-      const int64_t h = bi / om.cr, br = bi - h * om.cr;
-      rowoff[r] = h * om.hs + a_ * om.as + br * om.cg;
+    for (int u = 0; u < kPerT; ++u) {
+      const int bi = threadIdx.x + u * kThreads;
+      const int s_ = bi / (JT * 32);
+      if (bi < kBChunk2)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(cb + s_ * jt_total * 64 +
+                                                            2 * (bi - s_ * (JT * 32))),
+            (__attribute__((address_space(3))) void*)(st + (u * kThreads + wave * 64) * 2), 16,
+            0, 0);
     }
-  }
-  auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + hp * JT + t) * 16 + col; };
-  auto coloff = [&](int t) -> int64_t {
-    const int64_t j = colj(t);
-    if (kIdent) return j;
-    const int64_t jg = j / om.cg;
-    return jg * om.gs + (j - jg * om.cg);
+    double* sa = st + kBD + wave * kARows * 16;
+    const int64_t col = min(b0i + acol, M - 2);
+#pragma unroll
+    for (int j = 0; j < kAInstr; ++j) {
+      const int k = min(c * kARows + 8 * j + arow, q - 1);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(X + (int64_t)k * M + col),
+          (__attribute__((address_space(3))) void*)(sa + j * 128), 16, 0, 0);
+    }
+    is = is + 1 == kNS ? 0 : is + 1;
+    if (++ic == nchunks) {
+      ic = 0;
+      b0i += b0step;
+    }
   };
-  double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
-  const double* __restrict__ er = fz.er;
-  constexpr bool edots = kEpi == 2;
-  constexpr int kEB = edots ? 2 : kEpiBatch;
-  if (xs == nullptr) {
+
+  d4 acc[JT];
 #pragma unroll
-    for (int t = 0; t < JT; ++t) {
-      const bool cok = colj(t) < p;
-      const int64_t co = coloff(t);
+  for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
-    }
-  } else {
-    // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
-    // does not serialise one load round trip per output element
+  for (int g = 0; g < kNS - 1; ++g)
+    if (g < G) issue();
+
+  int c = 0, sc = 0;  // chunk of the current strip, its stage
+  int64_t i = 0;
+  for (int64_t g = 0; g < G; ++g) {
+    // retire chunk g (chunks g+1 .. g+kNS-2 may stay in flight)
+    if (kNS == 3 && g + 1 < G)
+      __builtin_amdgcn_s_waitcnt(kWaitN);
+    else if (kNS == 4 && g + 2 < G)
+      __builtin_amdgcn_s_waitcnt((((2 * kN) & 15) | ((((2 * kN) >> 4) & 3) << 14)) | (7 << 4) |
+                                 (15 << 8));
+    else if (kNS == 4 && g + 1 < G)
+      __builtin_amdgcn_s_waitcnt(kWaitN);
+    else
+      __builtin_amdgcn_s_waitcnt(kWait0);
+    __builtin_amdgcn_s_barrier();
+    if (g + kNS - 1 < G) issue();
+    const double* st = lds + sc * kStage;
+    sc = sc + 1 == kNS ? 0 : sc + 1;
+    const double* sa = st + kBD + wave * kARows * 16 + krow * 16 + (lane & 15);
+    const int kcn = min(kKC, KS - c * kKC);
+    const bool tail = c == nchunks - 1;
 #pragma unroll
-    for (int t0 = 0; t0 < JT; t0 += kEB) {
-      double xv[kEB][4], ev[kEB][4];
+    for (int s = 0; s < kKC; ++s) {
+      if (s < kcn) {
+        double a = sa[s * 64];
+        if (tail && (c * kARows + 4 * s + krow) >= q) a = 0.0;
 #pragma unroll
-      for (int tb = 0; tb < kEB; ++tb) {
-        const int t = t0 + tb < JT ? t0 + tb : JT - 1;
-        const bool cok = t0 + tb < JT && colj(t) < p;
-        const int64_t co = coloff(t);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = rowok[r] && cok;
-          xv[tb][r] = ok ? xs[rowoff[r] + co] : 0.0;
-          ev[tb][r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+        for (int t = 0; t < JT; ++t) {
+          const double b = st[(s * JT + t) * 64 + lane];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
         }
       }
+    }
+    if (tail) {
+      const int64_t blk = (int64_t)blockIdx.x + i * gridDim.x;
+      const int64_t b0 = (blk * kWaves + wave) * 16;
+      if (kEpi == 0) {
+        // plain role (no shift / dots: kron_apply never sends xs here)
+        const int col = lane & 15;
 #pragma unroll
-      for (int tb = 0; tb < kEB; ++tb) {
-        const int t = t0 + tb;
-        if (t < JT) {
-          const bool cok = colj(t) < p;
-          const int64_t co = coloff(t);
+        for (int t = 0; t < JT; ++t) {
+          const int j = (jt0 + t) * 16 + col;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if (rowok[r] && cok) {
-              const double v = fma(shift, xv[tb][r], acc[t][r]);
-              dsum = fma(xv[tb][r], v, dsum);
-              if (edots) {
-                rqsum = fma(ev[tb][r], v, rqsum);
-                qqsum = fma(v, v, qqsum);
-              }
-              Y[rowoff[r] + co] = v;
-            }
+            const int64_t row = b0 + krow + 4 * r;
+            if (row < M && j < p) Y[row * p + j] = acc[t][r];
           }
         }
-      }
-    }
-  }
-  // ---- per-workgroup partial sums: p.q (+ r.q, q.q) of the epilogue, r.r of
-  // the fused prologue.  The k-loop ended with a barrier: LDS is free.
-  const bool want_dot = dot_partials != nullptr;
-  const bool want_rr = CGP == 2 && fz.rr_part != nullptr;
-  if (want_dot || want_rr) {
-    double v4[4] = {dsum, rqsum, qqsum, rr_acc};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v4[i] += __shfl_xor(v4[i], off, 64);
-    if (lane == 0)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) lds[4 * wave + i] = v4[i];
-    __syncthreads();
-    if (threadIdx.x < 4) {
-      const int i = threadIdx.x;
-      double s = 0.0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) s += lds[4 * w + i];
-      if (i == 0 && want_dot) dot_partials[blockIdx.x] = s;
-      if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blockIdx.x] = s;
-      if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blockIdx.x] = s;
-      if (i == 3 && want_rr) fz.rr_part[blockIdx.x] = s;
-    }
-  }
-  // ---- side job (fused CG, second mode product): x += alpha p_old over this
-  // workgroup's slice.  The MFMA-bound kernel has HBM headroom; the other
-  // workgroups of the CU keep the matrix cores busy meanwhile.
-  if (fz.sx != nullptr && fz.sc->pending) {
-    const double al = fz.sc->alpha;
-    const int64_t lo = (int64_t)blockIdx.x * fz.schunk;
-    const int64_t hi = min(fz.sn, lo + fz.schunk);
-    double* __restrict__ sx = fz.sx;
-    const double* __restrict__ sp = fz.sp;
-    constexpr int kB = 4;
-    int64_t i = lo + 2 * threadIdx.x;
-    for (; i + 2 * kThreads * (kB - 1) + 1 < hi; i += 2 * kThreads * kB) {
-      double2 xv2[kB], pv2[kB];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        xv2[u] = *reinterpret_cast<const double2*>(sx + i + 2 * kThreads * u);
-        pv2[u] = *reinterpret_cast<const double2*>(sp + i + 2 * kThreads * u);
+      } else {
+        mp_finish<JT, kWaves, 1, true, kEpi, 0, true, 1>(acc, Y, M, p, jt0, xs, shift,
+                                                         dot_partials, om, fz, 0.0, b0, 0, red,
+                                                         blk);
       }
 #pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        xv2[u].x += al * pv2[u].x;
-        xv2[u].y += al * pv2[u].y;
-        *reinterpret_cast<double2*>(sx + i + 2 * kThreads * u) = xv2[u];
-      }
-    }
-    for (; i < hi; i += 2 * kThreads) {
-      sx[i] += al * sp[i];
-      if (i + 1 < hi) sx[i + 1] += al * sp[i + 1];
+      for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+      c = 0;
+      ++i;
+    } else {
+      ++c;
     }
   }
+}
+
+template <int JT, int KC, int NS>
+static constexpr size_t glds_lds_bytes() {
+  return ((size_t)NS * (KC * JT * 64 + 4 * KC * 4 * 16) + 16) * sizeof(double);
 }
 
 typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
@@ -412,7 +612,10 @@ typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, in
 // products only; the CG-fused ones always use the default).
 struct ModeConfig {
   mode_kernel_t fn;
-  int waves, kc, split, jtl;  // jtl: tiles staged per launch (LDS size)
+  int waves, kc, split, jtl;  // jtl: tiles staged per launch
+  size_t lds;                 // dynamic LDS bytes
+  bool glds;                  // all-LDS-DMA kernel: needs M even, X 16-B aligned
+  int pers;                   // > 0: persistent, at most pers workgroups per CU
 };
 
 // JT = output tiles of the launch; a split config gives each wave ceil(JT/2)
@@ -420,16 +623,25 @@ template <int JT, int W, int KC, int CGP, int MINW, int SPLIT, int OPT, int EPI 
 static ModeConfig cfg() {
   constexpr int JW = (JT + SPLIT - 1) / SPLIT;
   return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT, EPI>, W, KC,
-                    SPLIT, JW * SPLIT};
+                    SPLIT, JW * SPLIT, 2 * (size_t)KC * JW * SPLIT * 64 * sizeof(double), false,
+                    0};
+}
+
+template <int JT, int KC, int NS, int MINW, int EPI = 0, int PERS = 0>
+static ModeConfig cfg_glds() {
+  return ModeConfig{mode_product_glds_kernel<JT, KC, NS, MINW, EPI>, 4, KC, 1, JT,
+                    glds_lds_bytes<JT, KC, NS>(), true, PERS};
 }
 
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
-// cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG epilogue
+// cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG
+// epilogue (+ side job when d = 2), 4 fused CG side job
 template <int JT>
 static ModeConfig config_for(int variant, int cgp) {
   if (cgp == 1) return cfg<JT, 4, 3, 1, 3, 1, 2>();
   if (cgp == 2) return cfg<JT, 4, 3, 2, 3, 1, 2>();
   if (cgp == 3) return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
+  if (cgp == 4) return cfg<JT, 4, 3, 0, 3, 1, 2, 1>();
   switch (variant) {
     case 1: return cfg<JT, 12, 4, 0, 3, 1, 2>();
     case 2: return cfg<JT, 12, 4, 0, 3, 1, 0>();  // register-staged factor chunks
@@ -438,10 +650,13 @@ static ModeConfig config_for(int variant, int cgp) {
     case 5: return cfg<JT, 2, 2, 0, 3, 1, 2>();
     case 6: return cfg<JT, 8, 4, 0, 4, 2, 2>();   // columns split over two waves
     case 7: return cfg<JT, 12, 4, 0, 3, 1, 3>();  // + sched_barrier around the prefetch
+    case 8: return cfg_glds<JT, 2, 3, 3>();        // all-LDS-DMA, 3 stages
+    case 9: return cfg_glds<JT, 2, 4, 2>();        // all-LDS-DMA, 4 stages
+    case 10: return cfg_glds<JT, 2, 3, 3, 0, 3>();   // persistent, 3 workgroups / CU
     default: return cfg<JT, 4, 3, 0, 3, 1, 2>();
   }
 }
-constexpr int kNumVariants = 8;
+constexpr int kNumVariants = 11;
 
 static int mode_variant() {
   const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
@@ -470,8 +685,18 @@ static ModeConfig select_kernel(int jt, int variant, int cgp) {
   }
 }
 
-static size_t mode_lds_bytes(const ModeConfig& c) {
-  return 2 * (size_t)c.kc * c.jtl * 64 * sizeof(double);
+static size_t mode_lds_bytes(const ModeConfig& c) { return c.lds; }
+
+// compute units of the current device (persistent launches)
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    GG_HIP(hipGetDevice(&dev));
+    GG_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n <= 0) n = 256;
+  }
+  return n;
 }
 
 // One factor in fragment order, for the operator and for its transpose.
@@ -573,7 +798,12 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // step 0; the later launches of that step read the updated p
         const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? cgp : 0;
         const bool epi = cgp == 2 && last && dot_partials != nullptr;
-        const ModeConfig mc = select_kernel(jt, variant, epi ? 3 : pro);
+        const bool side = cgp == 2 && k == 1 && jt0 == 0;
+        ModeConfig mc = select_kernel(jt, variant, epi ? 3 : side ? 4 : pro);
+        const bool with_xs = last && (shift != 0.0 || dot_partials != nullptr);
+        if (mc.glds && (M % 2 != 0 || M < 2 || (reinterpret_cast<uintptr_t>(step_src) & 15) ||
+                        with_xs))
+          mc = select_kernel(jt, 0, epi ? 3 : side ? 4 : pro);
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         if (pro) {
@@ -585,7 +815,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             fz.rr_part = cg->rr_part;
           }
         }
-        if (cgp == 2 && k == 1 && jt0 == 0) {
+        if (side) {
           fz.sc = cg->sc;
           fz.sx = cg->sx;
           fz.sp = cg->sp;
@@ -601,7 +831,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             fz.pstride = cg->pstride;
           }
         }
-        hipLaunchKernelGGL(mc.fn, dim3((unsigned)nblk), dim3(mc.waves * 64),
+        int64_t grid = nblk;
+        if (mc.pers > 0) grid = std::min<int64_t>(nblk, (int64_t)cu_count() * mc.pers);
+        hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
                            mode_lds_bytes(mc), stream, step_src, dst, f.frag, M, (int)f.q,
                            (int)f.p, f.KS, f.JT, jt0,
                            last && (shift != 0.0 || parts) ? (cgp == 2 ? cg->p_out : x)
@@ -652,7 +884,7 @@ static void set_lds_limits() {
   if (done) return;
   for (int v = 0; v < kNumVariants; ++v)
     for (int jt = 1; jt <= kMaxJT; ++jt)
-      for (int cgp = 0; cgp < 4; ++cgp) {
+      for (int cgp = 0; cgp < 5; ++cgp) {
         const ModeConfig mc = select_kernel(jt, v, cgp);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
