@@ -108,9 +108,16 @@ struct MpFuse {
 // Output address map of a mode product (see gg_kron.hip epilogue):
 //   addr = (j / cg) * gs + (j % cg) + h * hs + a * as + br * cg,
 //   a = row / mi, h = (row % mi) / cr, br = (row % mi) % cr.
+// Push mode (sharded matvec over peer memory): the all-to-all chunk index
+// (destination rank) is h (push = 1) or j / cg (push = 2); instead of the
+// send buffer the element goes straight to peers[dest][self_off + rest], i.e.
+// into the destination rank's receive buffer over xGMI.
 struct OutMap {
   int identity;
   int64_t cg, gs, mi, cr, hs, as;
+  int push = 0;
+  int64_t self_off = 0;
+  double* const* peers = nullptr;  // device array of world pointers
   static OutMap ident() { return OutMap{1, 1, 0, 1, 1, 0, 0}; }
 };
 

@@ -63,17 +63,21 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
   const int col = lane & 15;
   const int64_t rbase = b0 + (lane >> 4);
   int64_t rowoff[4];
+  int rowdest[4];
   bool rowok[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int64_t row = rbase + 4 * r;
     rowok[r] = row < M;
+    rowdest[r] = 0;
     if (kIdent) {
       rowoff[r] = row * p;
     } else {
       const int64_t a_ = row / om.mi, bi = row - a_ * om.mi;
       const int64_t h = bi / om.cr, br = bi - h * om.cr;
-      rowoff[r] = h * om.hs + a_ * om.as + br * om.cg;
+      rowoff[r] = a_ * om.as + br * om.cg;
+      if (om.push == 1) rowdest[r] = (int)h;
+      else rowoff[r] += h * om.hs;
     }
   }
   auto colj = [&](int t) -> int64_t { return (int64_t)(jt0 + hp * JT + t) * 16 + col; };
@@ -83,6 +87,25 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
     const int64_t jg = j / om.cg;
     return jg * om.gs + (j - jg * om.cg);
   };
+  if (!kIdent && om.push != 0) {
+    // sharded matvec, push mode (gg_kron_dist_*_push): each element goes
+    // straight to its destination rank's buffer (peer memory over xGMI) at
+    // this rank's chunk -- the all-to-all is the epilogue's own stores
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const int64_t j = colj(t);
+      if (j >= p) continue;
+      const int64_t jg = j / om.cg;
+      const int64_t co = (j - jg * om.cg) + (om.push == 2 ? 0 : jg * om.gs);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!rowok[r]) continue;
+        const int dest = om.push == 1 ? rowdest[r] : (int)jg;
+        om.peers[dest][om.self_off + rowoff[r] + co] = acc[t][r];
+      }
+    }
+    return;
+  }
   double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
   const double* __restrict__ er = fz.er;
   constexpr bool edots = kEpi == 2;
@@ -980,6 +1003,12 @@ struct gg_kron_dist {
   std::vector<int64_t> m;
   std::vector<gg::Factor> f;
   int64_t n = 1, n_local = 1, s0 = 1;
+  // push mode: every rank's exchange buffer [recv | out] (2 n_local doubles),
+  // peers' opened through IPC handles or given directly (same process)
+  double* own_xbuf = nullptr;
+  double** peers_recv = nullptr;   // device array [world]
+  double** peers_out = nullptr;    // device array [world]
+  std::vector<void*> opened;       // hipIpcOpenMemHandle bases to close
 };
 
 namespace gg {
@@ -1078,7 +1107,57 @@ int gg_kron_dist_destroy(gg_kron_dist* D) {
     if (!D) return;
     for (gg::Factor& f : D->f)
       if (f.frag) (void)hipFree(f.frag);
+    for (void* b : D->opened) (void)hipIpcCloseMemHandle(b);
+    if (D->peers_recv) (void)hipFree(D->peers_recv);
+    if (D->peers_out) (void)hipFree(D->peers_out);
     delete D;
+  });
+}
+
+int gg_ipc_handle(const void* dev_ptr, void* handle_out, int64_t* offset_out) {
+  return gg::guard([&] {
+    GG_REQUIRE(dev_ptr && handle_out && offset_out, GG_ERR_VALUE, "NULL argument");
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    GG_HIP(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
+    hipIpcMemHandle_t h;
+    GG_HIP(hipIpcGetMemHandle(&h, (void*)base));
+    std::memcpy(handle_out, &h, sizeof(h));
+    *offset_out = (int64_t)((const char*)dev_ptr - (const char*)base);
+  });
+}
+
+int gg_kron_dist_set_peers(gg_kron_dist* D, double* own_xbuf, int use_ipc, const void* handles,
+                           const int64_t* offsets, void* const* ptrs) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && own_xbuf, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(use_ipc ? (handles && offsets) : (ptrs != nullptr), GG_ERR_VALUE,
+               "peer handles / pointers required");
+    GG_REQUIRE(D->peers_recv == nullptr, GG_ERR_VALUE, "peers already set");
+    const int G = D->world;
+    std::vector<double*> recv(G), out(G);
+    for (int g = 0; g < G; ++g) {
+      double* base = nullptr;
+      if (g == D->rank) {
+        base = own_xbuf;
+      } else if (use_ipc) {
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, (const char*)handles + (size_t)g * sizeof(h), sizeof(h));
+        void* b = nullptr;
+        GG_HIP(hipIpcOpenMemHandle(&b, h, hipIpcMemLazyEnablePeerAccess));
+        D->opened.push_back(b);
+        base = reinterpret_cast<double*>((char*)b + offsets[g]);
+      } else {
+        base = reinterpret_cast<double*>(ptrs[g]);
+      }
+      recv[g] = base;
+      out[g] = base + D->n_local;
+    }
+    D->own_xbuf = own_xbuf;
+    GG_HIP(hipMalloc(&D->peers_recv, G * sizeof(double*)));
+    GG_HIP(hipMalloc(&D->peers_out, G * sizeof(double*)));
+    GG_HIP(hipMemcpy(D->peers_recv, recv.data(), G * sizeof(double*), hipMemcpyHostToDevice));
+    GG_HIP(hipMemcpy(D->peers_out, out.data(), G * sizeof(double*), hipMemcpyHostToDevice));
   });
 }
 
@@ -1090,11 +1169,12 @@ int gg_kron_dist_sizes(const gg_kron_dist* D, int64_t* n_local, int64_t* work_el
   });
 }
 
-int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
-                        double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
-                        gg_stream stream) {
+static int dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
+                       double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
+                       gg_stream stream, bool push) {
   return gg::guard([&] {
     GG_REQUIRE(D && x_local_dev && send_dev && work_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(!push || D->peers_recv, GG_ERR_VALUE, "push mode needs gg_kron_dist_set_peers");
     GG_REQUIRE((cg_r_dev == nullptr) == (cg_scalars_dev == nullptr), GG_ERR_VALUE,
                "CG fusion needs both r and the scalars");
     hipStream_t s = gg::as_stream(stream);
@@ -1122,6 +1202,11 @@ int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send
           const int64_t cr = mi / G;
           om = gg::OutMap{0, f.p, 0, mi, cr, D->s0 * cr * f.p, cr * f.p};
         }
+        if (push) {  // chunk h goes to rank h's receive buffer, at this rank's slot
+          om.push = d == 2 ? 2 : 1;
+          om.self_off = (int64_t)D->rank * (D->n_local / G);
+          om.peers = D->peers_recv;
+        }
       } else {
         // alternate work / send so that the last local step lands in send
         dst = ((d - 1 - k) % 2 == 0) ? send_dev : work_dev;
@@ -1130,6 +1215,32 @@ int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send
       gg::dist_step(f, src, dst, M, om, fuse ? &pro : nullptr, s);
       src = dst;
     }
+  });
+}
+
+int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
+                        double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
+                        gg_stream stream) {
+  return dist_phase1(D, x_local_dev, send_dev, work_dev, cg_r_dev, cg_scalars_dev, stream, false);
+}
+
+int gg_kron_dist_phase1_push(const gg_kron_dist* D, double* x_local_dev, double* scratch_dev,
+                             double* work_dev, const double* cg_r_dev,
+                             const void* cg_scalars_dev, gg_stream stream) {
+  return dist_phase1(D, x_local_dev, scratch_dev, work_dev, cg_r_dev, cg_scalars_dev, stream,
+                     true);
+}
+
+int gg_kron_dist_phase2_push(const gg_kron_dist* D, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && D->peers_out, GG_ERR_VALUE, "push mode needs gg_kron_dist_set_peers");
+    const gg::Factor& f = D->f[0];
+    const int64_t C = D->n_local / f.q;
+    gg::OutMap om{0, D->s0, C * D->s0, C, C, 0, 0};
+    om.push = 2;  // destination = output column group j / s0
+    om.self_off = (int64_t)D->rank * (D->n_local / D->world);
+    om.peers = D->peers_out;
+    gg::dist_step(f, D->own_xbuf, nullptr, C, om, nullptr, gg::as_stream(stream));
   });
 }
 

@@ -94,6 +94,11 @@ SIGNATURES = {
     "gg_kron_dist_sizes": [_vp, _c_i64p, _c_i64p],
     "gg_kron_dist_phase1": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, _vp, _vp],
     "gg_kron_dist_phase2": [_vp, _c_dp, _c_dp, _vp],
+    "gg_ipc_handle": [_c_dp, ctypes.c_void_p, _c_i64p],
+    "gg_kron_dist_set_peers": [_vp, _c_dp, ctypes.c_int, ctypes.c_void_p, _c_i64p,
+                               ctypes.POINTER(ctypes.c_void_p)],
+    "gg_kron_dist_phase1_push": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, _vp, _vp],
+    "gg_kron_dist_phase2_push": [_vp, _vp],
     "gg_cgs_create": [ctypes.POINTER(ctypes.c_void_p)],
     "gg_cgs_destroy": [_vp],
     "gg_cgs_scalars": [_vp, ctypes.POINTER(ctypes.c_void_p)],

@@ -212,6 +212,22 @@ int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send
                         gg_stream stream);
 int gg_kron_dist_phase2(const gg_kron_dist* D, const double* recv_dev, double* send_dev,
                         gg_stream stream);
+/* Push mode: no all-to-all.  Each rank owns one exchange buffer xbuf = [recv |
+ * out] (2 n_local doubles, any device allocation); gg_kron_dist_set_peers
+ * learns every rank's xbuf, by IPC handle (one process per GPU: gg_ipc_handle
+ * gives the 64-byte hipIpcMemHandle of the allocation holding a pointer and
+ * the pointer's offset in it) or by plain pointer (ranks in one process).
+ * phase1_push's last mode product stores each element straight into its
+ * destination rank's recv over xGMI; after a barrier on all ranks,
+ * phase2_push reads the own recv and stores into the owners' out, which after
+ * a second barrier holds K x in the input layout.  scratch: n_local.       */
+int gg_ipc_handle(const void* dev_ptr, void* handle_out, int64_t* offset_out);
+int gg_kron_dist_set_peers(gg_kron_dist* D, double* own_xbuf, int use_ipc, const void* handles,
+                           const int64_t* offsets, void* const* ptrs);
+int gg_kron_dist_phase1_push(const gg_kron_dist* D, double* x_local_dev, double* scratch_dev,
+                             double* work_dev, const double* cg_r_dev,
+                             const void* cg_scalars_dev, gg_stream stream);
+int gg_kron_dist_phase2_push(const gg_kron_dist* D, gg_stream stream);
 
 /* Device CG scalars for a host-driven (sharded) CG: the same recurrence as
  * gg_cg_*, with each global dot product all-reduced by the caller between the

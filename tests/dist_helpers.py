@@ -122,6 +122,20 @@ class ThreadExchange(object):
             out[h * c:(h + 1) * c].copy_(self.slots[h][g * c:(g + 1) * c])
         self.bar.wait()
 
+    in_process = True  # peers' device buffers are plain pointers
+
+    def barrier(self):
+        torch.cuda.synchronize()
+        self.bar.wait()
+
+    def all_gather_object(self, obj):
+        g = self.local.rank
+        self.slots[g] = obj
+        self.bar.wait()
+        out = list(self.slots)
+        self.bar.wait()
+        return out
+
     def all_reduce(self, t):
         g = self.local.rank
         self.slots[g] = t.clone()
