@@ -103,7 +103,22 @@ def run_sharded(a, world, rank, torch, dev, dist):
     F = factors(m, d)
     eng = HipEngine(F, world, rank)
     y = local_rhs_device(m, d, world, rank, torch, dev)
-    cg = DistKronCG(eng, TorchExchange(), s)
+    ex = TorchExchange()
+    mode = os.environ.get("GG_DIST_MODE", "auto")
+    cg = DistKronCG(eng, ex, s, mode=mode)
+    if cg.mode == "push":
+        # one matvec through the peer-memory exchange against the all-to-all
+        # path on the same input; any disagreement falls back to all-to-all
+        ref = DistKronCG(eng, ex, s, mode="a2a")
+        ya, yp = eng.empty(), eng.empty()
+        ref.apply(y.clone(), ya)
+        cg.apply(y.clone(), yp)
+        err = torch.stack([(ya - yp).abs().max(), ya.abs().max()])
+        dist.all_reduce(err, op=dist.ReduceOp.MAX)
+        del ref, ya, yp
+        if not float(err[0]) <= 1e-12 * float(err[1]):
+            cg = DistKronCG(eng, ex, s, mode="a2a")
+        torch.cuda.empty_cache()
     cg.start(y, rtol=0.0, atol=0.0)
     cg.iterate(a.warmup)
     torch.cuda.synchronize()
@@ -136,8 +151,12 @@ def run_sharded(a, world, rank, torch, dev, dist):
         "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d, factor 0 "
                                "sharded over %d GPUs" % (m, d, s, n, world),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
-                   "parallelism": "shard factor-0 x%d: 2 all-to-all per matvec + 2 scalar "
-                                  "all-reduce per iteration (RCCL)" % world},
+                   "exchange": cg.mode,
+                   "parallelism": ("shard factor-0 x%d: matvec exchange by %s, 2 scalar "
+                                   "all-reduce per iteration (RCCL)"
+                                   % (world, "peer-memory stores in the mode-product "
+                                             "epilogues + 2 RCCL barriers"
+                                      if cg.mode == "push" else "2 RCCL all-to-all"))},
     }
 
 

@@ -4,10 +4,18 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
 Vectors are sharded along factor 0 (the slowest axis of the reference's
 flattening); every rank holds N/G elements in the local layout
 (m_1, ..., m_{d-1}, a), a = i_0 - rank * m_0/G fastest.  A matvec is two
-local MFMA phases around two all-to-alls (include/gp_grief_amd.h,
+local MFMA phases with one exchange after each (include/gp_grief_amd.h,
 gg_kron_dist_*); each CG dot product is one scalar all-reduce.  The CG
-recurrence and its stopping rule are the single-GPU ones (scipy's), so a
-sharded solve converges in the same number of iterations up to rounding.
+recurrence and its stopping rule are the single-GPU textbook ones (scipy's),
+so a sharded solve converges in the same number of iterations up to rounding.
+
+Two exchange modes (DistKronCG(mode=...)):
+  "push" (default when the engine supports it): the last mode product of each
+         phase stores its output straight into the destination ranks' buffers
+         in peer memory over xGMI (IPC-mapped), so the exchange overlaps the
+         MFMA work instead of following it; a stream-ordered barrier (an RCCL
+         all-reduce of one double) separates the phases;
+  "a2a": the phases write a send buffer and RCCL all_to_all_single moves it.
 
 The arithmetic lives in the "engine" (HipEngine: the C ABI on this rank's
 GPU).  The exchange is injected: `TorchExchange` (RCCL / gloo collectives) in
@@ -47,22 +55,53 @@ def gather_global(locals_, m):
 
 
 class TorchExchange(object):
-    """All-to-all and all-reduce over a torch.distributed process group."""
+    """All-to-all, all-reduce, barrier and handle exchange over a
+    torch.distributed process group (nccl = RCCL; gloo for CPU-side tests,
+    where device tensors are reduced through a host copy)."""
+
+    in_process = False
 
     def __init__(self, group=None):
+        import torch
         import torch.distributed as dist
+        self.torch = torch
         self.dist = dist
         self.group = group
+        self.backend = str(dist.get_backend(group))
+        self._tok = None
 
     def all_to_all(self, out, inp):
         self.dist.all_to_all_single(out, inp, group=self.group)
 
     def all_reduce(self, t):
-        self.dist.all_reduce(t, group=self.group)
+        if t.is_cuda and self.backend == "gloo":
+            h = t.cpu()
+            self.dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+        else:
+            self.dist.all_reduce(t, group=self.group)
+
+    def barrier(self):
+        """Stream-ordered barrier: every rank's earlier kernels have finished
+        (their peer stores landed) before any rank's later kernels start."""
+        if self.backend == "nccl":
+            if self._tok is None:
+                self._tok = self.torch.zeros(1, dtype=self.torch.float64, device="cuda")
+            self.dist.all_reduce(self._tok, group=self.group)  # RCCL, stream-ordered
+        else:
+            self.torch.cuda.synchronize()
+            self.dist.barrier(group=self.group)
+
+    def all_gather_object(self, obj):
+        out = [None] * self.dist.get_world_size(self.group)
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
 
 
 class HipEngine(object):
     """This rank's share of the sharded operator and CG scalars on its GPU."""
+
+    supports_push = True
 
     def __init__(self, factors, world, rank):
         L = native.lib()
@@ -72,6 +111,7 @@ class HipEngine(object):
                 raise ValueError("the sharded operator needs square factors")
         self._keep = mats
         self.m = [f.shape[0] for f in mats]
+        self.world, self.rank = int(world), int(rank)
         ptrs = (ctypes.c_void_p * len(mats))(*[f.ctypes.data for f in mats])
         h = ctypes.c_void_p()
         native.check(L.gg_kron_dist_create(len(mats), native.i64_array(self.m), ptrs, int(world),
@@ -88,12 +128,38 @@ class HipEngine(object):
         native.check(L.gg_cgs_scalars(self.cgs, ctypes.byref(sc)))
         self.sc = sc
         self.red = dev.zeros(2)  # [0]: the scalar being all-reduced
+        self.xbuf = None         # push mode: [recv | out], 2 n_local
 
     def empty(self):
         return dev.empty(self.n_local)
 
     def zeros(self):
         return dev.zeros(self.n_local)
+
+    # ---- push-mode exchange setup
+    def setup_push(self, exchange):
+        """Allocate this rank's exchange buffer and learn every peer's: by IPC
+        handle across processes, by pointer for ranks sharing a process.
+        Returns the view where K x lands (the "out" half)."""
+        L = native.lib()
+        self.xbuf = dev.zeros(2 * self.n_local)
+        ptr = self.xbuf.data_ptr()
+        if getattr(exchange, "in_process", False):
+            ptrs = exchange.all_gather_object(ptr)
+            arr = (ctypes.c_void_p * self.world)(*ptrs)
+            native.check(L.gg_kron_dist_set_peers(self.h, ctypes.c_void_p(ptr), 0, None, None,
+                                                  arr), "gg_kron_dist_set_peers")
+        else:
+            hbuf = ctypes.create_string_buffer(64)
+            off = ctypes.c_int64()
+            native.check(L.gg_ipc_handle(ctypes.c_void_p(ptr), hbuf, ctypes.byref(off)),
+                         "gg_ipc_handle")
+            allh = exchange.all_gather_object((hbuf.raw, off.value))
+            blob = ctypes.create_string_buffer(b"".join(h for h, _ in allh), 64 * self.world)
+            offs = native.i64_array([o for _, o in allh])
+            native.check(L.gg_kron_dist_set_peers(self.h, ctypes.c_void_p(ptr), 1, blob, offs,
+                                                  None), "gg_kron_dist_set_peers")
+        return self.xbuf[self.n_local:]
 
     def phase1(self, x, send, r=None):
         native.check(native.lib().gg_kron_dist_phase1(
@@ -105,6 +171,16 @@ class HipEngine(object):
         native.check(native.lib().gg_kron_dist_phase2(self.h, native.dptr(recv),
                                                       native.dptr(send), native.stream_ptr()),
                      "gg_kron_dist_phase2")
+
+    def phase1_push(self, x, scratch, r=None):
+        native.check(native.lib().gg_kron_dist_phase1_push(
+            self.h, native.dptr(x), native.dptr(scratch), native.dptr(self.work),
+            native.dptr(r) if r is not None else None, self.sc if r is not None else None,
+            native.stream_ptr()), "gg_kron_dist_phase1_push")
+
+    def phase2_push(self):
+        native.check(native.lib().gg_kron_dist_phase2_push(self.h, native.stream_ptr()),
+                     "gg_kron_dist_phase2_push")
 
     # ---- CG scalar steps; each writes / reads self.red[0]
     def local_dot(self, x, y):
@@ -166,28 +242,51 @@ class DistKronCG(object):
     """CG on (K + shift I) x = b with K sharded over the ranks of `exchange`.
 
     engine: HipEngine (or a test engine with the same methods); all vectors
-    are this rank's local shards.
+    are this rank's local shards.  mode: "push" (peer-memory exchange inside
+    the mode products, needs engine.supports_push) or "a2a" (RCCL all-to-all);
+    "auto" picks push when the engine supports it.
     """
 
-    def __init__(self, engine, exchange, shift):
+    def __init__(self, engine, exchange, shift, mode="auto"):
         self.e = engine
         self.x_ex = exchange
         self.shift = float(shift)
         n = engine.n_local
         self.n_local = n
-        self.r, self.p, self.q = engine.empty(), engine.zeros(), engine.empty()
-        self.send, self.recv = engine.empty(), engine.empty()
+        if mode == "auto":
+            mode = "push" if getattr(engine, "supports_push", False) else "a2a"
+        if mode not in ("push", "a2a"):
+            raise ValueError("mode must be 'push', 'a2a' or 'auto'")
+        self.mode = mode
+        self.r, self.p = engine.empty(), engine.zeros()
+        self.send = engine.empty()
+        if mode == "push":
+            self.q = engine.setup_push(exchange)   # K p lands in the peer-visible buffer
+            self.recv = None
+        else:
+            self.q, self.recv = engine.empty(), engine.empty()
         self.x = None
 
     def _allreduce(self):
         self.x_ex.all_reduce(self.e.reduce_buffer())
 
+    def _matvec_into_q(self, x, fuse_cg):
+        if self.mode == "push":
+            self.e.phase1_push(x, self.send, r=self.r if fuse_cg else None)
+            self.x_ex.barrier()   # every rank's chunks have landed in every recv
+            self.e.phase2_push()
+            self.x_ex.barrier()   # every rank's q is complete
+        else:
+            self.e.phase1(x, self.send, r=self.r if fuse_cg else None)
+            self.x_ex.all_to_all(self.recv, self.send)
+            self.e.phase2(self.recv, self.send)
+            self.x_ex.all_to_all(self.q, self.send)
+
     def apply(self, x, y, fuse_cg=False):
         """y = K x (no shift) for local shards; fuse_cg: x <- beta x + r first."""
-        self.e.phase1(x, self.send, r=self.r if fuse_cg else None)
-        self.x_ex.all_to_all(self.recv, self.send)
-        self.e.phase2(self.recv, self.send)
-        self.x_ex.all_to_all(y, self.send)
+        self._matvec_into_q(x, fuse_cg)
+        if y is not self.q:
+            self.e.copy(y, self.q)
 
     def start(self, b, rtol=1e-5, atol=0.0, x_out=None):
         self.x = self.e.zeros() if x_out is None else x_out
@@ -199,7 +298,7 @@ class DistKronCG(object):
 
     def iterate(self, n_iter):
         for _ in range(int(n_iter)):
-            self.apply(self.p, self.q, fuse_cg=True)        # p = r + beta p ; q = K p
+            self._matvec_into_q(self.p, fuse_cg=True)        # p = r + beta p ; q = K p
             self.e.shift_dot(self.q, self.p, self.shift)     # q += s p ; local p.q
             self._allreduce()
             self.e.cg_alpha()

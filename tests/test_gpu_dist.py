@@ -1,20 +1,30 @@
-"""Sharded Kronecker CG with the HIP engine on one MI355X: G virtual ranks run as
-threads, each with its own gg_kron_dist handle, exchanging through
-tests/dist_helpers.ThreadExchange.  Exercises the device phases and their
-all-to-all address maps (OutMap) against the single-GPU operator and the oracle.
+"""Sharded Kronecker CG with the HIP engine on one MI355X.
+
+Virtual ranks: G ranks run as threads of one process, each with its own
+gg_kron_dist handle, exchanging through tests/dist_helpers.ThreadExchange
+(all-to-all mode) or storing straight into each other's buffers (push mode,
+plain device pointers).  Process ranks: two processes share the GPU, learn
+each other's exchange buffers by IPC handle (the path a one-process-per-GPU
+run takes) and synchronise over gloo.  Both check the device phases and
+their address maps (OutMap) against the oracle.
 """
+import os
+import socket
+
 import numpy as np
 import pytest
 
 import oracle
+from conftest import ROOT
 from dist_helpers import ThreadExchange, reference_factors, run_threads
 
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("mode", ["push", "a2a"])
 @pytest.mark.parametrize("world,m,d", [(2, 8, 2), (2, 12, 3), (4, 16, 4), (8, 24, 3),
                                        (4, 40, 3)])
-def test_sharded_matvec_and_cg_virtual_ranks(gpu, world, m, d):
+def test_sharded_matvec_and_cg_virtual_ranks(gpu, world, m, d, mode):
     import torch
     from gp_grief_amd.distributed import (DistKronCG, HipEngine, gather_global,
                                           scatter_global)
@@ -27,7 +37,8 @@ def test_sharded_matvec_and_cg_virtual_ranks(gpu, world, m, d):
     def body(g):
         ex.bind(g)
         e = engines[g]
-        cg = DistKronCG(e, ex, shift)
+        cg = DistKronCG(e, ex, shift, mode=mode)
+        assert cg.mode == mode
         xl = torch.from_numpy(scatter_global(xg, [m] * d, world, g).copy()).cuda()
         yl = e.empty()
         cg.apply(xl.clone(), yl)
@@ -45,4 +56,61 @@ def test_sharded_matvec_and_cg_virtual_ranks(gpu, world, m, d):
     assert all(r[2] == 0 for r in res)
     assert len({r[3] for r in res}) == 1
     assert abs(res[0][3] - it) <= max(2, 0.02 * it)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _ipc_worker(rank, world, port, m, d, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp_grief_amd.distributed import DistKronCG, HipEngine, TorchExchange, scatter_global
+    from dist_helpers import reference_factors
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(11).standard_normal(m ** d)
+    eng = HipEngine(F, world, rank)
+    cg = DistKronCG(eng, TorchExchange(), 0.05, mode="push")
+    xl = torch.from_numpy(scatter_global(xg, [m] * d, world, rank).copy()).cuda()
+    yl = eng.empty()
+    for _ in range(3):  # repeated: the buffers are reused across matvecs
+        cg.apply(xl.clone(), yl)
+    x, info = cg.solve(xl, rtol=1e-10, maxiter=3000, check_every=25)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), y=yl.cpu().numpy(),
+             x=x.cpu().numpy(), info=info, iters=cg.status()[0])
+    dist.barrier()
+    del cg, eng
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,m,d", [(2, 16, 3), (4, 24, 3)])
+def test_push_exchange_over_ipc_processes(gpu, tmp_path, world, m, d):
+    """One process per rank on the same GPU: exchange buffers shared by IPC
+    handle (gg_ipc_handle / gg_kron_dist_set_peers), barriers over gloo."""
+    import torch.multiprocessing as mp
+    from gp_grief_amd.distributed import gather_global
+    port = _free_port()
+    mp.start_processes(_ipc_worker, args=(world, port, m, d, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(world)]
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(11).standard_normal(m ** d)
+    y = gather_global([r["y"] for r in res], [m] * d)
+    ref = oracle.kron_matvec(F, xg)
+    assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < 1e-12
+    x = gather_global([r["x"] for r in res], [m] * d)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + 0.05 * v, xg,
+                                   rtol=1e-10)
+    assert all(int(r["info"]) == 0 for r in res)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
