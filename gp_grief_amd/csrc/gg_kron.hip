@@ -46,8 +46,21 @@ constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued togethe
 // job slice.  kRaw: the reduction barrier is a raw s_barrier (LDS DMAs of the
 // next strip may be in flight, cdna_hip_programming.md "Pipelining across
 // barriers"); red: 4 * kWaves doubles of LDS scratch outside any DMA target.
+// value of lane l ^ 1 (DPP quad_perm [1,0,3,2] on both 32-bit halves)
+__device__ __forceinline__ double swap_lane_pair(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0xB1, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// kWide: plain stores as 16-byte pairs.  The MFMA result puts one column per
+// lane; a 2x2 exchange between lanes l and l ^ 1 gives the even lane rows
+// 0 / 2 and the odd lane rows 1 / 3 of two adjacent columns, so each lane
+// stores two double2 instead of four doubles per tile (needs p even and Y
+// 16-byte aligned, checked at run time).
 template <int JT, int kWaves, int kSplit, bool kIdent, int kEpi, int CGP, bool kRaw = false,
-          int kBatch = kEpiBatch>
+          int kBatch = kEpiBatch, bool kWide = false>
 __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restrict__ Y, int64_t M,
                                           int p, int jt0, const double* __restrict__ xs,
                                           double shift, double* __restrict__ dot_partials,
@@ -110,7 +123,24 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
   const double* __restrict__ er = fz.er;
   constexpr bool edots = kEpi == 2;
   constexpr int kEB = edots ? (kBatch < 2 ? kBatch : 2) : kBatch;
-  if (xs == nullptr) {
+  if (kWide && kIdent && xs == nullptr && (p & 1) == 0 &&
+      (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
+    const bool odd = (col & 1) != 0;
+    const int ra = odd ? 1 : 0, rb = odd ? 3 : 2;
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const int64_t j0 = colj(t) & ~(int64_t)1;
+      const double a0 = acc[t][0], a1 = acc[t][1], a2 = acc[t][2], a3 = acc[t][3];
+      const double g0 = swap_lane_pair(odd ? a0 : a1);
+      const double g1 = swap_lane_pair(odd ? a2 : a3);
+      const double2 v0 = odd ? double2{g0, a1} : double2{a0, g0};
+      const double2 v1 = odd ? double2{g1, a3} : double2{a2, g1};
+      if (j0 < p) {
+        if (rowok[ra]) *reinterpret_cast<double2*>(Y + rowoff[ra] + j0) = v0;
+        if (rowok[rb]) *reinterpret_cast<double2*>(Y + rowoff[rb] + j0) = v1;
+      }
+    }
+  } else if (xs == nullptr) {
 #pragma unroll
     for (int t = 0; t < JT; ++t) {
       const bool cok = colj(t) < p;
@@ -419,6 +449,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
         if (kOpt & 1) __builtin_amdgcn_sched_barrier(0);
       }
       if (s < kcn) {
+        if (kOpt & 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < JT; ++t) {
           if (kSplit == 1 || hp * JT + t < nt) {
@@ -426,6 +457,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
           }
         }
+        if (kOpt & 8) __builtin_amdgcn_s_setprio(0);
       }
     }
     if (more) {
@@ -445,8 +477,8 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 #undef GG_A_LOAD
 #undef GG_A_MASK
 
-  mp_finish<JT, kWaves, kSplit, kIdent, kEpi, CGP>(acc, Y, M, p, jt0, xs, shift, dot_partials, om,
-                                                   fz, rr_acc, b0, hp, lds, blockIdx.x);
+  mp_finish<JT, kWaves, kSplit, kIdent, kEpi, CGP, false, kEpiBatch, (kOpt & 4) != 0>(
+      acc, Y, M, p, jt0, xs, shift, dot_partials, om, fz, rr_acc, b0, hp, lds, blockIdx.x);
 }
 
 // All-LDS-DMA pipeline (plain / side-job / fused-epilogue roles, CGP = 0):
@@ -676,10 +708,13 @@ static ModeConfig config_for(int variant, int cgp) {
     case 8: return cfg_glds<JT, 2, 3, 3>();        // all-LDS-DMA, 3 stages
     case 9: return cfg_glds<JT, 2, 4, 2>();        // all-LDS-DMA, 4 stages
     case 10: return cfg_glds<JT, 2, 3, 3, 0, 3>();   // persistent, 3 workgroups / CU
+    case 11: return cfg<JT, 4, 3, 0, 3, 1, 2 | 4>();   // 16-byte paired stores
+    case 12: return cfg<JT, 4, 3, 0, 3, 1, 2 | 8>();   // s_setprio around the MFMAs
+    case 13: return cfg<JT, 4, 3, 0, 3, 1, 2 | 4 | 8>();
     default: return cfg<JT, 4, 3, 0, 3, 1, 2>();
   }
 }
-constexpr int kNumVariants = 11;
+constexpr int kNumVariants = 14;
 
 static int mode_variant() {
   const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
