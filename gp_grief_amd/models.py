@@ -246,18 +246,31 @@ def _dev_2d(x):
 class GPGriefModel(BaseModel):
     """GP-GRIEF (gp_grief_model.py:15-245) with every O(np), O(np^2), O(p^3)
     step on the MI355X (Phi build, SYRK Gram on FP64 MFMA, blocked Cholesky,
-    Woodbury solves, GEMV / GEMM predictions)."""
+    Woodbury solves, GEMV / GEMM predictions).
 
-    def __init__(self, X, Y, kern, noise_var=1.):
+    comm (optional, new): data-row sharding over GPUs.  Each
+    rank passes ITS rows of X and Y; the basis (grid, eigen-selection) is
+    replicated, Phi is built only for the local rows, and the three global
+    reductions of the Woodbury algebra are all-reduces through comm
+    (gp_grief_amd.distributed.TorchExchange = RCCL): the p x p Gram
+    Phi^T Phi, the p-vector Phi^T v of every solve / prediction, and the
+    scalars y.alpha, alpha.alpha and n.  The p x p Cholesky is replicated.
+    Results are the unsharded model's on the concatenated data, on every rank.
+    """
+
+    def __init__(self, X, Y, kern, noise_var=1., comm=None):
         super(GPGriefModel, self).__init__()
         assert X.ndim == 2
         assert Y.ndim == 2
         self.X = np.asarray(X)
         self.Y = np.asarray(Y)
         assert not np.any(np.isnan(Y))
-        self.num_data, self.input_dim = self.X.shape
-        if Y.shape[0] != self.num_data:
+        self.comm = comm
+        self._n_local, self.input_dim = self.X.shape
+        if Y.shape[0] != self._n_local:
             raise ValueError('X and Y sizes are inconsistent')
+        self.num_data = self._n_local if comm is None else \
+            int(round(self._sum_scalar(float(self._n_local))))
         self.output_dim = self.Y.shape[1]
         if self.output_dim != 1:
             raise RuntimeError('this only deals with 1 response for now')
@@ -284,6 +297,19 @@ class GPGriefModel(BaseModel):
             self.grad_method = ['adjoint', 'finite_difference'][0]
         self._Yd = None
 
+    # ---- global sums over the data-row shards (identity without comm)
+    def _sum(self, t):
+        if self.comm is not None:
+            self.comm.all_reduce(t)
+        return t
+
+    def _sum_scalar(self, v):
+        if self.comm is None:
+            return float(v)
+        t = dev.torch().tensor([float(v)], dtype=dev.torch().float64, device=dev.device())
+        self.comm.all_reduce(t)
+        return float(t.item())
+
     def _y_dev(self):
         if self._Yd is None:
             self._Yd = dev.to_device(self.Y[:, 0])
@@ -303,7 +329,7 @@ class GPGriefModel(BaseModel):
         if self._alpha is None:
             self.fit()
         if self._alpha_p is None:
-            t = dense.matvec(self._Phi, self._alpha, trans=True)
+            t = self._sum(dense.matvec(self._Phi, self._alpha, trans=True))
             self._alpha_p = dense.scale_rows(t, dev.to_device(self.kern.w), 0)
 
     def predict(self, Xnew):
@@ -328,7 +354,7 @@ class GPGriefModel(BaseModel):
         self._w = self.kern.w
         if self._A is None:
             self._Phi = self.kern.phi_device(self.X)          # n x p
-            self._A = dense.matmul(self._Phi, self._Phi, ta=True)  # Phi^T Phi
+            self._A = self._sum(dense.matmul(self._Phi, self._Phi, ta=True))  # Phi^T Phi
         wd = dev.to_device(np.asarray(self._w, dtype=np.float64))
         self._P = dense.add_diag(self._A, float(self.noise_var), wd)
         self._Pchol = dense.Cholesky(self._P)
@@ -349,12 +375,12 @@ class GPGriefModel(BaseModel):
         if self.kern.reweight_eig_funs or self.noise_var_constraint != 'fixed':
             pinv_diag = dense.host(self._Pchol.inverse_diag())
         if self.kern.reweight_eig_funs:
-            phia = dense.host(dense.matvec(self._Phi, self._alpha, trans=True))
+            phia = dense.host(self._sum(dense.matvec(self._Phi, self._alpha, trans=True)))
             data_fit_grad = 0.5 * phia ** 2
             complexity_grad = -0.5 * dvec * (1.0 - dvec * pinv_diag) / s
             gradient[-self.kern.n_eigs:] = data_fit_grad + complexity_grad
         if self.noise_var_constraint != 'fixed':
-            data_fit = 0.5 * dense.dot(self._alpha, self._alpha)
+            data_fit = 0.5 * self._sum_scalar(dense.dot(self._alpha, self._alpha))
             tr = float(self.kern.n_eigs) - float(np.sum(dvec * pinv_diag))
             gradient[0] = data_fit - 0.5 * (float(self.num_data) - tr) / s
         if self.kern.opt_kernel_params:
@@ -367,16 +393,16 @@ class GPGriefModel(BaseModel):
         self.parameters = parameters
         self.fit()
         yd = self._y_dev()
-        ll = -0.5 * (dense.dot(yd, self._alpha) + self._cov_log_det()
+        ll = -0.5 * (self._sum_scalar(dense.dot(yd, self._alpha)) + self._cov_log_det()
                      + self.num_data * np.log(np.pi * 2))
         return np.array([[ll]])
 
     def _mv_cov(self, x):
         """(Phi W Phi^T + s I) x (:217-225)."""
-        assert x.shape[0] == self.num_data
+        assert x.shape[0] == self._n_local
         assert self._Phi is not None, "cov has not been setup"
         xd = _dev_2d(x)
-        t = dense.matmul(self._Phi, xd, ta=True)
+        t = self._sum(dense.matmul(self._Phi, xd, ta=True))
         dense.scale_rows(t, dev.to_device(np.asarray(self._w, dtype=np.float64)), 0)
         out = xd.clone()
         dense.matmul(self._Phi, t, alpha=1.0, beta=float(self.noise_var), C=out)
@@ -384,7 +410,7 @@ class GPGriefModel(BaseModel):
 
     def _mv_cov_inv_dev(self, xd):
         """(x - Phi P^-1 Phi^T x) / s for a 1-D device vector."""
-        t = dense.matvec(self._Phi, xd, trans=True)
+        t = self._sum(dense.matvec(self._Phi, xd, trans=True))
         t = self._Pchol.solve(t, which=3)
         out = xd.clone()
         dense.matvec(self._Phi, t, alpha=-1.0, beta=1.0, y=out)
@@ -393,10 +419,10 @@ class GPGriefModel(BaseModel):
 
     def _mv_cov_inv(self, x):
         """(x - Phi cho_solve(P, Phi^T x)) / s (:228-235)."""
-        assert x.shape[0] == self.num_data
+        assert x.shape[0] == self._n_local
         assert self._Pchol is not None, "cov has not been setup"
         xd = _dev_2d(x)
-        t = dense.matmul(self._Phi, xd, ta=True)
+        t = self._sum(dense.matmul(self._Phi, xd, ta=True))
         t = self._Pchol.solve(t, which=3)
         out = xd.clone()
         dense.matmul(self._Phi, t, alpha=-1.0, beta=1.0, C=out)

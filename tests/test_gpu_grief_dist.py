@@ -1,0 +1,60 @@
+"""P2 (GRIEF) sharded over data rows: G virtual ranks (threads on one MI355X),
+each holding its rows of X / Y and its own replica of the basis, reduce the
+Gram, the Phi^T v products and the scalars through
+tests/dist_helpers.ThreadExchange (the stand-in for RCCL all-reduce).  Every
+rank must reproduce the reference-generated fixture values that the
+unsharded model matches (LML, gradient, predictive mean and covariance, to
+the north star's 1e-6 relative)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from dist_helpers import ThreadExchange, run_threads
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.mark.parametrize("case,world", [("3d", 2), ("6d", 3), ("8d", 4)])
+def test_grief_row_sharded_matches_fixture(gpu, case, world):
+    import gp_grief_amd as gg
+    import gp_grief_amd.grid  # noqa: F401
+    import gp_grief_amd.kern  # noqa: F401
+    import gp_grief_amd.models  # noqa: F401
+    z = golden("grief_small_%s.npz" % case)
+    d = z["x"].shape[1]
+    n = z["x"].shape[0]
+    kind = str(z["kind"])
+    bounds = np.linspace(0, n, world + 1).astype(int)  # uneven shards allowed
+    ex = ThreadExchange(world)
+
+    def body(g):
+        ex.bind(g)
+        kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=float(l))
+              for l in z["lengthscales"]]
+        grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, int(z["m"])).reshape(-1, 1)
+                                        for _ in range(d)])
+        kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=int(z["p"]))
+        lo, hi = bounds[g], bounds[g + 1]
+        m = gg.models.GPGriefModel(z["x"][lo:hi], z["y"][lo:hi].reshape(-1, 1), kern,
+                                   noise_var=float(z["sigma2"]), comm=ex)
+        assert m.num_data == n
+        ll, grad = m.log_likelihood(return_gradient=True)
+        mean, var = m.predict(z["xtest"])
+        return float(ll[0, 0]), grad.copy(), mean, var
+
+    res = run_threads(world, body)
+    p = int(z["p"])
+    for ll, grad, mean, var in res:
+        assert abs(ll - z["lml"]) < 1e-6 * abs(z["lml"])
+        assert rel(mean[:, 0], z["pred_mean"]) < 1e-6
+        assert rel(var, z["pred_var"]) < 1e-6
+        assert rel(grad[-p:], z["grad"][-p:]) < 1e-6
+        assert abs(grad[0] - z["grad"][0]) < 1e-6 * abs(z["grad"][0])
+    # every rank holds the same answer
+    assert max(abs(r[0] - res[0][0]) for r in res) <= 1e-9 * abs(res[0][0])
