@@ -435,3 +435,127 @@ class GPGriefModel(BaseModel):
         assert self._Pchol is not None, "cov has not been setup"
         return (self._Pchol.logdet + np.sum(np.log(self._w))
                 + float(self.num_data - self.kern.n_eigs) * np.log(self.noise_var))
+
+
+class GPGridModel(BaseModel):
+    """Gaussian process with Y observed on every point of a full Kronecker grid
+    (P1, the north star's grid model).  The reference has no such class; it
+    is composed from the reference's own primitives exactly as SURVEY 8c
+    prescribes: K = GridKernel.cov_grid(xg) (grid_kernel.py:56-115, input
+    dimension 0 fastest), the shifted solve KronMatrix.solve_schur
+    (kron_matrix.py:328-352) or CG, the log det from the Kronecker eigenvalues
+    (kron_matrix.py:466-474 extended to the shift) or stochastic Lanczos,
+    posterior mean K alpha and latent variance (Q o Q)-Kron (t s / (t + s)).
+
+    solver: 'exact' (per-factor eigendecomposition, two device Kron matvecs
+    and a decoded divide) or 'cg' (device CG, linalg.KronCG).  logdet: 'exact'
+    (streamed over the grid on the device) or 'slq'.  Y (N,1) numpy or CUDA
+    tensor; results come back in the same kind.  grad_method is finite
+    differences over (noise, kernel parameters) like the reference's
+    kernel-parameter path.
+    """
+
+    def __init__(self, xg, Y, kern, noise_var=1., solver='exact', logdet='exact',
+                 dim_noise_var=1e-12, cg_rtol=1e-10, slq_probes=8, slq_steps=50, seed=0):
+        super(GPGridModel, self).__init__()
+        from .kern import GridKernel
+        assert isinstance(kern, GridKernel)
+        if solver not in ('exact', 'cg'):
+            raise ValueError("solver must be 'exact' or 'cg'")
+        if logdet not in ('exact', 'slq'):
+            raise ValueError("logdet must be 'exact' or 'slq'")
+        self.xg = xg
+        self.kern = kern
+        self.num_data = int(np.prod([np.shape(g)[0] for g in xg]))
+        if tuple(Y.shape) != (self.num_data, 1):
+            raise ValueError('Y must be (%d,1), the flattened grid' % self.num_data)
+        self._y_is_dev = dev.is_device_array(Y)
+        self._yd = dev.to_device(Y)
+        self.noise_var = np.float64(noise_var)
+        self.solver, self.logdet = solver, logdet
+        self.dim_noise_var = float(dim_noise_var)
+        self.cg_rtol = float(cg_rtol)
+        self.slq = (int(slq_probes), int(slq_steps), int(seed))
+        self.grad_method = 'finite_difference'
+        self._K = self._QT = self._kern_key = None
+        self.dependent_attributes = list(self.dependent_attributes)
+        self._alpha = self._log_like = self._gradient = self._log_det = None
+
+    # ---- operator, cached on the kernel parameters (like grief_kernel.py:171-173)
+    def _operator(self):
+        key = np.asarray(self.kern.parameters).copy()
+        if self._K is None or not np.array_equal(key, self._kern_key):
+            self._K = self.kern.cov_grid(self.xg, dim_noise_var=self.dim_noise_var)
+            self._QT = None
+            self._kern_key = key
+        return self._K
+
+    def _schur(self):
+        K = self._operator()
+        if self._QT is None:
+            self._QT = K.schur()
+        return self._QT
+
+    def fit(self):
+        self.parameters
+        if self._alpha is not None:
+            return
+        s = float(self.noise_var)
+        y = self._yd.reshape(-1, 1)
+        if self.solver == 'exact':
+            Q, T = self._schur()
+            self._alpha = Q.solve_schur(T, y, shift=s).reshape(-1)
+        else:
+            from .linalg import cg
+            x, info = cg(self._operator(), y, shift=s, rtol=self.cg_rtol)
+            if info != 0:
+                logger.info('CG did not converge in %d iterations' % info)
+            self._alpha = x.reshape(-1)
+
+    def _cov_log_det(self):
+        if self._log_det is None:
+            s = float(self.noise_var)
+            if self.logdet == 'exact':
+                Q, T = self._schur()
+                self._log_det = T.diag().log_det_shifted(s)
+            else:
+                from .linalg import slq_logdet
+                probes, steps, seed = self.slq
+                self._log_det = slq_logdet(self._operator(), s, probes=probes, steps=steps,
+                                           seed=seed)[0]
+        return self._log_det
+
+    def _compute_log_likelihood(self, parameters):
+        self.parameters = parameters
+        self.fit()
+        ll = -0.5 * (dense.dot(self._yd, self._alpha) + self._cov_log_det()
+                     + self.num_data * np.log(2 * np.pi))
+        return np.array([[ll]])
+
+    def _out(self, vd):
+        return vd.reshape(-1, 1) if self._y_is_dev else dev.to_host(vd).reshape(-1, 1)
+
+    def predict_grid(self, compute_var=True):
+        """Posterior mean K alpha on the grid and the predictive variance
+        diag(K - K (K + s I)^-1 K) + s (the latent variance from the
+        eigenpairs, streamed on the device)."""
+        from . import native
+        from .tensors import KronMatrix
+        self.fit()
+        K = self._operator()
+        mean = K.matvec_device(self._alpha)
+        if not compute_var:
+            return self._out(mean), None
+        s = float(self.noise_var)
+        Q, T = self._schur()
+        lam = [np.asarray(e, dtype=np.float64).reshape(-1) for e in T.diag().K]
+        lamd = dev.to_device(np.concatenate(lam))
+        v = dev.empty(self.num_data)
+        native.check(native.lib().gg_kron_diag_scale(
+            len(lam), native.i64_array([l.size for l in lam]), native.dptr(lamd), s,
+            native.GG_DIAG_POSTVAR, None, native.dptr(v), native.stream_ptr()),
+            "gg_kron_diag_scale")
+        Q2 = KronMatrix([np.asarray(q) ** 2 for q in Q.K])
+        var = Q2.matvec_device(v)
+        var += s
+        return self._out(mean), self._out(var)

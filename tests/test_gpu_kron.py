@@ -332,3 +332,42 @@ def test_slq_logdet_vs_exact(gg):
                                probes=16, steps=60, seed=3)
     # same probes, same recurrence: the estimates agree far below the SLQ error
     assert abs(est - eo) < 1e-6 * abs(eo)
+
+
+# ---------------------------------------------------------------- GPGridModel (P1 model)
+def _grid_model(gg, z, **kw):
+    d = z["factors"].shape[0]
+    m = z["factors"].shape[1]
+    kerns = [gg.kern.RBF(1, variance=1.0, lengthscale=float(l)) for l in z["lengthscales"]]
+    xg = [np.linspace(0.0, 1.0, m).reshape(-1, 1) for _ in range(d)]
+    return gg.models.GPGridModel(xg, z["y"].reshape(-1, 1), gg.kern.GridKernel(kerns),
+                                 noise_var=float(z["sigma2"]), **kw)
+
+
+def test_grid_model_exact_golden(gg):
+    """Posterior mean, predictive variance and LML of the full-grid GP against
+    the reference-generated fixture (north-star bar 1e-6; achieved ~1e-9)."""
+    import gp_grief_amd.models  # noqa: F401
+    z = golden("grid_gp.npz")
+    mdl = _grid_model(gg, z)
+    np.testing.assert_allclose(np.stack(mdl._operator().K), z["factors"], rtol=0, atol=1e-14)
+    lml = mdl.log_likelihood()
+    assert lml.shape == (1, 1)
+    assert abs(lml[0, 0] - z["lml"]) < 1e-8 * abs(z["lml"])
+    mean, var = mdl.predict_grid()
+    assert rel(mean, z["mean"]) < 1e-8
+    assert rel(var, z["var_latent"] + float(z["sigma2"])) < 1e-9
+
+
+def test_grid_model_cg_and_slq(gg):
+    """The same model with the device CG solve (rtol 1e-10) and the SLQ log
+    det: LML to 1e-6 via CG + exact log det; SLQ is a statistical estimate
+    (parity unpinned), checked to 1 %."""
+    z = golden("grid_gp.npz")
+    cgm = _grid_model(gg, z, solver="cg")
+    assert abs(cgm.log_likelihood()[0, 0] - z["lml"]) < 1e-6 * abs(z["lml"])
+    assert rel(cgm._alpha.cpu().numpy(), z["alpha"]) < 1e-8
+    slq = _grid_model(gg, z, logdet="slq", slq_probes=16, slq_steps=60)
+    assert abs(slq._cov_log_det() - z["logdet"]) < 1e-2 * abs(z["logdet"])
+    with pytest.raises(ValueError):
+        _grid_model(gg, z, solver="lu")
