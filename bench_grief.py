@@ -1,0 +1,222 @@
+"""P2 (GRIEF) fit benchmark: SURVEY 8(d) configs C2 / C4 / C5 on one MI355X.
+
+Not the driver's bench line (that is bench.py, the P1 200^4 CG).  This
+measures the second half of the north star's hot path, GPGriefModel's fit
+(gp_grief_model.py:78-87, 137-153, 203-245) and its adjoint gradient /
+prediction, stage by stage with HIP events on the stream the C ABI launches
+on:
+
+  setup   GriefKernel._setup_inducing_cov: grid covariances, device Jacobi
+          eigensolve of the d factors, host top-p selection (grief_kernel.py:168-190)
+  phi     gg_grief_tables + gg_grief_phi (expand_SKC, tensors.py:97-128)
+  gram    A = Phi^T Phi on FP64 MFMA (gp_grief_model.py:148)
+  chol    P = A + diag(s/w), blocked potrf (:149-153)
+  alpha   Woodbury solve (:228-235) + LML (:203-214)
+  grad    adjoint gradient (:156-200)
+  predict M = 1000 test points, mean + full M x M covariance (:89-125)
+
+Inputs: xg_i = linspace(0, 1, m), x ~ U[0,1]^d (default_rng(0)),
+n = 100 000, y = sum_i sin(6 x_i) + 0.1 eps (default_rng(1)), s = 0.01,
+test points from default_rng(2); lengthscales 0.2 (1 + 0.05 i).
+
+Roofline per stage: gram is MFMA-bound (FLOP = 2 n p^2 for the full GEMM,
+n p^2 when only the lower triangle is formed; the JSON says which), phi is
+HBM-bound (bytes = 8 n p written + 16 n U table reads).
+
+cpu_baseline: the oracle (NumPy/OpenBLAS restatement of the same fit,
+oracle/grief.py) on a bounded row sample of the same workload, host cores
+threads; the GPU fit on the SAME sample is checked against it (LML relative
+difference reported) -- test infrastructure used only as the checker/baseline.
+
+Usage: python bench_grief.py [--configs C2,C4,C5] [--repeats 3] [--cpu auto|off]
+Prints one JSON line per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_MFMA_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (dims, m, kind, p, n, cpu sample rows)
+    "C2": (3, 128, "RBF", 1000, 100000, 100000),
+    "C4": (6, 64, "Matern52", 5000, 100000, 20000),
+    "C5": (8, 32, "RBF", 10000, 100000, 10000),
+}
+
+
+def make_data(d, n, M=1000):
+    x = np.random.default_rng(0).random((n, d))
+    eps = np.random.default_rng(1).standard_normal(n)
+    y = np.sin(6.0 * x).sum(axis=1) + 0.1 * eps
+    xt = np.random.default_rng(2).random((M, d))
+    return x, y.reshape(-1, 1), xt
+
+
+def lengthscales(d):
+    return [0.2 * (1.0 + 0.05 * i) for i in range(d)]
+
+
+def build_model(gg, d, m, kind, p, x, y, s):
+    kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=l) for l in lengthscales(d)]
+    grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1) for _ in range(d)])
+    kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+    return gg.models.GPGriefModel(x, y, kern, noise_var=s)
+
+
+class Stages(object):
+    """HIP events on torch's current stream (the one the C ABI launches on)."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.ev = []
+
+    def mark(self, name):
+        e = self.torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.ev.append((name, e))
+
+    def read(self):
+        self.torch.cuda.synchronize()
+        out = {}
+        for (n0, e0), (n1, e1) in zip(self.ev[:-1], self.ev[1:]):
+            out[n1] = e0.elapsed_time(e1)
+        return out
+
+
+def gpu_fit(gg, torch, d, m, kind, p, x, y, xt, s):
+    """One cold fit through the public API, stage-timed. Returns (times ms, model, ll)."""
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    st = Stages(torch)
+    st.mark("start")
+    mdl = build_model(gg, d, m, kind, p, x, y, s)
+    mdl.parameters                      # noqa: B018  (resolves dependent attributes)
+    mdl.kern._setup_inducing_cov()
+    st.mark("setup")
+    mdl._w = mdl.kern.w
+    mdl._Phi = mdl.kern.phi_device(mdl.X)
+    st.mark("phi")
+    mdl._A = mdl._gram()
+    st.mark("gram")
+    mdl._cov_setup()                    # A kept: P = A + diag(s/w), potrf
+    st.mark("chol")
+    ll = mdl.log_likelihood()           # alpha (Woodbury) + LML
+    st.mark("alpha")
+    torch.cuda.synchronize()
+    wall_fit = time.perf_counter() - w0
+    ll2, grad = mdl.log_likelihood(return_gradient=True)
+    st.mark("grad")
+    mean, var = mdl.predict(xt)
+    st.mark("predict")
+    times = st.read()
+    times["fit_wall"] = 1e3 * wall_fit
+    return times, mdl, float(np.squeeze(ll)), grad, mean, var
+
+
+def cpu_fit(d, m, kind, p, x, y, s):
+    import oracle
+    from oracle.grief import grief_inducing, grief_phi, grief_fit, grief_lml
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(limits=threads)
+    except Exception:  # pragma: no cover
+        ctx = None
+    specs = [(kind, 1.0, l) for l in lengthscales(d)]
+    xg = [np.linspace(0, 1, m) for _ in range(d)]
+    t0 = time.perf_counter()
+    ind = grief_inducing(specs, xg, p)
+    t1 = time.perf_counter()
+    Phi = grief_phi(x, specs, xg, ind)
+    t2 = time.perf_counter()
+    fit = grief_fit(Phi, np.ones(ind["p"]), y, s)
+    ll = grief_lml(fit, y)
+    t3 = time.perf_counter()
+    if ctx is not None:
+        ctx.__exit__(None, None, None)
+    del oracle
+    return {"setup_s": t1 - t0, "phi_s": t2 - t1, "gram_chol_alpha_s": t3 - t2,
+            "fit_s": t3 - t0, "threads": threads, "lml": ll}
+
+
+def run_config(gg, torch, name, repeats, cpu, s=0.01):
+    d, m, kind, p, n, n_cpu = CONFIGS[name]
+    x, y, xt = make_data(d, n)
+    runs = []
+    for _ in range(repeats):
+        times, mdl, ll, grad, mean, var = gpu_fit(gg, torch, d, m, kind, p, x, y, xt, s)
+        runs.append(times)
+        U = mdl.kern._dev_basis["U"]
+        uplo = mdl._gram_uplo
+        del mdl
+        torch.cuda.empty_cache()
+    best = {k: min(r[k] for r in runs) for k in runs[0]}
+    fit_ms = sum(best[k] for k in ("setup", "phi", "gram", "chol", "alpha"))
+    gram_flop = (1.0 if uplo else 2.0) * n * p * p
+    gram_tf = gram_flop / (best["gram"] * 1e-3) / 1e12
+    phi_bytes = 8.0 * n * p + 16.0 * n * U
+    phi_gbs = phi_bytes / (best["phi"] * 1e-3) / 1e9
+    res = {
+        "metric": "GRIEF fit (setup + Phi + Gram + Cholesky + alpha + LML)",
+        "value": 1e3 / fit_ms, "unit": "fits/s", "fit_ms": fit_ms,
+        "higher_is_better": True, "n_gpus": 1, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": name, "dims": d, "grid": m, "kernel": kind, "p": p, "n": n,
+                   "sigma2": s, "U_selected_rows": U, "repeats": repeats},
+        "stage_ms": best,
+        "gram": {"bound": "mfma", "flop": gram_flop,
+                 "flop_rule": "n p^2 (lower triangle only)" if uplo else "2 n p^2 (full GEMM)",
+                 "achieved": gram_tf, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": gram_tf / FP64_MFMA_PEAK_TFLOPS},
+        "phi": {"bound": "hbm", "bytes": phi_bytes, "achieved": phi_gbs,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": phi_gbs / HBM_PEAK_GBS},
+        "lml": ll,
+    }
+    if cpu:
+        xs, ys = x[:n_cpu], y[:n_cpu]
+        c = cpu_fit(d, m, kind, p, xs, ys, s)
+        # the GPU fit on the same sample, checked against the oracle
+        t, mdl, ll_s, _, _, _ = gpu_fit(gg, torch, d, m, kind, p, xs, ys, xt[:10], s)
+        gpu_sample_ms = sum(t[k] for k in ("setup", "phi", "gram", "chol", "alpha"))
+        res["cpu_baseline"] = {
+            "value": 1.0 / c["fit_s"], "unit": "fits/s", "cores": c["threads"], "kind": "port",
+            "sample": "oracle/grief.py fit on the first %d of the %d rows (NumPy/OpenBLAS, "
+                      "%d threads): setup %.2f s, Phi %.2f s, Gram+chol+alpha %.2f s"
+                      % (n_cpu, n, c["threads"], c["setup_s"], c["phi_s"],
+                         c["gram_chol_alpha_s"]),
+            "gpu_fit_ms_same_sample": gpu_sample_ms,
+            "speedup_same_sample": c["fit_s"] * 1e3 / gpu_sample_ms,
+            "lml_rel_diff_same_sample": abs(ll_s - c["lml"]) / abs(c["lml"]),
+        }
+        del mdl
+        torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="C2,C4,C5")
+    ap.add_argument("--repeats", type=int, default=3)
+    ap.add_argument("--cpu", default="auto", choices=["auto", "off"])
+    a = ap.parse_args()
+    import torch
+    import gp_grief_amd as gg
+    import gp_grief_amd.grid  # noqa: F401
+    import gp_grief_amd.kern  # noqa: F401
+    import gp_grief_amd.models  # noqa: F401
+    gg.native.load()
+    for name in a.configs.split(","):
+        print(json.dumps(run_config(gg, torch, name.strip(), a.repeats, a.cpu == "auto")),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

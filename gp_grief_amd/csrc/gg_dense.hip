@@ -427,41 +427,51 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
 
 // Solve (L L^T) X = B in place for B: n x r (ldb), using the factor and the
 // diagonal-block inverses from gg_potrf.  which: 1 = forward only (L^-1 B),
-// 2 = backward only (L^-T B), 3 = both (P^-1 B).
+// 2 = backward only (L^-T B), 3 = both (P^-1 B); | 4 = B is lower triangular
+// (e.g. the identity, for L^-1 itself: forward only), so block row k only
+// touches columns < k0 + nb.
+// Right-looking: after block k is solved, ONE GEMM updates every remaining
+// block row (M = rows left, K = nb), so each step is parallel over the rows
+// instead of a single row-tile reducing over all previous blocks.
 int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_dev,
              double* B_dev, int64_t ldb, int which, double* tmp_dev, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(n >= 1 && r >= 0 && L_dev && winv_dev && B_dev && tmp_dev, GG_ERR_VALUE,
                "bad argument");
+    GG_REQUIRE(!((which & 4) && (which & 2)), GG_ERR_VALUE,
+               "triangular right-hand side is forward-only");
     if (r == 0) return;
     hipStream_t s = gg::as_stream(stream);
     const int nblk = (int)gg::ceil_div(n, gg::kNB);
+    const bool tri = (which & 4) != 0;
     if (which & 1) {
       for (int b = 0; b < nblk; ++b) {
         const int k0 = b * gg::kNB, nb = std::min(gg::kNB, n - k0);
+        const int rc = tri ? std::min(r, k0 + nb) : r;   // live columns
         double* Bk = B_dev + (int64_t)k0 * ldb;
-        if (k0 > 0)  // B_k -= L[k0:k0+nb, 0:k0] Y[0:k0]
-          gg::gemm(false, false, nb, r, k0, -1.0, L_dev + (int64_t)k0 * lda, lda, B_dev, ldb,
-                   1.0, Bk, ldb, 0, s);
         // Y_k = W_k B_k  (through tmp: W_k reads all nb rows of B_k)
-        gg::gemm(false, false, nb, r, nb, 1.0, winv_dev + (int64_t)b * gg::kNB * gg::kNB,
-                 gg::kNB, Bk, ldb, 0.0, tmp_dev, r, 0, s);
-        GG_HIP(hipMemcpy2DAsync(Bk, ldb * sizeof(double), tmp_dev, r * sizeof(double),
-                                r * sizeof(double), nb, hipMemcpyDeviceToDevice, s));
+        gg::gemm(false, false, nb, rc, nb, 1.0, winv_dev + (int64_t)b * gg::kNB * gg::kNB,
+                 gg::kNB, Bk, ldb, 0.0, tmp_dev, rc, 0, s);
+        GG_HIP(hipMemcpy2DAsync(Bk, ldb * sizeof(double), tmp_dev, rc * sizeof(double),
+                                rc * sizeof(double), nb, hipMemcpyDeviceToDevice, s));
+        const int below = n - k0 - nb;
+        if (below > 0)  // B[k0+nb:n] -= L[k0+nb:n, k0:k0+nb] Y_k
+          gg::gemm(false, false, below, rc, nb, -1.0, L_dev + (int64_t)(k0 + nb) * lda + k0, lda,
+                   Bk, ldb, 1.0, B_dev + (int64_t)(k0 + nb) * ldb, ldb, 0, s);
       }
     }
     if (which & 2) {
       for (int b = nblk - 1; b >= 0; --b) {
         const int k0 = b * gg::kNB, nb = std::min(gg::kNB, n - k0);
-        const int below = n - k0 - nb;
         double* Bk = B_dev + (int64_t)k0 * ldb;
-        if (below > 0)  // Y_k -= L[k0+nb:n, k0:k0+nb]^T X[k0+nb:n]
-          gg::gemm(true, false, nb, r, below, -1.0, L_dev + (int64_t)(k0 + nb) * lda + k0, lda,
-                   B_dev + (int64_t)(k0 + nb) * ldb, ldb, 1.0, Bk, ldb, 0, s);
+        // X_k = W_k^T B_k
         gg::gemm(true, false, nb, r, nb, 1.0, winv_dev + (int64_t)b * gg::kNB * gg::kNB,
                  gg::kNB, Bk, ldb, 0.0, tmp_dev, r, 0, s);
         GG_HIP(hipMemcpy2DAsync(Bk, ldb * sizeof(double), tmp_dev, r * sizeof(double),
                                 r * sizeof(double), nb, hipMemcpyDeviceToDevice, s));
+        if (k0 > 0)  // B[0:k0] -= L[k0:k0+nb, 0:k0]^T X_k
+          gg::gemm(true, false, k0, r, nb, -1.0, L_dev + (int64_t)k0 * lda, lda, Bk, ldb, 1.0,
+                   B_dev, ldb, 0, s);
       }
     }
   });

@@ -80,7 +80,8 @@ class Cholesky(object):
         self.logdet = ld.value
 
     def solve(self, B, which=3):
-        """P^-1 B (which 3), L^-1 B (1) or L^-T B (2); B is (n,) or (n, r); returns new."""
+        """P^-1 B (which 3), L^-1 B (1) or L^-T B (2); B is (n,) or (n, r); returns new.
+        which | 4: B is lower triangular (forward only; L^-1 of the identity)."""
         t = dev.torch()
         X = B.contiguous().clone()
         r = 1 if X.dim() == 1 else int(X.shape[1])
@@ -95,7 +96,7 @@ class Cholesky(object):
         """diag(P^-1) = column sums of squares of L^-1."""
         t = dev.torch()
         I = t.eye(self.n, dtype=t.float64, device=self.L.device)
-        Linv = self.solve(I, which=1)
+        Linv = self.solve(I, which=5)
         out = dev.empty(self.n)
         native.check(_lib().gg_colsumsq_lower(self.n, native.dptr(Linv), self.n,
                                               native.dptr(out), native.stream_ptr()))

@@ -296,6 +296,7 @@ class GPGriefModel(BaseModel):
         else:
             self.grad_method = ['adjoint', 'finite_difference'][0]
         self._Yd = None
+        self._gram_uplo = 1   # A = Phi^T Phi is formed in its lower triangle only
 
     # ---- global sums over the data-row shards (identity without comm)
     def _sum(self, t):
@@ -354,10 +355,19 @@ class GPGriefModel(BaseModel):
         self._w = self.kern.w
         if self._A is None:
             self._Phi = self.kern.phi_device(self.X)          # n x p
-            self._A = self._sum(dense.matmul(self._Phi, self._Phi, ta=True))  # Phi^T Phi
+            self._A = self._gram()
         wd = dev.to_device(np.asarray(self._w, dtype=np.float64))
         self._P = dense.add_diag(self._A, float(self.noise_var), wd)
         self._Pchol = dense.Cholesky(self._P)
+
+    def _gram(self):
+        """A = Phi^T Phi (:148), summed over the data-row shards, in its lower
+        triangle only: half the MFMA work of the full GEMM, and potrf and the
+        adjoint gradient read nothing above the diagonal (the upper stays 0)."""
+        t = dev.torch()
+        p = int(self._Phi.shape[1])
+        A = t.zeros((p, p), dtype=t.float64, device=self._Phi.device)
+        return self._sum(dense.matmul(self._Phi, self._Phi, ta=True, C=A, uplo=self._gram_uplo))
 
     def _adjoint_gradient(self, parameters):
         """dL/dw and dL/dsigma^2 (:156-200) via diag(P^-1): with P = A + D,

@@ -32,7 +32,7 @@ def grief_inducing(kern_specs, xg, n_eigs, jitter=1e-12):
         g = np.asarray(xg[i], dtype=np.float64).reshape(-1)
         K.append(cov_1d(kind, g, g, var, ls) + jitter * np.eye(g.size))
     Q, lam = factor_eigh(K)
-    total = float(np.prod([g.size for g in K]))
+    total = float(np.prod([float(k.shape[0]) for k in K]))   # grid size, as float (no overflow)
     p = int(min(n_eigs, total))
     pos, log_lam, _ = find_extremum_eigs(lam, p, mode='largest', log_expand=True)
     return dict(K=K, Q=Q, lam=lam, eig_pos=pos, log_lam=log_lam, p=p)
