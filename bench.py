@@ -105,7 +105,19 @@ def run_sharded(a, world, rank, torch, dev, dist):
     y = local_rhs_device(m, d, world, rank, torch, dev)
     ex = TorchExchange()
     mode = os.environ.get("GG_DIST_MODE", "auto")
-    cg = DistKronCG(eng, ex, s, mode=mode)
+    # every rank must take the same exchange: a push setup that fails on any
+    # rank (IPC mapping of a peer's buffer) sends all ranks to all-to-all
+    try:
+        cg = DistKronCG(eng, ex, s, mode=mode)
+        ok = 1.0
+    except Exception as exc:  # noqa: BLE001
+        print("rank %d: %s exchange setup failed (%s); using a2a" % (rank, mode, exc),
+              file=sys.stderr, flush=True)
+        cg, ok = None, 0.0
+    flag = torch.tensor([ok], dtype=torch.float64, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if float(flag.item()) < 1.0:
+        cg = DistKronCG(eng, ex, s, mode="a2a")
     if cg.mode == "push":
         # one matvec through the peer-memory exchange against the all-to-all
         # path on the same input; any disagreement falls back to all-to-all

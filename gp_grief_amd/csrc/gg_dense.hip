@@ -283,17 +283,22 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* A, int64_t lda,
     }
     __syncthreads();
   }
-  // inverse of the lower-triangular factor, one column per thread
-  for (int j = tid; j < nb; j += blockDim.x) {
-    for (int i = 0; i < nb; ++i) Wi[i][j] = 0.0;
-    Wi[j][j] = 1.0 / L[j][j];
-    for (int i = j + 1; i < nb; ++i) {
+  // inverse of the lower-triangular factor, one row per step: W[i][j] for all
+  // j <= i at once (4 adjacent lanes split the k-sum, quad shuffle reduce)
+  for (int e = tid; e < kNB * kNB; e += blockDim.x) Wi[e / kNB][e % kNB] = 0.0;
+  __syncthreads();
+  {
+    const int j = tid >> 2, part = tid & 3;   // blockDim.x == 256 = kNB * 4
+    for (int i = 0; i < nb; ++i) {
       double s = 0.0;
-      for (int k = j; k < i; ++k) s = fma(L[i][k], Wi[k][j], s);
-      Wi[i][j] = -s / L[i][i];
+      if (j < i)
+        for (int k = j + part; k < i; k += 4) s = fma(L[i][k], Wi[k][j], s);
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      if (part == 0 && j <= i) Wi[i][j] = (j == i) ? 1.0 / L[i][i] : -s / L[i][i];
+      __syncthreads();
     }
   }
-  __syncthreads();
   for (int e = tid; e < nb * nb; e += blockDim.x) {
     const int i = e / nb, j = e % nb;
     if (j <= i) A[(int64_t)i * lda + j] = L[i][j];
@@ -331,15 +336,26 @@ __global__ void add_diag_kernel(int n, const double* __restrict__ A, int64_t lda
 }
 
 // out[j] = sum_i M[i][j]^2 (column sums of squares; lower-triangular M uses i >= j)
-__global__ void colsumsq_kernel(int n, const double* __restrict__ Mx, int64_t ld, double* out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+// 64 columns per workgroup x 16 row phases (1024 threads), fixed-order LDS
+// reduction over the phases (deterministic)
+__global__ __launch_bounds__(1024) void colsumsq_kernel(int n, const double* __restrict__ Mx,
+                                                        int64_t ld, double* out) {
+  __shared__ double part[16][65];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
   double s = 0.0;
-  for (int i = j; i < n; ++i) {
-    const double v = Mx[(int64_t)i * ld + j];
-    s = fma(v, v, s);
+  if (j < n)
+    for (int i = j + ph; i < n; i += 16) {
+      const double v = Mx[(int64_t)i * ld + j];
+      s = fma(v, v, s);
+    }
+  part[ph][c] = s;
+  __syncthreads();
+  if (ph == 0 && j < n) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += part[k][c];
+    out[j] = t;
   }
-  out[j] = s;
 }
 
 }  // namespace gg
@@ -396,21 +412,39 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     int* status = reinterpret_cast<int*>(winv_dev + (int64_t)nblk * gg::kNB * gg::kNB);
     double* ld = winv_dev + (int64_t)nblk * gg::kNB * gg::kNB + 8;
     GG_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
-    for (int b = 0; b < nblk; ++b) {
-      const int k0 = b * gg::kNB;
-      const int nb = std::min(gg::kNB, n - k0);
-      double* Akk = A_dev + (int64_t)k0 * lda + k0;
-      double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
-      hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(256), 0, s, Akk, lda, nb, Wk,
-                         status);
-      GG_LAUNCH_CHECK();
-      const int rest = n - k0 - nb;
-      if (rest > 0) {
-        double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
-        // L21 = A21 W^T (in place: one column tile, each block owns its rows)
-        gg::gemm(false, true, rest, nb, nb, 1.0, A21, lda, Wk, gg::kNB, 0.0, A21, lda, 0, s);
-        double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
-        gg::gemm(false, true, rest, rest, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
+    // Two-level blocking: 64-wide diagonal blocks inside 256-wide panels.  A
+    // block's update reaches only the columns left in its panel; the columns
+    // right of the panel take one K = 256 update per panel, so the trailing
+    // matrix is streamed n / 256 times instead of n / 64.
+    constexpr int kPanel = 4 * gg::kNB;
+    for (int P0 = 0; P0 < n; P0 += kPanel) {
+      const int pend = std::min(n, P0 + kPanel);
+      for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
+        const int b = k0 / gg::kNB;
+        const int nb = std::min(gg::kNB, n - k0);
+        double* Akk = A_dev + (int64_t)k0 * lda + k0;
+        double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
+        hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(256), 0, s, Akk, lda, nb, Wk,
+                           status);
+        GG_LAUNCH_CHECK();
+        const int rest = n - k0 - nb;
+        if (rest > 0) {
+          double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
+          // L21 = A21 W^T (in place: one column tile, each block owns its rows)
+          gg::gemm(false, true, rest, nb, nb, 1.0, A21, lda, Wk, gg::kNB, 0.0, A21, lda, 0, s);
+          const int pw = pend - (k0 + nb);   // panel columns right of this block
+          if (pw > 0) {
+            double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
+            gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
+          }
+        }
+      }
+      const int trail = n - pend;
+      if (trail > 0) {  // A[pend:, pend:] -= L[pend:, P0:pend] L[pend:, P0:pend]^T (lower)
+        const double* Lp = A_dev + (int64_t)pend * lda + P0;
+        double* A22 = A_dev + (int64_t)pend * lda + pend;
+        gg::gemm(false, true, trail, trail, pend - P0, -1.0, Lp, lda, Lp, lda, 1.0, A22, lda, 1,
+                 s);
       }
     }
     hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
@@ -482,7 +516,7 @@ int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
   return gg::guard([&] {
     GG_REQUIRE(n >= 0 && M_dev && out_dev, GG_ERR_VALUE, "bad argument");
     if (n == 0) return;
-    hipLaunchKernelGGL(gg::colsumsq_kernel, dim3((unsigned)gg::ceil_div(n, 256)), dim3(256), 0,
+    hipLaunchKernelGGL(gg::colsumsq_kernel, dim3((unsigned)gg::ceil_div(n, 64)), dim3(1024), 0,
                        gg::as_stream(stream), n, M_dev, ld, out_dev);
     GG_LAUNCH_CHECK();
   });

@@ -5,13 +5,15 @@
 // Here one workgroup owns one factor and runs two-sided Jacobi with the
 // round-robin (tournament) pairing: each round rotates m/2 disjoint index pairs
 // at once -- a row pass, then a column pass (+ the eigenvector update), with a
-// workgroup barrier between passes.  The matrix and the accumulated rotations
-// live in the caller's HBM scratch (L2-resident: 2 m^2 f64 per factor), so any
-// m fits; only the rotation table is in LDS.  Sweeps stop when a whole sweep
+// workgroup barrier between passes.  For m <= 128 the matrix lives in LDS
+// (padded rows); larger factors keep it in the caller's HBM scratch
+// (L2-resident), so any m fits.  The accumulated rotations are stored
+// transposed in the scratch, so their update rides on the coalesced row pass.  Sweeps stop when a whole sweep
 // applies no rotation (|a_pq| below eps*sqrt|a_pp a_qq|) or at max_sweeps.
 // Output: eigenvalues ascending with matching eigenvector columns (the same
 // convention as numpy.linalg.eigh; the reference's gees order is unsorted and
 // every consumer is order-invariant).
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -20,8 +22,23 @@
 namespace gg {
 
 constexpr int kEigThreads = 1024;
-constexpr int kMaxPairs = 1024;  // m <= 2048
+constexpr int kLdsMaxM = 128;  // A fits in LDS (m x (m+1) f64, 132 KB) up to here
 
+// Dynamic LDS carve-up (both variants): pair tables, rotation table, sort order,
+// then (kLds) the padded matrix A.
+__host__ __device__ inline int64_t eig_lds_bytes(int m, bool lds_a) {
+  const int mm = (m + 1) & ~1, np = mm / 2;
+  int64_t b = (int64_t)np * (2 * sizeof(double) + 2 * sizeof(int)) + (int64_t)mm * sizeof(int);
+  b = (b + 15) & ~int64_t(15);
+  if (lds_a) b += (int64_t)m * (m + 1) * sizeof(double);
+  return b;
+}
+
+// kLds: A lives in LDS with row stride m + 1 (conflict-free column access);
+// else in the HBM scratch (L2-resident).  The eigenvector matrix is kept
+// TRANSPOSED (Vt = V^T, row-major) so its update is a row pass -- coalesced --
+// fused with A's row pass.
+template <bool kLds>
 __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
     const int64_t* __restrict__ dims, const int64_t* __restrict__ offs,
     const double* __restrict__ Ain, double* __restrict__ Qout, double* __restrict__ lam_out,
@@ -30,28 +47,29 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
   const int f = blockIdx.x;
   const int m = (int)dims[f];
   const int mm = (m + 1) & ~1;  // padded to even (a dummy index pairs with nobody)
-  double* A = work + work_offs[f];          // m x m, row-major
-  double* V = A + (int64_t)m * m;           // m x m, row-major, columns = eigenvectors
+  const int npairs = mm / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char eig_lds[];
+  double* cs = reinterpret_cast<double*>(eig_lds);
+  double* sn = cs + npairs;
+  int* top = reinterpret_cast<int*>(sn + npairs);
+  int* bot = top + npairs;
+  int* order = bot + npairs;
+  const int64_t head = eig_lds_bytes(m, false);
+  const int ld = kLds ? m + 1 : m;
+  double* A = kLds ? reinterpret_cast<double*>(eig_lds + head) : work + work_offs[f];
+  double* Vt = work + work_offs[f] + (int64_t)m * m;   // m x m, row-major, rows = eigenvectors
   const double* Asrc = Ain + offs[f];
   const int tid = threadIdx.x;
   const int nt = blockDim.x;
-
-  __shared__ int top[kMaxPairs], bot[kMaxPairs];
-  __shared__ double cs[kMaxPairs], sn[kMaxPairs];
   __shared__ int rotated;
-  __shared__ int order[2048];
 
   for (int64_t i = tid; i < (int64_t)m * m; i += nt) {
     const int r = (int)(i / m), c = (int)(i % m);
-    A[i] = 0.5 * (Asrc[i] + Asrc[(int64_t)c * m + r]);
-    V[i] = (r == c) ? 1.0 : 0.0;
+    A[(int64_t)r * ld + c] = 0.5 * (Asrc[i] + Asrc[(int64_t)c * m + r]);
+    Vt[i] = (r == c) ? 1.0 : 0.0;
   }
-  const int npairs = mm / 2;
-  // tournament: positions 0..mm-1; pos 0 fixed, others rotate each round
-  for (int k = tid; k < npairs; k += nt) {  // circle method, round 0
-    top[k] = k;
-    bot[k] = mm - 1 - k;
-  }
+  // tournament (circle method): positions 0..mm-1; pos 0 fixed, the others
+  // rotate each round; step 1 derives the round's pairs
   __syncthreads();
 
   const double eps = 2.220446049250313e-16;
@@ -62,7 +80,11 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
     for (int round = 0; round < mm - 1; ++round) {
       // 1) rotation parameters for the disjoint pairs of this round
       for (int k = tid; k < npairs; k += nt) {
-        int p = top[k], q = bot[k];
+        // index sitting at ring position pos after `round` rotations
+        auto at = [&](int pos) -> int {
+          return pos == 0 ? 0 : 1 + ((pos - 1 + round) % (mm - 1));
+        };
+        int p = at(k), q = at(mm - 1 - k);
         if (p > q) {
           const int t = p;
           p = q;
@@ -70,9 +92,9 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
         }
         double c = 1.0, s = 0.0;
         if (q < m) {
-          const double apq = A[(int64_t)p * m + q];
-          const double app = A[(int64_t)p * m + p];
-          const double aqq = A[(int64_t)q * m + q];
+          const double apq = A[(int64_t)p * ld + q];
+          const double app = A[(int64_t)p * ld + p];
+          const double aqq = A[(int64_t)q * ld + q];
           if (fabs(apq) > eps * sqrt(fabs(app * aqq)) && apq != 0.0) {
             const double tau = (aqq - app) / (2.0 * apq);
             const double t = (tau >= 0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
@@ -87,57 +109,51 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
         bot[k] = q;
       }
       __syncthreads();
-      // 2) row pass: rows p, q of A  <-  J^T A
-      for (int64_t w = tid; w < (int64_t)npairs * m; w += nt) {
-        const int k = (int)(w / m), col = (int)(w % m);
+      // 2) row pass: rows p, q of A and of Vt  <-  J^T (.)   (adjacent threads:
+      //    adjacent columns of one row pair)
+      for (int w = tid; w < npairs * m; w += nt) {
+        const int k = w / m, col = w - k * m;
         const int p = top[k], q = bot[k];
         const double s = sn[k];
         if (q < m && s != 0.0) {
           const double c = cs[k];
-          const double ap = A[(int64_t)p * m + col], aq = A[(int64_t)q * m + col];
-          A[(int64_t)p * m + col] = c * ap - s * aq;
-          A[(int64_t)q * m + col] = s * ap + c * aq;
+          const double ap = A[p * ld + col], aq = A[q * ld + col];
+          A[p * ld + col] = c * ap - s * aq;
+          A[q * ld + col] = s * ap + c * aq;
+          double* vp_ = Vt + p * m + col;
+          double* vq_ = Vt + q * m + col;
+          const double vp = *vp_, vq = *vq_;
+          *vp_ = c * vp - s * vq;
+          *vq_ = s * vp + c * vq;
         }
       }
       __syncthreads();
-      // 3) column pass: columns p, q of A and V  <-  (.) J
-      for (int64_t w = tid; w < (int64_t)npairs * m; w += nt) {
-        const int k = (int)(w / m), row = (int)(w % m);
+      // 3) column pass: columns p, q of A  <-  (.) J.  Adjacent threads take
+      //    adjacent pairs of the SAME row (one row's cache lines per wave, not
+      //    one line per lane)
+      for (int w = tid; w < npairs * m; w += nt) {
+        const int row = w / npairs, k = w - row * npairs;
         const int p = top[k], q = bot[k];
         const double s = sn[k];
         if (q < m && s != 0.0) {
           const double c = cs[k];
-          double* Ar = A + (int64_t)row * m;
+          double* Ar = A + row * ld;
           const double ap = Ar[p], aq = Ar[q];
           Ar[p] = c * ap - s * aq;
           Ar[q] = s * ap + c * aq;
-          double* Vr = V + (int64_t)row * m;
-          const double vp = Vr[p], vq = Vr[q];
-          Vr[p] = c * vp - s * vq;
-          Vr[q] = s * vp + c * vq;
         }
       }
       __syncthreads();
-      // 4) annihilated entries are exactly zero
+      // 4) annihilated entries are exactly zero; 5) next pairing (circle
+      //    method: index 0 fixed, ring positions 1..mm-1 rotate by one per
+      //    round, position k meets position mm-1-k) is computed in closed form
+      //    by step 1 of the next round, after the barrier below.
       for (int k = tid; k < npairs; k += nt) {
         const int p = top[k], q = bot[k];
         if (q < m && sn[k] != 0.0) {
-          A[(int64_t)p * m + q] = 0.0;
-          A[(int64_t)q * m + p] = 0.0;
+          A[(int64_t)p * ld + q] = 0.0;
+          A[(int64_t)q * ld + p] = 0.0;
         }
-      }
-      // 5) next pairing: circle method, index 0 fixed, ring positions 1..mm-1
-      //    rotate by one per round, position k meets position mm-1-k
-      __syncthreads();
-      for (int k = tid; k < npairs; k += nt) {
-        // ring positions 1..mm-1 rotate by one per round; position 0 is index 0
-        const int r = round + 1;
-        auto at = [&](int pos) -> int {  // index sitting at ring position pos after r rotations
-          if (pos == 0) return 0;
-          return 1 + ((pos - 1 + r) % (mm - 1));
-        };
-        top[k] = at(k);
-        bot[k] = at(mm - 1 - k);
       }
       __syncthreads();
     }
@@ -150,9 +166,9 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
     for (int i = 0; i < m; ++i) order[i] = i;
     for (int i = 1; i < m; ++i) {  // insertion sort on the diagonal
       const int oi = order[i];
-      const double vi = A[(int64_t)oi * m + oi];
+      const double vi = A[(int64_t)oi * ld + oi];
       int j = i - 1;
-      while (j >= 0 && A[(int64_t)order[j] * m + order[j]] > vi) {
+      while (j >= 0 && A[(int64_t)order[j] * ld + order[j]] > vi) {
         order[j + 1] = order[j];
         --j;
       }
@@ -163,10 +179,10 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
   __syncthreads();
   double* Q = Qout + offs[f];
   double* lam = lam_out + lam_offs[f];
-  for (int i = tid; i < m; i += nt) lam[i] = A[(int64_t)order[i] * m + order[i]];
+  for (int i = tid; i < m; i += nt) lam[i] = A[(int64_t)order[i] * ld + order[i]];
   for (int64_t i = tid; i < (int64_t)m * m; i += nt) {
     const int r = (int)(i / m), c = (int)(i % m);
-    Q[i] = V[(int64_t)r * m + order[c]];
+    Q[i] = Vt[(int64_t)order[c] * m + r];
   }
 }
 
@@ -208,9 +224,21 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     GG_HIP(hipMemcpyAsync(dmeta, meta.data(), meta.size() * sizeof(int64_t),
                           hipMemcpyHostToDevice, s));
     int* dstatus = reinterpret_cast<int*>(dmeta + 4 * count);
-    hipLaunchKernelGGL(gg::jacobi_kernel, dim3(count), dim3(gg::kEigThreads), 0, s, dmeta,
-                       dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count, work_dev,
-                       dmeta + 3 * count, max_sweeps, dstatus);
+    int mmax = 1;
+    for (int i = 0; i < count; ++i) mmax = std::max<int>(mmax, (int)m[i]);
+    const bool lds_a = mmax <= gg::kLdsMaxM;
+    const int64_t lds = gg::eig_lds_bytes(mmax, lds_a);
+    if (lds_a) {
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::jacobi_kernel<true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(gg::jacobi_kernel<true>, dim3(count), dim3(gg::kEigThreads), lds, s,
+                         dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                         work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+    } else {
+      hipLaunchKernelGGL(gg::jacobi_kernel<false>, dim3(count), dim3(gg::kEigThreads), lds, s,
+                         dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                         work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+    }
     GG_LAUNCH_CHECK();
     std::vector<int> st(count);
     GG_HIP(hipMemcpyAsync(st.data(), dstatus, count * sizeof(int), hipMemcpyDeviceToHost, s));

@@ -104,7 +104,7 @@ def test_gemv(gg, R, C):
 
 
 # ------------------------------------------------------------------ Cholesky
-@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 300, 1000])
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 300, 1000, 2500])
 def test_cholesky_solve_logdet(gg, n):
     import torch
     from gp_grief_amd import dense
@@ -123,6 +123,13 @@ def test_cholesky_solve_logdet(gg, n):
     assert rel(x, np.linalg.solve(P, b)) < 1e-10
     dinv = ch.inverse_diag().cpu().numpy()
     assert rel(dinv, np.diag(np.linalg.inv(P))) < 1e-10
+    # the two triangular halves separately, and L^-1 of the identity
+    X1 = ch.solve(torch.from_numpy(B).cuda(), which=1).cpu().numpy()
+    assert rel(L.dot(X1), B) < 1e-12
+    X2 = ch.solve(torch.from_numpy(B).cuda(), which=2).cpu().numpy()
+    assert rel(L.T.dot(X2), B) < 1e-12
+    Li = ch.solve(torch.eye(n, dtype=torch.float64).cuda(), which=5).cpu().numpy()
+    assert rel(np.tril(Li), np.linalg.inv(L)) < 1e-10
 
 
 def test_cholesky_not_spd_raises(gg):
