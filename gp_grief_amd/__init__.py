@@ -5,7 +5,7 @@ Drop-in mirror of the reference package's API (scwolof/gp_grief):
     gp_grief_amd.linalg  (log_kron, solver_counter, LogexpTransformation, + device cg / slq)
     gp_grief_amd.kern    (RBF, Exponential, Matern32, Matern52, GridKernel, GriefKernel)
     gp_grief_amd.grid    (InducingGrid)
-    gp_grief_amd.models  (BaseModel, GPGriefModel, GPGridModel)
+    gp_grief_amd.models  (BaseModel, GPGriefModel, GPwebModel, GPwebTransformedModel, GPGridModel)
 The arithmetic runs in libgpgrief.so (hand-written HIP for gfx950) through the
 C ABI in include/gp_grief_amd.h; see DESIGN.md.
 """

@@ -9,6 +9,7 @@
   GriefKernel          gp_grief/kern/grief_kernel.py:12-190 (device eigensolve of the
                                                            grid factors, top-p selection,
                                                            Phi built on the device)
+  WEBKernel            gp_grief/kern/web_kernel.py:4-13     (weights of the WEB models)
 Parameter / constraint bookkeeping is host logic identical in behaviour to the
 reference (including the shared-kernel-object quirk of GridKernel's setter,
 grid_kernel.py:233-239).  Every covariance evaluation and the eigenfunction
@@ -24,7 +25,7 @@ import numpy as np
 from . import device as dev
 from . import native
 from .grid import InducingGrid
-from .tensors import KronMatrix, SelectionMatrixSparse, device_sym_eig
+from .tensors import KronMatrix, KhatriRaoMatrix, SelectionMatrixSparse, device_sym_eig
 
 logger = logging.getLogger(__name__)
 
@@ -280,8 +281,7 @@ class GridKernel(object):
         Kxz = [kern.cov(x=x[:, (i,)], z=z[i]) for i, kern in enumerate(self.kern_list)]
         Kxz = Kxz[::-1]
         if form_kr:
-            raise NotImplementedError("KhatriRaoMatrix is outside the ported hot path; "
-                                      "use form_kr=False")
+            Kxz = KhatriRaoMatrix(A=Kxz, partition=0)   # row partitioned
         return Kxz
 
     def cov_kr_grad(self, x, z, grad_dim):
@@ -459,3 +459,15 @@ class GriefKernel(GridKernel):
             qsel=qsel, xg=xg, u=us, m=ms, col0=col0, U=c,
             cidx=t.from_numpy(cidx.reshape(-1)).to(dev.device()),
             log_lam=dev.to_device(self._log_lam))
+
+
+class WEBKernel(object):
+    """Weighted basis-function kernel parametrisation (web_kernel.py:4-13): the
+    p weights are the parameters, each constrained '+ve'."""
+
+    def __init__(self, initial_weights):
+        assert isinstance(initial_weights, np.ndarray)
+        assert np.ndim(initial_weights) == 1
+        self.p = np.size(initial_weights)
+        self.parameters = initial_weights
+        self.constraints = ['+ve', ] * self.p

@@ -6,6 +6,10 @@
   GPGriefModel   gp_grief/models/gp_grief_model.py:15-245 -- Phi, the p x p
                  Gram, Cholesky, Woodbury solve, log det, LML, adjoint gradient,
                  predict: every O(n p) / O(p^3) step on the device
+  GPwebModel     gp_grief/models/gp_web_model.py:14-130 -- WEB kernel GP, device
+                 Gram / Cholesky / solves / predictions
+  GPwebTransformedModel  gp_grief/models/gp_web_transformed_model.py:13-127 -- thin
+                 SVD of Phi on the device (Gram + Jacobi), O(p) likelihood
   GPGridModel    (new, the north star's P1 model) exact or CG grid GP on a full
                  Kronecker-structured grid: KronMatrix operator, device CG /
                  exact eigen-solve, exact or Lanczos (SLQ) log det, posterior
@@ -569,3 +573,242 @@ class GPGridModel(BaseModel):
         var = Q2.matvec_device(v)
         var += s
         return self._out(mean), self._out(var)
+
+    def predict(self, Xnew, compute_var=True):
+        """Posterior at off-grid points Xnew (M x d): mean K(X*, grid) alpha
+        and the predictive variance k** - k*^T (K + s I)^-1 k* + s, both (M,1).
+
+        K(X*, grid) is GridKernel.cov_kr's row-partitioned Khatri-Rao matrix
+        (grid_kernel.py:148-179, khatri_rao_matrix.py:7-50), applied on the
+        device (gg_kr_contract).  The quadratic form uses the per-factor
+        eigenpairs K_f = Q_f T_f Q_f^T: Q^T k* = kron_f(Q_f^T k_f(x*)), so
+        k*^T (K + s I)^-1 k* = sum_g c[g] prod_f V_f[j, g_f]^2 with
+        V_f = K_f(X*, xg_f) Q_f (device GEMM) and c = 1 / (prod t + s) decoded
+        on the device -- the same Khatri-Rao contraction as the mean."""
+        from . import native
+        assert Xnew.ndim == 2 and Xnew.shape[1] == len(self.xg)
+        self.fit()
+        Kxz = self.kern.cov_kr(np.asarray(Xnew, dtype=np.float64), self.xg)
+        mean = Kxz.contract(self._alpha)
+        if not compute_var:
+            return dense.host(mean).reshape(-1, 1), None
+        s = float(self.noise_var)
+        Q, T = self._schur()
+        V2 = []
+        for Af, Qf in zip(Kxz.A, Q.K):
+            V = dense.matmul(_dev_matrix(Af), _dev_matrix(np.asarray(Qf)))
+            V2.append(dense.scale_rows(V.reshape(-1), None, 2).reshape(V.shape))
+        lam = [np.asarray(e, dtype=np.float64).reshape(-1) for e in T.diag().K]
+        lamd = dev.to_device(np.concatenate(lam))
+        ones = dev.torch().ones(self.num_data, dtype=dev.torch().float64, device=lamd.device)
+        c = dev.empty(self.num_data)
+        native.check(native.lib().gg_kron_diag_scale(
+            len(lam), native.i64_array([l.size for l in lam]), native.dptr(lamd), s,
+            native.GG_DIAG_DIVIDE, native.dptr(ones), native.dptr(c), native.stream_ptr()),
+            "gg_kron_diag_scale")
+        del ones
+        from .tensors import KhatriRaoMatrix
+        quad = KhatriRaoMatrix(V2, partition=0).contract(c)
+        kss = float(self.kern.diag_val)
+        var = kss - dense.host(quad) + s
+        return dense.host(mean).reshape(-1, 1), var.reshape(-1, 1)
+
+
+def _dev_matrix(Phi):
+    """Row-major float64 device copy of a 2-D basis matrix (or the tensor itself)."""
+    t = dev.torch()
+    if isinstance(Phi, t.Tensor):
+        Pd = Phi.detach()
+        if Pd.dtype != t.float64:
+            Pd = Pd.to(t.float64)
+        if not Pd.is_cuda:
+            Pd = Pd.to(dev.device())
+        return Pd.contiguous()
+    arr = np.ascontiguousarray(np.asarray(Phi, dtype=np.float64))
+    return t.from_numpy(arr).to(dev.device())
+
+
+class GPwebModel(BaseModel):
+    """GP with the weighted basis-function (WEB) kernel Phi W Phi^T + s I and
+    O(p^3) algebra (gp_web_model.py:14-130).  The O(n p^2) Gram A = Phi^T Phi
+    (lower triangle, FP64 MFMA), r = Phi^T y, the p x p Cholesky, the solves and
+    the predictions run on the MI355X.
+
+    The adjoint gradient avoids the reference's p x p cho_solve(P, A) with the
+    exact identities of P = A + D, D = diag(s/w), z = P^-1 r:
+      r - A z = D z,   colsum(A o P^-1 A)_j = A_jj - d_j + d_j^2 (P^-1)_jj,
+      tr(P^-1 A) = p - sum_j d_j (P^-1)_jj,   z^T A z = r^T z - sum_j d_j z_j^2,
+    so only diag(P^-1) (one triangular inverse, p^3/3) is needed; and the
+    posterior weights (r - A z) w / s = z exactly.
+    """
+
+    def __init__(self, Phi, y, noise_var=1.):
+        super(GPwebModel, self).__init__()
+        self.n = y.shape[0]
+        yd = dev.to_device(y)
+        assert yd.numel() == self.n
+        assert Phi.shape[0] == self.n
+        self.p = int(Phi.shape[1])
+        self._Phid = _dev_matrix(Phi)
+        self._r = dense.matvec(self._Phid, yd, trans=True)               # Phi^T y
+        self.yTy = np.array([[dense.dot(yd, yd)]])
+        t = dev.torch()
+        A = t.zeros((self.p, self.p), dtype=t.float64, device=self._Phid.device)
+        self._A_lower = dense.matmul(self._Phid, self._Phid, ta=True, C=A, uplo=1)
+        self.noise_var = np.float64(noise_var)
+        from .kern import WEBKernel
+        self.kern = WEBKernel(initial_weights=np.ones(self.p))
+        self.grad_method = 'adjoint'
+        self.dependent_attributes = np.unique(np.concatenate(
+            (self.dependent_attributes, ['_P', '_Pchol', '_Pinv_r', '_alpha_p'])))
+
+    @property
+    def r(self):
+        return dense.host(self._r).reshape((-1, 1))
+
+    @property
+    def A(self):
+        """Phi^T Phi as a full symmetric host array (device keeps the lower triangle)."""
+        L = dense.host(self._A_lower)
+        return np.tril(L) + np.tril(L, -1).T
+
+    def _compute_log_likelihood(self, parameters):
+        self.parameters = parameters
+        w = self.kern.parameters
+        s = float(self.noise_var)
+        if self._P is None:
+            wd = dev.to_device(np.asarray(w, dtype=np.float64))
+            self._P = dense.add_diag(self._A_lower, s, wd)
+            self._Pchol = dense.Cholesky(self._P)
+            self._Pinv_r = self._Pchol.solve(self._r, which=3)
+        datafit = (float(self.yTy[0, 0]) - dense.dot(self._r, self._Pinv_r)) / s
+        complexity = (self._Pchol.logdet + np.sum(np.log(w))
+                      + float(self.n - self.p) * np.log(s))
+        return np.array(-0.5 * (complexity + datafit + self.n * np.log(2. * np.pi)))
+
+    def _adjoint_gradient(self, parameters):
+        assert isinstance(parameters, np.ndarray)
+        free_inds = np.nonzero(np.logical_not(self._fixed_indicies))[0]
+        gradient = np.zeros(parameters.shape) + np.nan
+        log_like = self._compute_log_likelihood(parameters)
+        w = np.asarray(self.kern.parameters, dtype=np.float64)
+        s = float(self.noise_var)
+        dvec = s / w
+        z = dense.host(self._Pinv_r)
+        rz = dense.dot(self._r, self._Pinv_r)
+        pinv_diag = dense.host(self._Pchol.inverse_diag())
+        data_fit_grad = -(z / w) ** 2                            # -((r - A z)/s)^2
+        complexity_grad = (dvec - dvec ** 2 * pinv_diag) / s
+        gradient[1:] = -0.5 * data_fit_grad - 0.5 * complexity_grad
+        data_fit_grad = -(float(self.yTy[0, 0]) - rz - np.sum(dvec * z ** 2)) / s ** 2
+        complexity_grad = (float(self.n) - (float(self.p) - np.sum(dvec * pinv_diag))) / s
+        gradient[0] = -0.5 * (data_fit_grad + complexity_grad)
+        assert not np.any(np.isnan(gradient[free_inds])), "gradient missed!"
+        return log_like, gradient
+
+    def predict(self, Phi_new):
+        """(Yhat (M,1), Var (M,M)) = Phi* alpha_p, s Phi* P^-1 Phi*^T + s I (:109-129)."""
+        assert Phi_new.ndim == 2
+        assert Phi_new.shape[1] == self.p
+        parameters = self.parameters
+        if self._alpha_p is None:
+            if self._Pinv_r is None:
+                self._compute_log_likelihood(parameters)
+            self._alpha_p = self._Pinv_r                           # (r - A z) w / s = z
+        Pn = _dev_matrix(Phi_new)
+        yhat = dense.matvec(Pn, self._alpha_p)
+        V = self._Pchol.solve(Pn.t().contiguous(), which=1)         # L^-1 Phi*^T (p x M)
+        var = dense.matmul(V, V, ta=True, alpha=float(self.noise_var))
+        var = dense.add_diag(var, float(self.noise_var))
+        return dense.host(yhat).reshape((-1, 1)), dense.host(var)
+
+
+class GPwebTransformedModel(BaseModel):
+    """WEB GP with the basis rotated to Phi's left singular vectors so that the
+    likelihood and gradient are O(p) (gp_web_transformed_model.py:13-127).
+
+    The thin SVD is formed on the MI355X from the Gram matrix: A = Phi^T Phi
+    (FP64 MFMA), A = V S^2 V^T by the device Jacobi eigensolver, and
+    Phit^T y = S^-1 V^T (Phi^T y).  Bases with singular value <= 1e-7 are
+    dropped as in the reference (:27-35).  The Gram route squares the condition
+    number: singular values below ~sqrt(eps) * s_max lose relative accuracy, so
+    a nearly rank-deficient Phi can keep a different number of bases than
+    LAPACK's SVD would.  The O(p) likelihood / gradient stay on the host, as
+    in the reference; predictions are device GEMV / GEMM.
+    """
+
+    def __init__(self, Phi, y, noise_var=1.):
+        super(GPwebTransformedModel, self).__init__()
+        self.n = y.shape[0]
+        yd = dev.to_device(y)
+        assert yd.numel() == self.n
+        assert Phi.shape[0] == self.n
+        self.p_orig = int(Phi.shape[1])
+        Pd = _dev_matrix(Phi)
+        A = dense.host(dense.matmul(Pd, Pd, ta=True))
+        A = 0.5 * (A + A.T)
+        from .tensors import device_sym_eig
+        Qs, lams = device_sym_eig([A])
+        lam, V = lams[0], Qs[0]
+        order = np.argsort(-lam, kind='stable')
+        lam, V = lam[order], V[:, order]
+        sv = np.sqrt(np.maximum(lam, 0.0))
+        ikeep = sv > 1e-7
+        self.singular_vals = sv[ikeep]
+        self.V = np.ascontiguousarray(V[:, ikeep])
+        self.p = int(self.singular_vals.size)
+        if self.p < self.p_orig:
+            logger.info("Num Bases decreased from p=%d to p=%d. Only a subspace can now be "
+                        "searched." % (self.p_orig, self.p))
+        PhiTy = dense.host(dense.matvec(Pd, yd, trans=True))
+        self.PhitT_y = self.V.T.dot(PhiTy) / self.singular_vals
+        self.PhitT_y_2 = np.power(self.PhitT_y, 2)
+        self.yTy = dense.dot(yd, yd)
+        self.noise_var = np.float64(noise_var)
+        from .kern import WEBKernel
+        self.kern = WEBKernel(initial_weights=np.ones(self.p))
+        self.grad_method = 'adjoint'
+
+    def _compute_log_likelihood(self, parameters):
+        self.parameters = parameters
+        w = self.kern.parameters
+        sig2 = self.noise_var
+        Pdiag = sig2 / w + 1.
+        datafit = (self.yTy - np.sum(self.PhitT_y_2 / Pdiag)) / sig2
+        complexity = np.sum(np.log(Pdiag)) + np.sum(np.log(w)) + (self.n - self.p) * np.log(sig2)
+        return -0.5 * (complexity + datafit + self.n * np.log(2. * np.pi))
+
+    def _adjoint_gradient(self, parameters):
+        assert isinstance(parameters, np.ndarray)
+        free_inds = np.nonzero(np.logical_not(self._fixed_indicies))[0]
+        gradient = np.zeros(parameters.shape) + np.nan
+        log_like = self._compute_log_likelihood(parameters)
+        w = self.kern.parameters
+        sig2 = self.noise_var
+        gradient[1:] = -0.5 * (-self.PhitT_y_2 / np.power(sig2 + w, 2) + 1. / (sig2 + w))
+        data_fit_grad = (-self.yTy + np.sum(self.PhitT_y_2 * w * (sig2 * 2. + w)
+                                            / np.power(sig2 + w, 2))) / sig2 ** 2
+        complexity_grad = float(self.n - self.p) / sig2 + np.sum(1. / (sig2 + w))
+        gradient[0] = -0.5 * (data_fit_grad + complexity_grad)
+        assert not np.any(np.isnan(gradient[free_inds])), "gradient missed!"
+        return log_like, gradient
+
+    def predict(self, Phi_new):
+        """Yhat = Phi* V (alpha_p / S); Var = s Phi* diag(1/Pdiag) Phi*^T + s I (:101-121)."""
+        assert Phi_new.ndim == 2
+        assert Phi_new.shape[1] == self.p_orig
+        self.parameters
+        w = self.kern.parameters
+        sig2 = float(self.noise_var)
+        Pdiag = sig2 / w + 1.
+        alpha_p = (self.PhitT_y - self.PhitT_y / Pdiag) * w / sig2
+        coef = dev.to_device(self.V.dot(alpha_p / self.singular_vals))
+        Pn = _dev_matrix(Phi_new)
+        yhat = dense.matvec(Pn, coef)
+        if Pdiag.size != self.p_orig:
+            raise ValueError("the predictive variance needs every basis kept (p == p_orig)")
+        B = Pn.t().contiguous()
+        dense.scale_rows(B, dev.to_device(Pdiag), 1)                  # Phi*^T / Pdiag
+        var = dense.matmul(Pn, B, alpha=sig2)
+        var = dense.add_diag(var, sig2)
+        return dense.host(yhat).reshape((-1, 1)), dense.host(var)

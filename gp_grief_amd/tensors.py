@@ -1,7 +1,8 @@
 """Structured tensors: the drop-in KronMatrix backed by the HIP library.
 
-Mirrors gp_grief/tensors/kron_matrix.py (class KronMatrix, :12-474) and
-gp_grief/tensors/selection_matrix.py (SelectionMatrixSparse, :55-107): same
+Mirrors gp_grief/tensors/kron_matrix.py (class KronMatrix, :12-474),
+gp_grief/tensors/khatri_rao_matrix.py (row-partitioned KhatriRaoMatrix, :7-50)
+and gp_grief/tensors/selection_matrix.py (SelectionMatrixSparse, :55-107): same
 constructor, attributes (n, sshape, shape, ndim, square, sym, read-only K),
 method names, return shapes and exception types.
 
@@ -469,3 +470,78 @@ class SelectionMatrixSparse(object):
         if isinstance(key, tuple):
             key = key[0]
         return SelectionMatrixSparse(indicies=(np.atleast_1d(self.indicies[key]), self.shape[1]))
+
+
+def _dev_rows(A):
+    """(M, m) row-major float64 device matrix from numpy or a tensor."""
+    t = dev.torch()
+    if isinstance(A, t.Tensor):
+        Ad = A.detach().to(t.float64)
+        return (Ad if Ad.is_cuda else Ad.to(dev.device())).contiguous()
+    return t.from_numpy(np.ascontiguousarray(np.asarray(A, dtype=np.float64))).to(dev.device())
+
+
+class KhatriRaoMatrix(object):
+    """Row-partitioned Khatri-Rao matrix (khatri_rao_matrix.py:7-50, partition
+    0): row j is kron(A_0[j], ..., A_{d-1}[j]), A_f of shape (M, m_f), factor 0
+    slowest -- the form GridKernel.cov_kr returns for K(X*, grid).  The product
+    with an N-vector (BlockMatrix.__mul__, block_matrix.py:48-66) is the device
+    contraction gg_kr_contract: one FP64 MFMA GEMM against the fastest factor
+    plus a coalesced weighted column sum; the N-vector is read once per chunk.
+    Column partitioning (partition=1) is off the grid-prediction path."""
+
+    def __init__(self, A, partition=None):
+        if partition != 0:
+            raise NotImplementedError("only the row-partitioned (partition=0) form is provided")
+        A = list(A)
+        assert len(A) >= 1
+        M = int(A[0].shape[0])
+        for Ai in A:
+            assert Ai.ndim == 2 and int(Ai.shape[0]) == M, "blocks must share the row count"
+        self.A = A
+        self.d = len(A)
+        self.partition = 0
+        self.block_shape = (M, 1)
+        self.shape = (M, int(np.prod([int(Ai.shape[1]) for Ai in A])))
+        self._tabs = None
+
+    def _tables(self):
+        if self._tabs is None:
+            ulast = _dev_rows(self.A[-1])
+            uts = [_dev_rows(Ai).t().contiguous() for Ai in self.A[:-1]]   # U_f^T (m_f x M)
+            self._tabs = (ulast, uts)
+        return self._tabs
+
+    def contract(self, cd, out=None, work_elems=None):
+        """out (M,) device = self . cd for a 1-D float64 device vector of length N.
+        work_elems (optional) caps the scratch size (smaller = more GEMM chunks)."""
+        L = native.lib()
+        M, N = self.shape
+        if int(cd.numel()) != N:
+            raise ValueError('x is the wrong shape, must be (%d,1)' % N)
+        ulast, uts = self._tables()
+        m = [int(Ai.shape[1]) for Ai in self.A]
+        marr = native.i64_array(m)
+        need = ctypes.c_int64()
+        native.check(L.gg_kr_work_elems(self.d, marr, M, ctypes.byref(need)))
+        outer = N // m[-1]
+        # up to ~1 GiB of GEMM chunk beyond the minimum: few chunks, modest HBM
+        extra = min(outer * M, max(0, (1 << 27) - need.value))
+        if work_elems is not None:
+            extra = max(0, int(work_elems) - need.value)
+        work = dev.empty(need.value + extra)
+        if out is None:
+            out = dev.empty(M)
+        ptrs = (ctypes.c_void_p * max(1, len(uts)))(*[native.dptr(u) for u in uts])
+        native.check(L.gg_kr_contract(self.d, marr, native.dptr(dev.ensure_aligned(cd)),
+                                      native.dptr(ulast), ptrs, M, native.dptr(out),
+                                      native.dptr(work), int(work.numel()),
+                                      native.stream_ptr()), "gg_kr_contract")
+        return out
+
+    def __mul__(self, x):
+        M, N = self.shape
+        if tuple(x.shape) != (N, 1):
+            raise ValueError('x is the wrong shape, must be (%d,1), not %s' % (N, repr(x.shape)))
+        xd, was_dev = _vector_in(x, N, 'x is the wrong shape')
+        return _vector_out(self.contract(xd), was_dev)

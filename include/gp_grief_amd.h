@@ -195,6 +195,19 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
 int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
                       gg_stream stream);
 
+/* ------------------------------- Khatri-Rao contraction (off-grid P1 posterior)
+ * out[j] = sum_g c[g] prod_f U_f[j][g_f] over the grid g (factor 0 slowest):
+ * K(X*, grid) c for the row-partitioned Khatri-Rao cross covariance
+ * KhatriRaoMatrix(GridKernel.cov_kr(X*, xg)) (gp_grief/kern/grid_kernel.py:148-179,
+ * tensors/khatri_rao_matrix.py:7-50, BlockMatrix.__mul__ block_matrix.py:48-66).
+ * ulast_dev: U_{d-1}, M x m_{d-1} row-major.  ut_dev: host array of d-1 device
+ * pointers, ut_dev[f] = U_f^T (m_f x M row-major).  work_dev: at least
+ * gg_kr_work_elems doubles (more work = fewer GEMM chunks).  1 <= d <= 32.     */
+int gg_kr_work_elems(int d, const int64_t* m, int64_t M, int64_t* min_elems);
+int gg_kr_contract(int d, const int64_t* m, const double* c_dev, const double* ulast_dev,
+                   const double* const* ut_dev, int64_t M, double* out_dev, double* work_dev,
+                   int64_t work_elems, gg_stream stream);
+
 /* --------------------------------------------- P1 sharded over G ranks (RCCL)
  * The Kronecker operator with factor 0 split over `world` ranks (one per GPU).
  * Local vector layout: (m_1, ..., m_{d-1}, a) with a = i_0 - rank * m_0 / G the

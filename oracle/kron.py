@@ -170,3 +170,34 @@ def grid_latent_var(Q, eig_factors, shift):
     """
     t = _partial_products(eig_factors)
     return kron_matvec([np.asarray(q) ** 2 for q in Q], t * shift / (t + shift))
+
+
+def kr_contract(blocks, c):
+    """out[j] = kron(A_0[j], ..., A_{d-1}[j]) . c for a row-partitioned
+    Khatri-Rao matrix (khatri_rao_matrix.py:7-50; BlockMatrix.__mul__
+    block_matrix.py:48-66 applies it one KronMatrix row at a time).  Here each
+    row is contracted factor by factor: the slowest axis first, as a small GEMV."""
+    M = blocks[0].shape[0]
+    shape = [b.shape[1] for b in blocks]
+    C = np.asarray(c, dtype=np.float64).reshape(shape)
+    out = np.empty(M)
+    for j in range(M):
+        t = C
+        for b in blocks:
+            t = np.tensordot(b[j], t, axes=(0, 0))
+        out[j] = float(t)
+    return out
+
+
+def grid_offgrid_predict(factors, cross_blocks, kss, alpha, shift):
+    """Off-grid posterior of a full-grid GP (the f8 fixture's recipe,
+    grid_kernel.py:148-179 + kron_matrix.py:328-352): mean = K(X*, grid) alpha;
+    latent var = k** - sum_g (prod_f (Q_f^T k_f(x*))[g_f])^2 / (prod_f t_f[g_f] + s)."""
+    Q, t = factor_eigh(factors)
+    mean = kr_contract(cross_blocks, alpha)
+    lam = t[0]
+    for ti in t[1:]:
+        lam = np.multiply.outer(lam, ti).reshape(-1)
+    cinv = 1.0 / (lam + shift)
+    V2 = [(b.dot(q)) ** 2 for b, q in zip(cross_blocks, Q)]
+    return mean, kss - kr_contract(V2, cinv)

@@ -23,6 +23,11 @@ Fixtures:
   grief_small_*.npz  3-D / 6-D (Matern-5/2) / 8-D GRIEF fits with distinct
                      lengthscales and the p-boundary eigen-gap recorded
   automobile.npz     Type-II tutorial automobile case after optimize(max_iters=5)
+  grid_offgrid.npz   off-grid prediction of the grid GP: KhatriRaoMatrix(cov_kr)
+                     times alpha, and the dense predictive variance, on a
+                     7 x 9 x 8 (mixed sizes) and a 6^4 RBF grid
+  web.npz            GPwebModel / GPwebTransformedModel: the reference tests'
+                     setting (test_gp_web_model.py:12-31) and a 1200 x 48 case
 
 Usage:  python tests/golden/make_golden.py [--ref /root/reference]
 """
@@ -351,17 +356,101 @@ def f6_automobile(gg, ref_root):
     save("automobile.npz", **out)
 
 
+def f7_web(gg):
+    """GPwebModel / GPwebTransformedModel (gp_web_model.py:14-130,
+    gp_web_transformed_model.py:13-127): LML, adjoint gradient and predictions.
+    Case 't' replays test_gp_web_model.py:12-23 exactly (seed 0, intercept
+    column, rand + 1e-6 parameters); case 'b' is a 1200 x 48 Gaussian Phi."""
+    from gp_grief.models import GPwebModel, GPwebTransformedModel
+    out = {}
+    for tag in ("t", "b"):
+        if tag == "t":
+            np.random.seed(0)
+            X = np.random.randn(100, 4)
+            X[:, 0] = 1.
+            Y = np.dot(X, [0.5, 0.1, 0.25, 1.]) + 0.1 * np.random.randn(X.shape[0])
+            params = np.random.rand(5) + 1e-6
+        else:
+            rng = np.random.default_rng(7)
+            X = rng.standard_normal((1200, 48)) / 7.0
+            Y = np.sin(X.sum(axis=1) * 3.0) + 0.1 * rng.standard_normal(1200)
+            params = np.concatenate(([0.05], rng.uniform(0.5, 2.0, 48)))
+        Xnew = X[:7] + 0.01
+        out[tag + "_X"] = X
+        out[tag + "_Y"] = Y
+        out[tag + "_params"] = params
+        out[tag + "_Xnew"] = Xnew
+        for cls, key in ((GPwebModel, "web"), (GPwebTransformedModel, "tr")):
+            m = cls(Phi=X, y=Y)
+            m.parameters = params.copy()
+            ll, g = m._adjoint_gradient(m.parameters)
+            out["%s_%s_lml" % (tag, key)] = np.asarray(ll, dtype=np.float64)
+            out["%s_%s_grad" % (tag, key)] = g
+            yh, yv = m.predict(Xnew)
+            out["%s_%s_mean" % (tag, key)] = yh
+            out["%s_%s_var" % (tag, key)] = yv
+            if key == "tr":
+                out[tag + "_tr_singular"] = m.singular_vals
+                out[tag + "_tr_PhitTy2"] = m.PhitT_y_2
+    save("web.npz", **out)
+
+
+def f8_grid_offgrid(gg):
+    """Off-grid posterior of a full-grid GP: mean = K(X*, grid) alpha with
+    K(X*, grid) = GridKernel.cov_kr(X*, xg) (grid_kernel.py:148-179), a
+    row-partitioned KhatriRaoMatrix (khatri_rao_matrix.py:7-50) applied by
+    BlockMatrix.__mul__; latent variance k** - k*^T (K + s I)^-1 k* from the
+    expanded Khatri-Rao rows and KronMatrix.solve_schur (kron_matrix.py:328-352)."""
+    out = {}
+    for tag, ms, ls, M in (("a", [7, 9, 8], [0.15, 0.2, 0.25], 23),
+                           ("b", [6, 6, 6, 6], [0.2, 0.22, 0.24, 0.26], 17)):
+        d, sig2 = len(ms), 0.01
+        kerns, xg = rbf_grid(gg, ms, ls)
+        gk = gg.kern.GridKernel(kerns)
+        K = gk.cov_grid(xg, dim_noise_var=1e-12)
+        N = int(np.prod(ms))
+        y = (grid_targets(xg) + 0.1 * np.random.default_rng(3).standard_normal(N)).reshape(-1, 1)
+        Q, T = K.schur()
+        t = T.diag().expand()
+        alpha = Q.solve_schur(t, y, shift=sig2)
+        xs = np.random.default_rng(4).uniform(-0.05, 1.05, (M, d))
+        # cov_kr(form_kr=True) hands a ragged list to np.ndim, which numpy>=2
+        # rejects (khatri_rao_matrix.py:25); the same blocks as an object array:
+        blocks = gk.cov_kr(xs, xg, form_kr=False)
+        A = np.empty(len(blocks), dtype=object)
+        for i, b in enumerate(blocks):
+            A[i] = b
+        Kxz = gg.tensors.KhatriRaoMatrix(A=A, partition=0)
+        mean = Kxz * alpha
+        Kd = Kxz.expand()
+        quad = np.array([float(Kd[j].dot(Q.solve_schur(t, Kd[j].reshape(-1, 1), shift=sig2)[:, 0]))
+                         for j in range(M)])
+        kss = np.array([float(gk.cov(xs[(j,), :])[0, 0]) for j in range(M)])
+        out.update({tag + "_m": np.array(ms), tag + "_ls": np.array(ls),
+                    tag + "_sigma2": np.float64(sig2), tag + "_y": y[:, 0],
+                    tag + "_alpha": alpha[:, 0], tag + "_xs": xs, tag + "_mean": mean[:, 0],
+                    tag + "_var_latent": kss - quad})
+    save("grid_offgrid.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="comma list of fixture functions, e.g. f7_web")
     a = ap.parse_args()
     gg = import_reference(a.ref)
+    if a.only:
+        for name in a.only.split(","):
+            globals()[name](gg)
+        return
     f1_kron_matvec(gg)
     f2_kron_eig(gg)
     f3_grid_gp(gg)
     f4_grief_test(gg)
     f5_grief_small(gg)
     f6_automobile(gg, a.ref)
+    f7_web(gg)
+    f8_grid_offgrid(gg)
 
 
 if __name__ == "__main__":
