@@ -85,6 +85,30 @@ __global__ __launch_bounds__(kKrThreads) void kr_finish_kernel(const double* __r
   out[j] = s;
 }
 
+// Running product of row-col Khatri-Rao factor blocks (get_rows,
+// khatri_rao_matrix.py:117-140).  mode 0: P = X (first) or P *= X.
+// mode 1 (logged): S *= sgn(X); L += log|X| with X -> 1 where the running
+// sign S is 0 (the reference's rows_1d[sign == 0] = 1 rule).
+__global__ __launch_bounds__(kKrThreads) void kr_hadamard_kernel(int64_t n,
+                                                                 const double* __restrict__ X,
+                                                                 double* __restrict__ P,
+                                                                 double* __restrict__ S,
+                                                                 int mode, int first) {
+  for (int64_t e = (int64_t)blockIdx.x * kKrThreads + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * kKrThreads) {
+    const double x = X[e];
+    if (mode == 0) {
+      P[e] = first ? x : P[e] * x;
+    } else {
+      const double sx = (x > 0.0) ? 1.0 : ((x < 0.0) ? -1.0 : 0.0);
+      const double s = (first ? 1.0 : S[e]) * sx;
+      S[e] = s;
+      const double v = (s == 0.0) ? 1.0 : x;
+      P[e] = (first ? 0.0 : P[e]) + log(fabs(v));
+    }
+  }
+}
+
 static int kr_splits(int64_t M) {
   const int64_t bx = ceil_div(M, kKrThreads);
   return (int)std::max<int64_t>(1, std::min<int64_t>(kKrMaxSplits, ceil_div(4096, bx)));
@@ -101,6 +125,19 @@ int gg_kr_work_elems(int d, const int64_t* m, int64_t M, int64_t* min_elems) {
     int64_t outer = 1;
     for (int f = 0; f + 1 < d; ++f) outer *= m[f];
     *min_elems = (int64_t)gg::kr_splits(M) * M + std::min<int64_t>(outer, 1024) * M;
+  });
+}
+
+int gg_kr_hadamard(int64_t n, const double* X_dev, double* P_dev, double* S_dev, int mode,
+                   int first, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 0 && (mode == 0 || mode == 1), GG_ERR_VALUE, "bad argument");
+    if (n == 0) return;
+    GG_REQUIRE(X_dev && P_dev && (mode == 0 || S_dev), GG_ERR_VALUE, "NULL pointer");
+    const unsigned nb = (unsigned)std::min<int64_t>(8192, gg::ceil_div(n, gg::kKrThreads));
+    hipLaunchKernelGGL(gg::kr_hadamard_kernel, dim3(nb), dim3(gg::kKrThreads), 0,
+                       gg::as_stream(stream), n, X_dev, P_dev, S_dev, mode, first);
+    GG_LAUNCH_CHECK();
   });
 }
 

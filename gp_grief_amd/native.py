@@ -78,6 +78,7 @@ SIGNATURES = {
     "gg_kr_work_elems": [ctypes.c_int, _c_i64p, ctypes.c_int64, _c_i64p],
     "gg_kr_contract": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, ctypes.POINTER(ctypes.c_void_p),
                        ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int64, _vp],
+    "gg_kr_hadamard": [ctypes.c_int64, _c_dp, _c_dp, _c_dp, ctypes.c_int, ctypes.c_int, _vp],
     "gg_gemm": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                 ctypes.c_double, _c_dp, ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_double,
                 _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],

@@ -1,8 +1,8 @@
 """Structured tensors: the drop-in KronMatrix backed by the HIP library.
 
 Mirrors gp_grief/tensors/kron_matrix.py (class KronMatrix, :12-474),
-gp_grief/tensors/khatri_rao_matrix.py (row-partitioned KhatriRaoMatrix, :7-50)
-and gp_grief/tensors/selection_matrix.py (SelectionMatrixSparse, :55-107): same
+gp_grief/tensors/khatri_rao_matrix.py (row-partitioned KhatriRaoMatrix, :7-50;
+RowColKhatriRaoMatrix and its Transposed variant, :53-210) and gp_grief/tensors/selection_matrix.py (SelectionMatrixSparse, :55-107): same
 constructor, attributes (n, sshape, shape, ndim, square, sym, read-only K),
 method names, return shapes and exception types.
 
@@ -545,3 +545,124 @@ class KhatriRaoMatrix(object):
             raise ValueError('x is the wrong shape, must be (%d,1), not %s' % (N, repr(x.shape)))
         xd, was_dev = _vector_in(x, N, 'x is the wrong shape')
         return _vector_out(self.contract(xd), was_dev)
+
+
+class RowColKhatriRaoMatrix(object):
+    """A = R K C with A[a, b] = prod_i (R_i K_i C_i)[a, b]
+    (khatri_rao_matrix.py:53-178): R row-partitioned, C column-partitioned
+    Khatri-Rao factors, K a Kronecker product (merged into C at construction,
+    C_i <- K_i C_i, as the reference does).  The matrix is never formed whole:
+    products and get_rows work on chunks of n_rows_at_once rows (the
+    reference's nGb memory cap), each chunk = d FP64 MFMA GEMMs R_i[rows] C_i
+    combined elementwise on the device (gg_kr_hadamard), then one GEMV."""
+
+    def __init__(self, R, K, C, nGb=1.):
+        R = list(R)
+        C = list(C)
+        self.d = len(R)
+        if K is not None:
+            K = list(K)
+            assert len(K) == len(C) == self.d, "number of dims inconsistent"
+        self._init_blocks([_dev_rows(Ri) for Ri in R],
+                          [self._merge(K[i] if K is not None else None, C[i], R[i])
+                           for i in range(self.d)], nGb)
+
+    @staticmethod
+    def _merge(Ki, Ci, Ri):
+        from . import dense
+        Cd = _dev_rows(Ci)
+        if Ki is None:
+            return Cd
+        assert Ki.shape[0] == Ki.shape[1] == Ri.shape[1], \
+            "K must be a square Kronecker product matrix, and must be consistent with R"
+        return dense.matmul(_dev_rows(Ki), Cd)
+
+    def _init_blocks(self, Rd, Cd, nGb):
+        self._R, self._C = Rd, Cd
+        for Ri, Ci in zip(Rd, Cd):
+            assert int(Ri.shape[1]) == int(Ci.shape[0]), "inner dimensions differ"
+            assert int(Ri.shape[0]) == int(Rd[0].shape[0])
+            assert int(Ci.shape[1]) == int(Cd[0].shape[1])
+        self.shape = (int(Rd[0].shape[0]), int(Cd[0].shape[1]))
+        self.nGb = nGb
+        self.n_rows_at_once = 1
+        if nGb is not None:
+            self.n_rows_at_once = max(1, int(np.floor(nGb * 1e9 / (8 * self.shape[1]))))
+
+    @classmethod
+    def _from_blocks(cls, Rd, Cd, nGb):
+        obj = cls.__new__(cls)
+        obj.d = len(Rd)
+        RowColKhatriRaoMatrix._init_blocks(obj, Rd, Cd, nGb)
+        return obj
+
+    @property
+    def T(self):
+        """A^T = C^T K^T R^T: the same structure with R_i <- C_i^T, C_i <- R_i^T."""
+        return RowColKhatriRaoMatrix._from_blocks([c.t().contiguous() for c in self._C],
+                                                  [r.t().contiguous() for r in self._R],
+                                                  self.nGb)
+
+    def _rows_dev(self, Rsel, logged):
+        """Device rows for the row blocks Rsel[i] (k x m_i): product or (log, sign)."""
+        from . import dense
+        L = native.lib()
+        t = dev.torch()
+        k, n = int(Rsel[0].shape[0]), self.shape[1]
+        P = t.empty((k, n), dtype=t.float64, device=self._C[0].device)
+        S = t.empty((k, n), dtype=t.float64, device=P.device) if logged else None
+        X = t.empty((k, n), dtype=t.float64, device=P.device) if self.d > 1 or logged else P
+        for i in range(self.d):
+            Xi = dense.matmul(Rsel[i], self._C[i], C=X if (self.d > 1 or logged) else P)
+            if self.d > 1 or logged:
+                native.check(L.gg_kr_hadamard(k * n, native.dptr(Xi), native.dptr(P),
+                                              native.dptr(S) if logged else None,
+                                              int(logged), int(i == 0), native.stream_ptr()),
+                             "gg_kr_hadamard")
+        return (P, S) if logged else P
+
+    def get_rows(self, i_rows, logged=False):
+        """Rows i_rows (index array or slice) of A, as host arrays (:110-140)."""
+        idx = np.arange(self.shape[0])[i_rows]
+        idx = np.atleast_1d(idx)
+        t = dev.torch()
+        it = t.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)).to(self._R[0].device)
+        Rsel = [Ri.index_select(0, it).contiguous() for Ri in self._R]
+        out = self._rows_dev(Rsel, logged)
+        if logged:
+            return dev.to_host(out[0]), dev.to_host(out[1])
+        return dev.to_host(out)
+
+    def expand(self, logged=False):
+        return self.get_rows(slice(None), logged=logged)
+
+    def __mul__(self, x):
+        """y = A x chunk by chunk of rows (:143-158)."""
+        from . import dense
+        if tuple(x.shape) != (self.shape[1], 1):
+            raise AssertionError("x must be (%d,1)" % self.shape[1])
+        xd, was_dev = _vector_in(x, self.shape[1], 'x is the wrong shape')
+        y = dev.empty(self.shape[0])
+        step = self.n_rows_at_once
+        for i0 in range(0, self.shape[0], step):
+            i1 = min(self.shape[0], i0 + step)
+            P = self._rows_dev([Ri[i0:i1] for Ri in self._R], False)
+            dense.matvec(P, xd, y=y[i0:i1])
+        return _vector_out(y, was_dev)
+
+
+class RowColKhatriRaoMatrixTransposed(RowColKhatriRaoMatrix):
+    """(R K C)^T handled as rows of the transpose (khatri_rao_matrix.py:181-210):
+    shape (N, p), products A^T x; .T returns the untransposed matrix."""
+
+    def __init__(self, R, K, C, nGb=1.):
+        base = RowColKhatriRaoMatrix(R, K, C, nGb=None)
+        self.d = base.d
+        self._untransposed = (base._R, base._C)
+        RowColKhatriRaoMatrix._init_blocks(self, [c.t().contiguous() for c in base._C],
+                                           [r.t().contiguous() for r in base._R], nGb)
+
+    @property
+    def T(self):
+        R, C = self._untransposed
+        return RowColKhatriRaoMatrix._from_blocks(R, C, self.nGb)

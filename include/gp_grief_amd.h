@@ -207,6 +207,13 @@ int gg_kr_work_elems(int d, const int64_t* m, int64_t M, int64_t* min_elems);
 int gg_kr_contract(int d, const int64_t* m, const double* c_dev, const double* ulast_dev,
                    const double* const* ut_dev, int64_t M, double* out_dev, double* work_dev,
                    int64_t work_elems, gg_stream stream);
+/* Row-col Khatri-Rao running product (RowColKhatriRaoMatrix.get_rows,
+ * gp_grief/tensors/khatri_rao_matrix.py:117-140) over n elements of one factor
+ * block X_i = R_i K_i C_i.  mode 0: P = X (first != 0) or P *= X.  mode 1
+ * (logged): S *= sign(X), P += log|X| with X taken as 1 where S == 0 (first:
+ * S = 1, P = 0 before the update).                                            */
+int gg_kr_hadamard(int64_t n, const double* X_dev, double* P_dev, double* S_dev, int mode,
+                   int first, gg_stream stream);
 
 /* --------------------------------------------- P1 sharded over G ranks (RCCL)
  * The Kronecker operator with factor 0 split over `world` ranks (one per GPU).

@@ -23,7 +23,8 @@ Lanczos recurrence itself.
 """
 from .kron import (kron_matvec, kron_matvec_T, kron_expand, log_kron,
                    find_extremum_eigs, factor_eigh, solve_schur, eig_log_det,
-                   logdet_shifted, grid_latent_var, kr_contract, grid_offgrid_predict)
+                   logdet_shifted, grid_latent_var, kr_contract, grid_offgrid_predict,
+                   rowcol_kr_expand)
 from .kernels import cov_1d
 from .cg import cg_solve, slq_logdet, lanczos_tridiag
 from .grief import (grief_inducing, grief_phi, grief_fit, grief_lml,
@@ -34,7 +35,7 @@ from .web import (web_lml_grad, web_predict, web_transformed_setup,
 __all__ = [
     "kron_matvec", "kron_matvec_T", "kron_expand", "log_kron", "find_extremum_eigs",
     "factor_eigh", "solve_schur", "eig_log_det", "logdet_shifted", "grid_latent_var",
-    "kr_contract", "grid_offgrid_predict", "cov_1d", "cg_solve", "slq_logdet", "lanczos_tridiag", "grief_inducing", "grief_phi",
+    "kr_contract", "grid_offgrid_predict", "rowcol_kr_expand", "cov_1d", "cg_solve", "slq_logdet", "lanczos_tridiag", "grief_inducing", "grief_phi",
     "grief_fit", "grief_lml", "grief_adjoint_grad", "grief_predict",
     "web_lml_grad", "web_predict", "web_transformed_setup", "web_transformed_lml_grad",
     "web_transformed_predict",

@@ -201,3 +201,24 @@ def grid_offgrid_predict(factors, cross_blocks, kss, alpha, shift):
     cinv = 1.0 / (lam + shift)
     V2 = [(b.dot(q)) ** 2 for b, q in zip(cross_blocks, Q)]
     return mean, kss - kr_contract(V2, cinv)
+
+
+def rowcol_kr_expand(R, K, C, logged=False):
+    """A[a, b] = prod_i X_i[a, b], X_i = R_i (K_i C_i) -- RowColKhatriRaoMatrix
+    (khatri_rao_matrix.py:53-158: C_i <- K_i C_i at construction, get_rows /
+    expand).  logged: (log|A| accumulated until the running sign hits 0, sign)
+    with the reference's running-sign rule (:127-133)."""
+    if logged:
+        log, sign = 0., 1.
+    else:
+        prod = 1.
+    for Ri, Ki, Ci in zip(R, K, C):
+        X = Ri.dot(Ki.dot(Ci) if Ki is not None else Ci)
+        if logged:
+            sign = sign * np.int32(np.sign(X))
+            X = X.copy()
+            X[sign == 0] = 1.
+            log = log + np.log(np.abs(X))
+        else:
+            prod = prod * X
+    return (log, sign) if logged else prod

@@ -26,6 +26,9 @@ Fixtures:
   grid_offgrid.npz   off-grid prediction of the grid GP: KhatriRaoMatrix(cov_kr)
                      times alpha, and the dense predictive variance, on a
                      7 x 9 x 8 (mixed sizes) and a 6^4 RBF grid
+  rowcol_kr.npz      RowColKhatriRaoMatrix(R, K, C): matvec, transposed matvec,
+                     expand and logged expand (test_RowColKhatriRaoMatrix.py
+                     setting, plus a 300 x 800 case)
   web.npz            GPwebModel / GPwebTransformedModel: the reference tests'
                      setting (test_gp_web_model.py:12-31) and a 1200 x 48 case
 
@@ -433,6 +436,54 @@ def f8_grid_offgrid(gg):
     save("grid_offgrid.npz", **out)
 
 
+def f9_rowcol_kr(gg):
+    """RowColKhatriRaoMatrix (khatri_rao_matrix.py:53-178) and the Transposed
+    variant (:181-210): A[a, b] = prod_i (R_i K_i C_i)[a, b]."""
+    from gp_grief.tensors import RowColKhatriRaoMatrix, RowColKhatriRaoMatrixTransposed
+    out = {}
+    for tag in ("t", "b"):
+        if tag == "t":   # test_RowColKhatriRaoMatrix.py:9-22, same draws
+            np.random.seed(0)
+            N, p, d = 5, 6, 3
+            grid_shape = np.random.randint(low=2, high=15, size=d)
+            R = [np.random.rand(p, m) - 0.5 for m in grid_shape]
+            K = [np.random.rand(m, m) - 0.5 for m in grid_shape]
+            C = [np.random.rand(m, N) - 0.5 for m in grid_shape]
+            for i in range(d):
+                R[i][0, :] = 0.
+            vec = np.random.rand(N, 1) - 0.5
+            vecT = np.random.rand(p, 1) - 0.5
+        else:
+            rng = np.random.default_rng(12)
+            N, p, grid_shape = 800, 300, np.array([17, 9, 23])
+            d = 3
+            R = [rng.random((p, m)) - 0.5 for m in grid_shape]
+            K = [rng.random((m, m)) - 0.5 for m in grid_shape]
+            C = [rng.random((m, N)) - 0.5 for m in grid_shape]
+            R[1][:7, :] = 0.
+            vec = rng.random((N, 1)) - 0.5
+            vecT = rng.random((p, 1)) - 0.5
+        def objarr(L):
+            a = np.empty(len(L), dtype=object)
+            for i, x in enumerate(L):
+                a[i] = x
+            return a
+        A = RowColKhatriRaoMatrix(R=objarr(R), K=objarr(K), C=objarr(C))
+        AT = RowColKhatriRaoMatrixTransposed(R=objarr(R), K=objarr(K), C=objarr(C))
+        log_A, sign = A.expand(logged=True)
+        for i in range(d):
+            out["%s_R%d" % (tag, i)] = R[i]
+            out["%s_K%d" % (tag, i)] = K[i]
+            out["%s_C%d" % (tag, i)] = C[i]
+        out.update({tag + "_d": np.int64(d), tag + "_vec": vec, tag + "_vecT": vecT,
+                    tag + "_Avec": A * vec, tag + "_ATvecT": A.T * vecT,
+                    tag + "_ATT_vecT": AT * vecT,
+                    # first 24 rows only (fixture size); the products cover the rest
+                    tag + "_expand": A.expand()[:24], tag + "_log": log_A[:24],
+                    tag + "_sign": np.asarray(sign, dtype=np.float64)[:24]})
+    save("rowcol_kr.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -451,6 +502,7 @@ def main():
     f6_automobile(gg, a.ref)
     f7_web(gg)
     f8_grid_offgrid(gg)
+    f9_rowcol_kr(gg)
 
 
 if __name__ == "__main__":
