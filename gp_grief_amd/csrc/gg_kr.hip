@@ -15,6 +15,13 @@
 // a carry), with the tables stored transposed (U_f^T: m_f x M) so that each
 // row's loads are coalesced over the points j.  Partial sums over row splits
 // are combined in a fixed order: results are bitwise reproducible.
+//
+// For d <= 8 the two steps are fused (kr_stream_kernel): each wave streams 16
+// outer rows of C from HBM against up to 128 points whose U rows are staged in
+// LDS, and weights + sums its MFMA tile in the epilogue, so T never reaches
+// HBM (C is read once per 128-point column pass).  The outer digits of a row
+// are its block's base digits plus the row offset (< 16) carried through the
+// (compile-time many) outer factors.
 #include <algorithm>
 #include <climits>
 
@@ -109,6 +116,164 @@ __global__ __launch_bounds__(kKrThreads) void kr_hadamard_kernel(int64_t n,
   }
 }
 
+typedef double kd4 __attribute__((ext_vector_type(4)));
+constexpr int kSK = 16;          // k-chunk depth staged per barrier
+constexpr int kSMaxWG = 2048;    // workgroups per launch (partials per column pass)
+
+// Streaming fused contraction.  Each wave owns 16 consecutive outer rows o
+// and NT 16-column MFMA tiles (NT*16 <= 128 points of one column pass); C rows are
+// streamed straight from HBM -- lane l reads the 4 contiguous doubles
+// C[o0 + (l & 15)][k0 + 4 (l >> 4) + t], t = 0..3, so a row's 128-byte chunk
+// is one coalesced segment -- and MFMA step t pairs them with the B fragment
+// U[col][k0 + 4 (l >> 4) + t] from the LDS-staged U chunk (any assignment of
+// k to MFMA steps is valid as long as A and B agree).  U (M x K) is staged 16
+// k at a time, double-buffered, one barrier per chunk, shared by the 4 waves.
+// The epilogue weights each row by prod_{f<NF} U_f[col][g_f(o)] and adds it
+// into per-lane column sums kept across the wave's row blocks; C is read once
+// per column pass and T never exists.
+template <int NF, int NT>
+__global__ __launch_bounds__(kKrThreads, 2) void kr_stream_kernel(
+    int64_t O, int M, int K, const double* __restrict__ C, const double* __restrict__ U,
+    KrTabs tabs, double* __restrict__ part) {
+  constexpr int W = NT * 16;               // columns per pass
+  constexpr int LDW = W + 4;               // LDS row stride (doubles)
+  constexpr int kStage = (W * kSK + kKrThreads - 1) / kKrThreads;
+  __shared__ __attribute__((aligned(16))) double sU[2][kSK * LDW];
+  __shared__ double red[4][W];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c0 = blockIdx.x * W;           // first point of this column pass
+  const int kq = lane >> 4, li = lane & 15;
+  const int64_t nblocks = (O + 15) / 16;   // 16-row blocks
+  const int64_t groups = (nblocks + 3) / 4;
+  const int nk = (K + kSK - 1) / kSK;
+
+  double colsum[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) colsum[t] = 0.0;
+  double ru[kStage];
+  auto load_u = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const int e = tid + u * kKrThreads;       // e = col * kSK + kk
+      const int col = e / kSK, kk = e % kSK;
+      const int gc = c0 + col, gk = k0 + kk;
+      ru[u] = (e < W * kSK && gc < M && gk < K) ? U[(int64_t)gc * K + gk] : 0.0;
+    }
+  };
+  auto store_u = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const int e = tid + u * kKrThreads;
+      if (e < W * kSK) sU[buf][(e % kSK) * LDW + e / kSK] = ru[u];
+    }
+  };
+
+#pragma unroll 1
+  for (int64_t grp = blockIdx.y; grp < groups; grp += gridDim.y) {
+    const int64_t blk = grp * 4 + wave;
+    const int64_t o0 = blk * 16;
+    const int64_t myrow = o0 + li;
+    const bool rowok = blk < nblocks && myrow < O;
+    const double* __restrict__ crow = C + (rowok ? myrow : 0) * (int64_t)K;
+    double ca[4], cn[4];
+    auto load_c = [&](int k0, double* dst) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int gk = k0 + 4 * kq + t;
+        dst[t] = (rowok && gk < K) ? crow[gk] : 0.0;
+      }
+    };
+    kd4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = kd4{0.0, 0.0, 0.0, 0.0};
+    load_u(0);
+    store_u(0);
+    load_c(0, ca);
+    __syncthreads();
+#pragma unroll 1
+    for (int c = 0; c < nk; ++c) {
+      const bool more = c + 1 < nk;
+      if (more) {
+        load_u((c + 1) * kSK);
+        load_c((c + 1) * kSK, cn);
+      }
+      const double* b_s = sU[c & 1];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double* brow = b_s + (4 * kq + t) * LDW + li;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[t], brow[16 * j], acc[j], 0, 0, 0);
+      }
+      if (more) {
+        store_u((c + 1) & 1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ca[t] = cn[t];
+      }
+      __syncthreads();
+    }
+
+    // epilogue: lane holds T[o0 + kq + 4 r][c0 + 16 j + li]
+    if (blk < nblocks) {
+      int base[NF > 0 ? NF : 1];
+      {
+        int64_t rem = o0;
+#pragma unroll
+        for (int f = NF - 1; f >= 0; --f) {
+          base[f] = (int)(rem % tabs.m[f]);
+          rem /= tabs.m[f];
+        }
+      }
+#pragma unroll 1
+      for (int r = 0; r < 4; ++r) {
+        const int dlt = kq + 4 * r;
+        if (o0 + dlt >= O) continue;
+        int gd[NF > 0 ? NF : 1];
+#pragma unroll
+        for (int f = 0; f < NF; ++f) gd[f] = base[f];
+        if constexpr (NF > 0) {
+          gd[NF - 1] += dlt;
+#pragma unroll
+          for (int f = NF - 1; f >= 1; --f) {
+            const int mf = (int)tabs.m[f];
+            while (gd[f] >= mf) {
+              gd[f] -= mf;
+              ++gd[f - 1];
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int col = c0 + 16 * j + li;
+          if (col >= M) continue;
+          double w = 1.0;
+#pragma unroll
+          for (int f = 0; f < NF; ++f) w *= tabs.ut[f][(int64_t)gd[f] * M + col];
+          const double tv = r == 0 ? acc[j][0] : (r == 1 ? acc[j][1] : (r == 2 ? acc[j][2] : acc[j][3]));
+          colsum[j] = fma(tv, w, colsum[j]);
+        }
+      }
+    }
+  }
+
+  // reduce over the 4 row groups of each wave, then over the 4 waves
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    colsum[j] += __shfl_xor(colsum[j], 16);
+    colsum[j] += __shfl_xor(colsum[j], 32);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) red[wave][16 * j + lane] = colsum[j];
+  }
+  __syncthreads();
+  for (int col = tid; col < W; col += kKrThreads) {
+    const int gc = c0 + col;
+    if (gc < M)
+      part[(int64_t)blockIdx.y * M + gc] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
+  }
+}
+
 static int kr_splits(int64_t M) {
   const int64_t bx = ceil_div(M, kKrThreads);
   return (int)std::max<int64_t>(1, std::min<int64_t>(kKrMaxSplits, ceil_div(4096, bx)));
@@ -124,7 +289,8 @@ int gg_kr_work_elems(int d, const int64_t* m, int64_t M, int64_t* min_elems) {
                "bad argument");
     int64_t outer = 1;
     for (int f = 0; f + 1 < d; ++f) outer *= m[f];
-    *min_elems = (int64_t)gg::kr_splits(M) * M + std::min<int64_t>(outer, 1024) * M;
+    *min_elems = std::max<int64_t>((int64_t)gg::kr_splits(M) * M + std::min<int64_t>(outer, 1024) * M,
+                                   (int64_t)gg::kSMaxWG * M);
   });
 }
 
@@ -162,6 +328,41 @@ int gg_kr_contract(int d, const int64_t* m, const double* c_dev, const double* u
     }
     const int64_t mL = m[d - 1];
     GG_REQUIRE(mL <= INT_MAX, GG_ERR_VALUE, "fastest factor too large");
+    const hipStream_t st0 = gg::as_stream(stream);
+    if (d - 1 <= 7) {
+      // streaming fused contraction: T never reaches HBM
+      const int nt = M <= 16 ? 1 : (M <= 64 ? 4 : 8);
+      const int64_t groups = gg::ceil_div(gg::ceil_div(outer, (int64_t)16), (int64_t)4);
+      const unsigned gx = (unsigned)gg::ceil_div(M, (int64_t)16 * nt);
+      const int64_t gy = std::max<int64_t>(
+          1, std::min<int64_t>(groups, std::max<int64_t>(1, gg::kSMaxWG / gx)));
+      GG_REQUIRE(work_elems >= gy * M, GG_ERR_VALUE, "work too small (gg_kr_work_elems)");
+      const dim3 grid(gx, (unsigned)gy);
+#define GG_KR_STREAM(NF_, NT_)                                                                \
+  hipLaunchKernelGGL((gg::kr_stream_kernel<NF_, NT_>), grid, dim3(gg::kKrThreads), 0, st0,     \
+                     outer, (int)M, (int)mL, c_dev, ulast_dev, tabs, work_dev)
+#define GG_KR_NF(NT_)                         \
+  switch (d - 1) {                            \
+    case 0: GG_KR_STREAM(0, NT_); break;      \
+    case 1: GG_KR_STREAM(1, NT_); break;      \
+    case 2: GG_KR_STREAM(2, NT_); break;      \
+    case 3: GG_KR_STREAM(3, NT_); break;      \
+    case 4: GG_KR_STREAM(4, NT_); break;      \
+    case 5: GG_KR_STREAM(5, NT_); break;      \
+    case 6: GG_KR_STREAM(6, NT_); break;      \
+    default: GG_KR_STREAM(7, NT_); break;     \
+  }
+      if (nt == 1) { GG_KR_NF(1) }
+      else if (nt == 4) { GG_KR_NF(4) }
+      else { GG_KR_NF(8) }
+#undef GG_KR_NF
+#undef GG_KR_STREAM
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::kr_finish_kernel, dim3((unsigned)gg::ceil_div(M, gg::kKrThreads)),
+                         dim3(gg::kKrThreads), 0, st0, work_dev, (int)gy, M, out_dev, 0);
+      GG_LAUNCH_CHECK();
+      return;
+    }
     const int S = gg::kr_splits(M);
     GG_REQUIRE(work_elems > (int64_t)S * M, GG_ERR_VALUE, "work too small (gg_kr_work_elems)");
     int64_t chunk = std::min<int64_t>(outer, (work_elems - (int64_t)S * M) / M);

@@ -26,7 +26,10 @@ def gg(gpu):
 
 
 @pytest.mark.parametrize("ms,M", [([13], 5), ([7, 9], 37), ([5, 6, 7], 300),
-                                  ([4, 3, 5, 6], 1), ([3, 4, 2, 5, 3], 129)])
+                                  ([4, 3, 5, 6], 1), ([3, 4, 2, 5, 3], 129),
+                                  ([2, 3, 2, 2, 3, 2, 2, 3], 65),        # d = 8: fused, NF = 7
+                                  ([2, 3, 2, 2, 3, 2, 2, 2, 3], 70),     # d = 9: two-pass path
+                                  ([300, 1, 130], 200)])
 def test_kr_contract_vs_oracle(gg, ms, M):
     rng = np.random.default_rng(len(ms) * 100 + M)
     blocks = [rng.standard_normal((M, m)) for m in ms]
@@ -39,11 +42,12 @@ def test_kr_contract_vs_oracle(gg, ms, M):
 
 
 def test_kr_contract_chunked_equals_single(gg):
-    """A scratch of the minimum size forces many GEMM chunks; results agree
-    and repeated runs are bitwise identical (fixed-order reductions)."""
+    """A scratch of the minimum size forces several GEMM chunks on the
+    two-pass path (d > 8); results agree and repeated runs are bitwise
+    identical (fixed-order reductions)."""
     import torch
     rng = np.random.default_rng(5)
-    ms, M = [40, 30, 25], 70
+    ms, M = [3, 3, 3, 3, 3, 3, 3, 3, 2], 70      # d = 9: the chunked two-pass path
     blocks = [rng.standard_normal((M, m)) for m in ms]
     c = rng.standard_normal(int(np.prod(ms)))
     KR = gg.tensors.KhatriRaoMatrix(blocks, partition=0)
@@ -53,7 +57,20 @@ def test_kr_contract_chunked_equals_single(gg):
     b2 = KR.contract(cd, work_elems=1).cpu().numpy()
     assert np.array_equal(b, b2)
     assert rel(a, b) < 1e-14
-    assert rel(a, oracle.kr_contract(blocks, c)) < 1e-13
+    f1 = KR.contract(cd).cpu().numpy()
+    assert np.array_equal(a, f1)
+
+
+def test_kr_contract_fused_deterministic(gg):
+    import torch
+    rng = np.random.default_rng(6)
+    ms, M = [37, 41, 29], 333
+    blocks = [rng.standard_normal((M, m)) for m in ms]
+    c = torch.from_numpy(rng.standard_normal(int(np.prod(ms)))).cuda()
+    KR = gg.tensors.KhatriRaoMatrix(blocks, partition=0)
+    a = KR.contract(c).cpu().numpy()
+    assert np.array_equal(a, KR.contract(c).cpu().numpy())
+    assert rel(a, oracle.kr_contract(blocks, c.cpu().numpy())) < 1e-13
 
 
 def test_kr_wrong_shape_raises(gg):
