@@ -525,8 +525,9 @@ class KhatriRaoMatrix(object):
         need = ctypes.c_int64()
         native.check(L.gg_kr_work_elems(self.d, marr, M, ctypes.byref(need)))
         outer = N // m[-1]
+        # d <= 8 runs the fused kernel (partials only); the two-pass path gets
         # up to ~1 GiB of GEMM chunk beyond the minimum: few chunks, modest HBM
-        extra = min(outer * M, max(0, (1 << 27) - need.value))
+        extra = 0 if self.d <= 8 else min(outer * M, max(0, (1 << 27) - need.value))
         if work_elems is not None:
             extra = max(0, int(work_elems) - need.value)
         work = dev.empty(need.value + extra)
