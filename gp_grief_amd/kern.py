@@ -353,6 +353,7 @@ class GriefKernel(GridKernel):
         self._old_base_kern_params = None
         self.log_KRrowcol = log_KRrowcol
         self._dev_basis = None
+        self._eig_cache = {}   # base-kernel parameters -> per-factor (Q, lambda)
 
     # ------------------------------------------------------------------ Phi
     def cov(self, x, z=None):
@@ -426,17 +427,64 @@ class GriefKernel(GridKernel):
         if self._old_base_kern_params is not None and \
                 np.array_equal(self._old_base_kern_params, base):
             return
-        Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
-        Q, lam = device_sym_eig([np.asarray(k) for k in Kuu.K])
+        Q, lam = self._factor_eigs(base)
         self._Quu = KronMatrix(Q)
         all_eig_vals = KronMatrix(lam)
         n_eigs = int(min(self.n_eigs, all_eig_vals.shape[0]))
         eig_pos, self._log_lam = all_eig_vals.find_extremum_eigs(
             n_eigs=n_eigs, mode='largest', log_expand=True)[:2]
-        self._Sp = [SelectionMatrixSparse((col, Kuu.K[i].shape[0]))
+        self._Sp = [SelectionMatrixSparse((col, Q[i].shape[0]))
                     for i, col in enumerate(eig_pos.T)]
         self._old_base_kern_params = base
         self._build_device_basis()
+
+    _EIG_CACHE_MAX = 64
+
+    def _factor_eigs(self, base):
+        """Per-factor eigenpairs for the base-kernel parameters `base` (the
+        state the kernel objects hold now), from the cache or the device."""
+        key = np.asarray(base, dtype=np.float64).tobytes()
+        hit = self._eig_cache.get(key)
+        if hit is None:
+            Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
+            hit = device_sym_eig([np.asarray(k) for k in Kuu.K])
+            self._cache_put(key, hit)
+        return hit
+
+    def _cache_put(self, key, value):
+        while len(self._eig_cache) >= self._EIG_CACHE_MAX:
+            self._eig_cache.pop(next(iter(self._eig_cache)))
+        self._eig_cache[key] = value
+
+    def prefetch_eigs(self, parameter_sets):
+        """Eigendecompose the grid factors of several kernel parameter vectors
+        (GriefKernel.parameters layout) in ONE batched device launch and cache
+        them, so the finite-difference gradient of opt_kernel_params
+        (basemodel.py:328-361, one basis per perturbed parameter) pays one
+        eigensolver latency instead of one per perturbation.  Each vector is
+        applied through the parameters setter -- so the shared-kernel-object
+        rule (grid_kernel.py:233-239) decides the effective factors exactly as
+        in the sequential path -- and the kernel state is restored."""
+        saved = self.parameters.copy()
+        keys, mats, d = [], [], self.grid_dim
+        try:
+            for v in parameter_sets:
+                self.parameters = np.asarray(v, dtype=np.float64).copy()
+                key = np.asarray(super(GriefKernel, self).parameters,
+                                 dtype=np.float64).tobytes()
+                if key in self._eig_cache or key in keys:
+                    continue
+                Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
+                keys.append(key)
+                mats.extend(np.asarray(k) for k in Kuu.K)
+        finally:
+            self.parameters = saved
+        if not mats:
+            return 0
+        Q, lam = device_sym_eig(mats)
+        for i, key in enumerate(keys):
+            self._cache_put(key, (Q[i * d:(i + 1) * d], lam[i * d:(i + 1) * d]))
+        return len(keys)
 
     def _build_device_basis(self):
         d = self.grid_dim

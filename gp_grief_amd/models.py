@@ -373,6 +373,23 @@ class GPGriefModel(BaseModel):
         A = t.zeros((p, p), dtype=t.float64, device=self._Phi.device)
         return self._sum(dense.matmul(self._Phi, self._Phi, ta=True, C=A, uplo=self._gram_uplo))
 
+    def _finite_diff_gradient(self, parameters):
+        """Forward differences (basemodel.py:328-361).  With opt_kernel_params
+        every perturbed base-kernel parameter needs its own eigen-basis: those
+        eigendecompositions are batched into one device launch up front
+        (GriefKernel.prefetch_eigs); the LMLs then run as in the reference."""
+        if self.kern.opt_kernel_params:
+            free_inds = np.nonzero(np.logical_not(self._fixed_indicies))[0]
+            sets = [np.asarray(parameters[1:], dtype=np.float64)]
+            for idx in free_inds:
+                if idx == 0:
+                    continue                       # the noise leaves the basis unchanged
+                p_fs = np.array(parameters, dtype=np.float64)
+                p_fs[idx] += 1e-6
+                sets.append(p_fs[1:])
+            self.kern.prefetch_eigs(sets)
+        return super(GPGriefModel, self)._finite_diff_gradient(parameters)
+
     def _adjoint_gradient(self, parameters):
         """dL/dw and dL/dsigma^2 (:156-200) via diag(P^-1): with P = A + D,
         sum_i A_ij (P^-1 A)_ij = A_jj - d_j + d_j^2 (P^-1)_jj and

@@ -218,3 +218,34 @@ def test_automobile_optimize(gg):
     mean, var = m.predict(Xnew=x[~itr])
     rmse = np.linalg.norm((mean[:, 0] - y[~itr, 0]) * z["y_scale"]) / np.sqrt(mean.size)
     assert abs(rmse - z["rmse"]) < 1e-4 * z["rmse"]
+
+
+def test_fd_gradient_batched_eigs_equal_sequential(gg):
+    """opt_kernel_params: the finite-difference gradient with the perturbed
+    bases' eigendecompositions batched into one launch equals the sequential
+    one (distinct kernels per dim, and the shared-kernel-object case)."""
+    rng = np.random.default_rng(4)
+    d, m, n, p = 3, 20, 400, 60
+    x = rng.random((n, d))
+    y = (np.sin(6 * x).sum(axis=1) + 0.1 * rng.standard_normal(n)).reshape(-1, 1)
+    for shared in (False, True):
+        grads = []
+        for batched in (True, False):
+            if shared:
+                kl = [gg.kern.RBF(1, variance=1.0, lengthscale=0.3)] * d
+            else:
+                kl = [gg.kern.RBF(1, variance=1.0, lengthscale=0.2 + 0.05 * i) for i in range(d)]
+            grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1)] * d)
+            kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p,
+                                       reweight_eig_funs=False, opt_kernel_params=True)
+            if not batched:
+                kern.prefetch_eigs = lambda sets: 0
+            model = gg.models.GPGriefModel(x, y, kern, noise_var=0.05)
+            ll, g = model.log_likelihood(return_gradient=True)
+            if batched:
+                assert len(kern._eig_cache) >= 1
+            grads.append((float(np.squeeze(ll)), g.copy(), model.parameters.copy()))
+        (l1, g1, p1), (l2, g2, p2) = grads
+        assert np.array_equal(p1, p2)
+        assert abs(l1 - l2) <= 1e-12 * abs(l2)
+        assert np.allclose(g1, g2, rtol=1e-6, atol=1e-8), (g1, g2)
