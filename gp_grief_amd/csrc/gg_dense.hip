@@ -254,57 +254,62 @@ constexpr int kNB = 64;
 
 // Factor the nb x nb diagonal block at A (lda) in place (lower) and write its
 // inverse (lower) to W (ld kNB).  status <- 1 if a pivot is not positive/finite.
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* A, int64_t lda, int nb,
-                                                         double* W, int* status) {
-  __shared__ double L[kNB][kNB + 1];
-  __shared__ double Wi[kNB][kNB + 1];
-  __shared__ int bad;
-  const int tid = threadIdx.x;
-  if (tid == 0) bad = 0;
-  for (int e = tid; e < nb * nb; e += blockDim.x) {
-    const int i = e / nb, j = e % nb;
-    L[i][j] = (j <= i) ? A[(int64_t)i * lda + j] : 0.0;
+// One wave, no workgroup barriers on the critical path: lane i holds row i of
+// the block in registers (right-looking; pivots and L[j][k] broadcast with
+// v_readlane), then lane j forms column j of W = L^-1 by forward substitution
+// against L broadcast from LDS.  Rows >= nb are padded with the identity.
+__device__ inline double readlane_f64(double v, int lane) {
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
+  return __hiloint2double(hi, lo);
+}
+
+__global__ __launch_bounds__(kNB) void potrf_diag_kernel(double* A, int64_t lda, int nb,
+                                                        double* W, int* status) {
+  __shared__ double Ls[kNB][kNB + 1];
+  const int ln = threadIdx.x;   // row owner in the factorisation, column owner in the inverse
+  // coalesced stage of the (lower) block: lane = column
+  for (int r = 0; r < kNB; ++r)
+    Ls[r][ln] = (r < nb && ln <= r) ? A[(int64_t)r * lda + ln] : ((r == ln) ? 1.0 : 0.0);
+  __syncthreads();
+  double a[kNB];
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) a[j] = (j <= ln) ? Ls[ln][j] : 0.0;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < kNB; ++k) {
+    const double d = readlane_f64(a[k], k);
+    if (k < nb && (!(d > 0.0) || !isfinite(d))) bad = true;
+    const double lkk = sqrt(fmax(d, 0.0));
+    if (ln == k) a[k] = lkk;
+    else if (ln > k) a[k] = a[k] / lkk;
+    const double lik = (ln > k) ? a[k] : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < kNB; ++j) {
+      const double ljk = readlane_f64(a[k], j);   // L[j][k], held by lane j
+      a[j] = (j <= ln) ? fma(-lik, ljk, a[j]) : a[j];
+    }
   }
   __syncthreads();
-  for (int k = 0; k < nb; ++k) {
-    if (tid == 0) {
-      const double d = L[k][k];
-      if (!(d > 0.0) || !isfinite(d)) bad = 1;
-      L[k][k] = sqrt(fmax(d, 0.0));
-    }
-    __syncthreads();
-    const double dk = L[k][k];
-    for (int i = k + 1 + tid; i < nb; i += blockDim.x) L[i][k] = L[i][k] / dk;
-    __syncthreads();
-    const int rem = nb - k - 1;
-    for (int e = tid; e < rem * rem; e += blockDim.x) {
-      const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-      if (j <= i) L[i][j] -= L[i][k] * L[j][k];
-    }
-    __syncthreads();
-  }
-  // inverse of the lower-triangular factor, one row per step: W[i][j] for all
-  // j <= i at once (4 adjacent lanes split the k-sum, quad shuffle reduce)
-  for (int e = tid; e < kNB * kNB; e += blockDim.x) Wi[e / kNB][e % kNB] = 0.0;
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) Ls[ln][j] = a[j];
   __syncthreads();
-  {
-    const int j = tid >> 2, part = tid & 3;   // blockDim.x == 256 = kNB * 4
-    for (int i = 0; i < nb; ++i) {
-      double s = 0.0;
-      if (j < i)
-        for (int k = j + part; k < i; k += 4) s = fma(L[i][k], Wi[k][j], s);
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      if (part == 0 && j <= i) Wi[i][j] = (j == i) ? 1.0 / L[i][i] : -s / L[i][i];
-      __syncthreads();
-    }
+  for (int r = 0; r < nb; ++r)
+    if (ln <= r) A[(int64_t)r * lda + ln] = Ls[r][ln];
+  // W = L^-1, lane ln owns column ln: W[r][ln] = (delta - sum_c L[r][c] W[c][ln]) / L[r][r]
+  double w[kNB];
+#pragma unroll
+  for (int r = 0; r < kNB; ++r) {
+    double acc = (r == ln) ? 1.0 : 0.0;
+#pragma unroll
+    for (int c = 0; c < r; ++c) acc = fma(-Ls[r][c], w[c], acc);
+    w[r] = acc / Ls[r][r];
   }
-  for (int e = tid; e < nb * nb; e += blockDim.x) {
-    const int i = e / nb, j = e % nb;
-    if (j <= i) A[(int64_t)i * lda + j] = L[i][j];
-    W[(int64_t)i * kNB + j] = Wi[i][j];
-  }
-  if (tid == 0 && bad) *status = 1;
+#pragma unroll
+  for (int r = 0; r < kNB; ++r)
+    W[(int64_t)r * kNB + ln] = (r < nb && ln < nb && ln <= r) ? w[r] : 0.0;
+  if (ln == 0 && bad) *status = 1;
 }
 
 __global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
@@ -424,7 +429,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         const int nb = std::min(gg::kNB, n - k0);
         double* Akk = A_dev + (int64_t)k0 * lda + k0;
         double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
-        hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(256), 0, s, Akk, lda, nb, Wk,
+        hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(gg::kNB), 0, s, Akk, lda, nb, Wk,
                            status);
         GG_LAUNCH_CHECK();
         const int rest = n - k0 - nb;
