@@ -1,25 +1,40 @@
 """Benchmark: CG iterations/s on the 4-D RBF grid 200^4 (BASELINE.json configs[2]).
 
 One "step" = one CG iteration on (K + s I) x = y, K = K_0 (x) K_1 (x) K_2 (x) K_3
-(200 x 200 RBF factors, lengthscales 0.1*(1+0.05 i), jitter 1e-12, s = 0.01),
-all vectors (y, x, r, p, q, matvec scratch: 6 x 12.8 GB) resident in HBM.
+(200 x 200 RBF factors built by gp_grief_amd.kern.GridKernel.cov_grid -- the
+drop-in path, grid_kernel.py:56-115 -- lengthscales 0.1*(1+0.05 i), jitter
+1e-12, s = 0.01), all vectors (y, x, r, two p buffers, q, matvec scratch:
+7 x 12.8 GB) resident in HBM.
 
 Prints ONE JSON line (rank 0):
   metric/value/unit   CG iterations per second, whole job
-  roofline            the dominant kernel (the FP64 MFMA mode product) timed
-                      with HIP events on the stream it runs on, against the
-                      FP64 matrix peak; plus HBM GB/s of the whole matvec
-  cpu_baseline        the CPU oracle (oracle/, NumPy + OpenBLAS) timed on this
-                      host on a bounded sample of the same workload
+  roofline            the dominant kernel -- the mode-product launch position
+                      with the largest share of the timed region, from HIP
+                      events recorded by the library on the stream the kernels
+                      run on -- against its binding roof (FP64 MFMA or HBM,
+                      whichever floor is higher for that launch's algorithmic
+                      FLOP and bytes); plus whole-matvec and whole-iteration
+                      fractions
+  cpu_baseline        the reference's CPU arithmetic restated
+                      (oracle.kron_matvec_dsymm: kron_matrix.py:74-96's dsymm
+                      sequence; fidelity vs the reference in
+                      profiles/r02_cpu_fidelity.json) in a textbook CG on the
+                      full grid, 1 warm-up + 3 timed iterations, host threads
+  lanczos             (--lanczos K) K steps of device Lanczos on the same
+                      operator, timed with HIP events (SLQ log-det leg of C3)
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 200] [--dims 4]
-N > 1 is launched by torch.distributed.run (one process per GPU, RCCL): strong
-scaling of the same single CG, factor 0 sharded over the ranks (two all-to-alls
-per matvec, two scalar all-reduces per iteration); see DESIGN.md section 6.
+--gpus N > 1 without a launcher: this process starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child
+(before any GPU call) and exits with its status; under the launcher each rank
+is one GPU (RCCL): strong scaling of the same single CG, factor 0 sharded over
+the ranks.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +45,7 @@ sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, dense (AMD spec)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
+METRIC = "CG iters/sec + Kron-matvec achieved HBM GB/s, 4D RBF grid 200^4"
 
 
 def parse():
@@ -41,15 +57,44 @@ def parse():
     ap.add_argument("--dims", type=int, default=4)
     ap.add_argument("--sigma2", type=float, default=0.01)
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--recurrence", default="fused", choices=["fused", "textbook"])
+    ap.add_argument("--lanczos", type=int, default=0,
+                    help="also time this many device Lanczos steps (one probe)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "push", "a2a"])
+    ap.add_argument("--fusion", type=int, default=None, choices=[0, 1, 2],
+                    help="fused-CG layout (gg_cg_set_fusion); default: the library's")
     return ap.parse_args()
 
 
-def factors(m, d):
-    import oracle  # factor construction only (m x m); the CPU leg below times it
-    g = np.linspace(0.0, 1.0, m)
-    return [oracle.cov_1d("RBF", g, g, 1.0, 0.1 * (1 + 0.05 * (d - 1 - k))) + 1e-12 * np.eye(m)
-            for k in range(d)]
+# ---------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a):
+    """One process per GPU via torch.distributed.run, started as a CHILD of
+    this process before anything touched the GPU (never exec)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(a.gpus), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---------------------------------------------------------------- inputs
+def grid_factors(m, d):
+    """The 200^4 operator's factors through the drop-in API:
+    GridKernel([RBF_i]).cov_grid(xg, dim_noise_var=1e-12) (device kernels),
+    returned as host arrays (factor k = input dimension d-1-k)."""
+    import gp_grief_amd.kern as kern
+    kl = [kern.RBF(1, variance=1.0, lengthscale=0.1 * (1 + 0.05 * i)) for i in range(d)]
+    xg = [np.linspace(0.0, 1.0, m).reshape(-1, 1) for _ in range(d)]
+    K = kern.GridKernel(kl).cov_grid(xg, dim_noise_var=1e-12)
+    return K, [np.asarray(f, dtype=np.float64) for f in K.K]
 
 
 def grid_rhs_device(m, d, torch, dev, seed=1):
@@ -71,7 +116,7 @@ def grid_rhs_device(m, d, torch, dev, seed=1):
     return y
 
 
-def local_rhs_device(m, d, world, rank, torch, dev, seed=1):
+def local_rhs(m, d, world, rank, torch, dev, seed=1):
     """This rank's shard of the same right-hand side, in the sharded layout
     (m_1, ..., m_{d-1}, a) with a = i_0 - rank * m/world fastest."""
     s0 = m // world
@@ -95,16 +140,34 @@ def local_rhs_device(m, d, world, rank, torch, dev, seed=1):
     return y
 
 
-def run_sharded(a, world, rank, torch, dev, dist):
+# ---------------------------------------------------------------- sharded
+def _engine_factory():
+    """HipEngine, or (tests only) GG_BENCH_ENGINE=module:Class, whose module
+    may also provide make_factors(m, d) -- the CPU/gloo rehearsal of the
+    launcher and the sharded orchestration."""
+    spec = os.environ.get("GG_BENCH_ENGINE")
+    if not spec:
+        from gp_grief_amd.distributed import HipEngine
+        return HipEngine, None
+    import importlib
+    mod_name, cls_name = spec.split(":")
+    mod = importlib.import_module(mod_name)
+    return getattr(mod, cls_name), getattr(mod, "make_factors", None)
+
+
+def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     """Strong scaling: one CG on the full grid, factor 0 sharded over ranks."""
-    import gp_grief_amd as gg  # noqa: F401
-    from gp_grief_amd.distributed import DistKronCG, HipEngine, TorchExchange
+    from gp_grief_amd.distributed import DistKronCG, TorchExchange
     m, d, s = a.grid, a.dims, a.sigma2
-    F = factors(m, d)
-    eng = HipEngine(F, world, rank)
-    y = local_rhs_device(m, d, world, rank, torch, dev)
+    Engine, make_factors = _engine_factory()
+    F = make_factors(m, d) if make_factors is not None else grid_factors(m, d)[1]
+    eng = Engine(F, world, rank)
+    y = local_rhs(m, d, world, rank, torch, dev)
     ex = TorchExchange()
-    mode = os.environ.get("GG_DIST_MODE", "auto")
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    mode = os.environ.get("GG_DIST_MODE", a.exchange)
+    if mode == "auto":
+        mode = "push" if getattr(eng, "supports_push", False) else "a2a"
     # every rank must take the same exchange: a push setup that fails on any
     # rank (IPC mapping of a peer's buffer) sends all ranks to all-to-all
     try:
@@ -130,15 +193,16 @@ def run_sharded(a, world, rank, torch, dev, dist):
         del ref, ya, yp
         if not float(err[0]) <= 1e-12 * float(err[1]):
             cg = DistKronCG(eng, ex, s, mode="a2a")
-        torch.cuda.empty_cache()
+        if on_gpu:
+            torch.cuda.empty_cache()
     cg.start(y, rtol=0.0, atol=0.0)
     cg.iterate(a.warmup)
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     cg.iterate(a.steps)
-    torch.cuda.synchronize()
+    sync()
     dist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -148,10 +212,10 @@ def run_sharded(a, world, rank, torch, dev, dist):
     assert it == a.warmup + a.steps and np.isfinite(rho), (it, rho)
     n = m ** d
     return {
-        "metric": "CG iters/sec + Kron-matvec achieved HBM GB/s, 4D RBF grid 200^4",
+        "metric": METRIC,
         "value": a.steps / dt,
         "unit": "CG iters/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size(),
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
@@ -172,83 +236,197 @@ def run_sharded(a, world, rank, torch, dev, dist):
     }
 
 
-KERNEL_NAME = "gg::mode_product_kernel<13, 4, 3, 0, 3, true, 1, 2, 0>"
+# ---------------------------------------------------------------- roofline
+def launch_passes(d, recurrence, fusion=0):
+    """Algorithmic 8-byte passes over N of each mode-product launch position of
+    one CG iteration (reads + writes, gg_kron.hip kron_apply / MpFuse)."""
+    if d == 1:
+        return [4] if recurrence == "fused" else [5]
+    passes = [2] * d
+    if recurrence == "fused":
+        # prologue: r, q_old read, r written (p_old is X); layout 0 also writes p_new
+        passes[0] += 3 if fusion else 4
+        # epilogue: p and r read (shift, p.q, r.q); layouts 1/2 also write p_new
+        passes[d - 1] += 3 if fusion else 2
+        if fusion == 2:
+            passes[d - 1] += 2  # x += alpha p_old in the epilogue (x read + written)
+        else:
+            passes[1] += 3      # side job: x += alpha p_old (x, p_old read; x written)
+    else:
+        passes[0] += 2          # prologue: r read, p written in place
+        passes[d - 1] += 1      # epilogue: p read (shift, p.q)
+    return passes
 
 
-def pmc_traffic(m, d):
+def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
+    flop = 2.0 * n * m                     # one mode product (square factor m)
+    passes = launch_passes(d, recurrence, fusion)
+    dom = int(np.argmax(per_pos))          # largest share of the timed region
+    t = per_pos[dom] * 1e-3
+    byts = 8.0 * n * passes[dom]
+    f_mfma = flop / (FP64_MFMA_PEAK_TFLOPS * 1e12)
+    f_hbm = byts / (HBM_PEAK_GBS * 1e9)
+    bound = "mfma" if f_mfma >= f_hbm else "hbm"
+    tf = flop / t / 1e12
+    gbs = byts / t / 1e9
+    mv_s = sum(per_pos) * 1e-3
+    it_bytes = 8.0 * n * sum(passes)
+    floor_it = max(d * f_mfma, it_bytes / (HBM_PEAK_GBS * 1e9))
+    roof = {
+        "bound": bound,
+        "achieved": tf if bound == "mfma" else gbs,
+        "peak": FP64_MFMA_PEAK_TFLOPS if bound == "mfma" else HBM_PEAK_GBS,
+        "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
+        "frac": (f_mfma if bound == "mfma" else f_hbm) / t,
+        "traffic": None, "traffic_unit": "bytes per launch",
+        "kernel": "mode product, launch position %d of %d (%s CG, layout %d)"
+                  % (dom, d, recurrence, fusion),
+        "launch_ms": per_pos[dom],
+        "launch_ms_source": "HIP events the library records around each launch, on the "
+                            "stream it launches on, over the timed iterations",
+        "flop_per_launch": flop, "algorithmic_bytes_per_launch": byts,
+        "passes_per_launch": passes[dom],
+        "frac_mfma": f_mfma / t, "frac_hbm": f_hbm / t,
+        "achieved_tflops": tf, "achieved_gbs": gbs,
+    }
+    extra = {
+        "mode_product_ms_by_position": per_pos,
+        "passes_by_position": passes,
+        "matvec_ms": 1e3 * mv_s,
+        "matvec_tflops": d * flop / mv_s / 1e12,
+        "matvec_frac": d * flop / mv_s / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+        "matvec_hbm_gbs": 8.0 * n * (2 * d + 1) / mv_s / 1e9,
+        "matvec_hbm_frac": 8.0 * n * (2 * d + 1) / mv_s / 1e9 / HBM_PEAK_GBS,
+        "iteration_algorithmic_bytes": it_bytes,
+        "iteration_hbm_gbs": it_bytes / (ms_per_step * 1e-3) / 1e9,
+        "iteration_floor_ms": 1e3 * floor_it,
+        "iteration_frac_vs_fused_floor": 1e3 * floor_it / ms_per_step,
+        "outside_mode_products_ms": ms_per_step - 1e3 * mv_s,
+    }
+    return roof, extra
+
+
+def pmc_traffic(m, d, kernel_position, recurrence):
     """HBM bytes per launch of the dominant kernel from the committed PMC
-    passes (tools/pmc_traffic.py), if they were taken on this kernel and
-    workload; else None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_mode_product.json")
+    passes (tools/pmc_traffic.py) when they were taken on that launch, this
+    workload and a calibration of the kernel's own access pattern; else None."""
+    path = os.path.join(ROOT, "profiles", "r02_pmc_mode_product.json")
     if (m, d) != (200, 4) or not os.path.exists(path):
         return None, None
     rec = json.load(open(path))
-    if KERNEL_NAME.replace("gg::", "") not in str(rec.get("kernel")):
+    if rec.get("position") != kernel_position or rec.get("recurrence") != recurrence:
+        return None, None
+    if not rec.get("calibrated_on_own_pattern"):
         return None, None
     return rec["traffic_bytes"], os.path.relpath(path, ROOT)
 
 
-def cpu_baseline(m, d, sigma2):
-    """One CG iteration of the CPU oracle at the full grid (bounded sample)."""
+# ---------------------------------------------------------------- CPU leg
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
+def cpu_baseline(F, sigma2, iters):
+    """Textbook CG (oracle.cg_solve) on the full grid with the reference's BLAS
+    call sequence for the operator (oracle.kron_matvec_dsymm, restating
+    kron_matrix.py:74-96), 1 warm-up + `iters` timed iterations."""
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(limits=threads)
     except Exception:  # pragma: no cover
         ctx = None
-    F = factors(m, d)
+    m, d = F[0].shape[0], len(F)
     n = m ** d
     rng = np.random.default_rng(1)
     block = rng.standard_normal(m ** min(d, 3))
     b = np.tile(block, n // block.size)
-    mv = lambda v: oracle.kron_matvec(F, v) + sigma2 * v
-    t0 = time.perf_counter()
-    x, info, it = oracle.cg_solve(mv, b, rtol=0.0, maxiter=1)
-    dt = time.perf_counter() - t0
-    del x, b
+    mv = lambda v: oracle.kron_matvec_dsymm(F, v) + sigma2 * v
+    stamps = [time.perf_counter()]
+    oracle.cg_solve(mv, b, rtol=0.0, maxiter=1 + iters,
+                    callback=lambda x: stamps.append(time.perf_counter()))
+    del b
     if ctx is not None:
         ctx.__exit__(None, None, None)
-    return {"value": 1.0 / dt, "unit": "CG iters/s", "cores": threads, "kind": "port",
-            "sample": "1 CG iteration of oracle.cg_solve on the full %d^%d grid "
-                      "(NumPy/OpenBLAS, %d threads), %.1f s" % (m, d, threads, dt)}
+    per_it = np.diff(stamps)              # [warm-up, timed...]
+    timed = per_it[1:]
+    return {"value": 1.0 / float(np.mean(timed)), "unit": "CG iters/s", "cores": threads,
+            "kind": "port",
+            "host_cpu_count": os.cpu_count(), "host_cpu_model": cpu_model(),
+            "iteration_s": [float(v) for v in per_it],
+            "fidelity": "profiles/r02_cpu_fidelity.json",
+            "sample": "textbook CG on the full %d^%d grid, operator = the reference's dsymm "
+                      "sequence restated (oracle.kron_matvec_dsymm), %d threads "
+                      "(OMP_NUM_THREADS: this process's CPU share of the box), 1 warm-up "
+                      "iteration (%.1f s) + %d timed (mean %.1f s)"
+                      % (m, d, threads, per_it[0], iters, float(np.mean(timed)))}
 
 
+def time_lanczos(K, s, steps, torch):
+    """`steps` Lanczos steps of one probe on the same operator (the SLQ leg of
+    C3), timed with HIP events on the library's stream."""
+    from gp_grief_amd import linalg
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    a, b = linalg.lanczos_tridiag(K, s, steps, seed=0, probe=0)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    return {"steps": int(a.size), "ms": ms, "ms_per_step": ms / max(int(a.size), 1),
+            "steps_per_s": 1e3 * a.size / ms}
+
+
+# ---------------------------------------------------------------- main
 def main():
     a = parse()
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and a.gpus > 1:
+        sys.exit(launch_ranks(a))
+    world = int(world_env or 1)
+    if world != a.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    backend = os.environ.get("GG_BENCH_BACKEND", "nccl")
+    on_gpu = backend == "nccl"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    else:
-        dist = None
-    dev = torch.device("cuda", torch.cuda.current_device())
-    import gp_grief_amd as gg
-    if world > 1:
-        res = run_sharded(a, world, rank, torch, dev, dist)
+        if on_gpu:
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+        dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu \
+            else torch.device("cpu")
+        res = run_sharded(a, world, rank, torch, dev, dist, on_gpu)
         if rank == 0:
             print(json.dumps(res), flush=True)
         dist.destroy_process_group()
         return
 
+    dev = torch.device("cuda", torch.cuda.current_device())
+    import gp_grief_amd as gg
     m, d, s = a.grid, a.dims, a.sigma2
-    F = factors(m, d)
-    K = gg.tensors.KronMatrix(F, sym=True)
+    K, F = grid_factors(m, d)
     n = m ** d
     y = grid_rhs_device(m, d, torch, dev)
-    solver = gg.linalg.KronCG(K, s, recurrence=a.recurrence)
+    solver = gg.linalg.KronCG(K, s, recurrence=a.recurrence,
+                              fusion=a.fusion if a.recurrence == "fused" else None)
     solver.start(y, rtol=0.0, atol=0.0)   # never "converges": exactly the steps asked for
     torch.cuda.synchronize()
 
-    # ---- CG: warmup, then exactly `steps` iterations bracketed by barrier+sync
+    # ---- CG: warmup, then exactly `steps` iterations bracketed by sync
     solver.iterate(a.warmup, check_every=0)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
     # live kernel timing: HIP events around every mode product of the timed
     # iterations, recorded by the library on the stream the kernels run on
     solver.profile(True)
@@ -256,47 +434,28 @@ def main():
     t0 = time.perf_counter()
     solver.iterate(a.steps, check_every=0)
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
     dt = time.perf_counter() - t0
     n_mv, mode_ms = solver.profile_read()
     solver.profile(False)
     assert n_mv == a.steps, (n_mv, a.steps)
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     it, conv, res, tol = solver.status()
     assert it == a.warmup + a.steps, (it, a.warmup, a.steps)
     assert np.isfinite(res)
 
-    # dominant kernel: the plain mode product.  Positions of a matvec: 0 is the
-    # CG-fused first product (prologue), 1 carries the fused x-update side
-    # job, d-1 the fused epilogue (shift, p.q / r.q / q.q); the plain ones are
-    # 1..d-2 (textbook) or 2..d-2 (fused).
+    ms_per_step = 1e3 * dt / a.steps
     per_pos = [t / n_mv for t in mode_ms]
-    plain = list(range(2 if solver.recurrence == "fused" else 1, d - 1)) or [d - 1]
-    launch_ms = sum(per_pos[k] for k in plain) / len(plain)
-    mv_ms = sum(per_pos)
-    flop_launch = 2.0 * n * m
-    achieved_tf = flop_launch / (launch_ms * 1e-3) / 1e12
-    traffic, traffic_src = pmc_traffic(m, d)
-    # algorithmic HBM bytes of one iteration (8 B per element per pass):
-    # d mode products read + write 2N each; CG vectors (textbook) p-update
-    # r, p -> p 3N; +s p / p.q read p 1N; x/r update 6N.  Fused: the same
-    # vector passes ride on the mode products (first: r, q, p -> r, p; second:
-    # x, p -> x; last: p, r): 10N either way (+ one closing update per
-    # iterate() call in the fused case).
-    mv_bytes = 8.0 * n * (2 * d + 1)
-    it_bytes = 8.0 * n * (2 * d + 10)
+    roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
+                                  solver.fusion)
+    traffic, src = pmc_traffic(m, d, int(np.argmax(per_pos)), solver.recurrence)
+    roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
-        "metric": "CG iters/sec + Kron-matvec achieved HBM GB/s, 4D RBF grid 200^4",
+        "metric": METRIC,
         "value": a.steps / dt,
         "unit": "CG iters/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": 1e3 * dt / a.steps,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -306,32 +465,19 @@ def main():
                                % (m, d, s, n),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
                    "cg_recurrence": solver.recurrence,
+                   "cg_fusion_layout": solver.fusion,
                    "parallelism": "single-gpu"},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved_tf / FP64_MFMA_PEAK_TFLOPS,
-                     "traffic": traffic, "traffic_unit": "bytes per launch",
-                     "traffic_source": traffic_src,
-                     "kernel": KERNEL_NAME, "launch_ms": launch_ms,
-                     "launch_ms_source": "HIP events around each launch in the timed region",
-                     "algorithmic_bytes_per_launch": 16.0 * n,
-                     "flop_per_launch": flop_launch},
-        "mode_product_ms_by_position": per_pos,
-        "matvec_ms": mv_ms,
-        "matvec_tflops": 2.0 * n * m * d / (mv_ms * 1e-3) / 1e12,
-        "matvec_hbm_gbs": mv_bytes / (mv_ms * 1e-3) / 1e9,
-        "matvec_hbm_frac": mv_bytes / (mv_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-        "iteration_algorithmic_bytes": it_bytes,
-        "iteration_hbm_gbs": it_bytes / (dt / a.steps) / 1e9,
-        "outside_mode_products_ms": 1e3 * dt / a.steps - mv_ms,
+        "roofline": roof,
     }
-    if rank == 0 and world == 1 and a.cpu_baseline == "auto":
-        del solver, y
+    result.update(extra)
+    del solver, y
+    torch.cuda.empty_cache()
+    if a.lanczos > 0:
+        result["lanczos"] = time_lanczos(K, s, a.lanczos, torch)
         torch.cuda.empty_cache()
-        result["cpu_baseline"] = cpu_baseline(m, d, s)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if a.cpu_baseline == "auto":
+        result["cpu_baseline"] = cpu_baseline(F, s, a.cpu_iters)
+    print(json.dumps(result), flush=True)
 
 
 if __name__ == "__main__":

@@ -147,6 +147,17 @@ __global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restri
   }
 }
 
+// split-K factor gemm() chooses when the workspace is not the limit
+static int splitk_factor(int M, int N, int K) {
+  if (K <= 4 * kBK) return 1;
+  const int64_t tiles = ceil_div(M, kBM) * ceil_div(N, kBN);
+  const int64_t want = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
+  const int64_t cap_k = std::max<int64_t>(1, K / (4 * kBK));
+  const int S = (int)std::min(want, std::min<int64_t>(cap_k, 64));
+  const int kchunk = (int)(ceil_div(ceil_div(std::max(K, 1), S), kBK) * kBK);
+  return (int)ceil_div(std::max(K, 1), kchunk);
+}
+
 void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, int64_t lda,
           const double* B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
           hipStream_t s, double* splitk_buf = nullptr, int64_t splitk_elems = 0) {
@@ -366,6 +377,14 @@ __global__ __launch_bounds__(1024) void colsumsq_kernel(int n, const double* __r
 }  // namespace gg
 
 extern "C" {
+
+int gg_gemm_splitk_elems(int M, int N, int K, int64_t* elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(elems != nullptr && M >= 0 && N >= 0 && K >= 0, GG_ERR_VALUE, "bad argument");
+    const int S = (M > 0 && N > 0) ? gg::splitk_factor(M, N, K) : 1;
+    *elems = S > 1 ? (int64_t)S * M * N : 0;
+  });
+}
 
 int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const double* A_dev,
             int64_t lda, const double* B_dev, int64_t ldb, double beta, double* C_dev,

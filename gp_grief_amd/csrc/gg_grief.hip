@@ -143,6 +143,36 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
   }
 }
 
+// expand_SKC (tensors.py:97-128) for caller-supplied unique rows: X holds the
+// U selected rows x_unique_f = (K_f)[unique_f] . C_f of every factor stacked
+// (U x n row-major), cidx the p x d row index c_jf = row0_f + inverse_f[j].
+// logged: out = sum_f log|X[c_jf]| (zeros count as log 1), sign = prod_f
+// sign(X[c_jf]) (taken before the zeros are replaced); else out = prod_f X.
+// Lanes run over data points a: every load and store is a coalesced row run.
+__global__ __launch_bounds__(256) void expand_skc_kernel(const double* __restrict__ X,
+                                                         int64_t n,
+                                                         const int* __restrict__ cidx, int d,
+                                                         int p, int logged,
+                                                         double* __restrict__ out,
+                                                         int* __restrict__ sign) {
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y;
+  if (a >= n || j >= p) return;
+  double acc = logged ? 0.0 : 1.0;
+  int sg = 1;
+  for (int f = 0; f < d; ++f) {
+    const double v = X[(int64_t)cidx[(int64_t)j * d + f] * n + a];
+    if (logged) {
+      sg *= v > 0.0 ? 1 : (v < 0.0 ? -1 : 0);
+      acc += log(fabs(v == 0.0 ? 1.0 : v));
+    } else {
+      acc *= v;
+    }
+  }
+  out[(int64_t)j * n + a] = acc;
+  if (logged) sign[(int64_t)j * n + a] = sg;
+}
+
 }  // namespace gg
 
 extern "C" {
@@ -203,6 +233,20 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
     hipLaunchKernelGGL(gg::grief_phi_kernel, grid, dim3(gg::kPhiCols), lds,
                        gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
                        log_lam_dev, p, transposed, phi_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_expand_skc(const double* x_dev, int U, int64_t n, const int* cidx_dev, int d, int p,
+                  int logged, double* out_dev, int* sign_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(x_dev && cidx_dev && out_dev && (!logged || sign_dev), GG_ERR_VALUE, "NULL");
+    GG_REQUIRE(U >= 1 && d >= 1 && p >= 0 && n >= 0 && p < 65536, GG_ERR_VALUE,
+               "bad expand_SKC geometry");
+    if (n == 0 || p == 0) return;
+    dim3 grid((unsigned)gg::ceil_div(n, 256), (unsigned)p);
+    hipLaunchKernelGGL(gg::expand_skc_kernel, grid, dim3(256), 0, gg::as_stream(stream), x_dev,
+                       n, cidx_dev, d, p, logged, out_dev, sign_dev);
     GG_LAUNCH_CHECK();
   });
 }

@@ -78,6 +78,8 @@ struct CgScalars {
   int first;        // 1 = next p-update is p = r
   int pending;      // fused CG: x += alpha p, r -= alpha q not yet applied
   double rq, qq;    // fused CG: r.q and q.q of the last matvec
+  int repair;       // fused CG: |r - alpha q|^2 cancelled; apply x / r and take the
+                    // textbook beta before the next matvec
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
@@ -103,6 +105,12 @@ struct MpFuse {
   // partial arrays are pstride apart
   const double* er = nullptr;
   int64_t pstride = 0;
+  // fusion layouts 1 / 2 (gg_vec.hip, CG fusion): the prologue does not store
+  // p_new; the last mode product's epilogue reads p_old (its xs operand) and
+  // recomputes p_new = r + beta p_old (bitwise the prologue's value), stores it
+  // to ep_out, and (layout 2) applies x += alpha p_old to ex when pending
+  double* ep_out = nullptr;
+  double* ex = nullptr;
 };
 
 // Output address map of a mode product (see gg_kron.hip epilogue):

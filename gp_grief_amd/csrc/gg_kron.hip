@@ -117,12 +117,21 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
         om.peers[dest][om.self_off + rowoff[r] + co] = acc[t][r];
       }
     }
+    // the stores went to other GPUs' HBM over xGMI: release them at system
+    // scope before the kernel ends, so the stream-ordered barrier that follows
+    // (an RCCL all-reduce) cannot overtake them
+    __threadfence_system();
     return;
   }
   double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
   const double* __restrict__ er = fz.er;
-  constexpr bool edots = kEpi == 2;
-  constexpr int kEB = edots ? (kBatch < 2 ? kBatch : 2) : kBatch;
+  // kEpi 2: fused-CG epilogue (p.q, r.q, q.q) of fusion layout 0; 4: layout 1
+  // (p_new recomputed from p_old and r, and stored); 3: layout 2 (also the x
+  // update: one more operand per element, so one tile per load batch)
+  constexpr bool edots = kEpi >= 2;
+  constexpr bool kRecomp = kEpi == 3 || kEpi == 4;
+  constexpr bool kXUpd = kEpi == 3;
+  constexpr int kEB = kRecomp ? 1 : edots ? (kBatch < 2 ? kBatch : 2) : kBatch;
   if (kWide && kIdent && xs == nullptr && (p & 1) == 0 &&
       (reinterpret_cast<uintptr_t>(Y) & 15) == 0) {
     const bool odd = (col & 1) != 0;
@@ -150,11 +159,19 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
         if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
     }
   } else {
+    // fusion layouts 1 / 2: p_new recomputed here from p_old (xs) and r
+    double* __restrict__ ep_out = kRecomp ? fz.ep_out : nullptr;
+    const bool recompute = kRecomp;
+    double* __restrict__ ex =
+        (kXUpd && recompute && fz.ex != nullptr && fz.sc->pending) ? fz.ex : nullptr;
+    const bool first = recompute && fz.sc->first != 0;
+    const double beta = recompute ? fz.sc->beta : 0.0;
+    const double alpha = ex != nullptr ? fz.sc->alpha : 0.0;
     // batch the x loads so that CDNA4's in-order vmcnt (stores count too)
     // does not serialise one load round trip per output element
 #pragma unroll
     for (int t0 = 0; t0 < JT; t0 += kEB) {
-      double xv[kEB][4], ev[kEB][4];
+      double xv[kEB][4], ev[kEB][4], wv[kXUpd ? kEB : 1][4];
 #pragma unroll
       for (int tb = 0; tb < kEB; ++tb) {
         const int t = t0 + tb < JT ? t0 + tb : JT - 1;
@@ -165,6 +182,7 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
           const bool ok = rowok[r] && cok;
           xv[tb][r] = ok ? xs[rowoff[r] + co] : 0.0;
           ev[tb][r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+          if (kXUpd) wv[kXUpd ? tb : 0][r] = (ok && ex != nullptr) ? ex[rowoff[r] + co] : 0.0;
         }
       }
 #pragma unroll
@@ -176,13 +194,18 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             if (rowok[r] && cok) {
-              const double v = fma(shift, xv[tb][r], acc[t][r]);
-              dsum = fma(xv[tb][r], v, dsum);
+              double pv = xv[tb][r];
+              if (recompute) pv = first ? ev[tb][r] : fma(beta, xv[tb][r], ev[tb][r]);
+              const double v = fma(shift, pv, acc[t][r]);
+              dsum = fma(pv, v, dsum);
               if (edots) {
                 rqsum = fma(ev[tb][r], v, rqsum);
                 qqsum = fma(v, v, qqsum);
               }
               Y[rowoff[r] + co] = v;
+              if (recompute) ep_out[rowoff[r] + co] = pv;
+              if (kXUpd && ex != nullptr)
+                ex[rowoff[r] + co] = wv[kXUpd ? tb : 0][r] + alpha * xv[tb][r];
             }
           }
         }
@@ -403,7 +426,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
           }                                                                           \
         }                                                                             \
         v_ = cg_first ? r_ : fma(cg_beta, v_, r_);                                    \
-        if (ok_ && hp == 0) Pout[e_] = v_;                                            \
+        if (Pout != nullptr && ok_ && hp == 0) Pout[e_] = v_;                         \
       }                                                                               \
       a[s_] = ok_ ? v_ : 0.0;                                                         \
     }                                                                                 \
@@ -697,6 +720,8 @@ static ModeConfig config_for(int variant, int cgp) {
   if (cgp == 2) return cfg<JT, 4, 3, 2, 3, 1, 2>();
   if (cgp == 3) return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
   if (cgp == 4) return cfg<JT, 4, 3, 0, 3, 1, 2, 1>();
+  if (cgp == 5) return cfg<JT, 4, 3, 0, 3, 1, 2, 3>();
+  if (cgp == 6) return cfg<JT, 4, 3, 0, 3, 1, 2, 4>();
   switch (variant) {
     case 1: return cfg<JT, 12, 4, 0, 3, 1, 2>();
     case 2: return cfg<JT, 12, 4, 0, 3, 1, 0>();  // register-staged factor chunks
@@ -829,6 +854,8 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   if (cg == nullptr) cgp = 0;
   const int d = (int)fs.size();
   GG_REQUIRE(cgp != 2 || d >= 2, GG_ERR_VALUE, "the fused CG recurrence needs d >= 2");
+  GG_REQUIRE(cgp != 2 || cg->ep_out == nullptr || (cg->p_out == nullptr && fs[0].JT <= kMaxJT),
+             GG_ERR_VALUE, "fusion layouts 1 / 2 need one launch for the first factor");
   int64_t size = n_in;
   const double* src = x;
   int64_t np_total = 0;
@@ -856,12 +883,13 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // step 0; the later launches of that step read the updated p
         const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? cgp : 0;
         const bool epi = cgp == 2 && last && dot_partials != nullptr;
-        const bool side = cgp == 2 && k == 1 && jt0 == 0;
-        ModeConfig mc = select_kernel(jt, variant, epi ? 3 : side ? 4 : pro);
+        const bool side = cgp == 2 && k == 1 && jt0 == 0 && cg->sx != nullptr;
+        const int epi_kind = !epi ? 0 : cg->ep_out == nullptr ? 3 : cg->ex != nullptr ? 5 : 6;
+        ModeConfig mc = select_kernel(jt, variant, epi ? epi_kind : side ? 4 : pro);
         const bool with_xs = last && (shift != 0.0 || dot_partials != nullptr);
         if (mc.glds && (M % 2 != 0 || M < 2 || (reinterpret_cast<uintptr_t>(step_src) & 15) ||
                         with_xs))
-          mc = select_kernel(jt, 0, epi ? 3 : side ? 4 : pro);
+          mc = select_kernel(jt, 0, epi ? epi_kind : side ? 4 : pro);
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         if (pro) {
@@ -887,6 +915,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           if (cgp == 2) {
             fz.er = cg->er;
             fz.pstride = cg->pstride;
+            fz.ep_out = cg->ep_out;   // fusion layouts 1 / 2
+            fz.ex = cg->ex;
+            fz.sc = cg->sc;
           }
         }
         int64_t grid = nblk;
@@ -894,11 +925,12 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
                            mode_lds_bytes(mc), stream, step_src, dst, f.frag, M, (int)f.q,
                            (int)f.p, f.KS, f.JT, jt0,
-                           last && (shift != 0.0 || parts) ? (cgp == 2 ? cg->p_out : x)
-                                                           : nullptr,
+                           last && (shift != 0.0 || parts)
+                               ? ((cgp == 2 && cg->ep_out == nullptr) ? cg->p_out : x)
+                               : nullptr,
                            shift, parts, skip, OutMap::ident(), fz);
         GG_LAUNCH_CHECK();
-        if (pro) step_src = fz.p_out;
+        if (pro && fz.p_out != nullptr) step_src = fz.p_out;
       }
     }
     (void)out_size;
@@ -934,6 +966,9 @@ int64_t kron_work_elems(const gg_kron* K, bool transpose) {
   return square ? mx : 2 * mx;
 }
 
+// one launch covers the first (forward) mode product: fusion layouts 1 / 2
+bool kron_first_single_launch(const gg_kron* K) { return K->fwd[0].JT <= kMaxJT; }
+
 int64_t kron_n(const gg_kron* K) { return K->n_rows; }
 int kron_d(const gg_kron* K) { return K->d; }
 
@@ -942,7 +977,7 @@ static void set_lds_limits() {
   if (done) return;
   for (int v = 0; v < kNumVariants; ++v)
     for (int jt = 1; jt <= kMaxJT; ++jt)
-      for (int cgp = 0; cgp < 5; ++cgp) {
+      for (int cgp = 0; cgp < 7; ++cgp) {
         const ModeConfig mc = select_kernel(jt, v, cgp);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -22,6 +22,7 @@ int64_t kron_prologue_blocks(const gg_kron* K);
 int64_t kron_work_elems(const gg_kron* K, bool transpose);
 int64_t kron_n(const gg_kron* K);
 int kron_d(const gg_kron* K);
+bool kron_first_single_launch(const gg_kron* K);
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -120,7 +121,10 @@ __global__ __launch_bounds__(kVecThreads) void cg_xr_update_kernel(
     double* __restrict__ x, double* __restrict__ r, const double* __restrict__ p,
     const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
     double* __restrict__ partials, int need_pending) {
+  // need_pending: 0 always, 1 only with a pending fused update, 2 only when
+  // the fused recurrence asked for a repair (cancelled beta)
   if (sc->done || (need_pending && !sc->pending)) return;
+  if (need_pending == 2 && !sc->repair) return;
   const double a = sc->alpha;
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -155,6 +159,7 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
                                                       int64_t count, CgScalars* sc,
                                                       int need_pending) {
   if (sc->done || (need_pending && !sc->pending)) return;
+  if (need_pending == 2 && !sc->repair) return;
   double acc = 0.0;
   for (int64_t i = threadIdx.x; i < count; i += blockDim.x) acc += partials[i];
   const double s = block_sum(acc);
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
     sc->iters += 1;
     sc->first = 0;
     sc->pending = 0;
+    sc->repair = 0;
     if (!(sqrt(s) >= sc->tol)) sc->done = 1;  // also stops on NaN
   }
 }
@@ -216,7 +222,11 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     sc->rq = rq;
     sc->qq = qq;
     sc->alpha = alpha;
-    sc->beta = rt > 0.0 ? rt / rho : 0.0;  // cancellation guard: restart direction
+    // |r_{j+1}|^2 from three terms of size ~rho: when it is below 1e-6 rho
+    // the expansion has lost too many digits for beta -- apply the update
+    // and take the true r.r instead (repair kernels before the next matvec)
+    sc->repair = rt < 1e-6 * rho ? 1 : 0;
+    sc->beta = sc->repair ? 0.0 : rt / rho;
     sc->first = 0;
     sc->pending = 1;
   }
@@ -236,6 +246,7 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->first = 1;
     sc->pending = 0;
     sc->alpha = sc->beta = sc->pq = sc->rq = sc->qq = 0.0;
+    sc->repair = 0;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -425,6 +436,7 @@ struct gg_cg {
   double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
   double* p2 = nullptr;        // second direction buffer (fused recurrence)
   bool fused = true;           // recurrence: fused (default) or textbook
+  int fusion = 0;              // fused layout (gg_cg_set_fusion): 0, 1 or 2
   double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
   double* rr_part = nullptr;   // device, prologue r.r partials (fused)
   int64_t rr_count = 0;
@@ -664,6 +676,23 @@ int gg_cg_set_recurrence(gg_cg* cg, int fused) {
   });
 }
 
+int gg_cg_set_fusion(gg_cg* cg, int layout) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(layout >= 0 && layout <= 2, GG_ERR_VALUE, "fusion layout must be 0, 1 or 2");
+    GG_REQUIRE(layout == 0 || gg::kron_first_single_launch(cg->K), GG_ERR_VALUE,
+               "fusion layouts 1 / 2 need the first factor within one launch (<= 256 rows)");
+    cg->fusion = layout;
+  });
+}
+
+int gg_cg_get_fusion(const gg_cg* cg, int* layout) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && layout, GG_ERR_VALUE, "NULL argument");
+    *layout = cg->fusion;
+  });
+}
+
 int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
   return gg::guard([&] {
     GG_REQUIRE(cg && fused, GG_ERR_VALUE, "NULL argument");
@@ -704,13 +733,24 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         cg->events_used = need;
       }
       if (cg->fused) {
+        // repair (no-op unless the last beta cancelled): x += alpha p,
+        // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
+        // pending update
+        hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           cg->x, cg->r, cg->p, cg->q, n, cg->sc, cg->partials, 2);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                           (int64_t)nb, cg->sc, 2);
+        GG_LAUNCH_CHECK();
         gg::MpFuse fz;
         fz.r = cg->r;
         fz.q_old = cg->q;
-        fz.p_out = cg->p2;
+        fz.p_out = cg->fusion == 0 ? cg->p2 : nullptr;
+        fz.ep_out = cg->fusion == 0 ? nullptr : cg->p2;
+        fz.ex = cg->fusion == 2 ? cg->x : nullptr;
         fz.sc = cg->sc;
         fz.rr_part = cg->rr_part;
-        fz.sx = cg->x;
+        fz.sx = cg->fusion == 2 ? nullptr : cg->x;
         fz.sp = cg->p;
         fz.sn = n;
         fz.er = cg->r;

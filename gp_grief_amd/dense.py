@@ -30,8 +30,12 @@ def matmul(A, B, ta=False, tb=False, alpha=1.0, beta=0.0, C=None, uplo=0, splitk
     work = None
     welems = 0
     if splitk and K >= 4096 and M * N <= (1 << 26):
-        welems = min(64, max(1, K // 1024)) * M * N
-        work = dev.empty(welems)
+        # exactly the slabs gg_gemm will use (none when the tile grid alone
+        # fills the GPU): no oversized, never-touched workspace
+        need = ctypes.c_int64()
+        native.check(_lib().gg_gemm_splitk_elems(int(M), int(N), int(K), ctypes.byref(need)))
+        welems = need.value
+        work = dev.empty(welems) if welems > 0 else None
     native.check(_lib().gg_gemm(int(ta), int(tb), int(M), int(N), int(K), float(alpha),
                                 native.dptr(A), A.shape[1], native.dptr(B), B.shape[1],
                                 float(beta), native.dptr(C), C.shape[1], int(uplo),

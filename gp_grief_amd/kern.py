@@ -10,11 +10,13 @@
                                                            grid factors, top-p selection,
                                                            Phi built on the device)
   WEBKernel            gp_grief/kern/web_kernel.py:4-13     (weights of the WEB models)
+  RBF_RFF              gp_grief/kern/rbf_rff.py:8-54        (random Fourier features)
+  GPyKernel            gp_grief/kern/gpy_kernel.py:10-141   (only when GPy is importable)
 Parameter / constraint bookkeeping is host logic identical in behaviour to the
 reference (including the shared-kernel-object quirk of GridKernel's setter,
 grid_kernel.py:233-239).  Every covariance evaluation and the eigenfunction
-matrix Phi run on the MI355X.  GPyKernel is not provided: GPy is not part of
-this stack.
+matrix Phi run on the MI355X.  GPy is not part of this stack (SURVEY 2, row
+10): GPyKernel raises ImportError at construction unless GPy is importable.
 """
 import ctypes
 import logging
@@ -519,3 +521,102 @@ class WEBKernel(object):
         self.p = np.size(initial_weights)
         self.parameters = initial_weights
         self.constraints = ['+ve', ] * self.p
+
+
+class GPyKernel(BaseKernel):
+    """A GPy kernel behind the BaseKernel interface (gpy_kernel.py:10-141).
+
+    GPy is not part of this stack (no network, not
+    installed), so construction raises ImportError unless GPy is importable;
+    then the covariance is GPy's own (host) and composes like the reference's.
+    The in-house device kernels (RBF, Matern52, ...) cover every config."""
+
+    def __init__(self, n_dims, kernel=None, name=None, **kwargs):
+        try:
+            import GPy  # noqa: F401
+        except ImportError as exc:
+            raise ImportError("GPyKernel needs GPy, which is not installed; use the "
+                              "device kernels gp_grief.kern.RBF / Matern52 / ...") from exc
+        import GPy
+        if isinstance(kernel, str):
+            name = "GPy - " + kernel if name is None else name
+            BaseKernel.__init__(self, n_dims=n_dims, active_dims=None, name=name)
+            self.kern = getattr(GPy.kern, kernel)(input_dim=n_dims, **kwargs)
+        elif isinstance(kernel, GPy.kern.Kern):
+            name = "GPy - " + repr(kernel) if name is None else name
+            BaseKernel.__init__(self, n_dims=n_dims, active_dims=None, name=name)
+            self.kern = kernel
+        else:
+            raise TypeError("must specify kernel as str or a GPy kernel object")
+        self.constraint_list = [['+ve'] * np.size(p.values)
+                                for p in self.kern.flattened_parameters]
+
+    def cov(self, x, z=None):
+        K = self.kern.K(x, z)
+        for op, child in self._children:
+            K = K * child.cov(x, z) if op == 'mul' else K + child.cov(x, z)
+        return K
+
+    @property
+    def parameters(self):
+        parts = [np.ravel(p.values) for p in self.kern.flattened_parameters]
+        parts += [child.parameters for _, child in self._children]
+        return np.concatenate(parts, axis=0) if parts else np.array([])
+
+    @parameters.setter
+    def parameters(self, value):
+        assert isinstance(value, np.ndarray) and value.ndim == 1
+        i0 = 0
+        for p in self.kern.flattened_parameters:
+            p[:] = value[i0:i0 + np.size(p)].reshape(np.shape(p))
+            i0 += np.size(p)
+        for _, child in self._children:
+            old = child.parameters
+            child.parameters = value[i0:i0 + np.size(old)].reshape(np.shape(old))
+            i0 += np.size(old)
+
+    @property
+    def constraints(self):
+        parts = [np.ravel(c) for c in self.constraint_list]
+        parts += [child.constraints for _, child in self._children]
+        return np.concatenate(parts, axis=0) if parts else np.array([])
+
+    def fix_variance(self):
+        i_var = np.where(['variance' in p._name.lower()
+                          for p in self.kern.flattened_parameters])[0]
+        if np.size(i_var) == 0:
+            raise RuntimeError("No variance parameter found")
+        self.constraint_list[i_var[0]][0] = 'fixed'
+
+
+class RBF_RFF(object):
+    """Random Fourier features of an ARD RBF kernel (rbf_rff.py:8-54):
+    Phi(x) = [cos(x W / ell), sin(x W / ell)] / sqrt(n_rffs), W ~ N(0, 1)^(d x
+    n_rffs) drawn from numpy's global generator as the reference does.  The
+    (n x d)(d x n_rffs) product runs on FP64 MFMA; cos / sin on the device."""
+
+    def __init__(self, d, log_lengthscale=0, n_rffs=1000, dtype=np.float64, tune_len=True):
+        logger.info("initializing RBF kernel")
+        self.d = int(d)
+        self.n_rffs = int(n_rffs)
+        self.n_features = 2 * n_rffs
+        self.dtype = dtype
+        self.freq_weights = np.asarray(np.random.normal(size=(self.d, self.n_rffs), loc=0,
+                                                        scale=1.), dtype=self.dtype)
+        self.bf_scale = 1. / np.sqrt(self.n_rffs)
+        if np.size(log_lengthscale) == 1 and log_lengthscale == 0:
+            log_lengthscale = np.zeros((d, 1), dtype=self.dtype)
+        else:
+            log_lengthscale = np.asarray(log_lengthscale, dtype=self.dtype).reshape((d, 1))
+        self.log_ell = log_lengthscale
+
+    def Phi(self, x):
+        """(n, 2 n_rffs) basis matrix at the inputs x (n, d)."""
+        from . import dense
+        t = dev.torch()
+        on_dev = dev.is_device_array(x)
+        xd = dev.to_device(x).reshape(-1, self.d)
+        W = dev.to_device(self.freq_weights / np.exp(self.log_ell)).reshape(self.d, self.n_rffs)
+        F = dense.matmul(xd, W)
+        out = t.cat([t.cos(F), t.sin(F)], dim=1).mul_(self.bf_scale)
+        return out if on_dev else dev.to_host(out)

@@ -1,6 +1,7 @@
 """linalg: the reference's helpers plus the device Krylov solvers.
 
 Host utilities with the reference's behaviour (gp_grief/linalg.py):
+  solve_schur, solve_chol :10-50   (dense helpers of the reference's GPRegressionModel)
   solver_counter          :53-71   (iteration callback / best-parameter backup)
   log_kron                :74-89
   uniquetol               :92-104
@@ -36,6 +37,27 @@ class solver_counter:
             sys.stdout.flush()
         if store is not None:
             self.backup = store
+
+
+def solve_schur(Q, t, x, shift=0.0):
+    """(K + shift I) y = x for a dense K = Q diag(t) Q^T (linalg.py:10-32);
+    the Kronecker form is KronMatrix.solve_schur (device).  Dense host helper
+    of the reference's GPRegressionModel, kept for the import surface."""
+    if x.shape != (Q.shape[0], 1):
+        raise ValueError('x is the wrong shape, must be (%d,1)' % Q.shape[0])
+    y = np.dot(Q.T, x)
+    y = y / np.reshape(t + shift, y.shape)
+    return np.dot(Q, y)
+
+
+def solve_chol(U, x):
+    """y = U \\ (U^T \\ x) for an upper Cholesky factor U (linalg.py:35-50);
+    dense host helper (the models use the device gg_potrs)."""
+    from scipy.linalg import solve_triangular
+    if x.shape != (U.shape[0], 1):
+        raise ValueError('x is the wrong shape, must be (%d,1)' % U.shape[0])
+    y = solve_triangular(U, x, trans=1, lower=False, check_finite=False)
+    return solve_triangular(U, y, trans=0, lower=False, check_finite=False)
 
 
 def log_kron(a, b, a_logged=False, b_logged=False):
@@ -93,7 +115,7 @@ class KronCG(object):
     x / r update pass.  Both leave iterate() in the textbook state.
     """
 
-    def __init__(self, K, shift, recurrence="fused"):
+    def __init__(self, K, shift, recurrence="fused", fusion=None):
         from . import device as dev
         from . import native
         self.K = K
@@ -114,6 +136,10 @@ class KronCG(object):
         f = ctypes.c_int()
         native.check(L.gg_cg_get_recurrence(h, ctypes.byref(f)))
         self.recurrence = "fused" if f.value else "textbook"
+        if fusion is not None:
+            native.check(L.gg_cg_set_fusion(h, int(fusion)), "gg_cg_set_fusion")
+        native.check(L.gg_cg_get_fusion(h, ctypes.byref(f)))
+        self.fusion = f.value
         self.n = int(K.shape[0])
         self.x = None
 
@@ -168,7 +194,7 @@ class KronCG(object):
 
 
 def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None,
-       recurrence="fused"):
+       recurrence="fused", fusion=None):
     """Solve (K + shift I) x = b with CG on the device (x0 = 0).
 
     Same stopping rule and iterates as scipy.sparse.linalg.cg (recurrence:
@@ -189,7 +215,7 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         maxiter = n * 10
     if check_every is None:
         check_every = 10 if n >= 1 << 20 else 50
-    solver = KronCG(K, shift, recurrence)
+    solver = KronCG(K, shift, recurrence, fusion=fusion)
     solver.start(bd, rtol, atol)
     # one call: the library polls the device's done flag every check_every
     # iterations and stops issuing work once converged

@@ -10,6 +10,8 @@
                  Gram / Cholesky / solves / predictions
   GPwebTransformedModel  gp_grief/models/gp_web_transformed_model.py:13-127 -- thin
                  SVD of Phi on the device (Gram + Jacobi), O(p) likelihood
+  GPRegressionModel  gp_grief/models/gpr_model.py:14-127 -- dense exact GP,
+                 device covariance and Cholesky (off the GRIEF hot path)
   GPGridModel    (new, the north star's P1 model) exact or CG grid GP on a full
                  Kronecker-structured grid: KronMatrix operator, device CG /
                  exact eigen-solve, exact or Lanczos (SLQ) log det, posterior
@@ -241,6 +243,79 @@ class BaseModel(object):
         raise NotImplementedError('')
 
 
+class GPRegressionModel(BaseModel):
+    """Dense exact GP regression (gpr_model.py:14-127): the n x n covariance
+    from the kernel's device cov, a device Cholesky of K + s I, alpha, the LML
+    and predictions.  Outside the GRIEF hot path but part of
+    the reference's model surface.  The reference's 'svd' / mvn branches are
+    broken; this keeps its default 'finite_difference chol'
+    route, and compute_var='diag' returns the diagonal as intended."""
+
+    def __init__(self, X, Y, kernel, noise_var=1.):
+        super(GPRegressionModel, self).__init__()
+        assert X.ndim == 2
+        assert Y.ndim == 2
+        self.X = np.asarray(X)
+        self.Y = np.asarray(Y)
+        assert not np.any(np.isnan(Y))
+        self.num_data, self.input_dim = self.X.shape
+        if Y.shape[0] != self.num_data:
+            raise ValueError('X and Y sizes are inconsistent')
+        self.output_dim = self.Y.shape[1]
+        if self.output_dim != 1:
+            raise RuntimeError('this only deals with 1 response for now')
+        assert isinstance(kernel, BaseKernel)
+        self.kern = kernel
+        self.noise_var = np.float64(noise_var)
+        self.grad_method = 'finite_difference chol'
+        self.dependent_attributes = list(self.dependent_attributes) + ['_chol']
+        self._chol = None
+
+    def _cov_dev(self, x, z=None):
+        xd = dev.to_device(x).reshape(np.shape(x))
+        zd = None if z is None else dev.to_device(z).reshape(np.shape(z))
+        return self.kern.cov(xd, zd)
+
+    def _factor(self):
+        if self._chol is None:
+            K = self._cov_dev(self.X)
+            self._chol = dense.Cholesky(dense.add_diag(K, float(self.noise_var)))
+        return self._chol
+
+    def fit(self):
+        self.parameters
+        if self._alpha is None:
+            self._alpha = self._factor().solve(dev.to_device(self.Y[:, 0]), which=3)
+
+    def predict(self, Xnew, compute_var=None):
+        """Yhat (M,1), and with compute_var 'diag' (M,1) / 'full' (M,M) the
+        predictive covariance k** + s I - k*^T (K + s I)^-1 k*."""
+        assert Xnew.ndim == 2
+        assert Xnew.shape[1] == self.input_dim
+        self.parameters
+        self.fit()
+        Khat = self._cov_dev(Xnew, self.X)                         # M x n
+        yhat = dense.matvec(Khat, self._alpha)
+        if compute_var is None:
+            return dense.host(yhat).reshape((-1, 1))
+        if compute_var not in ('diag', 'full'):
+            raise ValueError('Unknown compute_var = %s' % repr(compute_var))
+        V = self._factor().solve(Khat.t().contiguous(), which=1)  # L^-1 k*  (n x M)
+        var = dense.matmul(V, V, ta=True, alpha=-1.0, beta=1.0,
+                           C=dense.add_diag(self._cov_dev(Xnew), float(self.noise_var)))
+        var = dense.host(var)
+        if compute_var == 'diag':
+            var = np.diag(var).reshape((-1, 1))
+        return dense.host(yhat).reshape((-1, 1)), var
+
+    def _compute_log_likelihood(self, parameters):
+        self.parameters = parameters
+        self.fit()
+        yd = dev.to_device(self.Y[:, 0])
+        return -0.5 * (dense.dot(yd, self._alpha) + self._factor().logdet
+                       + self.num_data * np.log(np.pi * 2))
+
+
 def _dev_2d(x):
     xd = dev.to_device(x)
     shape = tuple(x.shape)
@@ -260,9 +335,19 @@ class GPGriefModel(BaseModel):
     Phi^T Phi, the p-vector Phi^T v of every solve / prediction, and the
     scalars y.alpha, alpha.alpha and n.  The p x p Cholesky is replicated.
     Results are the unsharded model's on the concatenated data, on every rank.
+
+    p_solver (new): how the Woodbury p-system P z = Phi^T v (P = A + diag(s/w),
+    gp_grief_model.py:228-235) is solved.  'chol' (default, the reference's
+    cho_solve): the p x p Gram and its Cholesky.  'cg': Jacobi-preconditioned
+    CG whose operator P v = sum_g Phi_g^T (Phi_g v) + (s/w) v is two device
+    GEMVs over the local rows and ONE all-reduce of p doubles per iteration
+    (the "RCCL all-reduce CG" of config C5) -- no Gram, no
+    factorisation for alpha and the predictive mean.  The log det (LML) and
+    the predictive covariance still need P's Cholesky and build it on demand.
     """
 
-    def __init__(self, X, Y, kern, noise_var=1., comm=None):
+    def __init__(self, X, Y, kern, noise_var=1., comm=None, p_solver='chol', cg_rtol=1e-12,
+                 cg_maxiter=None):
         super(GPGriefModel, self).__init__()
         assert X.ndim == 2
         assert Y.ndim == 2
@@ -301,6 +386,16 @@ class GPGriefModel(BaseModel):
             self.grad_method = ['adjoint', 'finite_difference'][0]
         self._Yd = None
         self._gram_uplo = 1   # A = Phi^T Phi is formed in its lower triangle only
+        if p_solver not in ('chol', 'cg'):
+            raise ValueError("p_solver must be 'chol' or 'cg'")
+        self.p_solver = p_solver
+        self.cg_rtol = float(cg_rtol)
+        self.cg_maxiter = cg_maxiter
+        self.cg_iters = []    # p-system CG iteration counts of the solves so far
+        self._Adiag = None
+        if self.kern.opt_kernel_params:
+            self.dependent_attributes = np.unique(np.concatenate(
+                (self.dependent_attributes, ['_Adiag'])))
 
     # ---- global sums over the data-row shards (identity without comm)
     def _sum(self, t):
@@ -324,7 +419,10 @@ class GPGriefModel(BaseModel):
         self.parameters
         if self._alpha is not None:
             return
-        self._cov_setup()
+        if self.p_solver == 'chol':
+            self._cov_setup()
+        else:
+            self._phi_setup()
         self._alpha = self._mv_cov_inv_dev(self._y_dev())
 
     def predict_precompute(self, Xnew):
@@ -345,6 +443,7 @@ class GPGriefModel(BaseModel):
             self._X_last_pred = Xnew
         PhiT = self._Phi_last_pred
         yhat = dense.matvec(PhiT, self._alpha_p, trans=True)
+        self._cov_setup()
         V = self._Pchol.solve(PhiT, which=1)                  # L^-1 Phi*^T  (p x M)
         var = dense.matmul(V, V, ta=True, alpha=float(self.noise_var))
         var = dense.add_diag(var, float(self.noise_var))
@@ -353,12 +452,18 @@ class GPGriefModel(BaseModel):
     def d_Yhat_d_x(self, Xnew, dim):
         raise NotImplementedError  # needs GriefKernel.cov_grad (GPyKernel only)
 
+    def _phi_setup(self):
+        self._w = self.kern.w
+        if self._Phi is None:
+            self._Phi = self.kern.phi_device(self.X)          # n x p
+
     def _cov_setup(self):
         if self._P is not None:
             return
         self._w = self.kern.w
         if self._A is None:
-            self._Phi = self.kern.phi_device(self.X)          # n x p
+            if self._Phi is None:
+                self._Phi = self.kern.phi_device(self.X)      # n x p
             self._A = self._gram()
         wd = dev.to_device(np.asarray(self._w, dtype=np.float64))
         self._P = dense.add_diag(self._A, float(self.noise_var), wd)
@@ -439,10 +544,65 @@ class GPGriefModel(BaseModel):
         dense.matmul(self._Phi, t, alpha=1.0, beta=float(self.noise_var), C=out)
         return dense.host(out).reshape(np.shape(x))
 
+    # ---- the p-system by preconditioned CG (p_solver='cg')
+    def _p_matvec(self, v, dvec):
+        """P v = sum_g Phi_g^T (Phi_g v) + (s / w) v: two local GEMVs and one
+        all-reduce of the p-vector."""
+        u = self._sum(dense.matvec(self._Phi, dense.matvec(self._Phi, v), trans=True))
+        dv = dense.scale_rows(v.clone(), dvec, 0)
+        return dense.axpby(1.0, dv, 1.0, u)
+
+    def _jacobi_diag(self, dvec):
+        """diag(P) = column sums of squares of Phi (all ranks) + s / w."""
+        if self._Adiag is None:
+            sq = dense.scale_rows(self._Phi.clone(), None, 2)
+            ones = dev.torch().ones(int(sq.shape[0]), dtype=sq.dtype, device=sq.device)
+            self._Adiag = self._sum(dense.matvec(sq, ones, trans=True))
+            del sq
+        return dense.axpby(1.0, dvec, 1.0, self._Adiag.clone())
+
+    def solve_p_cg(self, b, rtol=None, maxiter=None):
+        """z = P^-1 b by Jacobi-preconditioned CG (b: device p-vector, the
+        same on every rank).  Stops when ||b - P z|| <= rtol ||b||
+        (recursive residual); every p-sized scalar and vector stays replicated,
+        so the only communication is the operator's all-reduce."""
+        rtol = self.cg_rtol if rtol is None else float(rtol)
+        p = int(b.numel())
+        maxiter = (self.cg_maxiter or 10 * p) if maxiter is None else int(maxiter)
+        dvec = dev.to_device(float(self.noise_var) / np.asarray(self._w, dtype=np.float64))
+        minv = self._jacobi_diag(dvec)
+        x = dev.zeros(p)
+        r = b.clone()
+        bnorm = np.sqrt(dense.dot(b, b))
+        if bnorm == 0.0:
+            self.cg_iters.append(0)
+            return x
+        z = dense.scale_rows(r.clone(), minv, 1)
+        d = z.clone()
+        rz = dense.dot(r, z)
+        it = 0
+        while it < maxiter:
+            q = self._p_matvec(d, dvec)
+            alpha = rz / dense.dot(d, q)
+            dense.axpby(alpha, d, 1.0, x)
+            dense.axpby(-alpha, q, 1.0, r)
+            it += 1
+            if np.sqrt(dense.dot(r, r)) <= rtol * bnorm:
+                break
+            z = dense.scale_rows(r.clone(), minv, 1)
+            rz_new = dense.dot(r, z)
+            dense.axpby(1.0, z, rz_new / rz, d)
+            rz = rz_new
+        self.cg_iters.append(it)
+        return x
+
     def _mv_cov_inv_dev(self, xd):
         """(x - Phi P^-1 Phi^T x) / s for a 1-D device vector."""
         t = self._sum(dense.matvec(self._Phi, xd, trans=True))
-        t = self._Pchol.solve(t, which=3)
+        if self.p_solver == 'cg':
+            t = self.solve_p_cg(t)
+        else:
+            t = self._Pchol.solve(t, which=3)
         out = xd.clone()
         dense.matvec(self._Phi, t, alpha=-1.0, beta=1.0, y=out)
         dense.axpby(0.0, out, 1.0 / float(self.noise_var), out)
@@ -451,7 +611,8 @@ class GPGriefModel(BaseModel):
     def _mv_cov_inv(self, x):
         """(x - Phi cho_solve(P, Phi^T x)) / s (:228-235)."""
         assert x.shape[0] == self._n_local
-        assert self._Pchol is not None, "cov has not been setup"
+        assert self._Phi is not None, "cov has not been setup"
+        self._cov_setup()
         xd = _dev_2d(x)
         t = self._sum(dense.matmul(self._Phi, xd, ta=True))
         t = self._Pchol.solve(t, which=3)
@@ -463,7 +624,8 @@ class GPGriefModel(BaseModel):
 
     def _cov_log_det(self):
         """2 sum log diag chol(P) + sum log w + (n - p) log s (:238-245)."""
-        assert self._Pchol is not None, "cov has not been setup"
+        assert self._Phi is not None or self._P is not None, "cov has not been setup"
+        self._cov_setup()
         return (self._Pchol.logdet + np.sum(np.log(self._w))
                 + float(self.num_data - self.kern.n_eigs) * np.log(self.noise_var))
 
@@ -770,7 +932,14 @@ class GPwebTransformedModel(BaseModel):
         order = np.argsort(-lam, kind='stable')
         lam, V = lam[order], V[:, order]
         sv = np.sqrt(np.maximum(lam, 0.0))
-        ikeep = sv > 1e-7
+        # The reference keeps LAPACK singular values above 1e-7 (at most
+        # min(n, p) of them).  Gram eigenvalues carry an absolute error of
+        # ~eps * s_max^2, so null directions surface as ~sqrt(eps) * s_max
+        # "singular values": drop eigenvalues under the Gram's own rounding
+        # floor, and never keep more than min(n, p_orig) bases.
+        floor = max(self.n, self.p_orig) * np.finfo(np.float64).eps * max(float(lam[0]), 0.0)
+        ikeep = (sv > 1e-7) & (lam > floor)
+        ikeep &= np.arange(lam.size) < min(self.n, self.p_orig)
         self.singular_vals = sv[ikeep]
         self.V = np.ascontiguousarray(V[:, ikeep])
         self.p = int(self.singular_vals.size)

@@ -56,6 +56,8 @@ SIGNATURES = {
     "gg_cg_iterate": [_vp, ctypes.c_int, ctypes.c_int, _vp],
     "gg_cg_set_recurrence": [_vp, ctypes.c_int],
     "gg_cg_get_recurrence": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_set_fusion": [_vp, ctypes.c_int],
+    "gg_cg_get_fusion": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
     "gg_cg_profile": [_vp, ctypes.c_int],
@@ -82,6 +84,9 @@ SIGNATURES = {
     "gg_gemm": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                 ctypes.c_double, _c_dp, ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_double,
                 _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
+    "gg_gemm_splitk_elems": [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64p],
+    "gg_expand_skc": [_c_dp, ctypes.c_int, ctypes.c_int64, _c_dp, ctypes.c_int, ctypes.c_int,
+                      ctypes.c_int, _c_dp, _c_dp, _vp],
     "gg_gemv": [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _c_dp,
                 ctypes.c_int64, _c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
     "gg_add_diag": [ctypes.c_int, _c_dp, ctypes.c_int64, ctypes.c_double, _c_dp, _c_dp,

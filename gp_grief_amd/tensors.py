@@ -667,3 +667,199 @@ class RowColKhatriRaoMatrixTransposed(RowColKhatriRaoMatrix):
     def T(self):
         R, C = self._untransposed
         return RowColKhatriRaoMatrix._from_blocks(R, C, self.nGb)
+
+
+# ------------------------------------------------------------ structure helpers
+# The reference's small composition classes (selection_matrix.py:6-52,
+# tensors.py:6-94, block_matrix.py:4-96).  They hold no arithmetic of their own:
+# every product is delegated to the operands (KronMatrix / KhatriRaoMatrix
+# products run on the device), so they are kept as host bookkeeping for the
+# drop-in import surface.
+
+class SelectionMatrix(object):
+    """One nonzero per row: (S x)[r] = x[idx[r]] (selection_matrix.py:6-52).
+    `indicies`: a bool mask (its True positions, in order) or (int_idx, size)."""
+    ndim = 2
+
+    def __init__(self, indicies):
+        if isinstance(indicies, tuple):
+            assert len(indicies) == 2
+            assert indicies[0].ndim == 1
+            self.shape = [indicies[0].size, indicies[1]]
+            self.idx = np.asarray(indicies[0], dtype=np.int64)
+        else:
+            assert indicies.ndim == 1
+            assert indicies.dtype == bool
+            self.shape = [int(np.count_nonzero(indicies)), indicies.size]
+            self.idx = np.nonzero(indicies)[0]
+
+    def mul(self, x):
+        return x[self.idx]
+
+    def mul_T(self, x):
+        """S^T x: scatter-add of the rows of x into a zero (size, ...) array."""
+        if dev.is_device_array(x):
+            t = dev.torch()
+            out = t.zeros((self.shape[1],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            return out.index_add_(0, t.as_tensor(self.idx, device=x.device), x)
+        out = np.zeros((self.shape[1],) + np.shape(x)[1:], dtype=np.result_type(x))
+        np.add.at(out, self.idx, x)
+        return out
+
+
+class Array(object):
+    """Wraps a plain matrix so it composes with the tensor classes (tensors.py:77-94)."""
+
+    def __init__(self, A):
+        self.A = A
+        self.shape = A.shape
+
+    def __mul__(self, x):
+        return self.A.dot(x)
+
+    @property
+    def T(self):
+        return Array(self.A.T)
+
+    def expand(self):
+        return self.A
+
+
+class TensorProduct(object):
+    """(T_0 T_1 ... T_{k-1}) x applied right to left, never expanded (tensors.py:6-38)."""
+
+    def __init__(self, tensor_list):
+        self.tensors = tensor_list
+        self.n_tensors = len(tensor_list)
+        self.shape = (self.tensors[0].shape[0], self.tensors[-1].shape[1])
+        for a, b in zip(self.tensors[:-1], self.tensors[1:]):
+            assert a.shape[1] == b.shape[0]
+
+    @property
+    def T(self):
+        raise NotImplementedError('easy to do this')
+
+    def __mul__(self, x):
+        assert x.shape == (self.shape[1], 1), "vector is wrong shape"
+        for T in reversed(self.tensors):
+            x = T * x
+        return x
+
+
+class TensorSum(object):
+    """(T_0 + ... + T_{k-1}) x without expansion (tensors.py:41-74)."""
+
+    def __init__(self, tensor_list):
+        self.tensors = tensor_list
+        self.n_tensors = len(tensor_list)
+        self.shape = self.tensors[0].shape
+        for a in self.tensors[1:]:
+            assert np.array_equal(np.asarray(a.shape), np.asarray(self.shape))
+
+    @property
+    def T(self):
+        raise NotImplementedError('easy to do this')
+
+    def __mul__(self, x):
+        assert x.shape == (self.shape[1], 1), "vector is wrong shape"
+        y = None
+        for T in self.tensors:
+            v = T * x
+            y = v if y is None else y + v
+        return y
+
+
+class BlockMatrix(object):
+    """Matrix of blocks; products block row by block row (block_matrix.py:4-96).
+    A: 2-D object array of blocks with shape, __mul__, T and expand."""
+
+    def __init__(self, A):
+        assert A.ndim == 2, 'A must be 2d'
+        self.A = A
+        self.block_shape = A.shape
+        self._partition_shape = ([int(b.shape[0]) for b in A[:, 0]],
+                                 [int(b.shape[1]) for b in A[0, :]])
+        self.shape = tuple(int(np.sum(s)) for s in self._partition_shape)
+        for i in range(self.block_shape[0]):
+            for j in range(self.block_shape[1]):
+                assert tuple(A[i, j].shape) == self.partition_shape(i, j), \
+                    "A[%d,%d].shape should be %s, not %s" % (
+                        i, j, repr(self.partition_shape(i, j)), repr(A[i, j].shape))
+        self.vec_split = np.cumsum([0] + self._partition_shape[1], dtype='i')
+
+    def partition_shape(self, i, j):
+        return (self._partition_shape[0][i], self._partition_shape[1][j])
+
+    def __mul__(self, x):
+        assert x.shape == (self.shape[1], 1)
+        cut = self.vec_split
+        xs = [x[cut[j]:cut[j + 1]] for j in range(self.block_shape[1])]
+        rows = []
+        for i in range(self.block_shape[0]):
+            acc = None
+            for j in range(self.block_shape[1]):
+                v = self.A[i, j] * xs[j]
+                acc = v if acc is None else acc + v
+            rows.append(acc)
+        if dev.is_device_array(rows[0]):
+            return dev.torch().cat(rows, 0)
+        return np.concatenate(rows, axis=0)
+
+    def transpose(self):
+        At = np.empty(self.block_shape[::-1], dtype=object)
+        for i in range(self.block_shape[0]):
+            for j in range(self.block_shape[1]):
+                At[j, i] = self.A[i, j].T
+        return self.__class__(A=At)
+    T = property(transpose)
+
+    def expand(self):
+        out = np.zeros(self.shape)
+        rs = np.cumsum([0] + self._partition_shape[0])
+        cs = np.cumsum([0] + self._partition_shape[1])
+        for i in range(self.block_shape[0]):
+            for j in range(self.block_shape[1]):
+                out[rs[i]:rs[i + 1], cs[j]:cs[j + 1]] = self.A[i, j].expand()
+        return out
+
+
+def expand_SKC(S, K, C, logged=True):
+    """Rows of (selection Khatri-Rao) x (Kronecker) x (column Khatri-Rao), the
+    GRIEF eigenfunction core (tensors.py:97-128).
+
+    S: list of SelectionMatrixSparse (p rows each); K: list of m_i x m_i (the
+    grid eigenvector factors transposed); C: list of m_i x n cross covariances.
+    Per factor only the unique selected rows are formed, X_i = K_i[unique_i] C_i
+    (FP64 MFMA GEMM), then one device pass gathers them through the inverse
+    indices into the p x n result: (sum log|X|, prod sign) with the sign taken
+    before zeros are replaced (logged), or prod X.  numpy in -> numpy out;
+    CUDA tensors stay on the device.
+    """
+    from . import dense
+    assert isinstance(S, (list, np.ndarray))
+    assert isinstance(S[0], SelectionMatrixSparse)
+    assert isinstance(K, (list, np.ndarray))
+    assert isinstance(C, (list, np.ndarray))
+    t = dev.torch()
+    on_dev = dev.is_device_array(C[0])
+    rows, cols, row0 = [], [], 0
+    for s, k, c in zip(S, K, C):
+        kd = _dev_rows(k)[t.as_tensor(s.unique, device=dev.device())]
+        rows.append(dense.matmul(kd, _dev_rows(c)))               # u_i x n
+        cols.append(row0 + np.asarray(s.unique_inverse, dtype=np.int64).reshape(-1))
+        row0 += int(np.size(s.unique))
+    X = t.cat(rows, 0).contiguous()
+    n = int(X.shape[1])
+    p = int(np.size(cols[0]))
+    d = len(cols)
+    cidx = t.as_tensor(np.stack(cols, axis=1).astype(np.int32), device=X.device).contiguous()
+    out = dev.empty(p * n)
+    sign = t.empty(p * n, dtype=t.int32, device=X.device) if logged else None
+    native.check(native.lib().gg_expand_skc(
+        native.dptr(X), row0, n, native.dptr(cidx), d, p, int(bool(logged)), native.dptr(out),
+        native.dptr(sign) if logged else None, native.stream_ptr()), "gg_expand_skc")
+    out = out.reshape(p, n)
+    if logged:
+        sign = sign.reshape(p, n)
+        return (out, sign) if on_dev else (dev.to_host(out), dev.to_host(sign))
+    return out if on_dev else dev.to_host(out)

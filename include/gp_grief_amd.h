@@ -109,6 +109,15 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
                 gg_stream stream);
 int gg_cg_set_recurrence(gg_cg* cg, int fused);
 int gg_cg_get_recurrence(const gg_cg* cg, int* fused);
+/* Where the fused recurrence's vector passes ride (any time; same iterates):
+ *   0: prologue writes r and p_new (first mode product), x update after the
+ *      second mode product, epilogue reads p_new and r;
+ *   1: the epilogue (last mode product) recomputes p_new = r + beta p_old and
+ *      stores it, so the prologue only writes r;
+ *   2: as 1, and the epilogue also applies x += alpha p_old (no side job).
+ * Layouts 1 / 2 need the first factor's rows within one launch (<= 256).   */
+int gg_cg_set_fusion(gg_cg* cg, int layout);
+int gg_cg_get_fusion(const gg_cg* cg, int* layout);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
@@ -165,6 +174,13 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
 int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t n,
                  const int* cidx_dev, int d, const double* log_lam_dev, int p, int transposed,
                  double* phi_dev, gg_stream stream);
+/* expand_SKC(S, K, C, logged) (gp_grief/tensors/tensors.py:97-128) from the
+ * stacked unique rows X (U x n row-major: rows row0_f .. row0_f + u_f - 1 are
+ * (K_f)[unique_f] . C_f) and cidx (p x d int32, c_jf = row0_f + inverse_f[j]):
+ * logged -> out = sum_f log|X[c_jf]| (0 for X == 0), sign_dev = prod_f sign;
+ * else out = prod_f X[c_jf].  out: p x n.                                     */
+int gg_expand_skc(const double* x_dev, int U, int64_t n, const int* cidx_dev, int d, int p,
+                  int logged, double* out_dev, int* sign_dev, gg_stream stream);
 
 /* ----------------------------------------- dense FP64 (GRIEF p x p system)
  * C = alpha op(A) op(B) + beta C on FP64 MFMA, row-major with leading dims.
@@ -174,6 +190,8 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
 int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const double* A_dev,
             int64_t lda, const double* B_dev, int64_t ldb, double beta, double* C_dev,
             int64_t ldc, int uplo, double* splitk_dev, int64_t splitk_elems, gg_stream stream);
+/* splitk_dev elements gg_gemm uses for this shape (0: it will not split K).  */
+int gg_gemm_splitk_elems(int M, int N, int K, int64_t* elems);
 /* y = alpha op(A) x + beta y, A: rows x cols row-major (Phi^T y, Phi v).    */
 int gg_gemv(int trans, int64_t rows, int cols, double alpha, const double* A_dev, int64_t lda,
             const double* x_dev, double beta, double* y_dev, double* work_dev,

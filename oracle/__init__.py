@@ -21,7 +21,7 @@ has no reference implementation at all: it is pinned only against the exact
 eigenvalue log-det (statistical tolerance), i.e. "parity unpinned" for the
 Lanczos recurrence itself.
 """
-from .kron import (kron_matvec, kron_matvec_T, kron_expand, log_kron,
+from .kron import (kron_matvec, kron_matvec_T, kron_matvec_dsymm, kron_matvec_entries, kron_expand, log_kron,
                    find_extremum_eigs, factor_eigh, solve_schur, eig_log_det,
                    logdet_shifted, grid_latent_var, kr_contract, grid_offgrid_predict,
                    rowcol_kr_expand)
@@ -33,7 +33,7 @@ from .web import (web_lml_grad, web_predict, web_transformed_setup,
                   web_transformed_lml_grad, web_transformed_predict)
 
 __all__ = [
-    "kron_matvec", "kron_matvec_T", "kron_expand", "log_kron", "find_extremum_eigs",
+    "kron_matvec", "kron_matvec_T", "kron_matvec_dsymm", "kron_matvec_entries", "kron_expand", "log_kron", "find_extremum_eigs",
     "factor_eigh", "solve_schur", "eig_log_det", "logdet_shifted", "grid_latent_var",
     "kr_contract", "grid_offgrid_predict", "rowcol_kr_expand", "cov_1d", "cg_solve", "slq_logdet", "lanczos_tridiag", "grief_inducing", "grief_phi",
     "grief_fit", "grief_lml", "grief_adjoint_grad", "grief_predict",

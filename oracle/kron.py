@@ -32,6 +32,57 @@ def kron_matvec(factors, x):
     return y
 
 
+def kron_matvec_dsymm(factors, x):
+    """y = (K_0 (x) ... (x) K_{d-1}) x for symmetric factors, in the reference's
+    own BLAS call sequence -- the CPU baseline of bench.py.
+
+    Restates the `sym` branch of KronMatrix.kronvec_prod
+    (kron_matrix.py:74-96): factors are visited last to first; each step views
+    the running vector as (m_i, N/m_i) in Fortran order (a copy whenever the
+    previous transpose left it C-ordered), applies BLAS3 dsymm with the factor
+    on the left (side=0) or, for a C-ordered operand, on the right (side=1),
+    and keeps the transposed product.  Same arithmetic as kron_matvec; the
+    point is the cost profile (F-order copies + dsymm) of the reference.
+    """
+    from scipy.linalg import blas
+    y = np.asarray(x, dtype=np.float64).reshape(-1, 1)
+    for K in reversed(list(factors)):
+        K = np.asarray(K, dtype=np.float64)
+        a = K if np.isfortran(K) else K.T     # symmetric: either is K
+        y = np.reshape(y, (K.shape[1], -1), order='F')
+        if np.isfortran(y):
+            y = blas.dsymm(1.0, a, y, side=0).T
+        else:
+            y = blas.dsymm(1.0, a, y.T, side=1)
+    return y.reshape(-1, order='F')
+
+
+def kron_matvec_entries(factors, x, idx):
+    """Selected entries (K x)[idx] of a Kronecker matvec without forming K x.
+
+    Entry i of (K_0 (x) ... (x) K_{d-1}) x is x (as the C-order tensor over the
+    factors, factor 0 slowest) contracted with row i_k of every K_k -- the
+    definition of the Kronecker product (np.kron order, kron_matrix.py:19-42).
+    Entries sharing i_0 share the first (N-flop) contraction, so a handful of
+    entries of a 200^4 product cost a few GEMVs over x.  For spot checks of a
+    full-size device matvec against the reference arithmetic.
+    """
+    F = [np.asarray(K, dtype=np.float64) for K in factors]
+    shape = [K.shape[1] for K in F]
+    X = np.asarray(x, dtype=np.float64).reshape(shape)
+    rows = [np.unravel_index(int(i), [K.shape[0] for K in F]) for i in np.ravel(idx)]
+    out = np.empty(len(rows))
+    cache = {}
+    for n, r in enumerate(rows):
+        if r[0] not in cache:
+            cache[r[0]] = np.tensordot(F[0][r[0]], X, axes=(0, 0))
+        t = cache[r[0]]
+        for k in range(1, len(F)):
+            t = np.tensordot(F[k][r[k]], t, axes=(0, 0))
+        out[n] = float(t)
+    return out
+
+
 def kron_matvec_T(factors, x):
     """(K_0 (x) ... )^T x -- KronMatrix.transpose (kron_matrix.py:203-213) then *."""
     return kron_matvec([np.asarray(k).T for k in factors], x)

@@ -174,3 +174,8 @@ def reference_factors(m, d, seed=0):
     g = np.linspace(0, 1, m)
     return [oracle.cov_1d("RBF", g, g, 1.0, 0.15 * (1 + 0.1 * k)) + 1e-12 * np.eye(m)
             for k in range(d)]
+
+
+def make_factors(m, d):
+    """bench.py's GG_BENCH_ENGINE hook: the factors of the CPU rehearsal."""
+    return reference_factors(m, d)

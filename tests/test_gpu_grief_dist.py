@@ -58,3 +58,67 @@ def test_grief_row_sharded_matches_fixture(gpu, case, world):
         assert abs(grad[0] - z["grad"][0]) < 1e-6 * abs(z["grad"][0])
     # every rank holds the same answer
     assert max(abs(r[0] - res[0][0]) for r in res) <= 1e-9 * abs(res[0][0])
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _grief_rank(rank, world, port, case, solver, out_dir):
+    """One process per rank (all on cuda:0 here; on a node, one GPU each):
+    GPGriefModel(comm=TorchExchange()) over a real torch.distributed group."""
+    import os
+    import sys
+    from conftest import ROOT
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gp_grief_amd as gg
+    import gp_grief_amd.grid  # noqa: F401
+    import gp_grief_amd.kern  # noqa: F401
+    import gp_grief_amd.models  # noqa: F401
+    from gp_grief_amd.distributed import TorchExchange
+    z = golden("grief_small_%s.npz" % case)
+    d, n = z["x"].shape[1], z["x"].shape[0]
+    kl = [getattr(gg.kern, str(z["kind"]))(1, variance=1.0, lengthscale=float(l))
+          for l in z["lengthscales"]]
+    grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, int(z["m"])).reshape(-1, 1)
+                                    for _ in range(d)])
+    kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=int(z["p"]))
+    lo, hi = np.linspace(0, n, world + 1).astype(int)[rank:rank + 2]
+    m = gg.models.GPGriefModel(z["x"][lo:hi], z["y"][lo:hi].reshape(-1, 1), kern,
+                               noise_var=float(z["sigma2"]), comm=TorchExchange(),
+                               p_solver=solver)
+    ll, grad = m.log_likelihood(return_gradient=True)
+    mean, var = m.predict(z["xtest"])
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), ll=float(ll[0, 0]), grad=grad,
+             mean=mean, var=var, n=m.num_data)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,world,solver", [("3d", 2, "chol"), ("8d", 2, "cg")])
+def test_grief_row_sharded_processes(gpu, tmp_path, case, world, solver):
+    """The sharded GRIEF fit across real processes (torch.distributed, gloo;
+    the driver's multi-GPU runs use the same code over RCCL): every rank
+    reproduces the fixture at 1e-6."""
+    import os
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.start_processes(_grief_rank, args=(world, port, case, solver, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    z = golden("grief_small_%s.npz" % case)
+    p = int(z["p"])
+    for g in range(world):
+        r = np.load(os.path.join(tmp_path, "rank%d.npz" % g))
+        assert int(r["n"]) == z["x"].shape[0]
+        assert abs(float(r["ll"]) - z["lml"]) < 1e-6 * abs(z["lml"])
+        assert rel(r["mean"][:, 0], z["pred_mean"]) < 1e-6
+        assert rel(r["var"], z["pred_var"]) < 1e-6
+        assert rel(r["grad"][-p:], z["grad"][-p:]) < 1e-6

@@ -282,6 +282,27 @@ def test_cg_fused_state_is_textbook_after_iterate(gg):
         assert abs(c.status()[2] - np.linalg.norm(r30)) < 1e-3 * np.linalg.norm(r30)
 
 
+@pytest.mark.parametrize("shift", [5.0, 200.0])
+def test_cg_fused_repair_on_large_shift(gg, shift):
+    """Well-conditioned (large-shift) systems shrink |r|^2 by far more than
+    1e-6 per step, where the expanded beta cancels: the fused recurrence then
+    takes the textbook beta (repair kernels) and keeps scipy's iteration
+    count and iterates at rtol 1e-10."""
+    F = _rbf_factors((12, 10, 8))
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = 12 * 10 * 8
+    b = np.random.default_rng(9).standard_normal((n, 1))
+    xf, inf = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, recurrence="fused")
+    itf = gg.linalg.cg.last.iters
+    xt, intb = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, recurrence="textbook")
+    itt = gg.linalg.cg.last.iters
+    xo, _, ito = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b[:, 0],
+                                 rtol=1e-10)
+    assert inf == 0 and intb == 0
+    assert itf == ito and itt == ito, (itf, itt, ito)
+    assert rel(xf, xo) < 1e-12 and rel(xt, xo) < 1e-12
+
+
 def test_cg_fused_falls_back_to_textbook(gg):
     """Odd n (no double2 side job) and d = 1 run the textbook recurrence."""
     F = _rbf_factors((13, 11, 9))
@@ -371,3 +392,43 @@ def test_grid_model_cg_and_slq(gg):
     assert abs(slq._cov_log_det() - z["logdet"]) < 1e-2 * abs(z["logdet"])
     with pytest.raises(ValueError):
         _grid_model(gg, z, solver="lu")
+
+
+@pytest.mark.parametrize("fusion", [1, 2])
+def test_cg_fusion_layouts_same_iterates(gg, fusion):
+    """Fusion layouts 1 / 2 move where the fused recurrence's vector passes ride
+    (p_new recomputed and stored by the last mode product; layout 2 also does
+    the x update there) -- the same arithmetic, so the same iterates as
+    layout 0, step for step, and the same converged solve."""
+    import torch
+    F = _rbf_factors((20, 16, 12))
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = 20 * 16 * 12
+    b = torch.tensor(np.random.default_rng(6).standard_normal(n), device="cuda")
+    s = 0.5
+    runs = []
+    for layout in (0, fusion):
+        c = gg.linalg.KronCG(K, s, fusion=layout)
+        assert c.fusion == layout
+        c.start(b, rtol=0.0)
+        for k in (5, 1, 14):          # chunked: each call closes the pending update
+            c.iterate(k)
+        runs.append((c.x.clone(), c.status()))
+    (x0, st0), (x1, st1) = runs
+    assert st0[0] == st1[0] == 20
+    assert float((x1 - x0).norm() / x0.norm()) < 1e-13
+    assert abs(st1[2] - st0[2]) <= 1e-12 * st0[2]
+    xs, info = gg.linalg.cg(K, b.cpu().numpy().reshape(-1, 1), shift=s, rtol=1e-10,
+                            fusion=fusion)
+    xo, _, ito = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + s * v,
+                                 b.cpu().numpy(), rtol=1e-10)
+    assert info == 0 and abs(gg.linalg.cg.last.iters - ito) <= max(3, 0.05 * ito)
+    assert rel(xs, xo) < 1e-8
+
+
+def test_cg_fusion_layout_needs_single_launch(gg):
+    """Layouts 1 / 2 need the first factor within one 256-column launch."""
+    F = _rbf_factors((300, 30))
+    K = gg.tensors.KronMatrix(F, sym=True)
+    with pytest.raises(ValueError):
+        gg.linalg.KronCG(K, 0.1, fusion=1)

@@ -109,3 +109,34 @@ def test_web_shape_asserts(models):
     m = models.GPwebModel(Phi=X, y=np.ones(30))
     with pytest.raises(AssertionError):
         m.predict(np.ones((3, 4)))
+
+
+@pytest.mark.parametrize("case", ["wide", "rank_deficient"])
+def test_web_transformed_basis_count_matches_lapack(models, case):
+    """The kept basis count and the LML follow the reference's LAPACK thin SVD
+    (gp_web_transformed_model.py:31-38: singular values > 1e-7, at most
+    min(n, p)) when p_orig > n and when Phi is rank deficient.  (The
+    reference's own log message for p < p_orig has a format bug and raises;
+    the arithmetic is what is compared here.)"""
+    rng = np.random.default_rng(8)
+    if case == "wide":
+        n, p = 30, 60
+        Phi = rng.standard_normal((n, p))
+    else:
+        n, p = 200, 40
+        Phi = rng.standard_normal((n, p))
+        Phi[:, 20:] = Phi[:, :20]
+    y = rng.standard_normal(n)
+    U, S, VT = np.linalg.svd(Phi, full_matrices=False)
+    keep = S > 1e-7
+    S, U = S[keep], U[:, keep]
+    m = models.GPwebTransformedModel(Phi, y, noise_var=0.3)
+    assert m.p == S.size == (30 if case == "wide" else 20)
+    np.testing.assert_allclose(m.singular_vals, S, rtol=1e-8)
+    w = np.linspace(0.5, 2.0, m.p)
+    m.kern.parameters = w
+    c2 = (U.T.dot(y)) ** 2
+    Pd = 0.3 / w + 1.0
+    ll_ref = -0.5 * (np.sum(np.log(Pd)) + np.sum(np.log(w)) + (n - m.p) * np.log(0.3)
+                     + (y.dot(y) - np.sum(c2 / Pd)) / 0.3 + n * np.log(2 * np.pi))
+    assert abs(float(np.squeeze(m.log_likelihood())) - ll_ref) < 1e-9 * abs(ll_ref)
