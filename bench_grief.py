@@ -234,7 +234,7 @@ def run_config(gg, ctx, name, repeats, cpu, with_cg, s=0.01):
         torch.cuda.empty_cache()
     best = {k: min(rr[k] for rr in runs) for k in runs[0]}
     fit_ms = sum(best[k] for k in ("setup", "phi", "gram", "reduce", "chol", "alpha"))
-    n_rank = hi - lo
+    n_rank = int(hi - lo)
     gram_flop = (1.0 if uplo else 2.0) * n_rank * p * p
     gram_tf = gram_flop / (best["gram"] * 1e-3) / 1e12
     phi_bytes = 8.0 * n_rank * p + 16.0 * n_rank * U
