@@ -15,6 +15,8 @@
 // every consumer is order-invariant).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "gg_internal.h"
@@ -186,6 +188,267 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Householder tridiagonalisation + implicit QL (the LAPACK route: sytd2 /
+// orgtr / steqr), one workgroup per matrix.  O(m^3) arithmetic in ~3m
+// barrier-separated parallel steps instead of Jacobi's ~10 sweeps x m rounds.
+//   1. for i = 0 .. m-3: Householder vector v of A[i+1:, i]; p = tau A22 v;
+//      w = p - tau/2 (p.v) v; A22 -= v w^T + w v^T (symmetric rank-2; the
+//      full square is kept).  v is stored in A[i+2:, i], tau in LDS.
+//   2. Z = H_0 ... H_{m-3}, accumulated backwards in the A storage (the
+//      diagonal d and off-diagonal e are in LDS by then).
+//   3. implicit QL with Wilkinson shifts on (d, e): one thread runs each
+//      sweep's scalar rotation chain into LDS (c, s), then every thread
+//      applies the chain to its own rows of Z (rotations act on columns).
+//   4. eigenvalues ascending by parallel rank; Q columns permuted to match.
+// A / Z live in LDS (row stride m + 1) up to kLdsMaxM, else in the HBM
+// scratch (L2-resident).
+constexpr int kTqThreads = 512;
+
+__device__ __forceinline__ double tq_block_sum(double v, double* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  __syncthreads();
+  if (lane == 0) red[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+  return s;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
+    const int64_t* __restrict__ dims, const int64_t* __restrict__ offs,
+    const double* __restrict__ Ain, double* __restrict__ Qout, double* __restrict__ lam_out,
+    const int64_t* __restrict__ lam_offs, double* __restrict__ work,
+    const int64_t* __restrict__ work_offs, int max_iter, int* __restrict__ status) {
+  const int f = blockIdx.x;
+  const int m = (int)dims[f];
+  extern __shared__ __attribute__((aligned(16))) unsigned char tq_lds[];
+  // LDS: d, e, tau, v (m each), p/w (m), cs, sn (m each), rank (m ints), red (16)
+  double* d = reinterpret_cast<double*>(tq_lds);
+  double* e = d + m;
+  double* tau = e + m;
+  double* v = tau + m;
+  double* pw = v + m;
+  double* cs = pw + m;
+  double* sn = cs + m;
+  double* red = sn + m;
+  int* rank = reinterpret_cast<int*>(red + 16);
+  __shared__ int chain_lo, chain_hi, bad;
+  const int64_t head = (((int64_t)7 * m + 16) * sizeof(double) + (int64_t)m * sizeof(int) + 15) &
+                       ~int64_t(15);
+  const int ld = kLds ? m + 1 : m;
+  double* A = kLds ? reinterpret_cast<double*>(tq_lds + head) : work + work_offs[f];
+  const double* Asrc = Ain + offs[f];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if (tid == 0) bad = 0;
+  for (int64_t i = tid; i < (int64_t)m * m; i += nt) {
+    const int r = (int)(i / m), c = (int)(i % m);
+    A[(int64_t)r * ld + c] = 0.5 * (Asrc[i] + Asrc[(int64_t)c * m + r]);
+  }
+  __syncthreads();
+
+  // ---- 1. tridiagonalisation
+  for (int i = 0; i + 2 < m; ++i) {
+    const int L = m - i - 1;             // trailing size
+    const int r0 = i + 1;
+    // Householder of x = A[r0:, i]
+    double xs = 0.0;
+    for (int t = tid; t < L - 1; t += nt) {
+      const double xv = A[(int64_t)(r0 + 1 + t) * ld + i];
+      xs = fma(xv, xv, xs);
+    }
+    const double xnorm2 = tq_block_sum(xs, red);
+    const double alpha = A[(int64_t)r0 * ld + i];
+    double ti = 0.0, beta = alpha, scal = 0.0;
+    if (xnorm2 > 0.0) {
+      beta = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+      ti = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    for (int t = tid; t < L; t += nt)
+      v[t] = (t == 0) ? 1.0 : (xnorm2 > 0.0 ? A[(int64_t)(r0 + t) * ld + i] * scal : 0.0);
+    if (tid == 0) {
+      d[i] = A[(int64_t)i * ld + i];
+      e[i] = beta;
+      tau[i] = ti;
+    }
+    __syncthreads();
+    if (ti != 0.0) {
+      // p = tau A22 v  (thread per row)
+      double pv = 0.0;
+      for (int t = tid; t < L; t += nt) {
+        const double* Ar = A + (int64_t)(r0 + t) * ld + r0;
+        double s = 0.0;
+        for (int c = 0; c < L; ++c) s = fma(Ar[c], v[c], s);
+        s *= ti;
+        pw[t] = s;
+        pv = fma(s, v[t], pv);
+      }
+      const double ptv = tq_block_sum(pv, red);
+      const double k = 0.5 * ti * ptv;
+      for (int t = tid; t < L; t += nt) pw[t] -= k * v[t];   // w
+      __syncthreads();
+      // A22 -= v w^T + w v^T
+      for (int64_t q = tid; q < (int64_t)L * L; q += nt) {
+        const int r = (int)(q / L), c = (int)(q - (int64_t)r * L);
+        double* a = A + (int64_t)(r0 + r) * ld + r0 + c;
+        *a -= v[r] * pw[c] + pw[r] * v[c];
+      }
+    }
+    // keep v (below its implicit unit head) in A[r0+1:, i] for step 2
+    for (int t = tid + 1; t < L; t += nt) A[(int64_t)(r0 + t) * ld + i] = v[t];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (m >= 2) {
+      d[m - 2] = A[(int64_t)(m - 2) * ld + (m - 2)];
+      e[m - 2] = A[(int64_t)(m - 1) * ld + (m - 2)];
+      tau[m - 2] = 0.0;
+    }
+    d[m - 1] = A[(int64_t)(m - 1) * ld + (m - 1)];
+    e[m - 1] = 0.0;
+  }
+  __syncthreads();
+
+  // ---- 2. Z = H_0 H_1 ... H_{m-3}, backwards, into the same storage.  The
+  // reflector vectors sit in the strictly-lower columns 0..m-3, below the
+  // subdiagonal; Z's block for step i touches rows/cols > i only, and column
+  // i's vector is consumed before column i is overwritten.
+  // Z starts as the identity in rows/cols >= m-2 (no reflector there).
+  for (int64_t q = tid; q < 4; q += nt) {
+    const int r = m - 2 + (int)(q / 2), c = m - 2 + (int)(q % 2);
+    if (r >= 0 && c >= 0) A[(int64_t)r * ld + c] = (r == c) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  for (int i = m - 3; i >= 0; --i) {
+    const int L = m - i - 1, r0 = i + 1;
+    for (int t = tid; t < L; t += nt) v[t] = (t == 0) ? 1.0 : A[(int64_t)(r0 + t) * ld + i];
+    __syncthreads();
+    // the block Z[r0:, r0:] so far is Z[r0+1:, r0+1:] with row/col r0 = e_r0
+    for (int t = tid; t < L; t += nt) {
+      A[(int64_t)r0 * ld + r0 + t] = (t == 0) ? 1.0 : 0.0;
+      if (t > 0) A[(int64_t)(r0 + t) * ld + r0] = 0.0;
+    }
+    __syncthreads();
+    const double ti = tau[i];
+    if (ti != 0.0) {
+      // u[c] = tau sum_r v[r] Z[r0 + r][r0 + c]  (thread per column)
+      for (int t = tid; t < L; t += nt) {
+        double s = 0.0;
+        for (int r = 0; r < L; ++r) s = fma(v[r], A[(int64_t)(r0 + r) * ld + r0 + t], s);
+        pw[t] = ti * s;
+      }
+      __syncthreads();
+      for (int64_t q = tid; q < (int64_t)L * L; q += nt) {
+        const int r = (int)(q / L), c = (int)(q - (int64_t)r * L);
+        A[(int64_t)(r0 + r) * ld + r0 + c] -= v[r] * pw[c];
+      }
+    }
+    __syncthreads();
+  }
+  // row / column 0 of Z: e_0
+  for (int t = tid; t < m; t += nt) {
+    A[t] = (t == 0) ? 1.0 : 0.0;
+    if (t > 0) A[(int64_t)t * ld] = 0.0;
+  }
+  __syncthreads();
+
+  // ---- 3. implicit QL (tql2 / tqli) on (d, e) accumulating into Z's columns
+  const double eps = 2.220446049250313e-16;
+  for (int l = 0; l < m; ++l) {
+    int iter = 0;
+    while (true) {
+      // thread 0: find the split point and run one sweep's scalar chain
+      if (tid == 0) {
+        int mm = l;
+        for (; mm < m - 1; ++mm) {
+          const double dd = fabs(d[mm]) + fabs(d[mm + 1]);
+          if (fabs(e[mm]) <= eps * dd) break;
+        }
+        chain_hi = mm;   // rotations for i = mm-1 down to chain_lo
+        chain_lo = mm;   // empty chain: converged
+        if (mm != l) {
+          if (iter >= max_iter) {
+            bad = 1;
+          } else {
+            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+            double r = hypot(g, 1.0);
+            g = d[mm] - d[l] + e[l] / (g + copysign(r, g));
+            double s = 1.0, c = 1.0, p = 0.0;
+            int i = mm - 1;
+            bool early = false;
+            for (; i >= l; --i) {
+              const double fo = s * e[i], b = c * e[i];
+              r = hypot(fo, g);
+              e[i + 1] = r;
+              if (r == 0.0) {
+                d[i + 1] -= p;
+                e[mm] = 0.0;
+                early = true;
+                break;
+              }
+              s = fo / r;
+              c = g / r;
+              g = d[i + 1] - p;
+              r = (d[i] - g) * s + 2.0 * c * b;
+              p = s * r;
+              d[i + 1] = g + p;
+              g = c * r - b;
+              cs[i] = c;
+              sn[i] = s;
+            }
+            chain_lo = early ? i + 1 : l;
+            if (!early) {
+              d[l] -= p;
+              e[l] = g;
+              e[mm] = 0.0;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int lo = chain_lo, hi = chain_hi;
+      if (bad || hi == l) break;   // failed, or d[l] has converged
+      // rotations i = hi-1 .. lo on columns (i, i+1) of every row of Z
+      for (int k = tid; k < m; k += nt) {
+        double* Zk = A + (int64_t)k * ld;
+        double cur = Zk[hi];
+        for (int i = hi - 1; i >= lo; --i) {
+          const double zi = Zk[i];
+          Zk[i + 1] = sn[i] * zi + cs[i] * cur;
+          cur = cs[i] * zi - sn[i] * cur;
+        }
+        Zk[lo] = cur;
+      }
+      __syncthreads();
+      ++iter;
+    }
+    if (bad) break;
+  }
+  __syncthreads();
+
+  // ---- 4. ascending order (parallel rank, ties by index) and output
+  for (int i = tid; i < m; i += nt) {
+    int r = 0;
+    const double di = d[i];
+    for (int j = 0; j < m; ++j) r += (d[j] < di || (d[j] == di && j < i)) ? 1 : 0;
+    rank[i] = r;
+  }
+  __syncthreads();
+  double* Q = Qout + offs[f];
+  double* lam = lam_out + lam_offs[f];
+  for (int i = tid; i < m; i += nt) lam[rank[i]] = d[i];
+  for (int64_t q = tid; q < (int64_t)m * m; q += nt) {
+    const int r = (int)(q / m), c = (int)(q % m);
+    Q[(int64_t)r * m + rank[c]] = A[(int64_t)r * ld + c];
+  }
+  if (tid == 0) status[f] = bad;
+}
+
 }  // namespace gg
 
 extern "C" {
@@ -227,17 +490,41 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     int mmax = 1;
     for (int i = 0; i < count; ++i) mmax = std::max<int>(mmax, (int)m[i]);
     const bool lds_a = mmax <= gg::kLdsMaxM;
-    const int64_t lds = gg::eig_lds_bytes(mmax, lds_a);
-    if (lds_a) {
-      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::jacobi_kernel<true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(gg::jacobi_kernel<true>, dim3(count), dim3(gg::kEigThreads), lds, s,
-                         dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
-                         work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+    // tridiagonalisation + implicit QL (default), or the round-robin Jacobi
+    // (GG_EIG=jacobi: reference implementation kept for A/B)
+    const char* ev = getenv("GG_EIG");
+    const bool jacobi = ev != nullptr && std::string(ev) == "jacobi";
+    if (!jacobi) {
+      const int64_t head = (((int64_t)7 * mmax + 16) * sizeof(double) +
+                            (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
+      const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
+      const int iters = std::max(30, max_sweeps);
+      if (lds_a) {
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(gg::tridiag_ql_kernel<true>, dim3(count), dim3(gg::kTqThreads), lds, s,
+                           dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                           work_dev, dmeta + 3 * count, iters, dstatus);
+      } else {
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<false>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(gg::tridiag_ql_kernel<false>, dim3(count), dim3(gg::kTqThreads), lds,
+                           s, dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                           work_dev, dmeta + 3 * count, iters, dstatus);
+      }
     } else {
-      hipLaunchKernelGGL(gg::jacobi_kernel<false>, dim3(count), dim3(gg::kEigThreads), lds, s,
-                         dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
-                         work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+      const int64_t lds = gg::eig_lds_bytes(mmax, lds_a);
+      if (lds_a) {
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::jacobi_kernel<true>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL(gg::jacobi_kernel<true>, dim3(count), dim3(gg::kEigThreads), lds, s,
+                           dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                           work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+      } else {
+        hipLaunchKernelGGL(gg::jacobi_kernel<false>, dim3(count), dim3(gg::kEigThreads), lds, s,
+                           dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
+                           work_dev, dmeta + 3 * count, max_sweeps, dstatus);
+      }
     }
     GG_LAUNCH_CHECK();
     std::vector<int> st(count);
@@ -246,7 +533,7 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     GG_HIP(hipStreamSynchronize(s));
     for (int i = 0; i < count; ++i)
       GG_REQUIRE(st[i] == 0, GG_ERR_LINALG,
-                 "Jacobi eigensolver did not converge on factor " + std::to_string(i));
+                 "eigensolver did not converge on factor " + std::to_string(i));
   });
 }
 

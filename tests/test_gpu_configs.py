@@ -92,7 +92,10 @@ def check_against_oracle(gg, name, n_rows):
     mean, var = mdl.predict(xt)
     ref = oracle_fit(d, m, kind, p, x, y, xt)
     assert ref["gap"] > 1e-9, "tie at the p boundary"
-    np.testing.assert_allclose(mdl.kern._log_lam, ref["log_lam"], rtol=1e-9, atol=1e-10)
+    # per-factor eigenvalues carry an absolute error ~eps ||K_f|| (LAPACK's
+    # syevd / gees and the device tridiagonal QL alike), so the log of the
+    # small factor eigenvalues inside a product is only good to ~1e-8
+    np.testing.assert_allclose(mdl.kern._log_lam, ref["log_lam"], rtol=1e-9, atol=1e-7)
     assert abs(ll[0, 0] - ref["ll"]) < 1e-6 * abs(ref["ll"])
     assert rel(alpha, ref["alpha"]) < 1e-6
     assert rel(mean[:, 0], ref["mean"]) < 1e-6
