@@ -250,6 +250,9 @@ def launch_passes(d, recurrence, fusion=0):
         passes[d - 1] += 3 if fusion else 2
         if fusion == 2:
             passes[d - 1] += 2  # x += alpha p_old in the epilogue (x read + written)
+        elif d >= 4:
+            passes[1] += 1.5    # side job x += alpha p_old, first half of x
+            passes[2] += 1.5    # ... second half (gg_kron.hip kron_apply split_side)
         else:
             passes[1] += 3      # side job: x += alpha p_old (x, p_old read; x written)
     else:

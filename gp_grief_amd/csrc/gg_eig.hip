@@ -198,9 +198,9 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
 //      full square is kept).  v is stored in A[i+2:, i], tau in LDS.
 //   2. Z = H_0 ... H_{m-3}, accumulated backwards in the A storage (the
 //      diagonal d and off-diagonal e are in LDS by then).
-//   3. implicit QL with Wilkinson shifts on (d, e): one thread runs each
-//      sweep's scalar rotation chain into LDS (c, s), then every thread
-//      applies the chain to its own rows of Z (rotations act on columns).
+//   3. implicit QL with Wilkinson shifts on (d, e): wave 0 runs each sweep's
+//      scalar rotation chain into LDS (c, s) while the other waves apply the
+//      previous sweep's chain to their rows of Z (rotations act on columns).
 //   4. eigenvalues ascending by parallel rank; Q columns permuted to match.
 // A / Z live in LDS (row stride m + 1) up to kLdsMaxM, else in the HBM
 // scratch (L2-resident).
@@ -218,14 +218,31 @@ __device__ __forceinline__ double tq_block_sum(double v, double* red) {
   return s;
 }
 
+// lanes per row / column for an L-long reduction with nt threads: the largest
+// power of two <= nt / L, at most a wave (groups stay inside one wave)
+__device__ __forceinline__ int tq_group(int L, int nt) {
+  int g = 1;
+  while (g < 64 && 2 * g * L <= nt) g *= 2;
+  return g;
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     const int64_t* __restrict__ dims, const int64_t* __restrict__ offs,
     const double* __restrict__ Ain, double* __restrict__ Qout, double* __restrict__ lam_out,
     const int64_t* __restrict__ lam_offs, double* __restrict__ work,
-    const int64_t* __restrict__ work_offs, int max_iter, int* __restrict__ status) {
+    const int64_t* __restrict__ work_offs, int max_iter, int* __restrict__ status,
+    long long* __restrict__ stamps) {
   const int f = blockIdx.x;
   const int m = (int)dims[f];
+  // optional phase timing (GG_EIG_PROF): s_memtime at the phase boundaries
+  // (every lane of wave 0 writes its own slot: lane-varying addresses keep
+  // these vector stores)
+  auto stamp = [&](int k) {
+    if (stamps != nullptr && threadIdx.x < 64)
+      stamps[((int64_t)f * 8 + k) * 64 + threadIdx.x] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   extern __shared__ __attribute__((aligned(16))) unsigned char tq_lds[];
   // LDS: d, e, tau, v (m each), p/w (m), cs, sn (m each), rank (m ints), red (16)
   double* d = reinterpret_cast<double*>(tq_lds);
@@ -237,7 +254,7 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   double* sn = cs + m;
   double* red = sn + m;
   int* rank = reinterpret_cast<int*>(red + 16);
-  __shared__ int chain_lo, chain_hi, bad;
+  __shared__ int bad;
   const int64_t head = (((int64_t)7 * m + 16) * sizeof(double) + (int64_t)m * sizeof(int) + 15) &
                        ~int64_t(15);
   const int ld = kLds ? m + 1 : m;
@@ -278,15 +295,20 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     }
     __syncthreads();
     if (ti != 0.0) {
-      // p = tau A22 v  (thread per row)
+      // p = tau A22 v: a group of tpr lanes per row (strided columns, then a
+      // shuffle reduction inside the group)
+      const int tpr = tq_group(L, nt);
       double pv = 0.0;
-      for (int t = tid; t < L; t += nt) {
-        const double* Ar = A + (int64_t)(r0 + t) * ld + r0;
+      for (int t0 = tid / tpr; t0 < L; t0 += nt / tpr) {
+        const double* Ar = A + (int64_t)(r0 + t0) * ld + r0;
         double s = 0.0;
-        for (int c = 0; c < L; ++c) s = fma(Ar[c], v[c], s);
+        for (int c = tid % tpr; c < L; c += tpr) s = fma(Ar[c], v[c], s);
+        for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
         s *= ti;
-        pw[t] = s;
-        pv = fma(s, v[t], pv);
+        if (tid % tpr == 0) {
+          pw[t0] = s;
+          pv = fma(s, v[t0], pv);
+        }
       }
       const double ptv = tq_block_sum(pv, red);
       const double k = 0.5 * ti * ptv;
@@ -314,6 +336,7 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   }
   __syncthreads();
 
+  stamp(1);
   // ---- 2. Z = H_0 H_1 ... H_{m-3}, backwards, into the same storage.  The
   // reflector vectors sit in the strictly-lower columns 0..m-3, below the
   // subdiagonal; Z's block for step i touches rows/cols > i only, and column
@@ -336,11 +359,14 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     __syncthreads();
     const double ti = tau[i];
     if (ti != 0.0) {
-      // u[c] = tau sum_r v[r] Z[r0 + r][r0 + c]  (thread per column)
-      for (int t = tid; t < L; t += nt) {
+      // u[c] = tau sum_r v[r] Z[r0 + r][r0 + c]  (a lane group per column)
+      const int tpc = tq_group(L, nt);
+      for (int t0 = tid / tpc; t0 < L; t0 += nt / tpc) {
         double s = 0.0;
-        for (int r = 0; r < L; ++r) s = fma(v[r], A[(int64_t)(r0 + r) * ld + r0 + t], s);
-        pw[t] = ti * s;
+        for (int r = tid % tpc; r < L; r += tpc)
+          s = fma(v[r], A[(int64_t)(r0 + r) * ld + r0 + t0], s);
+        for (int off = tpc >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (tid % tpc == 0) pw[t0] = ti * s;
       }
       __syncthreads();
       for (int64_t q = tid; q < (int64_t)L * L; q += nt) {
@@ -357,80 +383,160 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   }
   __syncthreads();
 
-  // ---- 3. implicit QL (tql2 / tqli) on (d, e) accumulating into Z's columns
+  stamp(2);
+  // ---- 3. implicit QL (tql2 / tqli) on (d, e) accumulating into Z's columns.
+  // Wave 0 owns (d, e): it finds the next split point (ballot over its
+  // lanes) and runs the sweep's scalar rotation chain (every lane computes
+  // the same values in lockstep; lane 0 stores), writing (c, s) to buffer
+  // k & 1.  Meanwhile waves 1.. apply sweep k-1's chain (buffer (k-1) & 1) to
+  // their rows of Z -- the chains pipeline against the Z updates, one
+  // barrier per sweep.
   const double eps = 2.220446049250313e-16;
-  for (int l = 0; l < m; ++l) {
-    int iter = 0;
-    while (true) {
-      // thread 0: find the split point and run one sweep's scalar chain
-      if (tid == 0) {
-        int mm = l;
-        for (; mm < m - 1; ++mm) {
-          const double dd = fabs(d[mm]) + fabs(d[mm + 1]);
-          if (fabs(e[mm]) <= eps * dd) break;
+  const int lane = tid & 63, wave = tid >> 6;
+  __shared__ int lo_b[2], hi_b[2], ql_done;
+  if (tid == 0) {
+    ql_done = 0;
+    lo_b[0] = lo_b[1] = 0;
+    hi_b[0] = hi_b[1] = 0;
+  }
+  __syncthreads();
+  // the chain buffers: cs / sn hold buffer 0, pw / v hold buffer 1
+  double* cbuf[2] = {cs, pw};
+  double* sbuf[2] = {sn, v};
+  int l = 0, iter = 0;   // wave-0 state
+  int kswp = 0;
+  for (int k = 0;; ++k) {
+    kswp = k;
+    if (wave == 0) {
+      int mm = l;
+      bool have = false;
+      while (l < m && !bad) {
+        // first split point mm >= l: |e[mm]| <= eps (|d[mm]| + |d[mm+1]|), or m - 1
+        mm = m - 1;
+        for (int base = l; base < m - 1; base += 64) {
+          const int i = base + lane;
+          const bool split = i < m - 1 &&
+                             fabs(e[i]) <= eps * (fabs(d[i]) + fabs(d[i + 1]));
+          const unsigned long long bal = __ballot(split);
+          if (bal) {
+            mm = base + __ffsll((long long)bal) - 1;
+            break;
+          }
         }
-        chain_hi = mm;   // rotations for i = mm-1 down to chain_lo
-        chain_lo = mm;   // empty chain: converged
-        if (mm != l) {
-          if (iter >= max_iter) {
-            bad = 1;
-          } else {
-            double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-            double r = hypot(g, 1.0);
-            g = d[mm] - d[l] + e[l] / (g + copysign(r, g));
-            double s = 1.0, c = 1.0, p = 0.0;
-            int i = mm - 1;
-            bool early = false;
-            for (; i >= l; --i) {
-              const double fo = s * e[i], b = c * e[i];
-              r = hypot(fo, g);
-              e[i + 1] = r;
-              if (r == 0.0) {
-                d[i + 1] -= p;
-                e[mm] = 0.0;
-                early = true;
-                break;
-              }
-              s = fo / r;
-              c = g / r;
-              g = d[i + 1] - p;
-              r = (d[i] - g) * s + 2.0 * c * b;
-              p = s * r;
-              d[i + 1] = g + p;
-              g = c * r - b;
-              cs[i] = c;
-              sn[i] = s;
-            }
-            chain_lo = early ? i + 1 : l;
-            if (!early) {
-              d[l] -= p;
-              e[l] = g;
+        if (mm == l) {   // d[l] converged
+          ++l;
+          iter = 0;
+          continue;
+        }
+        have = true;
+        break;
+      }
+      const int b = k & 1;
+      if (!have) {
+        if (lane == 0) {
+          lo_b[b] = hi_b[b] = 0;
+          ql_done = 1;
+        }
+      } else if (iter >= max_iter) {
+        if (lane == 0) {
+          bad = 1;
+          lo_b[b] = hi_b[b] = 0;
+          ql_done = 1;
+        }
+      } else {
+        ++iter;
+        double* cb = cbuf[b];
+        double* sb = sbuf[b];
+        const double el = e[l], dl = d[l];
+        double g = (d[l + 1] - dl) / (2.0 * el);
+        double r = sqrt(fma(g, g, 1.0));
+        g = d[mm] - dl + el / (g + copysign(r, g));
+        double sv = 1.0, cv = 1.0, pv = 0.0;
+        double dip1 = d[mm];            // d[i+1] before this step's update
+        double ei = e[mm - 1], di = d[mm - 1];
+        int i = mm - 1;
+        bool early = false;
+        for (; i >= l; --i) {
+          // prefetch the next step's operands (not written by this sweep yet)
+          const double ei_n = i > l ? e[i - 1] : 0.0;
+          const double di_n = i > l ? d[i - 1] : 0.0;
+          const double fo = sv * ei, bb = cv * ei;
+          const double h2 = fma(fo, fo, g * g);
+          if (h2 == 0.0) {
+            if (lane == 0) {
+              e[i + 1] = 0.0;
+              d[i + 1] = dip1 - pv;
               e[mm] = 0.0;
             }
+            early = true;
+            break;
+          }
+          // 1/r by the hardware reciprocal square root and two Newton steps
+          // (the chain's latency: no IEEE sqrt + divide sequences).  h2 is a
+          // sum of squares of O(|A|) numbers, far from the f64 range limits.
+          double y = __builtin_amdgcn_rsq(h2);
+          double hh = h2 * y;
+          y = fma(0.5 * y, fma(-hh, y, 1.0), y);
+          hh = h2 * y;
+          y = fma(0.5 * y, fma(-hh, y, 1.0), y);
+          r = h2 * y;
+          if (lane == 0) e[i + 1] = r;
+          sv = fo * y;
+          cv = g * y;
+          g = dip1 - pv;
+          r = fma(di - g, sv, 2.0 * cv * bb);
+          pv = sv * r;
+          if (lane == 0) {
+            d[i + 1] = g + pv;
+            cb[i] = cv;
+            sb[i] = sv;
+          }
+          g = fma(cv, r, -bb);
+          dip1 = di;
+          ei = ei_n;
+          di = di_n;
+        }
+        if (lane == 0) {
+          lo_b[b] = early ? i + 1 : l;
+          hi_b[b] = mm;
+          if (!early) {
+            d[l] = dl - pv;
+            e[l] = g;
+            e[mm] = 0.0;
           }
         }
       }
-      __syncthreads();
-      const int lo = chain_lo, hi = chain_hi;
-      if (bad || hi == l) break;   // failed, or d[l] has converged
-      // rotations i = hi-1 .. lo on columns (i, i+1) of every row of Z
-      for (int k = tid; k < m; k += nt) {
-        double* Zk = A + (int64_t)k * ld;
-        double cur = Zk[hi];
+    } else if (k > 0) {
+      // apply sweep k-1: rotations i = hi-1 .. lo on columns (i, i+1) of Z
+      const int b = (k - 1) & 1;
+      const int lo = lo_b[b], hi = hi_b[b];
+      const double* cb = cbuf[b];
+      const double* sb = sbuf[b];
+      for (int row = tid - 64; row < m && hi > lo; row += nt - 64) {
+        double* Zr = A + (int64_t)row * ld;
+        double cur = Zr[hi];
+        // software pipelined: step i - 1's operands are loaded before step
+        // i's store (Zr[i - 1] is not written by step i), so the carried
+        // dependency is the two FMAs on cur, not an LDS round trip
+        double zi = Zr[hi - 1], ci = cb[hi - 1], si = sb[hi - 1];
         for (int i = hi - 1; i >= lo; --i) {
-          const double zi = Zk[i];
-          Zk[i + 1] = sn[i] * zi + cs[i] * cur;
-          cur = cs[i] * zi - sn[i] * cur;
+          const int j = i > lo ? i - 1 : i;
+          const double zn = Zr[j], cn = cb[j], sn_ = sb[j];
+          Zr[i + 1] = fma(si, zi, ci * cur);
+          cur = fma(ci, zi, -si * cur);
+          zi = zn;
+          ci = cn;
+          si = sn_;
         }
-        Zk[lo] = cur;
+        Zr[lo] = cur;
       }
-      __syncthreads();
-      ++iter;
     }
-    if (bad) break;
+    __syncthreads();
+    if (ql_done) break;
   }
   __syncthreads();
-
+  stamp(3);
+  if (stamps != nullptr && tid < 64) stamps[((int64_t)f * 8 + 6) * 64 + tid] = kswp;
   // ---- 4. ascending order (parallel rank, ties by index) and output
   for (int i = tid; i < m; i += nt) {
     int r = 0;
@@ -447,6 +553,7 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     Q[(int64_t)r * m + rank[c]] = A[(int64_t)r * ld + c];
   }
   if (tid == 0) status[f] = bad;
+  stamp(4);
 }
 
 }  // namespace gg
@@ -494,6 +601,12 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     // (GG_EIG=jacobi: reference implementation kept for A/B)
     const char* ev = getenv("GG_EIG");
     const bool jacobi = ev != nullptr && std::string(ev) == "jacobi";
+    long long* dstamps = nullptr;
+    const bool prof = getenv("GG_EIG_PROF") != nullptr;
+    if (!jacobi && prof) {
+      GG_HIP(hipMallocAsync(&dstamps, 8 * 64 * sizeof(long long) * count, s));
+      GG_HIP(hipMemsetAsync(dstamps, 0, 8 * 64 * sizeof(long long) * count, s));
+    }
     if (!jacobi) {
       const int64_t head = (((int64_t)7 * mmax + 16) * sizeof(double) +
                             (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
@@ -504,13 +617,13 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(gg::tridiag_ql_kernel<true>, dim3(count), dim3(gg::kTqThreads), lds, s,
                            dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
-                           work_dev, dmeta + 3 * count, iters, dstatus);
+                           work_dev, dmeta + 3 * count, iters, dstatus, dstamps);
       } else {
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<false>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL(gg::tridiag_ql_kernel<false>, dim3(count), dim3(gg::kTqThreads), lds,
                            s, dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
-                           work_dev, dmeta + 3 * count, iters, dstatus);
+                           work_dev, dmeta + 3 * count, iters, dstatus, dstamps);
       }
     } else {
       const int64_t lds = gg::eig_lds_bytes(mmax, lds_a);
@@ -531,6 +644,20 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     GG_HIP(hipMemcpyAsync(st.data(), dstatus, count * sizeof(int), hipMemcpyDeviceToHost, s));
     GG_HIP(hipFreeAsync(dmeta, s));
     GG_HIP(hipStreamSynchronize(s));
+    if (dstamps) {
+      std::vector<long long> h64(8 * 64 * (size_t)count), h(8 * (size_t)count);
+      GG_HIP(hipMemcpy(h64.data(), dstamps, h64.size() * sizeof(long long),
+                       hipMemcpyDeviceToHost));
+      for (size_t q = 0; q < h.size(); ++q) h[q] = h64[q * 64];
+      GG_HIP(hipFree(dstamps));
+      for (int i = 0; i < count; ++i)
+        fprintf(stderr,
+                "eig m=%lld phases(us at 100MHz): tridiag %.1f form-Q %.1f QL %.1f sort %.1f "
+                "sweeps %lld\n",
+                (long long)m[i], (h[8 * i + 1] - h[8 * i]) / 100.0,
+                (h[8 * i + 2] - h[8 * i + 1]) / 100.0, (h[8 * i + 3] - h[8 * i + 2]) / 100.0,
+                (h[8 * i + 4] - h[8 * i + 3]) / 100.0, h[8 * i + 6]);
+    }
     for (int i = 0; i < count; ++i)
       GG_REQUIRE(st[i] == 0, GG_ERR_LINALG,
                  "eigensolver did not converge on factor " + std::to_string(i));

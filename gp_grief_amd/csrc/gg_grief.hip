@@ -12,9 +12,10 @@
 //     selected eigenvector rows; writes log|X| and sign(X) as an n x U table
 //     (U = sum_f u_f), i.e. exactly the reference's x_unique, per point.
 //   grief_phi_kernel: HBM-bound writer of Phi (n x p row-major, or p x n):
-//     one block owns 16 data points (their table rows in LDS) and a 256-wide
-//     range of eigenfunctions j (their table columns c_{j,f} in LDS); every
-//     Phi element is d LDS adds, d sign multiplies and one exp.
+//     one block owns 16 (32 transposed) data points (their table rows, as
+//     signed values S exp(L), in LDS) and a 256-wide range of eigenfunctions
+//     j (their table columns c_{j,f} in LDS); every Phi element is d LDS
+//     loads and d multiplies, and the transposed tile is stored through LDS.
 // Also the dense stationary covariance used for the grid factors K_f.
 #include <cmath>
 #include <vector>
@@ -101,45 +102,54 @@ __global__ __launch_bounds__(256) void grief_tables_kernel(
   }
 }
 
-constexpr int kPhiRows = 16;
+constexpr int kPhiRows = 16;    // data points per block (row-major Phi)
+constexpr int kPhiRowsT = 32;   // data points per block (transposed Phi)
 constexpr int kPhiCols = 256;
 constexpr int kMaxDim = 64;
 
 // Phi[a][j] = prod_f S[a][c_jf] * exp(sum_f L[a][c_jf] - 0.5 log_lam[j])
+//           = prod_f T[a][c_jf] * exp(-0.5 log_lam[j]),  T = S exp(L) = X
 // cidx: p x d column index into the tables (c_jf = col0_f + inverse_f[j]).
+// The block forms its kR x U slice of T once in LDS (kR U exps instead of
+// kR kPhiCols), so each Phi element is d LDS loads and d multiplies: the
+// kernel is bound by the Phi store.  Transposed (p x n): the kR x 256 tile
+// goes through LDS so each eigenfunction row is stored as a kR-long run.
+template <int kR, bool kT>
 __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
     const double* __restrict__ Ltab, const double* __restrict__ Stab, int U, int64_t n,
     const int* __restrict__ cidx, int d, const double* __restrict__ log_lam, int p,
-    int transposed, double* __restrict__ Phi) {
+    double* __restrict__ Phi) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* sL = sm;                          // kPhiRows x U
-  double* sS = sm + kPhiRows * U;           // kPhiRows x U
-  int* sC = reinterpret_cast<int*>(sm + 2 * kPhiRows * U);  // d x kPhiCols
-  const int64_t a0 = (int64_t)blockIdx.x * kPhiRows;
-  const int j = blockIdx.y * kPhiCols + threadIdx.x;
-  const int rows = (int)min<int64_t>(kPhiRows, n - a0);
-  for (int e = threadIdx.x; e < rows * U; e += blockDim.x) {
-    sL[e] = Ltab[a0 * U + e];
-    sS[e] = Stab[a0 * U + e];
-  }
+  double* sT = sm;                                    // kR x U
+  double* sO = sm + kR * U;                           // kT: kPhiCols x (kR + 1)
+  int* sC = reinterpret_cast<int*>(sm + kR * U + (kT ? kPhiCols * (kR + 1) : 0));  // d x 256
+  const int64_t a0 = (int64_t)blockIdx.x * kR;
+  const int j0 = blockIdx.y * kPhiCols;
+  const int j = j0 + threadIdx.x;
+  const int rows = (int)min<int64_t>(kR, n - a0);
+  for (int e = threadIdx.x; e < rows * U; e += blockDim.x)
+    sT[e] = Stab[a0 * U + e] * exp(Ltab[a0 * U + e]);
   if (j < p)
     for (int f = 0; f < d; ++f) sC[f * kPhiCols + threadIdx.x] = cidx[(int64_t)j * d + f];
   __syncthreads();
-  if (j >= p) return;
-  const double hl = 0.5 * log_lam[j];
-  for (int r = 0; r < rows; ++r) {
-    double lg = 0.0, sg = 1.0;
-    for (int f = 0; f < d; ++f) {
-      const int c = sC[f * kPhiCols + threadIdx.x];
-      lg += sL[r * U + c];
-      sg *= sS[r * U + c];
+  if (j < p) {
+    const double sc = exp(-0.5 * log_lam[j]);
+    for (int r = 0; r < rows; ++r) {
+      double v = sc;
+      for (int f = 0; f < d; ++f) v *= sT[r * U + sC[f * kPhiCols + threadIdx.x]];
+      if (kT)
+        sO[threadIdx.x * (kR + 1) + r] = v;
+      else
+        Phi[(a0 + r) * p + j] = v;
     }
-    const double v = sg * exp(lg - hl);
-    const int64_t a = a0 + r;
-    if (transposed)
-      Phi[(int64_t)j * n + a] = v;
-    else
-      Phi[a * p + j] = v;
+  }
+  if (kT) {
+    __syncthreads();
+    const int cols = min(kPhiCols, p - j0);
+    for (int e = threadIdx.x; e < cols * kR; e += blockDim.x) {
+      const int jj = e / kR, r = e - jj * kR;
+      if (r < rows) Phi[(int64_t)(j0 + jj) * n + a0 + r] = sO[jj * (kR + 1) + r];
+    }
   }
 }
 
@@ -220,19 +230,30 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
     GG_REQUIRE(d >= 1 && d <= gg::kMaxDim && U >= 1 && p >= 1 && n >= 0, GG_ERR_VALUE,
                "bad Phi geometry");
     if (n == 0) return;
-    const size_t lds = (size_t)2 * gg::kPhiRows * U * sizeof(double) +
+    const int kr = transposed ? gg::kPhiRowsT : gg::kPhiRows;
+    const size_t lds = (size_t)kr * U * sizeof(double) +
+                       (transposed ? (size_t)gg::kPhiCols * (kr + 1) * sizeof(double) : 0) +
                        (size_t)d * gg::kPhiCols * sizeof(int);
     GG_REQUIRE(lds <= 160 * 1024, GG_ERR_VALUE, "too many selected eigenvector rows");
     static bool attr = false;
     if (!attr) {
-      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gg::grief_phi_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      GG_HIP(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(gg::grief_phi_kernel<gg::kPhiRows, false>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      GG_HIP(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(gg::grief_phi_kernel<gg::kPhiRowsT, true>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
       attr = true;
     }
-    dim3 grid((unsigned)gg::ceil_div(n, gg::kPhiRows), (unsigned)gg::ceil_div(p, gg::kPhiCols));
-    hipLaunchKernelGGL(gg::grief_phi_kernel, grid, dim3(gg::kPhiCols), lds,
-                       gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
-                       log_lam_dev, p, transposed, phi_dev);
+    dim3 grid((unsigned)gg::ceil_div(n, kr), (unsigned)gg::ceil_div(p, gg::kPhiCols));
+    if (transposed)
+      hipLaunchKernelGGL((gg::grief_phi_kernel<gg::kPhiRowsT, true>), grid, dim3(gg::kPhiCols),
+                         lds, gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
+                         log_lam_dev, p, phi_dev);
+    else
+      hipLaunchKernelGGL((gg::grief_phi_kernel<gg::kPhiRows, false>), grid, dim3(gg::kPhiCols),
+                         lds, gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
+                         log_lam_dev, p, phi_dev);
     GG_LAUNCH_CHECK();
   });
 }

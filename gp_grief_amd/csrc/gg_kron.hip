@@ -158,6 +158,73 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
       for (int r = 0; r < 4; ++r)
         if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
     }
+  } else if (!kRecomp) {
+    // shift / dots epilogue (textbook p.q, fused-CG p.q, r.q, q.q): the loads
+    // of tile t + 1 are issued before tile t's stores.  CDNA4 retires vmcnt in
+    // order and stores count, so a load issued after a store cannot be waited
+    // for without also waiting for that store's write acknowledgement; issued
+    // first, the wait for tile t + 1 skips the stores of tile t.
+    double xv[2][4], ev[2][4];
+    // kIdent: the wave's 16 x p output block is contiguous, so every address
+    // is a uniform base (SGPRs) plus a 32-bit lane byte offset (saddr form):
+    // one VGPR per address instead of a 64-bit pair
+    const int64_t b0u = kIdent ? (int64_t)__builtin_amdgcn_readfirstlane((int)b0) |
+                                     ((int64_t)__builtin_amdgcn_readfirstlane((int)(b0 >> 32))
+                                      << 32)
+                               : 0;
+    const char* xbase = reinterpret_cast<const char*>(xs + (kIdent ? b0u * p : 0));
+    const char* ebase = reinterpret_cast<const char*>(er + (kIdent ? b0u * p : 0));
+    char* ybase = reinterpret_cast<char*>(Y + (kIdent ? b0u * p : 0));
+    auto boff = [&](int r, int t) -> uint32_t {
+      return (uint32_t)(((lane >> 4) + 4 * r) * p + (int)colj(t)) * 8u;
+    };
+    // rows past M: the block's row count, uniform (kIdent)
+    const int rows_left = kIdent ? (int)min<int64_t>(16, M - b0u) : 16;
+    auto row_ok = [&](int r) -> bool {
+      return kIdent ? ((lane >> 4) + 4 * r) < rows_left : rowok[r];
+    };
+    auto load_tile = [&](int t, double (&xo)[4], double (&eo)[4]) {
+      const bool cok = colj(t) < p;
+      const int64_t co = kIdent ? 0 : coloff(t);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = row_ok(r) && cok;
+        if (kIdent) {
+          const uint32_t o = boff(r, t);
+          xo[r] = ok ? *reinterpret_cast<const double*>(xbase + o) : 0.0;
+          eo[r] = (ok && edots) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
+        } else {
+          xo[r] = ok ? xs[rowoff[r] + co] : 0.0;
+          eo[r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+        }
+      }
+    };
+    load_tile(0, xv[0], ev[0]);
+#pragma unroll
+    for (int t = 0; t < JT; ++t) {
+      const int cb = t & 1;
+      // keep the scheduler from hoisting later tiles' loads (register budget)
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 1 < JT) load_tile(t + 1, xv[cb ^ 1], ev[cb ^ 1]);
+      const bool cok = colj(t) < p;
+      const int64_t co = kIdent ? 0 : coloff(t);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (row_ok(r) && cok) {
+          const double pv = xv[cb][r];
+          const double v = fma(shift, pv, acc[t][r]);
+          dsum = fma(pv, v, dsum);
+          if (edots) {
+            rqsum = fma(ev[cb][r], v, rqsum);
+            qqsum = fma(v, v, qqsum);
+          }
+          if (kIdent)
+            *reinterpret_cast<double*>(ybase + boff(r, t)) = v;
+          else
+            Y[rowoff[r] + co] = v;
+        }
+      }
+    }
   } else {
     // fusion layouts 1 / 2: p_new recomputed here from p_old (xs) and r
     double* __restrict__ ep_out = kRecomp ? fz.ep_out : nullptr;
@@ -883,7 +950,11 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // step 0; the later launches of that step read the updated p
         const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? cgp : 0;
         const bool epi = cgp == 2 && last && dot_partials != nullptr;
-        const bool side = cgp == 2 && k == 1 && jt0 == 0 && cg->sx != nullptr;
+        // the x side job rides on the second mode product; with d >= 4 the
+        // third (also a plain, MFMA-bound one) takes the second half of x
+        const bool split_side = cgp == 2 && d >= 4 && cg->sx != nullptr;
+        const bool side = cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
+                          (k == 1 || (split_side && k == 2));
         const int epi_kind = !epi ? 0 : cg->ep_out == nullptr ? 3 : cg->ex != nullptr ? 5 : 6;
         ModeConfig mc = select_kernel(jt, variant, epi ? epi_kind : side ? 4 : pro);
         const bool with_xs = last && (shift != 0.0 || dot_partials != nullptr);
@@ -902,11 +973,16 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           }
         }
         if (side) {
+          // [off, off + len): all of x, or its half (even split: 16-byte
+          // aligned double2 accesses stay aligned)
+          const int64_t h = split_side ? 2 * ceil_div(cg->sn, 4) : cg->sn;
+          const int64_t off = (split_side && k == 2) ? h : 0;
+          const int64_t len = (split_side && k == 2) ? cg->sn - h : h;
           fz.sc = cg->sc;
-          fz.sx = cg->sx;
-          fz.sp = cg->sp;
-          fz.sn = cg->sn;
-          fz.schunk = 2 * ceil_div(cg->sn, 2 * nblk);
+          fz.sx = cg->sx + off;
+          fz.sp = cg->sp + off;
+          fz.sn = len;
+          fz.schunk = 2 * ceil_div(std::max<int64_t>(len, 1), 2 * nblk);
         }
         double* parts = nullptr;
         if (last && dot_partials != nullptr) {

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round 2, session g: eigensolver (pipelined QL) tests + phase stamps; TN-GEMM
+# variants: tests and timing.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+O=gpurun_out/r02g
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kron.py tests/test_gpu_grief.py -m gpu -x -q --timeout 120 --timeout-method thread -k "eigensolver or schur or grid_gp or fixture or automobile or fd_gradient" > $O/pytest_eig.log 2>&1 || { tail -30 $O/pytest_eig.log; exit 1; }
+echo "eig tests: $(tail -1 $O/pytest_eig.log)"
+GG_EIG_PROF=1 timeout -k 10 120 python -u tools/p2_kernels_bench.py --what eig > $O/eig_prof.log 2>&1 || { tail -5 $O/eig_prof.log; exit 1; }
+grep -E "\"eig\"" $O/eig_prof.log; grep "eig m=" $O/eig_prof.log | awk '!seen[$2]++'
+for v in 1 2 3 4 5 0; do
+  GG_GEMM_TN=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_grief.py -m gpu -x -q --timeout 120 --timeout-method thread -k "gemm or cholesky or fixtures_model" > $O/pytest_tn$v.log 2>&1 || { echo "variant $v FAILED"; grep -E "^E |FAILED" $O/pytest_tn$v.log | head; continue; }
+  echo "variant $v tests: $(tail -1 $O/pytest_tn$v.log)"
+  GG_GEMM_TN=$v timeout -k 10 300 python -u tools/p2_kernels_bench.py --what gram > $O/gram_tn$v.jsonl 2>> $O/gram.err || exit $?
+  python -c "import json;[print('variant $v', json.loads(l)['p'], round(json.loads(l)['ms'],2), round(json.loads(l)['tflops'],1)) for l in open('$O/gram_tn$v.jsonl')]"
+done

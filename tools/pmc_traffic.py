@@ -1,56 +1,77 @@
-"""HBM traffic per launch of the dominant kernel from rocprofv3 PMC passes.
+"""HBM traffic per launch of the fused-CG mode products from rocprofv3 PMC passes.
 
-usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR CALIB_FETCH_DIR KERNEL_SUBSTR OUT_JSON
+usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON
 
-FETCH_SIZE is calibrated for the mode product's A-operand access shape by
-tools/fetch_calib (kernel `kfrag`: 8 B per lane, 4 rows x 128 B per wave
-instruction): bytes = FETCH_SIZE[KB] * 1024 * (true bytes / counted bytes of
-kfrag).  WRITE_SIZE is taken as bytes (MI355X_MICROARCH.md: exact for
-streaming stores).  Counters were collected in separate passes with
---kernel-trace only, as the guide prescribes.
+Counters (two separate --pmc runs of `bench.py --steps 2 --warmup 1`, kernel
+trace only, as MI355X_MICROARCH.md prescribes):
+  reads   TCC_EA0_RDREQ_32B_sum, _64B_sum, _128B_sum (L2 -> fabric requests by size)
+  writes  TCC_EA0_WRREQ_sum, TCC_EA0_WRREQ_64B_sum
+bytes = 32 N32 + 64 N64 + 128 N128 (reads), 64 N64 (writes) -- the request
+sizes themselves, not FETCH_SIZE (which tallies 128-B requests at 64 B on
+gfx950).  Calibration on the kernel's own access pattern: the plain mode
+product (launch position 2) reads X exactly once (12.8 GB at 200^4) and
+writes Y once, so its counted bytes must equal those; the result records the
+ratio.  The dominant launch (position 0, CG prologue) is read from the
+iterations whose fused update was pending (the third CG iteration onwards).
 """
 import csv
 import glob
 import json
 import os
 import sys
+from collections import defaultdict
+
+SIZES = {"TCC_EA0_RDREQ_32B_sum": 32, "TCC_EA0_RDREQ_64B_sum": 64,
+         "TCC_EA0_RDREQ_128B_sum": 128}
 
 
-def rows(d):
-    out = []
+def dispatches(d):
+    out = defaultdict(dict)
+    names = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        out += list(csv.DictReader(open(f)))
-    return out
-
-
-def mean_counter(d, sub, counter):
-    v = [float(r["Counter_Value"]) for r in rows(d)
-         if sub in r["Kernel_Name"] and r["Counter_Name"] == counter]
-    names = {r["Kernel_Name"].split("(")[0] for r in rows(d) if sub in r["Kernel_Name"]}
-    return sum(v) / len(v), len(v), sorted(names)
+        for r in csv.DictReader(open(f)):
+            if "mode_product" not in r["Kernel_Name"]:
+                continue
+            did = int(r["Dispatch_Id"])
+            out[did][r["Counter_Name"]] = float(r["Counter_Value"])
+            names[did] = r["Kernel_Name"].split("(")[0]
+    return out, names
 
 
 def main():
-    fdir, wdir, cdir, sub, out = sys.argv[1:6]
-    calib_bytes = 2147483200.0  # tools/fetch_calib kfrag: R * M * 8
-    kf, _, _ = mean_counter(cdir, "kfrag", "FETCH_SIZE")
-    factor = calib_bytes / (kf * 1024.0)
-    fetch, n, names = mean_counter(fdir, sub, "FETCH_SIZE")
-    write, _, _ = mean_counter(wdir, sub, "WRITE_SIZE")
+    rd_dir, wr_dir, out = sys.argv[1:4]
+    rd, names = dispatches(rd_dir)
+    wr, _ = dispatches(wr_dir)
+    ids = sorted(rd)
+    d = 4
+    iters = [ids[i:i + d] for i in range(0, len(ids) - d + 1, d)]
+    last = iters[-1]                     # a pending (fully fused) iteration
+    per_pos = []
+    for k, did in enumerate(last):
+        rbytes = sum(rd[did].get(c, 0.0) * s for c, s in SIZES.items())
+        wbytes = wr.get(did, {}).get("TCC_EA0_WRREQ_64B_sum", 0.0) * 64
+        per_pos.append({"position": k, "kernel": names[did], "read_bytes": rbytes,
+                        "write_bytes": wbytes, "traffic_bytes": rbytes + wbytes})
+    n = 200 ** 4
+    plain = per_pos[2]
+    calib = {"read_ratio": plain["read_bytes"] / (8.0 * n),
+             "write_ratio": plain["write_bytes"] / (8.0 * n)}
+    dom = per_pos[0]
     res = {
-        "kernel": names[0] if len(names) == 1 else names,
-        "dispatches": n,
-        "fetch_size_kb": fetch,
-        "write_size_kb": write,
-        "fetch_calibration": factor,
-        "read_bytes": fetch * 1024.0 * factor,
-        "write_bytes": write * 1024.0,
-        "traffic_bytes": fetch * 1024.0 * factor + write * 1024.0,
-        "method": "separate --pmc FETCH_SIZE / WRITE_SIZE passes (kernel trace only); "
-                  "FETCH_SIZE scaled by the kfrag calibration of tools/fetch_calib",
+        "position": 0, "recurrence": "fused", "fusion_layout": 0,
+        "kernel": dom["kernel"], "traffic_bytes": dom["traffic_bytes"],
+        "read_bytes": dom["read_bytes"], "write_bytes": dom["write_bytes"],
+        "algorithmic_bytes": 6 * 8.0 * n,
+        "calibrated_on_own_pattern": abs(calib["read_ratio"] - 1) < 0.02
+        and abs(calib["write_ratio"] - 1) < 0.02,
+        "calibration": calib, "per_position": per_pos,
+        "method": "separate rocprofv3 --pmc passes (reads by request size / writes), kernel "
+                  "trace only, bench.py --steps 2 --warmup 1 at 200^4; bytes = request "
+                  "counts x request sizes; calibrated on the plain mode product (12.8 GB "
+                  "read + 12.8 GB written by construction)",
     }
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps(res))
+    print(json.dumps({k: v for k, v in res.items() if k != "per_position"}))
 
 
 if __name__ == "__main__":
