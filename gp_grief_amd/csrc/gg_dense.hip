@@ -9,6 +9,9 @@
 //   Phi.T.dot(y), Phi.dot(v)            :97, 173, 224, 234            -> gg_gemv
 // Layout: every matrix is row-major with an explicit leading dimension.
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "gg_internal.h"
@@ -131,6 +134,123 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
       }
 }
 
+// TN GEMM for Gram-type products C = alpha A^T B (+ beta C), A: K x M and
+// B: K x N both k-major (row-major, row = k) -- A = Phi^T Phi with Phi n x p.
+// Same 128 x 128 workgroup tile and 64 x 64 wave tiles as gemm_kernel, but the
+// operand tiles move global -> LDS by LDS-DMA (global_load_lds, 16 B per
+// lane: one 1 KB wave instruction per 128-double k-row), kNS stages in flight,
+// each retired by a counted s_waitcnt vmcnt + one raw s_barrier: no staging
+// registers, no ds_write, and the HBM / L2 stream runs kNS - 1 stages ahead of
+// the MFMAs.  Rows are padded to kLdT doubles (the DMA base of each k-row
+// instruction), so fragment reads stay conflict-free.  Needs M, N, lda, ldb
+// even and 16-byte aligned A, B (the host checks).  Rows k >= kend of the
+// last stage are clamped reads, zeroed in the A fragment.
+template <int kBKg, int kNSg, int kMinWg>
+__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial) {
+  constexpr int kStageD = 2 * kBKg * kLdT;       // doubles per stage (A then B)
+  constexpr int kPerWave = kBKg / 4;             // k-rows of A (and of B) per wave
+  static_assert(kBKg % 4 == 0 && kGemmThreads == 256, "four waves share a stage's k-rows");
+  constexpr int kInstr = 2 * kPerWave;           // DMA instructions per wave per stage
+  extern __shared__ __attribute__((aligned(16))) double gl[];
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+  if (uplo == 1 && n0 > m0 + kBM - 1) return;
+  if (uplo == 2 && m0 > n0 + kBN - 1) return;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nst = (kend - kbeg + kBKg - 1) / kBKg;
+  const int acol = min(m0 + 2 * lane, M - 2);
+  const int bcol = min(n0 + 2 * lane, N - 2);
+
+  auto issue = [&](int g) {
+    double* st = gl + (g % kNSg) * kStageD;
+    const int k0 = kbeg + g * kBKg;
+#pragma unroll
+    for (int j = 0; j < kPerWave; ++j) {
+      const int r = wave * kPerWave + j;
+      const int k = min(k0 + r, kend - 1);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(A + (int64_t)k * lda + acol),
+          (__attribute__((address_space(3))) void*)(st + r * kLdT), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(B + (int64_t)k * ldb + bcol),
+          (__attribute__((address_space(3))) void*)(st + kBKg * kLdT + r * kLdT), 16, 0, 0);
+    }
+  };
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+#pragma unroll
+  for (int g = 0; g < kNSg - 1; ++g)
+    if (g < nst) issue(g);
+  constexpr int kWait0 = (7 << 4) | (15 << 8);
+  for (int g = 0; g < nst; ++g) {
+    // retire stage g: the younger stages g+1 .. g+kNS-2 may stay in flight
+    const int younger = min(kNSg - 2, nst - 1 - g);
+    if (younger >= 2)
+      __builtin_amdgcn_s_waitcnt(((2 * kInstr) & 15) | ((((2 * kInstr) >> 4) & 3) << 14) |
+                                 (7 << 4) | (15 << 8));
+    else if (younger == 1)
+      __builtin_amdgcn_s_waitcnt((kInstr & 15) | (((kInstr >> 4) & 3) << 14) | (7 << 4) |
+                                 (15 << 8));
+    else
+      __builtin_amdgcn_s_waitcnt(kWait0);
+    __builtin_amdgcn_s_barrier();
+    if (g + kNSg - 1 < nst) issue(g + kNSg - 1);
+    const double* a_s = gl + (g % kNSg) * kStageD;
+    const double* b_s = a_s + kBKg * kLdT;
+    const int krem = kend - (kbeg + g * kBKg);   // valid k-rows in this stage
+#pragma unroll
+    for (int s = 0; s < kBKg / 4; ++s) {
+      const int kk = 4 * s + (lane >> 4);
+      const int kr = kk * kLdT + (lane & 15);
+      double af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = kk < krem ? a_s[kr + wm + 16 * i] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = b_s[kr + wn + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  double* P = partial ? partial + (int64_t)blockIdx.z * M * N : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + (lane >> 4) + 4 * r;
+        const int col = n0 + wn + 16 * j + (lane & 15);
+        if (row >= M || col >= N) continue;
+        if (uplo == 1 && col > row) continue;
+        if (uplo == 2 && row > col) continue;
+        const double v = acc[i][j][r];
+        if (P) {
+          P[(int64_t)row * N + col] = v;
+        } else {
+          double* c = C + (int64_t)row * ldc + col;
+          *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
+        }
+      }
+}
+
+template <int kBKg, int kNSg>
+constexpr size_t tn_glds_lds() {
+  return (size_t)kNSg * 2 * kBKg * kLdT * sizeof(double);
+}
+
 __global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restrict__ partial,
                                      double alpha, double beta, double* C, int64_t ldc,
                                      int uplo) {
@@ -145,6 +265,31 @@ __global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restri
     double* c = C + (int64_t)row * ldc + col;
     *c = (beta == 0.0) ? alpha * s : fma(alpha, s, beta * *c);
   }
+}
+
+template <int BK, int NS, int MW>
+static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alpha, const double* A,
+                      int64_t lda, const double* B, int64_t ldb, double beta, double* C,
+                      int64_t ldc, int uplo, int kchunk, double* part) {
+  static bool attr = false;
+  const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_kernel<BK, NS, MW>);
+  if (!attr) {
+    GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)tn_glds_lds<BK, NS>()));
+    attr = true;
+  }
+  const size_t lds = tn_glds_lds<BK, NS>();
+  hipLaunchKernelGGL((gemm_tn_glds_kernel<BK, NS, MW>), grid, dim3(kGemmThreads), lds, s, M, N,
+                     K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
+}
+
+// TN-GEMM variant (A/B knob, read per call): GG_GEMM_TN=0 register-staged
+// gemm_kernel, 1..5 the LDS-DMA kernel's stage shapes.  Default 3 (BK 8,
+// 2 stages, 3 waves/SIMD): 53.0 TF on the C5 Gram (n 1e5, p 1e4) against
+// 46.9 TF for the register-staged kernel (profiles/r02_g_gram_tn_variants.jsonl)
+static int gemm_tn_variant() {
+  const char* e = getenv("GG_GEMM_TN");
+  return e ? atoi(e) : 3;
 }
 
 // split-K factor gemm() chooses when the workspace is not the limit
@@ -175,6 +320,29 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
   S = (int)ceil_div(std::max(K, 1), kchunk);
   dim3 grid(gn, gm, S);
   double* part = (S > 1) ? splitk_buf : nullptr;
+  // TN with even shapes and 16-byte aligned operands: the LDS-DMA kernel
+  // (GG_GEMM_TN selects its stage shape for A/B; 0 = the register-staged one)
+  const int tnv = gemm_tn_variant();
+  if (ta && !tb && tnv > 0 && M >= 2 && N >= 2 && (M % 2) == 0 && (N % 2) == 0 &&
+      (lda % 2) == 0 && (ldb % 2) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
+      ((reinterpret_cast<uintptr_t>(B) & 15) == 0)) {
+    switch (tnv) {
+      case 1: launch_tn<16, 2, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 2: launch_tn<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 3: launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 4: launch_tn<16, 3, 1>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      default: launch_tn<8, 4, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+    }
+    GG_LAUNCH_CHECK();
+    if (part) {
+      const int64_t total = (int64_t)M * N;
+      const int nb = (int)std::min<int64_t>(4096, ceil_div(total, 256));
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(nb), dim3(256), 0, s, M, N, S, part, alpha,
+                         beta, C, ldc, uplo);
+      GG_LAUNCH_CHECK();
+    }
+    return;
+  }
 #define GG_GEMM_LAUNCH(TA_, TB_)                                                              \
   hipLaunchKernelGGL((gemm_kernel<TA_, TB_>), grid, dim3(kGemmThreads), 0, s, M, N, K, alpha, \
                      A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part)
@@ -263,64 +431,154 @@ void gemv(bool trans, int64_t R, int Cn, double alpha, const double* A, int64_t 
 // ------------------------------------------------------------------ Cholesky
 constexpr int kNB = 64;
 
-// Factor the nb x nb diagonal block at A (lda) in place (lower) and write its
-// inverse (lower) to W (ld kNB).  status <- 1 if a pivot is not positive/finite.
-// One wave, no workgroup barriers on the critical path: lane i holds row i of
-// the block in registers (right-looking; pivots and L[j][k] broadcast with
-// v_readlane), then lane j forms column j of W = L^-1 by forward substitution
-// against L broadcast from LDS.  Rows >= nb are padded with the identity.
-__device__ inline double readlane_f64(double v, int lane) {
-  const long long bits = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(bits & 0xffffffffLL), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), lane);
-  return __hiloint2double(hi, lo);
+// Second stream of the calling device for gg_potrf's look-ahead (created once
+// per device at the lowest priority, never destroyed: it lives as long as the
+// process)
+hipStream_t aux_stream() {
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  int dev = 0;
+  GG_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find(dev);
+  if (it != streams.end()) return it->second;
+  // lowest priority: the wide trailing updates yield the CUs to the
+  // factorisation chain on the caller's stream (the critical path)
+  int least = 0, greatest = 0;
+  GG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t st;
+  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least));
+  streams[dev] = st;
+  return st;
 }
 
-__global__ __launch_bounds__(kNB) void potrf_diag_kernel(double* A, int64_t lda, int nb,
-                                                        double* W, int* status) {
-  __shared__ double Ls[kNB][kNB + 1];
-  const int ln = threadIdx.x;   // row owner in the factorisation, column owner in the inverse
-  // coalesced stage of the (lower) block: lane = column
-  for (int r = 0; r < kNB; ++r)
-    Ls[r][ln] = (r < nb && ln <= r) ? A[(int64_t)r * lda + ln] : ((r == ln) ? 1.0 : 0.0);
-  __syncthreads();
-  double a[kNB];
+// Fused diagonal-block factor + panel TRSM of one 64-column block (k0, nb):
+//   L_bb = chol(A[k0:k0+nb, k0:k0+nb])              (every workgroup, in LDS)
+//   L[rows, k0:k0+nb] = A[rows, k0:k0+nb] L_bb^-T    (workgroup b: 64 rows
+//                                                     k0 + nb + 64 b ...)
+// The last workgroup to arrive also stores L_bb and W = L_bb^-1 (ld kNB) for gg_potrs.  The
+// 64 x 64 factor is cheap enough to repeat in every workgroup, so a block
+// step is ONE launch with no dependency between its workgroups.
+// Thread t owns row i = t / 4 and the columns j = (t & 3) + 4 u, u < 16, of
+// the block in registers (factor: D; TRSM: its row of the panel).
+// Factor: right-looking, two barriers per column k (pivot, then column k in
+// LDS).  TRSM: right-looking over the columns; x_j is exchanged among the four
+// threads of a row by lane shuffles (they share a wave) -- no barriers.
+// Padding rows / columns >= nb form an identity block (no effect on < nb).
+__global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
+                                                           int n, int k0, int nb,
+                                                           double* __restrict__ W,
+                                                           int* __restrict__ status,
+                                                           int* __restrict__ arrived) {
+  __shared__ double Lf[kNB][kNB + 1];
+  __shared__ double colk[kNB];
+  __shared__ double invd[kNB];
+  __shared__ double piv;
+  __shared__ int last;
+  const int tid = threadIdx.x;
+  const int i = tid >> 2, q = tid & 3;
+  double* Abb = A + (int64_t)k0 * lda + k0;
+  double d[16];
 #pragma unroll
-  for (int j = 0; j < kNB; ++j) a[j] = (j <= ln) ? Ls[ln][j] : 0.0;
+  for (int u = 0; u < 16; ++u) {
+    const int j = q + 4 * u;
+    d[u] = (i < nb && j <= i) ? Abb[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
+  }
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < kNB; ++k) {
-    const double d = readlane_f64(a[k], k);
-    if (k < nb && (!(d > 0.0) || !isfinite(d))) bad = true;
-    const double lkk = sqrt(fmax(d, 0.0));
-    if (ln == k) a[k] = lkk;
-    else if (ln > k) a[k] = a[k] / lkk;
-    const double lik = (ln > k) ? a[k] : 0.0;
+    if (i == k && q == (k & 3)) piv = d[k >> 2];
+    __syncthreads();
+    const double dkk = piv;
+    if (k < nb && (!(dkk > 0.0) || !isfinite(dkk))) bad = true;
+    const double lkk = sqrt(fmax(dkk, 0.0));
+    const double il = 1.0 / lkk;
+    if (q == (k & 3) && i >= k) {
+      const double l = (i == k) ? lkk : d[k >> 2] * il;
+      d[k >> 2] = l;
+      colk[i] = l;
+      if (i == k) invd[k] = il;
+    }
+    __syncthreads();
+    const double li = colk[i];
 #pragma unroll
-    for (int j = k + 1; j < kNB; ++j) {
-      const double ljk = readlane_f64(a[k], j);   // L[j][k], held by lane j
-      a[j] = (j <= ln) ? fma(-lik, ljk, a[j]) : a[j];
+    for (int u = 0; u < 16; ++u) {
+      const int j = q + 4 * u;
+      if (j > k && j <= i) d[u] = fma(-li, colk[j], d[u]);
     }
   }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = q + 4 * u;
+    Lf[i][j] = (j <= i) ? d[u] : 0.0;
+  }
+  // The block is factored in place: the LAST workgroup to have read it (every
+  // workgroup holds the same L_bb) stores L_bb and W, so no workgroup can
+  // read a half-written block.  No waiting: the counter only picks the writer.
+  if (tid == 0) last = atomicAdd(arrived, 1) == (int)gridDim.x - 1;
   __syncthreads();
+  if (last) {
+    if (bad && tid == 0) *status = 1;
 #pragma unroll
-  for (int j = 0; j < kNB; ++j) Ls[ln][j] = a[j];
-  __syncthreads();
-  for (int r = 0; r < nb; ++r)
-    if (ln <= r) A[(int64_t)r * lda + ln] = Ls[r][ln];
-  // W = L^-1, lane ln owns column ln: W[r][ln] = (delta - sum_c L[r][c] W[c][ln]) / L[r][r]
-  double w[kNB];
+    for (int u = 0; u < 16; ++u) {
+      const int j = q + 4 * u;
+      if (i < nb && j <= i) Abb[(int64_t)i * lda + j] = d[u];
+    }
+    // W = L^-1: column c by the four threads of "row" c (c = i here): the
+    // sum over s < r splits by s mod 4, two shuffles reduce it, and the
+    // owner (s = r mod 4) keeps W[r][c] in w[r >> 2]
+    const int c = i;
+    double w[16];
 #pragma unroll
-  for (int r = 0; r < kNB; ++r) {
-    double acc = (r == ln) ? 1.0 : 0.0;
+    for (int u = 0; u < 16; ++u) w[u] = 0.0;
 #pragma unroll
-    for (int c = 0; c < r; ++c) acc = fma(-Ls[r][c], w[c], acc);
-    w[r] = acc / Ls[r][r];
+    for (int r = 0; r < kNB; ++r) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int s_ = q + 4 * u;
+        if (s_ < r && s_ >= c) sacc = fma(Lf[r][s_], w[u], sacc);
+      }
+      sacc += __shfl_xor(sacc, 1, 64);
+      sacc += __shfl_xor(sacc, 2, 64);
+      if (q == (r & 3)) w[r >> 2] = r < c ? 0.0 : ((r == c ? 1.0 : 0.0) - sacc) * invd[r];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = q + 4 * u;
+      W[(int64_t)r * kNB + c] = (r < nb && c < nb && c <= r) ? w[u] : 0.0;
+    }
+  }
+  // ---- TRSM for this workgroup's 64 rows below the block
+  const int64_t row = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB + i;
+  if (row >= n) return;
+  double* Ar = A + row * lda + k0;
+  double x[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = q + 4 * u;
+    x[u] = j < nb ? Ar[j] : 0.0;
+  }
+  const int lane = tid & 63;
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) {
+    double xj = 0.0;
+    if (q == (j & 3)) {
+      xj = x[j >> 2] * invd[j];
+      x[j >> 2] = xj;
+    }
+    xj = __shfl(xj, (lane & ~3) | (j & 3), 64);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int c = q + 4 * u;
+      if (c > j) x[u] = fma(-xj, Lf[c][j], x[u]);
+    }
   }
 #pragma unroll
-  for (int r = 0; r < kNB; ++r)
-    W[(int64_t)r * kNB + ln] = (r < nb && ln < nb && ln <= r) ? w[r] : 0.0;
-  if (ln == 0 && bad) *status = 1;
+  for (int u = 0; u < 16; ++u) {
+    const int j = q + 4 * u;
+    if (j < nb) Ar[j] = x[u];
+  }
 }
 
 __global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
@@ -423,7 +681,9 @@ int gg_add_diag(int n, const double* A_dev, int64_t lda, double s, const double*
 int gg_potrf_work_elems(int n, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(n >= 0 && elems, GG_ERR_VALUE, "bad argument");
-    *elems = gg::ceil_div(n, gg::kNB) * gg::kNB * gg::kNB + 16;
+    // W blocks, status / log-det slots, one arrival counter per block
+    const int64_t nblk = gg::ceil_div(n, gg::kNB);
+    *elems = nblk * gg::kNB * gg::kNB + 16 + gg::ceil_div(nblk, 2) + 1;
   });
 }
 
@@ -435,41 +695,80 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     const int nblk = (int)gg::ceil_div(n, gg::kNB);
     int* status = reinterpret_cast<int*>(winv_dev + (int64_t)nblk * gg::kNB * gg::kNB);
     double* ld = winv_dev + (int64_t)nblk * gg::kNB * gg::kNB + 8;
+    int* arrived = reinterpret_cast<int*>(winv_dev + (int64_t)nblk * gg::kNB * gg::kNB + 16);
     GG_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
-    // Two-level blocking: 64-wide diagonal blocks inside 256-wide panels.  A
-    // block's update reaches only the columns left in its panel; the columns
-    // right of the panel take one K = 256 update per panel, so the trailing
-    // matrix is streamed n / 256 times instead of n / 64.
+    GG_HIP(hipMemsetAsync(arrived, 0, (size_t)nblk * sizeof(int), s));
+    // Blocked right-looking factorisation with look-ahead.  Panels of kPanel
+    // columns; inside a panel each 64-column block is ONE launch (fused
+    // diagonal factor + TRSM, potrf_ftrsm_kernel) plus the in-panel update.
+    // After panel P:
+    //   narrow (stream s): the next panel's columns -= L_P L_P^T
+    //   wide (aux stream): every column right of the next panel -= L_P L_P^T
+    // so the next panel factors on s while the wide update (the bulk of the
+    // flops, one K = kPanel MFMA GEMM) runs beside it.  Ordering: wide(P)
+    // waits for panel P's factor; narrow(P -> P + 1) waits for wide(P - 1),
+    // which wrote the same columns.
     constexpr int kPanel = 4 * gg::kNB;
+    // GG_POTRF_LOOKAHEAD=0: the wide updates stay on s (A/B and debugging)
+    const char* la = getenv("GG_POTRF_LOOKAHEAD");
+    hipStream_t aux = (la != nullptr && atoi(la) == 0) ? s : gg::aux_stream();
+    std::vector<hipEvent_t> evs;
+    auto new_event = [&]() {
+      hipEvent_t e;
+      GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      evs.push_back(e);
+      return e;
+    };
+    hipEvent_t ev_wide = nullptr;   // last wide update issued on aux
+    {
+      hipEvent_t e0 = new_event();
+      GG_HIP(hipEventRecord(e0, s));
+      GG_HIP(hipStreamWaitEvent(aux, e0, 0));
+    }
     for (int P0 = 0; P0 < n; P0 += kPanel) {
       const int pend = std::min(n, P0 + kPanel);
       for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
         const int b = k0 / gg::kNB;
         const int nb = std::min(gg::kNB, n - k0);
-        double* Akk = A_dev + (int64_t)k0 * lda + k0;
-        double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
-        hipLaunchKernelGGL(gg::potrf_diag_kernel, dim3(1), dim3(gg::kNB), 0, s, Akk, lda, nb, Wk,
-                           status);
-        GG_LAUNCH_CHECK();
         const int rest = n - k0 - nb;
-        if (rest > 0) {
-          double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
-          // L21 = A21 W^T (in place: one column tile, each block owns its rows)
-          gg::gemm(false, true, rest, nb, nb, 1.0, A21, lda, Wk, gg::kNB, 0.0, A21, lda, 0, s);
-          const int pw = pend - (k0 + nb);   // panel columns right of this block
-          if (pw > 0) {
-            double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
-            gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
-          }
+        double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
+        const int grid = std::max(1, (int)gg::ceil_div(rest, gg::kNB));
+        hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, s, A_dev, lda, n, k0,
+                           nb, Wk, status, arrived + b);
+        GG_LAUNCH_CHECK();
+        const int pw = pend - (k0 + nb);   // panel columns right of this block
+        if (rest > 0 && pw > 0) {
+          const double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
+          double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
+          gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
         }
       }
-      const int trail = n - pend;
-      if (trail > 0) {  // A[pend:, pend:] -= L[pend:, P0:pend] L[pend:, P0:pend]^T (lower)
-        const double* Lp = A_dev + (int64_t)pend * lda + P0;
-        double* A22 = A_dev + (int64_t)pend * lda + pend;
-        gg::gemm(false, true, trail, trail, pend - P0, -1.0, Lp, lda, Lp, lda, 1.0, A22, lda, 1,
-                 s);
+      if (pend >= n) break;
+      const int nend = std::min(n, pend + kPanel);
+      const double* Lp = A_dev + (int64_t)pend * lda + P0;   // L[pend:, P0:pend]
+      // narrow: A[pend:, pend:nend] -= L[pend:, P] L[pend:nend, P]^T (lower)
+      if (ev_wide) GG_HIP(hipStreamWaitEvent(s, ev_wide, 0));
+      gg::gemm(false, true, n - pend, nend - pend, pend - P0, -1.0, Lp, lda, Lp, lda, 1.0,
+               A_dev + (int64_t)pend * lda + pend, lda, 1, s);
+      if (nend < n) {
+        // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on aux
+        hipEvent_t ef = new_event();
+        GG_HIP(hipEventRecord(ef, s));
+        GG_HIP(hipStreamWaitEvent(aux, ef, 0));
+        const double* Lw = A_dev + (int64_t)nend * lda + P0;
+        gg::gemm(false, true, n - nend, n - nend, pend - P0, -1.0, Lw, lda, Lw, lda, 1.0,
+                 A_dev + (int64_t)nend * lda + nend, lda, 1, aux);
+        ev_wide = new_event();
+        GG_HIP(hipEventRecord(ev_wide, aux));
+      } else {
+        ev_wide = nullptr;
       }
+    }
+    {
+      // join: s waits for everything issued on aux
+      hipEvent_t ej = new_event();
+      GG_HIP(hipEventRecord(ej, aux));
+      GG_HIP(hipStreamWaitEvent(s, ej, 0));
     }
     hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
     GG_LAUNCH_CHECK();
@@ -478,6 +777,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     GG_HIP(hipMemcpyAsync(&st, status, sizeof(int), hipMemcpyDeviceToHost, s));
     GG_HIP(hipMemcpyAsync(&lds, ld, sizeof(double), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
+    for (hipEvent_t e : evs) GG_HIP(hipEventDestroy(e));
     GG_REQUIRE(st == 0, GG_ERR_LINALG, "Matrix is not positive definite (device Cholesky)");
     if (logdet_host) *logdet_host = 2.0 * lds;
   });

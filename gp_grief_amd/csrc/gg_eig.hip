@@ -400,14 +400,16 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     hi_b[0] = hi_b[1] = 0;
   }
   __syncthreads();
-  // the chain buffers: cs / sn hold buffer 0, pw / v hold buffer 1
-  double* cbuf[2] = {cs, pw};
-  double* sbuf[2] = {sn, v};
+  // the chain buffers: cs / sn hold buffer 0, pw / v hold buffer 1 (selected
+  // per sweep, never through a pointer array: the stores must stay ds_write)
+  // Wave 0's loop state is wave-uniform (readfirstlane): its branches are
+  // scalar, and every lane runs the chain's arithmetic in lockstep.
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
   int l = 0, iter = 0;   // wave-0 state
   int kswp = 0;
   for (int k = 0;; ++k) {
     kswp = k;
-    if (wave == 0) {
+    if (wv == 0) {
       int mm = l;
       bool have = false;
       while (l < m && !bad) {
@@ -423,6 +425,7 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
             break;
           }
         }
+        mm = __builtin_amdgcn_readfirstlane(mm);
         if (mm == l) {   // d[l] converged
           ++l;
           iter = 0;
@@ -445,8 +448,8 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
         }
       } else {
         ++iter;
-        double* cb = cbuf[b];
-        double* sb = sbuf[b];
+        double* cb = b ? pw : cs;
+        double* sb = b ? v : sn;
         const double el = e[l], dl = d[l];
         double g = (d[l + 1] - dl) / (2.0 * el);
         double r = sqrt(fma(g, g, 1.0));
@@ -457,12 +460,15 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
         int i = mm - 1;
         bool early = false;
         for (; i >= l; --i) {
-          // prefetch the next step's operands (not written by this sweep yet)
-          const double ei_n = i > l ? e[i - 1] : 0.0;
-          const double di_n = i > l ? d[i - 1] : 0.0;
+          // prefetch the next step's operands (not written by this sweep yet;
+          // clamped, so the load is unconditional)
+          const int in = i > l ? i - 1 : l;
+          const double ei_n = e[in];
+          const double di_n = d[in];
           const double fo = sv * ei, bb = cv * ei;
+          const double bb2 = 2.0 * bb;
           const double h2 = fma(fo, fo, g * g);
-          if (h2 == 0.0) {
+          if (__builtin_amdgcn_readfirstlane(h2 == 0.0 ? 1 : 0)) {
             if (lane == 0) {
               e[i + 1] = 0.0;
               d[i + 1] = dip1 - pv;
@@ -480,13 +486,13 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
           hh = h2 * y;
           y = fma(0.5 * y, fma(-hh, y, 1.0), y);
           r = h2 * y;
-          if (lane == 0) e[i + 1] = r;
           sv = fo * y;
           cv = g * y;
           g = dip1 - pv;
-          r = fma(di - g, sv, 2.0 * cv * bb);
+          r = fma(di - g, sv, cv * bb2);
           pv = sv * r;
           if (lane == 0) {
+            e[i + 1] = h2 * y;
             d[i + 1] = g + pv;
             cb[i] = cv;
             sb[i] = sv;
@@ -510,8 +516,8 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
       // apply sweep k-1: rotations i = hi-1 .. lo on columns (i, i+1) of Z
       const int b = (k - 1) & 1;
       const int lo = lo_b[b], hi = hi_b[b];
-      const double* cb = cbuf[b];
-      const double* sb = sbuf[b];
+      const double* cb = b ? pw : cs;
+      const double* sb = b ? v : sn;
       for (int row = tid - 64; row < m && hi > lo; row += nt - 64) {
         double* Zr = A + (int64_t)row * ld;
         double cur = Zr[hi];

@@ -201,7 +201,9 @@ int gg_add_diag(int n, const double* A_dev, int64_t lda, double s, const double*
                 double* P_dev, int64_t ldp, gg_stream stream);
 /* Blocked Cholesky P = L L^T in place (lower), cho_factor, :153.  winv_dev
  * (gg_potrf_work_elems) receives the inverted diagonal blocks used by
- * gg_potrs; logdet_host = log det P.  Non-SPD -> GG_ERR_LINALG (synchronising). */
+ * gg_potrs; logdet_host = log det P.  Non-SPD -> GG_ERR_LINALG (synchronising).
+ * The trailing updates run on a second stream of the device (look-ahead);
+ * the call returns with all of its work complete. */
 int gg_potrf_work_elems(int n, int64_t* elems);
 int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet_host,
              gg_stream stream);
