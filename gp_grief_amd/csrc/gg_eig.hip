@@ -253,9 +253,10 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   double* cs = pw + m;
   double* sn = cs + m;
   double* red = sn + m;
-  int* rank = reinterpret_cast<int*>(red + 16);
+  double* junk = red + 16;   // 64 per-lane dummy slots (wave 0's chain stores)
+  int* rank = reinterpret_cast<int*>(junk + 64);
   __shared__ int bad;
-  const int64_t head = (((int64_t)7 * m + 16) * sizeof(double) + (int64_t)m * sizeof(int) + 15) &
+  const int64_t head = (((int64_t)7 * m + 80) * sizeof(double) + (int64_t)m * sizeof(int) + 15) &
                        ~int64_t(15);
   const int ld = kLds ? m + 1 : m;
   double* A = kLds ? reinterpret_cast<double*>(tq_lds + head) : work + work_offs[f];
@@ -456,15 +457,27 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
         g = d[mm] - dl + el / (g + copysign(r, g));
         double sv = 1.0, cv = 1.0, pv = 0.0;
         double dip1 = d[mm];            // d[i+1] before this step's update
-        double ei = e[mm - 1], di = d[mm - 1];
+        // operands e[i], d[i] of the step, of the next step, and two steps
+        // ahead: three slots whose roles rotate (the loop is unrolled by
+        // hand), so a load is consumed two steps after it is issued and no
+        // register move waits on it.  Loads are clamped to l: unconditional.
+        double ea = e[mm - 1], da = d[mm - 1];
+        const int i2 = mm - 2 > l ? mm - 2 : l;
+        double eb = e[i2], db = d[i2];
+        double ec = 0.0, dc = 0.0;
+        // lane 0 stores the chain's results; the other lanes store the same
+        // values to their own dummy slot, so the stores need no exec branch and
+        // the LDS counter waits stay exact
+        const bool l0 = lane == 0;
+        double* jk = junk + lane;
         int i = mm - 1;
         bool early = false;
-        for (; i >= l; --i) {
-          // prefetch the next step's operands (not written by this sweep yet;
-          // clamped, so the load is unconditional)
-          const int in = i > l ? i - 1 : l;
-          const double ei_n = e[in];
-          const double di_n = d[in];
+        // one rotation: cur (ei, di) -> results; loads e/d[i - 2] into (en, dn)
+        auto step = [&](double& ei, double& di, double& en, double& dn) -> bool {
+          if (i < l) return false;
+          const int i3 = i - 2 > l ? i - 2 : l;
+          en = e[i3];
+          dn = d[i3];
           const double fo = sv * ei, bb = cv * ei;
           const double bb2 = 2.0 * bb;
           const double h2 = fma(fo, fo, g * g);
@@ -475,7 +488,7 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
               e[mm] = 0.0;
             }
             early = true;
-            break;
+            return false;
           }
           // 1/r by the hardware reciprocal square root and two Newton steps
           // (the chain's latency: no IEEE sqrt + divide sequences).  h2 is a
@@ -485,22 +498,24 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
           y = fma(0.5 * y, fma(-hh, y, 1.0), y);
           hh = h2 * y;
           y = fma(0.5 * y, fma(-hh, y, 1.0), y);
-          r = h2 * y;
           sv = fo * y;
           cv = g * y;
           g = dip1 - pv;
           r = fma(di - g, sv, cv * bb2);
           pv = sv * r;
-          if (lane == 0) {
-            e[i + 1] = h2 * y;
-            d[i + 1] = g + pv;
-            cb[i] = cv;
-            sb[i] = sv;
-          }
+          *(l0 ? &e[i + 1] : jk) = h2 * y;
+          *(l0 ? &d[i + 1] : jk) = g + pv;
+          *(l0 ? &cb[i] : jk) = cv;
+          *(l0 ? &sb[i] : jk) = sv;
           g = fma(cv, r, -bb);
           dip1 = di;
-          ei = ei_n;
-          di = di_n;
+          --i;
+          return true;
+        };
+        for (;;) {
+          if (!step(ea, da, ec, dc)) break;
+          if (!step(eb, db, ea, da)) break;
+          if (!step(ec, dc, eb, db)) break;
         }
         if (lane == 0) {
           lo_b[b] = early ? i + 1 : l;
@@ -614,7 +629,7 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
       GG_HIP(hipMemsetAsync(dstamps, 0, 8 * 64 * sizeof(long long) * count, s));
     }
     if (!jacobi) {
-      const int64_t head = (((int64_t)7 * mmax + 16) * sizeof(double) +
+      const int64_t head = (((int64_t)7 * mmax + 80) * sizeof(double) +
                             (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
       const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
       const int iters = std::max(30, max_sweeps);

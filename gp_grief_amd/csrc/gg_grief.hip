@@ -12,7 +12,7 @@
 //     selected eigenvector rows; writes log|X| and sign(X) as an n x U table
 //     (U = sum_f u_f), i.e. exactly the reference's x_unique, per point.
 //   grief_phi_kernel: HBM-bound writer of Phi (n x p row-major, or p x n):
-//     one block owns 16 (32 transposed) data points (their table rows, as
+//     one block owns 64 (32 transposed) data points (their table rows, as
 //     signed values S exp(L), in LDS) and a 256-wide range of eigenfunctions
 //     j (their table columns c_{j,f} in LDS); every Phi element is d LDS
 //     loads and d multiplies, and the transposed tile is stored through LDS.
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void grief_tables_kernel(
   }
 }
 
-constexpr int kPhiRows = 16;    // data points per block (row-major Phi)
+constexpr int kPhiRows = 64;    // data points per block (row-major Phi)
 constexpr int kPhiRowsT = 32;   // data points per block (transposed Phi)
 constexpr int kPhiCols = 256;
 constexpr int kMaxDim = 64;
