@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "gg_internal.h"
@@ -431,39 +432,62 @@ void gemv(bool trans, int64_t R, int Cn, double alpha, const double* A, int64_t 
 // ------------------------------------------------------------------ Cholesky
 constexpr int kNB = 64;
 
-// Second stream of the calling device for gg_potrf's look-ahead (created once
-// per device at the lowest priority, never destroyed: it lives as long as the
-// process)
-hipStream_t aux_stream() {
+// Streams of the calling device for gg_potrf's look-ahead (created once per
+// device, never destroyed: they live as long as the process).  which 0: the
+// factorisation chain (the critical path) at the highest priority; 1: the
+// wide trailing updates at the lowest.
+hipStream_t aux_stream(int which) {
   static std::mutex mu;
-  static std::map<int, hipStream_t> streams;
+  static std::map<std::pair<int, int>, hipStream_t> streams;
   int dev = 0;
   GG_HIP(hipGetDevice(&dev));
   std::lock_guard<std::mutex> lk(mu);
-  auto it = streams.find(dev);
+  auto it = streams.find({dev, which});
   if (it != streams.end()) return it->second;
-  // lowest priority: the wide trailing updates yield the CUs to the
-  // factorisation chain on the caller's stream (the critical path)
   int least = 0, greatest = 0;
   GG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t st;
-  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, least));
-  streams[dev] = st;
+  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 0 ? greatest : least));
+  streams[{dev, which}] = st;
   return st;
+}
+
+// Lane-quad broadcast: the value of lane (lane & ~3) | s (DPP quad_perm).
+template <int s>
+__device__ __forceinline__ double quad_bcast(double v) {
+  constexpr int perm = s | (s << 2) | (s << 4) | (s << 6);
+  const long long bits = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)bits, perm, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(bits >> 32), perm, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// Sum over the four lanes of a quad (DPP quad_perm xor 1, then xor 2).
+__device__ __forceinline__ double quad_sum(double v) {
+  const long long b1 = __double_as_longlong(v);
+  const int lo1 = __builtin_amdgcn_mov_dpp((int)b1, 0xB1, 0xF, 0xF, false);
+  const int hi1 = __builtin_amdgcn_mov_dpp((int)(b1 >> 32), 0xB1, 0xF, 0xF, false);
+  v += __longlong_as_double(((long long)hi1 << 32) | (unsigned int)lo1);
+  const long long b2 = __double_as_longlong(v);
+  const int lo2 = __builtin_amdgcn_mov_dpp((int)b2, 0x4E, 0xF, 0xF, false);
+  const int hi2 = __builtin_amdgcn_mov_dpp((int)(b2 >> 32), 0x4E, 0xF, 0xF, false);
+  return v + __longlong_as_double(((long long)hi2 << 32) | (unsigned int)lo2);
 }
 
 // Fused diagonal-block factor + panel TRSM of one 64-column block (k0, nb):
 //   L_bb = chol(A[k0:k0+nb, k0:k0+nb])              (every workgroup, in LDS)
 //   L[rows, k0:k0+nb] = A[rows, k0:k0+nb] L_bb^-T    (workgroup b: 64 rows
 //                                                     k0 + nb + 64 b ...)
-// The last workgroup to arrive also stores L_bb and W = L_bb^-1 (ld kNB) for gg_potrs.  The
-// 64 x 64 factor is cheap enough to repeat in every workgroup, so a block
-// step is ONE launch with no dependency between its workgroups.
+// The last workgroup to arrive also stores L_bb and W = L_bb^-1 (ld kNB) for
+// gg_potrs.  The 64 x 64 factor is cheap enough to repeat in every workgroup,
+// so a block step is ONE launch with no dependency between its workgroups.
 // Thread t owns row i = t / 4 and the columns j = (t & 3) + 4 u, u < 16, of
-// the block in registers (factor: D; TRSM: its row of the panel).
-// Factor: right-looking, two barriers per column k (pivot, then column k in
-// LDS).  TRSM: right-looking over the columns; x_j is exchanged among the four
-// threads of a row by lane shuffles (they share a wave) -- no barriers.
+// the block in registers (factor: D; TRSM: its row of the panel).  Every loop
+// is unrolled, so "is column j past k" is a compile-time fact except inside
+// one group of four columns, handled by a select: the code has no divergent
+// branches.  Factor: right-looking, two barriers per column k (pivot, then
+// column k in LDS).  TRSM: right-looking over the columns; x_j is broadcast
+// among the four threads of a row (one quad) by DPP.  Entries above the
+// diagonal take harmless updates and are never stored.
 // Padding rows / columns >= nb form an identity block (no effect on < nb).
 __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
                                                            int n, int k0, int nb,
@@ -471,7 +495,7 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
                                                            int* __restrict__ status,
                                                            int* __restrict__ arrived) {
   __shared__ double Lf[kNB][kNB + 1];
-  __shared__ double colk[kNB];
+  __shared__ double colk[kNB + 256];   // column k, then one dummy slot per thread
   __shared__ double invd[kNB];
   __shared__ double piv;
   __shared__ int last;
@@ -487,24 +511,24 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < kNB; ++k) {
-    if (i == k && q == (k & 3)) piv = d[k >> 2];
+    const int ku = k >> 2, kq = k & 3;
+    if (tid == 4 * k + kq) piv = d[ku];
     __syncthreads();
     const double dkk = piv;
     if (k < nb && (!(dkk > 0.0) || !isfinite(dkk))) bad = true;
     const double lkk = sqrt(fmax(dkk, 0.0));
     const double il = 1.0 / lkk;
-    if (q == (k & 3) && i >= k) {
-      const double l = (i == k) ? lkk : d[k >> 2] * il;
-      d[k >> 2] = l;
-      colk[i] = l;
-      if (i == k) invd[k] = il;
-    }
+    const bool own = q == kq && i >= k;
+    const double lv = (i == k) ? lkk : d[ku] * il;
+    d[ku] = own ? lv : d[ku];
+    colk[own ? i : kNB + tid] = lv;
     __syncthreads();
     const double li = colk[i];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int j = q + 4 * u;
-      if (j > k && j <= i) d[u] = fma(-li, colk[j], d[u]);
+      if (4 * u + 3 <= k) continue;             // columns j <= k: final
+      const double upd = fma(-li, colk[q + 4 * u], d[u]);
+      d[u] = (4 * u > k) ? upd : (q > kq ? upd : d[u]);
     }
   }
 #pragma unroll
@@ -512,6 +536,8 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
     const int j = q + 4 * u;
     Lf[i][j] = (j <= i) ? d[u] : 0.0;
   }
+  __syncthreads();
+  if (tid < kNB) invd[tid] = 1.0 / Lf[tid][tid];
   // The block is factored in place: the LAST workgroup to have read it (every
   // workgroup holds the same L_bb) stores L_bb and W, so no workgroup can
   // read a half-written block.  No waiting: the counter only picks the writer.
@@ -524,9 +550,9 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
       const int j = q + 4 * u;
       if (i < nb && j <= i) Abb[(int64_t)i * lda + j] = d[u];
     }
-    // W = L^-1: column c by the four threads of "row" c (c = i here): the
-    // sum over s < r splits by s mod 4, two shuffles reduce it, and the
-    // owner (s = r mod 4) keeps W[r][c] in w[r >> 2]
+    // W = L^-1: column c = i by the four threads of the quad: the sum over
+    // s < r splits by s mod 4 (W[s][c] = 0 for s < c), a quad sum reduces it,
+    // and the owner (s = r mod 4) keeps W[r][c] in w[r >> 2]
     const int c = i;
     double w[16];
 #pragma unroll
@@ -536,12 +562,13 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
       double sacc = 0.0;
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
-        const int s_ = q + 4 * u;
-        if (s_ < r && s_ >= c) sacc = fma(Lf[r][s_], w[u], sacc);
+        if (4 * u >= r) continue;                 // s >= r for every q
+        const double t = fma(Lf[r][q + 4 * u], w[u], sacc);
+        sacc = (4 * u + 3 < r) ? t : (q + 4 * u < r ? t : sacc);
       }
-      sacc += __shfl_xor(sacc, 1, 64);
-      sacc += __shfl_xor(sacc, 2, 64);
-      if (q == (r & 3)) w[r >> 2] = r < c ? 0.0 : ((r == c ? 1.0 : 0.0) - sacc) * invd[r];
+      sacc = quad_sum(sacc);
+      const double wr = r < c ? 0.0 : ((r == c ? 1.0 : 0.0) - sacc) * invd[r];
+      w[r >> 2] = (q == (r & 3)) ? wr : w[r >> 2];
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -559,21 +586,26 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
     const int j = q + 4 * u;
     x[u] = j < nb ? Ar[j] : 0.0;
   }
-  const int lane = tid & 63;
+#define GG_TRSM_STEP(J, jq_)                                                         \
+  do {                                                                               \
+    const int ju_ = (J) >> 2;                                                        \
+    const double own_ = x[ju_] * invd[J];                                            \
+    x[ju_] = q == jq_ ? own_ : x[ju_];                                               \
+    const double xj_ = quad_bcast<jq_>(own_);                                        \
+    _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                 \
+      if (4 * u + 3 <= (J)) continue;                                                \
+      const double upd_ = fma(-xj_, Lf[q + 4 * u][J], x[u]);                         \
+      x[u] = (4 * u > (J)) ? upd_ : (q > jq_ ? upd_ : x[u]);                         \
+    }                                                                                \
+  } while (0)
 #pragma unroll
-  for (int j = 0; j < kNB; ++j) {
-    double xj = 0.0;
-    if (q == (j & 3)) {
-      xj = x[j >> 2] * invd[j];
-      x[j >> 2] = xj;
-    }
-    xj = __shfl(xj, (lane & ~3) | (j & 3), 64);
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int c = q + 4 * u;
-      if (c > j) x[u] = fma(-xj, Lf[c][j], x[u]);
-    }
+  for (int j = 0; j < kNB; j += 4) {
+    GG_TRSM_STEP(j, 0);
+    GG_TRSM_STEP(j + 1, 1);
+    GG_TRSM_STEP(j + 2, 2);
+    GG_TRSM_STEP(j + 3, 3);
   }
+#undef GG_TRSM_STEP
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int j = q + 4 * u;
@@ -702,16 +734,20 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     // columns; inside a panel each 64-column block is ONE launch (fused
     // diagonal factor + TRSM, potrf_ftrsm_kernel) plus the in-panel update.
     // After panel P:
-    //   narrow (stream s): the next panel's columns -= L_P L_P^T
-    //   wide (aux stream): every column right of the next panel -= L_P L_P^T
-    // so the next panel factors on s while the wide update (the bulk of the
-    // flops, one K = kPanel MFMA GEMM) runs beside it.  Ordering: wide(P)
-    // waits for panel P's factor; narrow(P -> P + 1) waits for wide(P - 1),
-    // which wrote the same columns.
+    //   narrow (chain stream cs, high priority): the next panel's columns
+    //     -= L_P L_P^T
+    //   wide (stream ws, low priority): every column right of the next panel
+    //     -= L_P L_P^T
+    // so the next panel factors on cs while the wide update (the bulk of the
+    // flops, one K = kPanel MFMA GEMM) runs beside it and yields CUs to the
+    // chain.  Ordering: wide(P) waits for panel P's factor; narrow(P -> P + 1)
+    // waits for wide(P - 1), which wrote the same columns; s joins both.
     constexpr int kPanel = 4 * gg::kNB;
-    // GG_POTRF_LOOKAHEAD=0: the wide updates stay on s (A/B and debugging)
+    // GG_POTRF_LOOKAHEAD=0: everything on s (A/B and debugging)
     const char* la = getenv("GG_POTRF_LOOKAHEAD");
-    hipStream_t aux = (la != nullptr && atoi(la) == 0) ? s : gg::aux_stream();
+    const bool lookahead = !(la != nullptr && atoi(la) == 0);
+    hipStream_t cs = lookahead ? gg::aux_stream(0) : s;   // factor chain, high priority
+    hipStream_t ws = lookahead ? gg::aux_stream(1) : s;   // wide updates, low priority
     std::vector<hipEvent_t> evs;
     auto new_event = [&]() {
       hipEvent_t e;
@@ -719,11 +755,12 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       evs.push_back(e);
       return e;
     };
-    hipEvent_t ev_wide = nullptr;   // last wide update issued on aux
-    {
+    hipEvent_t ev_wide = nullptr;   // last wide update issued on ws
+    if (lookahead) {
       hipEvent_t e0 = new_event();
       GG_HIP(hipEventRecord(e0, s));
-      GG_HIP(hipStreamWaitEvent(aux, e0, 0));
+      GG_HIP(hipStreamWaitEvent(cs, e0, 0));
+      GG_HIP(hipStreamWaitEvent(ws, e0, 0));
     }
     for (int P0 = 0; P0 < n; P0 += kPanel) {
       const int pend = std::min(n, P0 + kPanel);
@@ -733,42 +770,48 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         const int rest = n - k0 - nb;
         double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
         const int grid = std::max(1, (int)gg::ceil_div(rest, gg::kNB));
-        hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, s, A_dev, lda, n, k0,
-                           nb, Wk, status, arrived + b);
+        hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n,
+                           k0, nb, Wk, status, arrived + b);
         GG_LAUNCH_CHECK();
         const int pw = pend - (k0 + nb);   // panel columns right of this block
         if (rest > 0 && pw > 0) {
           const double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
           double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
-          gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, s);
+          gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, cs);
         }
       }
       if (pend >= n) break;
       const int nend = std::min(n, pend + kPanel);
       const double* Lp = A_dev + (int64_t)pend * lda + P0;   // L[pend:, P0:pend]
       // narrow: A[pend:, pend:nend] -= L[pend:, P] L[pend:nend, P]^T (lower)
-      if (ev_wide) GG_HIP(hipStreamWaitEvent(s, ev_wide, 0));
+      if (ev_wide) GG_HIP(hipStreamWaitEvent(cs, ev_wide, 0));
       gg::gemm(false, true, n - pend, nend - pend, pend - P0, -1.0, Lp, lda, Lp, lda, 1.0,
-               A_dev + (int64_t)pend * lda + pend, lda, 1, s);
+               A_dev + (int64_t)pend * lda + pend, lda, 1, cs);
       if (nend < n) {
-        // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on aux
-        hipEvent_t ef = new_event();
-        GG_HIP(hipEventRecord(ef, s));
-        GG_HIP(hipStreamWaitEvent(aux, ef, 0));
+        // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on ws
+        if (lookahead) {
+          hipEvent_t ef = new_event();
+          GG_HIP(hipEventRecord(ef, cs));
+          GG_HIP(hipStreamWaitEvent(ws, ef, 0));
+        }
         const double* Lw = A_dev + (int64_t)nend * lda + P0;
         gg::gemm(false, true, n - nend, n - nend, pend - P0, -1.0, Lw, lda, Lw, lda, 1.0,
-                 A_dev + (int64_t)nend * lda + nend, lda, 1, aux);
-        ev_wide = new_event();
-        GG_HIP(hipEventRecord(ev_wide, aux));
+                 A_dev + (int64_t)nend * lda + nend, lda, 1, ws);
+        if (lookahead) {
+          ev_wide = new_event();
+          GG_HIP(hipEventRecord(ev_wide, ws));
+        }
       } else {
         ev_wide = nullptr;
       }
     }
-    {
-      // join: s waits for everything issued on aux
-      hipEvent_t ej = new_event();
-      GG_HIP(hipEventRecord(ej, aux));
-      GG_HIP(hipStreamWaitEvent(s, ej, 0));
+    if (lookahead) {
+      // join: s waits for everything issued on cs and ws
+      hipEvent_t ec = new_event(), ew = new_event();
+      GG_HIP(hipEventRecord(ec, cs));
+      GG_HIP(hipEventRecord(ew, ws));
+      GG_HIP(hipStreamWaitEvent(s, ec, 0));
+      GG_HIP(hipStreamWaitEvent(s, ew, 0));
     }
     hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
     GG_LAUNCH_CHECK();
