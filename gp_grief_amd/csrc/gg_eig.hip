@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -226,7 +227,85 @@ __device__ __forceinline__ int tq_group(int L, int nt) {
   return g;
 }
 
-template <bool kLds>
+// Eigenvalues of the symmetric tridiagonal (d, e[0..m-2]) by multisection on
+// Sturm counts (ascending: group k finds the k-th smallest).  A group of G
+// lanes (G = the largest power of two <= blockDim / m, at most 8; the lanes of
+// a group share a wave) evaluates the count at G interior points of the
+// bracket at once, so each round shrinks it by G + 1; a ballot over the group
+// picks the new bracket.  Stops at an absolute width of 4 eps ||T|| -- the
+// accuracy of the QL path (LAPACK dstebz with abstol = 0 uses the same
+// absolute ulp * ||T|| tolerance).  The pivots' reciprocal is v_rcp_f64 + one
+// Newton step (only the sign of each pivot is counted).  e2 (m doubles of LDS)
+// receives e^2; red (>= 16) holds the Gershgorin bounds.
+__device__ void tq_bisect(const double* __restrict__ d, const double* __restrict__ e,
+                          double* __restrict__ e2, double* __restrict__ red, int m,
+                          double* __restrict__ lam) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < m; i += nt) e2[i] = (i < m - 1) ? e[i] * e[i] : 0.0;
+  if (tid == 0) {
+    double lo = d[0], hi = d[0], emax = 0.0;
+    for (int i = 0; i < m; ++i) {
+      const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < m - 1 ? fabs(e[i]) : 0.0);
+      lo = fmin(lo, d[i] - r);
+      hi = fmax(hi, d[i] + r);
+      if (i < m - 1) emax = fmax(emax, e[i] * e[i]);
+    }
+    const double nrm = fmax(fabs(lo), fabs(hi));
+    // widen the bracket as dstebz does (rounding of the Gershgorin bounds)
+    red[0] = lo - 2.1 * 2.220446049250313e-16 * nrm * m - 1e-300;
+    red[1] = hi + 2.1 * 2.220446049250313e-16 * nrm * m + 1e-300;
+    red[2] = fmax(2.2250738585072014e-308, 2.2250738585072014e-308 * emax);   // pivmin
+    red[3] = 4.0 * 2.220446049250313e-16 * fmax(nrm, 1e-300);                 // width
+  }
+  __syncthreads();
+  const double glo = red[0], ghi = red[1], pivmin = red[2], width = red[3];
+  int G = 1;
+  while (G < 8 && 2 * G * m <= nt) G *= 2;
+  const int lane = tid & 63, j = tid % G;
+  const int gbase = lane - j;                                  // group's first lane
+  const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << gbase;
+  const int ngroups = nt / G;
+  // every lane of a wave runs the same number of rounds (ballots need the
+  // whole group); groups past m idle through them
+  const int kmax = ((m + ngroups - 1) / ngroups) * ngroups;
+  for (int k = tid / G; k < kmax; k += ngroups) {
+    double lo = glo, hi = ghi;
+    bool live = k < m;
+    for (int it = 0; it < 200; ++it) {
+      const bool more = live && (hi - lo > width);
+      if (!__ballot(more)) break;
+      const double x = lo + (hi - lo) * (double)(j + 1) / (double)(G + 1);
+      int cnt = 0;
+      double q = d[0] - x;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+      for (int i = 1; i < m; ++i) {
+        double rq = __builtin_amdgcn_rcp(q);
+        rq = fma(rq, fma(-q, rq, 1.0), rq);
+        q = fma(-e2[i - 1], rq, d[i] - x);
+        if (fabs(q) < pivmin) q = -pivmin;
+        cnt += q < 0.0;
+      }
+      // first point of the group with more than k eigenvalues below it
+      const unsigned long long above = __ballot(cnt > k) & gmask;
+      if (more) {
+        const int first = above ? __ffsll((long long)above) - 1 - gbase : G;
+        const double nlo = first == 0 ? lo : lo + (hi - lo) * (double)first / (double)(G + 1);
+        const double nhi = first == G ? hi : lo + (hi - lo) * (double)(first + 1) / (double)(G + 1);
+        lo = nlo;
+        hi = nhi;
+      }
+    }
+    if (live && j == 0) lam[k] = 0.5 * (lo + hi);
+  }
+}
+
+// kMode 0: full decomposition (phases 1-4).  kMode 1: eigenvalues only, by
+// bisection on the tridiagonal (phases 1, 2, then tq_bisect): Z goes to Qout,
+// the tridiagonal (d, e) to work + work_offs[f] + m * m, the eigenvalues
+// (ascending) to lam_out -- the input of tridiag_invit_kernel, which computes
+// selected eigenvectors y of the tridiagonal (the eigenvectors are Z y).
+template <bool kLds, int kMode>
 __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     const int64_t* __restrict__ dims, const int64_t* __restrict__ offs,
     const double* __restrict__ Ain, double* __restrict__ Qout, double* __restrict__ lam_out,
@@ -385,6 +464,23 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   __syncthreads();
 
   stamp(2);
+  if (kMode == 1) {
+    // Z out (row-major), (d, e) to the work tail, eigenvalues by bisection
+    double* Q = Qout + offs[f];
+    for (int64_t q = tid; q < (int64_t)m * m; q += nt) {
+      const int r = (int)(q / m), c = (int)(q % m);
+      Q[q] = A[(int64_t)r * ld + c];
+    }
+    double* de = work + work_offs[f] + (int64_t)m * m;
+    for (int i = tid; i < m; i += nt) {
+      de[i] = d[i];
+      de[m + i] = e[i];
+    }
+    tq_bisect(d, e, v, red, m, lam_out + lam_offs[f]);
+    if (tid == 0) status[f] = 0;
+    stamp(3);
+    return;
+  }
   // ---- 3. implicit QL (tql2 / tqli) on (d, e) accumulating into Z's columns.
   // Wave 0 owns (d, e): it finds the next split point (ballot over its
   // lanes) and runs the sweep's scalar rotation chain (every lane computes
@@ -577,6 +673,186 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   stamp(4);
 }
 
+// Selected eigenvectors of the tridiagonal T = (d, e) by inverse iteration
+// (LAPACK dstein's scheme without its cluster reorthogonalisation: the host
+// only takes this path when every selected eigenvalue is separated from its
+// neighbours, so the vectors come out orthogonal to ~eps ||T|| / gap).
+// One wave per job (a factor and up to kInvB of its selected eigenvalues),
+// one lane per eigenvalue lambda: LU of T - lambda I with partial pivoting
+// (U with two superdiagonals), three solves from a pseudo-random start (the
+// grid factors are centrosymmetric: a symmetric start would miss every odd
+// eigenvector), scaled by the max norm each time; output the unit vector y
+// (largest component positive) as a row of Y.  The per-lane arrays live in
+// LDS, interleaved by lane.
+constexpr int kInvThreads = 64;
+
+__global__ __launch_bounds__(kInvThreads) void tridiag_invit_kernel(
+    const int* __restrict__ job_f, const int* __restrict__ job_s0, const int* __restrict__ job_n,
+    const int64_t* __restrict__ dims, const int64_t* __restrict__ de_offs,
+    const double* __restrict__ work, const double* __restrict__ lam,
+    const int64_t* __restrict__ lam_offs, const int* __restrict__ sel,
+    const int64_t* __restrict__ sel_offs, const int64_t* __restrict__ y_offs,
+    double* __restrict__ Y, int B) {
+  extern __shared__ __attribute__((aligned(16))) double iv[];
+  const int job = blockIdx.x;
+  const int f = job_f[job];
+  const int m = (int)dims[f];
+  const int v = threadIdx.x;
+  if (v >= job_n[job]) return;
+  const double* d = work + de_offs[f];
+  const double* e = d + m;
+  const int s = job_s0[job] + v;                       // global selection index
+  const int local = s - (int)sel_offs[f];
+  const double lmb = lam[lam_offs[f] + sel[s]];
+  // lane-interleaved LDS arrays: u0, u1, u2, lm, pv, y
+  auto at = [&](int a, int i) -> double& { return iv[((int64_t)a * m + i) * B + v]; };
+  double tn = 0.0;   // ||T||_inf
+  for (int i = 0; i < m; ++i)
+    tn = fmax(tn, fabs(d[i]) + (i > 0 ? fabs(e[i - 1]) : 0.0) + (i < m - 1 ? fabs(e[i]) : 0.0));
+  const double tiny = fmax(2.220446049250313e-16 * tn, 1e-300);
+  auto guard = [&](double p) { return fabs(p) < tiny ? (p < 0.0 ? -tiny : tiny) : p; };
+  // ---- LU with partial pivoting of T - lambda I
+  double p = d[0] - lmb, q = m > 1 ? e[0] : 0.0, r = 0.0;
+  for (int i = 0; i + 1 < m; ++i) {
+    const double c = e[i], an = d[i + 1] - lmb, bn = (i + 2 < m) ? e[i + 1] : 0.0;
+    if (fabs(p) >= fabs(c)) {
+      const double pg = guard(p);
+      const double mult = c / pg;
+      at(0, i) = pg;
+      at(1, i) = q;
+      at(2, i) = r;
+      at(3, i) = mult;
+      at(4, i) = 0.0;
+      p = an - mult * q;
+      q = bn - mult * r;
+    } else {
+      const double mult = p / c;
+      at(0, i) = c;
+      at(1, i) = an;
+      at(2, i) = bn;
+      at(3, i) = mult;
+      at(4, i) = 1.0;
+      p = q - mult * an;
+      q = r - mult * bn;
+    }
+    r = 0.0;
+  }
+  at(0, m - 1) = guard(p);
+  at(1, m - 1) = 0.0;
+  at(2, m - 1) = 0.0;
+  // ---- start vector: hashed, in (-1, 1)
+  for (int i = 0; i < m; ++i) {
+    unsigned h = (unsigned)i * 2654435761u ^ ((unsigned)(sel[s] + 1) * 40503u);
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    at(5, i) = (double)(h >> 8) * (1.0 / 8388608.0) - 1.0;
+  }
+  for (int it = 0; it < 3; ++it) {
+    // forward: the row operations of the factorisation on y
+    for (int i = 0; i + 1 < m; ++i) {
+      double yi = at(5, i), yn = at(5, i + 1);
+      if (at(4, i) != 0.0) {
+        const double t = yi;
+        yi = yn;
+        yn = t;
+      }
+      at(5, i) = yi;
+      at(5, i + 1) = yn - at(3, i) * yi;
+    }
+    // back substitution with U (diag, two superdiagonals)
+    double y1 = 0.0, y2 = 0.0, ymax = 0.0;
+    for (int i = m - 1; i >= 0; --i) {
+      const double yi = (at(5, i) - at(1, i) * y1 - at(2, i) * y2) / at(0, i);
+      at(5, i) = yi;
+      y2 = y1;
+      y1 = yi;
+      ymax = fmax(ymax, fabs(yi));
+    }
+    const double sc = ymax > 0.0 ? 1.0 / ymax : 1.0;
+    for (int i = 0; i < m; ++i) at(5, i) *= sc;
+  }
+  double nrm = 0.0, big = 0.0;
+  int ib = 0;
+  for (int i = 0; i < m; ++i) {
+    const double yi = at(5, i);
+    nrm = fma(yi, yi, nrm);
+    if (fabs(yi) > big) {
+      big = fabs(yi);
+      ib = i;
+    }
+  }
+  const double sc = (at(5, ib) < 0.0 ? -1.0 : 1.0) / sqrt(nrm);
+  double* yo = Y + y_offs[f] + (int64_t)local * m;
+  for (int i = 0; i < m; ++i) yo[i] = at(5, i) * sc;
+}
+
+// Orthonormalise the rows of V (k x m, row-major) in place by classical
+// Gram-Schmidt applied twice ("CGS2"), last row first: row v loses its
+// components along rows v+1 .. k-1, twice, then is normalised.  One workgroup
+// per matrix; the dot products split over (row, column stripe) and reduce
+// through LDS, so each row costs a handful of barriers.  Used on inverse
+// iteration's eigenvectors, which are already orthogonal to ~eps ||T|| / gap:
+// the second pass takes the result to ~eps.
+constexpr int kOrthoThreads = 256;
+
+__global__ __launch_bounds__(kOrthoThreads) void rows_orthonormalize_kernel(
+    const int64_t* __restrict__ ks, const int64_t* __restrict__ ms,
+    const int64_t* __restrict__ offs, double* __restrict__ Vall) {
+  __shared__ double cdot[kOrthoThreads];
+  __shared__ double red[kOrthoThreads / 64];
+  const int f = blockIdx.x;
+  const int k = (int)ks[f], m = (int)ms[f];
+  double* V = Vall + offs[f];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int v = k - 1; v >= 0; --v) {
+    double* Vv = V + (int64_t)v * m;
+    const int nw = k - 1 - v;   // rows already orthonormal: v+1 .. k-1
+    for (int pass = 0; pass < 2 && nw > 0; ++pass) {
+      // c_w = V_w . V_v: thread group per row w (up to nt rows at a time)
+      for (int w0 = 0; w0 < nw; w0 += nt) {
+        const int nrow = min(nt, nw - w0);
+        const int tpr = max(1, nt / nrow) >= 64 ? 64 : (nt / nrow >= 32 ? 32 :
+                        nt / nrow >= 16 ? 16 : nt / nrow >= 8 ? 8 : nt / nrow >= 4 ? 4 :
+                        nt / nrow >= 2 ? 2 : 1);
+        const int w = w0 + tid / tpr, l = tid % tpr;
+        double acc = 0.0;
+        if (tid / tpr < nrow) {
+          const double* Vw = V + (int64_t)(v + 1 + w) * m;
+          for (int i = l; i < m; i += tpr) acc = fma(Vw[i], Vv[i], acc);
+        }
+        for (int off = tpr >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        __syncthreads();
+        if (tid / tpr < nrow && l == 0) cdot[tid / tpr] = acc;
+        __syncthreads();
+        // V_v -= sum_w c_w V_w over this batch of rows
+        for (int i = tid; i < m; i += nt) {
+          double s = Vv[i];
+          for (int ww = 0; ww < nrow; ++ww)
+            s = fma(-cdot[ww], V[(int64_t)(v + 1 + w0 + ww) * m + i], s);
+          Vv[i] = s;
+        }
+        __syncthreads();
+      }
+    }
+    // normalise
+    double ss = 0.0;
+    for (int i = tid; i < m; i += nt) ss = fma(Vv[i], Vv[i], ss);
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    double tot = 0.0;
+    for (int q = 0; q < nt / 64; ++q) tot += red[q];
+    const double inv = tot > 0.0 ? 1.0 / sqrt(tot) : 1.0;
+    for (int i = tid; i < m; i += nt) Vv[i] *= inv;
+    __syncthreads();
+  }
+}
+
+// work doubles per factor: the HBM copy of A / Z (m x m) and, for the
+// eigenvalue-only mode, the tridiagonal (d, e) after it
+inline int64_t eig_work_per(int64_t m) { return std::max(2 * m * m, m * m + 2 * m); }
+
 }  // namespace gg
 
 extern "C" {
@@ -585,7 +861,7 @@ int gg_sym_eig_work_elems(int count, const int64_t* m, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(count >= 0 && elems, GG_ERR_VALUE, "bad argument");
     int64_t e = 0;
-    for (int i = 0; i < count; ++i) e += 2 * m[i] * m[i];
+    for (int i = 0; i < count; ++i) e += gg::eig_work_per(m[i]);
     *elems = e;
   });
 }
@@ -606,7 +882,7 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
       meta[3 * count + i] = woff;
       off += m[i] * m[i];
       loff += m[i];
-      woff += 2 * m[i] * m[i];
+      woff += gg::eig_work_per(m[i]);
     }
     GG_REQUIRE(work_elems >= woff, GG_ERR_VALUE, "eigensolver work buffer too small");
     hipStream_t s = gg::as_stream(stream);
@@ -634,15 +910,15 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
       const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
       const int iters = std::max(30, max_sweeps);
       if (lds_a) {
-        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<true>),
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<true, 0>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(gg::tridiag_ql_kernel<true>, dim3(count), dim3(gg::kTqThreads), lds, s,
+        hipLaunchKernelGGL((gg::tridiag_ql_kernel<true, 0>), dim3(count), dim3(gg::kTqThreads), lds, s,
                            dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
                            work_dev, dmeta + 3 * count, iters, dstatus, dstamps);
       } else {
-        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<false>),
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<false, 0>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL(gg::tridiag_ql_kernel<false>, dim3(count), dim3(gg::kTqThreads), lds,
+        hipLaunchKernelGGL((gg::tridiag_ql_kernel<false, 0>), dim3(count), dim3(gg::kTqThreads), lds,
                            s, dmeta, dmeta + count, A_dev, Q_dev, lam_dev, dmeta + 2 * count,
                            work_dev, dmeta + 3 * count, iters, dstatus, dstamps);
       }
@@ -682,6 +958,148 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     for (int i = 0; i < count; ++i)
       GG_REQUIRE(st[i] == 0, GG_ERR_LINALG,
                  "eigensolver did not converge on factor " + std::to_string(i));
+  });
+}
+
+
+int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double* Z_dev,
+                       double* lam_dev, double* work_dev, int64_t work_elems, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(count >= 1 && m && A_dev && Z_dev && lam_dev && work_dev, GG_ERR_VALUE,
+               "bad argument");
+    std::vector<int64_t> meta(5 * (size_t)count, 0);
+    int64_t off = 0, loff = 0, woff = 0;
+    int mmax = 1;
+    for (int i = 0; i < count; ++i) {
+      GG_REQUIRE(m[i] >= 1 && m[i] <= 2048, GG_ERR_VALUE, "factor size must be in [1, 2048]");
+      meta[i] = m[i];
+      meta[count + i] = off;
+      meta[2 * count + i] = loff;
+      meta[3 * count + i] = woff;
+      off += m[i] * m[i];
+      loff += m[i];
+      woff += gg::eig_work_per(m[i]);
+      mmax = std::max<int>(mmax, (int)m[i]);
+    }
+    GG_REQUIRE(work_elems >= woff, GG_ERR_VALUE, "eigensolver work buffer too small");
+    hipStream_t s = gg::as_stream(stream);
+    int64_t* dmeta = nullptr;
+    GG_HIP(hipMallocAsync(&dmeta, meta.size() * sizeof(int64_t), s));
+    GG_HIP(hipMemcpyAsync(dmeta, meta.data(), meta.size() * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+    int* dstatus = reinterpret_cast<int*>(dmeta + 4 * count);
+    const bool lds_a = mmax <= gg::kLdsMaxM;
+    const int64_t head = (((int64_t)7 * mmax + 80) * sizeof(double) +
+                          (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
+    const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
+    if (lds_a) {
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<true, 1>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL((gg::tridiag_ql_kernel<true, 1>), dim3(count), dim3(gg::kTqThreads), lds,
+                         s, dmeta, dmeta + count, A_dev, Z_dev, lam_dev, dmeta + 2 * count,
+                         work_dev, dmeta + 3 * count, 0, dstatus, nullptr);
+    } else {
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<false, 1>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL((gg::tridiag_ql_kernel<false, 1>), dim3(count), dim3(gg::kTqThreads), lds,
+                         s, dmeta, dmeta + count, A_dev, Z_dev, lam_dev, dmeta + 2 * count,
+                         work_dev, dmeta + 3 * count, 0, dstatus, nullptr);
+    }
+    GG_LAUNCH_CHECK();
+    GG_HIP(hipFreeAsync(dmeta, s));
+  });
+}
+
+int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_dev,
+                               int64_t work_elems, const double* lam_dev, const int* nsel,
+                               const int* sel, double* Y_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(count >= 1 && m && work_dev && lam_dev && nsel && sel && Y_dev, GG_ERR_VALUE,
+               "bad argument");
+    // per factor: m, (d, e) offset, lambda offset, selection offset, Y offset
+    std::vector<int64_t> fm(5 * (size_t)count);
+    int64_t woff = 0, loff = 0, soff = 0, yoff = 0;
+    int mmax = 1;
+    for (int i = 0; i < count; ++i) {
+      GG_REQUIRE(m[i] >= 1 && m[i] <= 2048 && nsel[i] >= 0 && nsel[i] <= m[i], GG_ERR_VALUE,
+                 "bad selection");
+      for (int k = 0; k < nsel[i]; ++k)
+        GG_REQUIRE(sel[soff + k] >= 0 && sel[soff + k] < m[i], GG_ERR_VALUE,
+                   "selected index out of range");
+      fm[i] = m[i];
+      fm[count + i] = woff + m[i] * m[i];
+      fm[2 * count + i] = loff;
+      fm[3 * count + i] = soff;
+      fm[4 * count + i] = yoff;
+      woff += gg::eig_work_per(m[i]);
+      loff += m[i];
+      soff += nsel[i];
+      yoff += (int64_t)nsel[i] * m[i];
+      mmax = std::max<int>(mmax, (int)m[i]);
+    }
+    GG_REQUIRE(work_elems >= woff, GG_ERR_VALUE, "eigensolver work buffer too small");
+    if (soff == 0) return;
+    // lanes per wave: the interleaved per-lane arrays (6 m doubles) fit LDS
+    const int B = (int)std::max<int64_t>(
+        1, std::min<int64_t>(gg::kInvThreads, (150 * 1024) / (6 * (int64_t)mmax * 8)));
+    std::vector<int> jf, js, jn;
+    for (int i = 0, s0 = 0; i < count; s0 += nsel[i], ++i)
+      for (int k = 0; k < nsel[i]; k += B) {
+        jf.push_back(i);
+        js.push_back(s0 + k);
+        jn.push_back(std::min(B, nsel[i] - k));
+      }
+    const int njobs = (int)jf.size();
+    // one device block: int64 factor table, then int job tables and selection
+    const size_t bytes = fm.size() * sizeof(int64_t) + (3 * (size_t)njobs + soff) * sizeof(int);
+    hipStream_t s = gg::as_stream(stream);
+    unsigned char* dbuf = nullptr;
+    GG_HIP(hipMallocAsync(&dbuf, bytes, s));
+    std::vector<unsigned char> hbuf(bytes);
+    memcpy(hbuf.data(), fm.data(), fm.size() * sizeof(int64_t));
+    int* ip = reinterpret_cast<int*>(hbuf.data() + fm.size() * sizeof(int64_t));
+    memcpy(ip, jf.data(), njobs * sizeof(int));
+    memcpy(ip + njobs, js.data(), njobs * sizeof(int));
+    memcpy(ip + 2 * njobs, jn.data(), njobs * sizeof(int));
+    memcpy(ip + 3 * njobs, sel, soff * sizeof(int));
+    GG_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, s));
+    const int64_t* dfm = reinterpret_cast<const int64_t*>(dbuf);
+    const int* dip = reinterpret_cast<const int*>(dbuf + fm.size() * sizeof(int64_t));
+    const size_t lds = (size_t)6 * mmax * B * sizeof(double);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_invit_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(gg::tridiag_invit_kernel, dim3(njobs), dim3(gg::kInvThreads), lds, s, dip,
+                       dip + njobs, dip + 2 * njobs, dfm, dfm + count, work_dev, lam_dev,
+                       dfm + 2 * count, dip + 3 * njobs, dfm + 3 * count, dfm + 4 * count, Y_dev,
+                       B);
+    GG_LAUNCH_CHECK();
+    GG_HIP(hipFreeAsync(dbuf, s));
+  });
+}
+
+
+int gg_rows_orthonormalize(int count, const int64_t* k, const int64_t* m, double* V_dev,
+                           gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(count >= 1 && k && m && V_dev, GG_ERR_VALUE, "bad argument");
+    std::vector<int64_t> meta(3 * (size_t)count);
+    int64_t off = 0;
+    for (int i = 0; i < count; ++i) {
+      GG_REQUIRE(k[i] >= 0 && m[i] >= 1 && k[i] <= m[i], GG_ERR_VALUE, "bad row block");
+      meta[i] = k[i];
+      meta[count + i] = m[i];
+      meta[2 * count + i] = off;
+      off += k[i] * m[i];
+    }
+    hipStream_t s = gg::as_stream(stream);
+    int64_t* dmeta = nullptr;
+    GG_HIP(hipMallocAsync(&dmeta, meta.size() * sizeof(int64_t), s));
+    GG_HIP(hipMemcpyAsync(dmeta, meta.data(), meta.size() * sizeof(int64_t),
+                          hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(gg::rows_orthonormalize_kernel, dim3(count), dim3(gg::kOrthoThreads), 0,
+                       s, dmeta, dmeta + count, dmeta + 2 * count, V_dev);
+    GG_LAUNCH_CHECK();
+    GG_HIP(hipFreeAsync(dmeta, s));
   });
 }
 

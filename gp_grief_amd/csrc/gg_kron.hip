@@ -158,12 +158,16 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
       for (int r = 0; r < 4; ++r)
         if (rowok[r] && cok) Y[rowoff[r] + co] = acc[t][r];
     }
-  } else if (!kRecomp) {
-    // shift / dots epilogue (textbook p.q, fused-CG p.q, r.q, q.q): the loads
-    // of tile t + 1 are issued before tile t's stores.  CDNA4 retires vmcnt in
-    // order and stores count, so a load issued after a store cannot be waited
-    // for without also waiting for that store's write acknowledgement; issued
-    // first, the wait for tile t + 1 skips the stores of tile t.
+  } else if (!kXUpd) {
+    // shift / dots epilogue (textbook p.q, fused-CG p.q, r.q, q.q; layout 1
+    // also recomputes p_new = r + beta p_old from xs = p_old and stores it):
+    // the loads of tile t + 1 are issued before tile t's stores.  CDNA4
+    // retires vmcnt in order and stores count, so a load issued after a store
+    // cannot be waited for without also waiting for that store's write
+    // acknowledgement; issued first, the wait for tile t + 1 skips the stores
+    // of tile t.
+    const bool first = kRecomp && fz.sc->first != 0;
+    const double beta = kRecomp ? fz.sc->beta : 0.0;
     double xv[2][4], ev[2][4];
     // kIdent: the wave's 16 x p output block is contiguous, so every address
     // is a uniform base (SGPRs) plus a 32-bit lane byte offset (saddr form):
@@ -175,6 +179,7 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
     const char* xbase = reinterpret_cast<const char*>(xs + (kIdent ? b0u * p : 0));
     const char* ebase = reinterpret_cast<const char*>(er + (kIdent ? b0u * p : 0));
     char* ybase = reinterpret_cast<char*>(Y + (kIdent ? b0u * p : 0));
+    char* pbase = kRecomp ? reinterpret_cast<char*>(fz.ep_out + (kIdent ? b0u * p : 0)) : nullptr;
     auto boff = [&](int r, int t) -> uint32_t {
       return (uint32_t)(((lane >> 4) + 4 * r) * p + (int)colj(t)) * 8u;
     };
@@ -211,17 +216,21 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (row_ok(r) && cok) {
-          const double pv = xv[cb][r];
+          double pv = xv[cb][r];
+          if (kRecomp) pv = first ? ev[cb][r] : fma(beta, pv, ev[cb][r]);
           const double v = fma(shift, pv, acc[t][r]);
           dsum = fma(pv, v, dsum);
           if (edots) {
             rqsum = fma(ev[cb][r], v, rqsum);
             qqsum = fma(v, v, qqsum);
           }
-          if (kIdent)
+          if (kIdent) {
             *reinterpret_cast<double*>(ybase + boff(r, t)) = v;
-          else
+            if (kRecomp) *reinterpret_cast<double*>(pbase + boff(r, t)) = pv;
+          } else {
             Y[rowoff[r] + co] = v;
+            if (kRecomp) fz.ep_out[rowoff[r] + co] = pv;
+          }
         }
       }
     }

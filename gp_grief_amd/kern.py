@@ -20,6 +20,7 @@ matrix Phi run on the MI355X.  GPy is not part of this stack (SURVEY 2, row
 """
 import ctypes
 import logging
+import os
 from copy import deepcopy
 
 import numpy as np
@@ -27,7 +28,8 @@ import numpy as np
 from . import device as dev
 from . import native
 from .grid import InducingGrid
-from .tensors import KronMatrix, KhatriRaoMatrix, SelectionMatrixSparse, device_sym_eig
+from .tensors import (KronMatrix, KhatriRaoMatrix, SelectionMatrixSparse, device_sym_eig,
+                      device_sym_eig_tridiag, device_sym_eig_tridiag_vectors)
 
 logger = logging.getLogger(__name__)
 
@@ -423,22 +425,80 @@ class GriefKernel(GridKernel):
     def _setup_inducing_cov(self):
         """Factors, device eigendecomposition, top-p selection (:168-190).
 
-        Cached on the base-kernel parameters like the reference.
+        Cached on the base-kernel parameters like the reference.  Every factor
+        eigenvalue enters the selection, but Phi needs only the eigenvectors of
+        the selected indices: on a cache miss the factors are tridiagonalised,
+        their eigenvalues found by bisection, and only the selected
+        eigenvectors computed (inverse iteration + one GEMM) -- unless a
+        selected eigenvalue is not separated from its neighbours (relative gap
+        below _SUBSET_GAP), then the full QL decomposition is used.  With
+        opt_kernel_params the finite-difference gradient compares LMLs of
+        perturbed bases, which must all come from the same eigensolver (the
+        batched prefetch is the full one): those kernels always take the full
+        path.  GG_EIG_SUBSET=0 forces the full path.
         """
         base = super(GriefKernel, self).parameters
         if self._old_base_kern_params is not None and \
                 np.array_equal(self._old_base_kern_params, base):
             return
-        Q, lam = self._factor_eigs(base)
-        self._Quu = KronMatrix(Q)
+        key = np.asarray(base, dtype=np.float64).tobytes()
+        hit = self._eig_cache.get(key)
+        qsel_dev = None
+        if hit is None and not self.opt_kernel_params and \
+                os.environ.get("GG_EIG_SUBSET", "1") != "0":
+            Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
+            factors = [np.asarray(k) for k in Kuu.K]
+            lam, handle = device_sym_eig_tridiag(factors)
+            eig_pos, log_lam = self._select(lam)
+            Sp = [SelectionMatrixSparse((col, lam[i].shape[0])) for i, col in enumerate(eig_pos.T)]
+            if self._separated(lam, [S.unique for S in Sp]):
+                qsel_dev = device_sym_eig_tridiag_vectors(handle, [S.unique for S in Sp])
+                self._Quu_factors = factors
+                self._Quu_full = None
+        if qsel_dev is None:
+            Q, lam = self._factor_eigs(base)
+            eig_pos, log_lam = self._select(lam)
+            Sp = [SelectionMatrixSparse((col, Q[i].shape[0])) for i, col in enumerate(eig_pos.T)]
+            self._Quu_full = KronMatrix(Q)
+        self._log_lam = log_lam
+        self._Sp = Sp
+        self._old_base_kern_params = base
+        self._build_device_basis(qsel_dev)
+
+    # inverse iteration converges by eps ||T|| / gap per step and the Cholesky
+    # QR restores orthogonality: a gap of 1e-10 ||T|| leaves each vector within
+    # ~2e-6 of the true one -- the same bound any backward-stable solver (QL,
+    # LAPACK) has at that gap
+    _SUBSET_GAP = 1e-10
+
+    def _select(self, lam):
         all_eig_vals = KronMatrix(lam)
         n_eigs = int(min(self.n_eigs, all_eig_vals.shape[0]))
-        eig_pos, self._log_lam = all_eig_vals.find_extremum_eigs(
-            n_eigs=n_eigs, mode='largest', log_expand=True)[:2]
-        self._Sp = [SelectionMatrixSparse((col, Q[i].shape[0]))
-                    for i, col in enumerate(eig_pos.T)]
-        self._old_base_kern_params = base
-        self._build_device_basis()
+        return all_eig_vals.find_extremum_eigs(n_eigs=n_eigs, mode='largest',
+                                               log_expand=True)[:2]
+
+    def _separated(self, lam, selections):
+        """Every selected eigenvalue at least _SUBSET_GAP * max|lambda| away from
+        its neighbours (inverse iteration then gives orthogonal vectors)."""
+        for l, sel in zip(lam, selections):
+            l = np.asarray(l)
+            if l.size < 2:
+                continue
+            tol = self._SUBSET_GAP * np.abs(l).max()
+            gaps = np.diff(l)
+            for k in np.asarray(sel).reshape(-1):
+                if (k > 0 and gaps[k - 1] < tol) or (k < l.size - 1 and gaps[k] < tol):
+                    return False
+        return True
+
+    @property
+    def _Quu(self):
+        """Per-factor eigenvectors (KronMatrix); after a subset setup the full
+        decomposition is computed on first access."""
+        if getattr(self, "_Quu_full", None) is None and getattr(self, "_Quu_factors", None):
+            Q, _ = device_sym_eig(self._Quu_factors)
+            self._Quu_full = KronMatrix(Q)
+        return self._Quu_full
 
     _EIG_CACHE_MAX = 64
 
@@ -488,7 +548,9 @@ class GriefKernel(GridKernel):
             self._cache_put(key, (Q[i * d:(i + 1) * d], lam[i * d:(i + 1) * d]))
         return len(keys)
 
-    def _build_device_basis(self):
+    def _build_device_basis(self, qsel_dev=None):
+        """Device basis tables; qsel_dev (subset setup): the selected
+        eigenvector rows Q_f^T[unique_f, :] already on the device."""
         d = self.grid_dim
         qsel, xg, us, ms, col0 = [], [], [], [], []
         cidx = np.zeros((self.n_eigs, d), dtype=np.int32)
@@ -496,11 +558,15 @@ class GriefKernel(GridKernel):
         for f in range(d):
             i = d - 1 - f
             S = self._Sp[f]
-            Qf = np.asarray(self._Quu.K[f])
-            qsel.append(dev.to_device(np.ascontiguousarray(Qf.T[S.unique, :])))
+            if qsel_dev is not None:
+                qsel.append(qsel_dev[f].contiguous())
+                ms.append(int(qsel_dev[f].shape[1]))
+            else:
+                Qf = np.asarray(self._Quu.K[f])
+                qsel.append(dev.to_device(np.ascontiguousarray(Qf.T[S.unique, :])))
+                ms.append(int(Qf.shape[0]))
             xg.append(dev.to_device(np.asarray(self.grid.xg[i], dtype=np.float64).reshape(-1)))
             us.append(int(S.unique.size))
-            ms.append(int(Qf.shape[0]))
             col0.append(c)
             cidx[:, f] = c + np.asarray(S.unique_inverse).reshape(-1)
             c += int(S.unique.size)

@@ -70,6 +70,12 @@ SIGNATURES = {
     "gg_sym_eig_batched": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
                            ctypes.c_int, _vp],
     "gg_sym_eig_work_elems": [ctypes.c_int, _c_i64p, _c_i64p],
+    "gg_sym_eig_tridiag": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
+                           _vp],
+    "gg_sym_eig_tridiag_vectors": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_int64, _c_dp,
+                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                   _c_dp, _vp],
+    "gg_rows_orthonormalize": [ctypes.c_int, _c_i64p, _c_i64p, _c_dp, _vp],
     "gg_cov": [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_dp,
                ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
     "gg_grief_tables": [ctypes.c_int, ctypes.c_double, ctypes.c_double, _c_dp, ctypes.c_int64,

@@ -10,7 +10,9 @@ Where the arithmetic lives:
   * every N-sized operation (matvec, transposed matvec, the eigenvalue divide of
     solve_schur, shifted log-det, Kronecker-structured solves) runs on the
     device through the C ABI (gp_grief_amd.native);
-  * per-factor eigendecompositions run on the device (parallel Jacobi);
+  * per-factor eigendecompositions run on the device (Householder
+    tridiagonalisation + implicit QL; for the GRIEF setup, bisection + inverse
+    iteration for the selected eigenvectors only);
   * factor-sized bookkeeping (diag of factors, expand of small Kronecker
     products, per-factor Cholesky / inverse used to build a device operator,
     the top-p eigen-selection) stays on the host exactly as in the reference,
@@ -144,6 +146,74 @@ def device_sym_eig(factors, max_sweeps=40):
         o += mi * mi
         lo += mi
     return outQ, outL
+
+
+def device_sym_eig_tridiag(factors):
+    """Eigenvalues of symmetric factors (ascending, host arrays) by Householder
+    tridiagonalisation + bisection on the device, plus a handle for
+    device_sym_eig_tridiag_vectors (the GRIEF setup needs every eigenvalue but
+    only the selected eigenvectors: grief_kernel.py:168-190)."""
+    L = native.lib()
+    mats = [np.asarray(f, dtype=np.float64) for f in factors]
+    for f in mats:
+        if f.ndim != 2 or f.shape[0] != f.shape[1]:
+            raise AssertionError("factor must be square")
+    m = [f.shape[0] for f in mats]
+    A = dev.to_device(np.concatenate([f.reshape(-1) for f in mats]))
+    Z = dev.empty(A.numel())
+    lam = dev.empty(sum(m))
+    marr = native.i64_array(m)
+    we = ctypes.c_int64()
+    native.check(L.gg_sym_eig_work_elems(len(m), marr, ctypes.byref(we)))
+    work = dev.empty(max(we.value, 1))
+    native.check(L.gg_sym_eig_tridiag(len(m), marr, native.dptr(A), native.dptr(Z),
+                                      native.dptr(lam), native.dptr(work), we.value,
+                                      native.stream_ptr()), "gg_sym_eig_tridiag")
+    lh = dev.to_host(lam)
+    out, o = [], 0
+    for mi in m:
+        out.append(lh[o:o + mi].copy())
+        o += mi
+    return out, dict(m=m, Z=Z, lam=lam, work=work, work_elems=we.value)
+
+
+def device_sym_eig_tridiag_vectors(handle, selections):
+    """Unit eigenvectors of the selected (ascending-order) indices per factor as
+    device tensors V_f (len(sel_f) x m_f; row k = eigenvector sel_f[k], i.e.
+    the rows Q_f^T[sel_f, :]): inverse iteration on the tridiagonal, then
+    V_f = Y_f Z_f^T on the MFMA GEMM and a re-orthonormalisation of the rows
+    (gg_rows_orthonormalize) so they are orthonormal to ~eps."""
+    from . import dense
+    L = native.lib()
+    m = handle["m"]
+    assert len(selections) == len(m)
+    sel = [np.asarray(s, dtype=np.int64).reshape(-1) for s in selections]
+    nsel = (ctypes.c_int * len(m))(*[int(s.size) for s in sel])
+    flat = np.concatenate(sel) if sum(s.size for s in sel) else np.zeros(0, dtype=np.int64)
+    carr = (ctypes.c_int * max(flat.size, 1))(*[int(v) for v in flat])
+    Y = dev.empty(max(sum(int(s.size) * mi for s, mi in zip(sel, m)), 1))
+    native.check(L.gg_sym_eig_tridiag_vectors(
+        len(m), native.i64_array(m), native.dptr(handle["work"]), handle["work_elems"],
+        native.dptr(handle["lam"]), nsel, carr, native.dptr(Y), native.stream_ptr()),
+        "gg_sym_eig_tridiag_vectors")
+    V = dev.empty(max(sum(int(s.size) * mi for s, mi in zip(sel, m)), 1))
+    out, oy, oz = [], 0, 0
+    for s, mi in zip(sel, m):
+        k = int(s.size)
+        Yf = Y[oy:oy + k * mi].view(k, mi)
+        Zf = handle["Z"][oz:oz + mi * mi].view(mi, mi)
+        Vf = V[oy:oy + k * mi].view(k, mi)
+        if k:
+            dense.matmul(Yf, Zf, tb=True, C=Vf)
+        out.append(Vf)
+        oy += k * mi
+        oz += mi * mi
+    # inverse iteration leaves neighbours ~eps ||T|| / gap from orthogonal:
+    # classical Gram-Schmidt twice, largest eigenvalue (last row) first
+    native.check(L.gg_rows_orthonormalize(len(m), native.i64_array([int(s.size) for s in sel]),
+                                          native.i64_array(m), native.dptr(V),
+                                          native.stream_ptr()), "gg_rows_orthonormalize")
+    return out
 
 
 class KronMatrix(object):

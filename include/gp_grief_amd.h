@@ -140,13 +140,34 @@ int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream 
 
 /* --------------------------------------- per-factor symmetric eigensolver
  * KronMatrix.schur / svd / eig_vals per factor   kron_matrix.py:161-200, 355-366
- * Parallel cyclic (two-sided) Jacobi on device, one workgroup per matrix.  A_dev: `count`
- * row-major m[i] x m[i] symmetric matrices concatenated; on return Q_dev holds
- * the eigenvectors (columns) and lam_dev the eigenvalues, ascending.          */
+ * Householder tridiagonalisation + implicit QL on device, one workgroup per
+ * matrix (GG_EIG=jacobi: parallel cyclic Jacobi).  A_dev: `count` row-major
+ * m[i] x m[i] symmetric matrices concatenated; on return Q_dev holds the
+ * eigenvectors (columns) and lam_dev the eigenvalues, ascending.              */
 int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double* Q_dev,
                        double* lam_dev, double* work_dev, int64_t work_elems,
                        int max_sweeps, gg_stream stream);
 int gg_sym_eig_work_elems(int count, const int64_t* m, int64_t* elems);
+/* Subset path (GRIEF setup, grief_kernel.py:168-190 needs every eigenvalue but
+ * only the eigenvectors of the selected indices):
+ *   gg_sym_eig_tridiag: Householder tridiagonalisation A = Z T Z^T; Z_dev gets
+ *     Z (row-major, like Q_dev), lam_dev the eigenvalues of T (= of A,
+ *     ascending) by bisection; T is kept in work_dev (gg_sym_eig_work_elems).
+ *   gg_sym_eig_tridiag_vectors: for factor i the nsel[i] eigenvalue indices
+ *     sel (host, concatenated over factors) -> unit eigenvectors y of T by
+ *     inverse iteration, rows of Y_dev (concatenated nsel[i] x m[i] blocks);
+ *     the eigenvectors of A are Z y (one GEMM).  Valid when every selected
+ *     eigenvalue is separated from its neighbours (the caller checks; no
+ *     cluster reorthogonalisation).                                           */
+int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double* Z_dev,
+                       double* lam_dev, double* work_dev, int64_t work_elems, gg_stream stream);
+int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_dev,
+                               int64_t work_elems, const double* lam_dev, const int* nsel,
+                               const int* sel, double* Y_dev, gg_stream stream);
+/* Rows of each k[i] x m[i] block of V_dev (concatenated, row-major)
+ * orthonormalised in place (classical Gram-Schmidt twice, last row first). */
+int gg_rows_orthonormalize(int count, const int64_t* k, const int64_t* m, double* V_dev,
+                           gg_stream stream);
 
 
 /* ------------------------------------------------------- GRIEF basis (P2)

@@ -280,3 +280,81 @@ def test_grief_p_system_cg_matches_cholesky(gg, case):
     assert rel(mean_g[:, 0], z["pred_mean"]) < 1e-6
     ll = float(np.squeeze(mg.log_likelihood()))
     assert abs(ll - z["lml"]) < 1e-6 * abs(z["lml"])
+
+
+# ------------------------------------------------ eigensolver subset path
+def _grid_factor(m, ls, var=1.0, noise=1e-12):
+    g = np.linspace(0, 1, m)
+    return var * np.exp(-0.5 * (g[:, None] - g[None, :]) ** 2 / ls ** 2) + noise * np.eye(m)
+
+
+@pytest.mark.parametrize("m,ls,k", [(128, 0.1, 20), (200, 0.05, 30), (32, 0.2, 8), (5, 0.5, 5)])
+def test_eig_subset_vs_full(gg, m, ls, k):
+    """Bisection eigenvalues and inverse-iteration eigenvectors of the
+    tridiagonalised factor (the GRIEF setup's subset path) against the full
+    QL decomposition and numpy's LAPACK eigh: eigenvalues to 1e-13 ||K||,
+    the top-k eigenvectors to 1e-9 (up to sign), orthonormal to 1e-12."""
+    from gp_grief_amd.tensors import (device_sym_eig, device_sym_eig_tridiag,
+                                      device_sym_eig_tridiag_vectors)
+    F = [_grid_factor(m, ls), _grid_factor(m, 1.3 * ls, var=2.0)]
+    lam, h = device_sym_eig_tridiag(F)
+    Q, lamq = device_sym_eig(F)
+    for f in range(len(F)):
+        ln = np.linalg.eigvalsh(F[f])
+        scale = np.abs(ln).max()
+        assert np.all(np.diff(lam[f]) >= 0)
+        assert np.abs(lam[f] - ln).max() <= 1e-13 * scale * m
+        assert np.abs(lam[f] - lamq[f]).max() <= 1e-13 * scale * m
+    sel = [np.arange(m - k, m), np.arange(m - k // 2, m)]
+    V = device_sym_eig_tridiag_vectors(h, sel)
+    for f in range(len(F)):
+        Vh = V[f].cpu().numpy()
+        assert Vh.shape == (sel[f].size, m)
+        assert np.abs(Vh @ Vh.T - np.eye(sel[f].size)).max() < 1e-12
+        Qs = Q[f][:, sel[f]].T
+        signs = np.sign(np.sum(Vh * Qs, axis=1)).reshape(-1, 1)
+        assert np.abs(Vh - signs * Qs).max() < 1e-9
+        # eigen-residual against the input factor
+        lv = lam[f][sel[f]]
+        assert np.abs(Vh @ F[f] - lv[:, None] * Vh).max() < 1e-12 * np.abs(lam[f]).max()
+
+
+def test_grief_subset_setup_matches_full(gg, monkeypatch):
+    """GPGriefModel on the subset setup (default) and on the full QL setup
+    (GG_EIG_SUBSET=0): same selection, LML to 1e-10, predictions to 1e-9."""
+    rng = np.random.default_rng(7)
+    d, m, n, p = 3, 48, 3000, 300
+    x = rng.random((n, d))
+    y = (np.sin(5 * x).sum(axis=1) + 0.1 * rng.standard_normal(n)).reshape(-1, 1)
+    xt = rng.random((200, d))
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GG_EIG_SUBSET", flag)
+        kl = [gg.kern.RBF(1, variance=1.0, lengthscale=0.15 + 0.03 * i) for i in range(d)]
+        grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1)] * d)
+        kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+        model = gg.models.GPGriefModel(x, y, kern, noise_var=0.05)
+        ll = float(np.squeeze(model.log_likelihood()))
+        mean = np.asarray(model.predict(xt)[0]).reshape(-1)
+        subset = kern._Quu_full is None
+        out.append((ll, mean, kern._log_lam.copy(), subset))
+    (l1, m1, g1, s1), (l0, m0, g0, s0) = out
+    assert s1 and not s0
+    assert np.allclose(g1, g0, rtol=1e-11, atol=1e-11)
+    assert abs(l1 - l0) <= 1e-10 * abs(l0)
+    assert rel(m1, m0) < 1e-9
+
+
+def test_grief_subset_falls_back_on_clusters(gg, monkeypatch):
+    """A factor with a clustered spectrum (a kernel so short that K ~ I) fails
+    the separation test: the setup takes the full QL path and stays correct."""
+    monkeypatch.setenv("GG_EIG_SUBSET", "1")
+    rng = np.random.default_rng(8)
+    d, m, n, p = 2, 24, 800, 40
+    x = rng.random((n, d))
+    y = rng.standard_normal((n, 1))
+    kl = [gg.kern.RBF(1, variance=1.0, lengthscale=1e-4) for _ in range(d)]
+    grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1)] * d)
+    kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+    kern._setup_inducing_cov()
+    assert kern._Quu_full is not None
