@@ -613,6 +613,86 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
   }
 }
 
+// Triangular solve with ONE right-hand side as a single launch: workgroup j
+// owns block row b (forward: b = j; backward, L^T: b = nblk - 1 - j), so the
+// dependency order equals the dispatch order and every block it waits on
+// belongs to a workgroup dispatched before it (no deadlock: the waits only
+// ever point backwards).  It streams its off-diagonal blocks in readiness
+// order -- each block's L values are loaded before its flag is polled, so
+// the critical step after the flag is one vector load and 16 FMAs -- then
+// applies the stored inverse diagonal block W_b, stores its part of the
+// solution and releases its flag.  Thread (i, q) = (t / 4, t % 4) owns row i
+// of the block and the quarter q of each 64-wide inner product; the quad
+// sums by DPP.  Flags: agent-scope release / acquire (the L2 is per XCD), a
+// bounded spin (status <- 2 instead of a hang; the host raises).
+constexpr int kTrsvSpin = 1 << 24;
+
+template <bool kTrans>
+__global__ __launch_bounds__(256) void trsv_chain_kernel(int n, const double* __restrict__ L,
+                                                         int64_t lda,
+                                                         const double* __restrict__ Winv,
+                                                         double* B, int* flags,
+                                                         int* __restrict__ status) {
+  __shared__ double rhs[kNB];
+  __shared__ int ok;
+  const int nblk = (n + kNB - 1) / kNB;
+  const int b = kTrans ? nblk - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int k0 = b * kNB, nb = min(kNB, n - k0);
+  const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
+  const int row = k0 + i;
+  if (tid == 0) ok = 1;
+  double acc = 0.0;
+  const int ndep = kTrans ? nblk - 1 - b : b;
+  for (int t = 0; t < ndep; ++t) {
+    const int c = kTrans ? nblk - 1 - t : t;       // dependencies in readiness order
+    const int c0 = c * kNB;
+    double lv[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = c0 + 16 * q + u;
+      // forward: L[row][j]; backward (L^T): L[j][row]
+      lv[u] = (row < n && j < n) ? (kTrans ? L[(int64_t)j * lda + row] : L[(int64_t)row * lda + j])
+                                 : 0.0;
+    }
+    if (tid == 0) {
+      int spin = 0;
+      while (__hip_atomic_load(&flags[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spin > kTrsvSpin) {
+          ok = 0;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (!ok) break;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = c0 + 16 * q + u;
+      if (j < n) acc = fma(lv[u], B[j], acc);
+    }
+  }
+  acc = quad_sum(acc);
+  if (q == 0) rhs[i] = (i < nb) ? B[row] - acc : 0.0;
+  __syncthreads();
+  // x_b = W_b rhs (forward) or W_b^T rhs (backward)
+  const double* W = Winv + (int64_t)b * kNB * kNB;
+  double y = 0.0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int k = 16 * q + u;
+    y = fma(kTrans ? W[(int64_t)k * kNB + i] : W[(int64_t)i * kNB + k], rhs[k], y);
+  }
+  y = quad_sum(y);
+  if (q == 0 && i < nb) B[row] = y;
+  __threadfence();   // every thread's stores visible device-wide before the flag
+  __syncthreads();
+  if (tid == 0) {
+    if (!ok) *status = 2;
+    __hip_atomic_store(&flags[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += log(A[(int64_t)i * lda + i]);
@@ -845,6 +925,28 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
     hipStream_t s = gg::as_stream(stream);
     const int nblk = (int)gg::ceil_div(n, gg::kNB);
     const bool tri = (which & 4) != 0;
+    // one right-hand side: each direction is ONE chained launch
+    // (trsv_chain_kernel) instead of a GEMM pair per block row
+    const char* ch = getenv("GG_TRSV_CHAIN");
+    if (r == 1 && !tri && ldb == 1 && !(ch != nullptr && atoi(ch) == 0)) {
+      int* flags = nullptr;
+      GG_HIP(hipMallocAsync(&flags, (2 * (size_t)nblk + 1) * sizeof(int), s));
+      GG_HIP(hipMemsetAsync(flags, 0, (2 * (size_t)nblk + 1) * sizeof(int), s));
+      int* st = flags + 2 * nblk;
+      if (which & 1)
+        hipLaunchKernelGGL(gg::trsv_chain_kernel<false>, dim3(nblk), dim3(256), 0, s, n, L_dev,
+                           lda, winv_dev, B_dev, flags, st);
+      if (which & 2)
+        hipLaunchKernelGGL(gg::trsv_chain_kernel<true>, dim3(nblk), dim3(256), 0, s, n, L_dev,
+                           lda, winv_dev, B_dev, flags + nblk, st);
+      GG_LAUNCH_CHECK();
+      int hst = 0;
+      GG_HIP(hipMemcpyAsync(&hst, st, sizeof(int), hipMemcpyDeviceToHost, s));
+      GG_HIP(hipFreeAsync(flags, s));
+      GG_HIP(hipStreamSynchronize(s));
+      GG_REQUIRE(hst == 0, GG_ERR_RUNTIME, "chained triangular solve timed out");
+      return;
+    }
     if (which & 1) {
       for (int b = 0; b < nblk; ++b) {
         const int k0 = b * gg::kNB, nb = std::min(gg::kNB, n - k0);
