@@ -490,23 +490,71 @@ __device__ __forceinline__ double quad_sum(double v) {
 // diagonal take harmless updates and are never stored.
 // Padding rows / columns >= nb form an identity block (no effect on < nb).
 __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
-                                                           int n, int k0, int nb,
+                                                           int n, int k0, int nb, int P0,
                                                            double* __restrict__ W,
                                                            int* __restrict__ status,
                                                            int* __restrict__ arrived) {
   __shared__ double Lf[kNB][kNB + 1];
+  __shared__ double Lb[kNB][kNB + 1];   // panel rows of the block / its update
+  __shared__ double Lr[kNB][kNB + 1];   // panel rows of this workgroup's rows / their update
   __shared__ double colk[kNB + 256];   // column k, then one dummy slot per thread
   __shared__ double invd[kNB];
   __shared__ double piv;
   __shared__ int last;
   const int tid = threadIdx.x;
   const int i = tid >> 2, q = tid & 3;
+  const int lane = tid & 63, wave = tid >> 6;
   double* Abb = A + (int64_t)k0 * lda + k0;
+  const int64_t rbase = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB;   // this WG's rows
+  // ---- left-looking update by the panel's earlier columns [P0, k0) (the
+  // in-panel update, MFMA): D -= L_b L_b^T, R -= L_r L_b^T with L_b =
+  // L[k0:k0+64, P0:k0], L_r = L[rows, P0:k0], 64 columns per LDS chunk.  Wave
+  // w owns output rows 16w .. 16w+15 (4 column tiles of each product).
+  const bool upd = k0 > P0;
+  d4 dacc[4], racc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    dacc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    racc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  }
+  for (int c0 = P0; c0 < k0; c0 += kNB) {
+    for (int e = tid; e < kNB * kNB; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      Lb[r][c] = r < nb ? A[(int64_t)(k0 + r) * lda + c0 + c] : 0.0;
+      Lr[r][c] = (rbase + r < n) ? A[(rbase + r) * lda + c0 + c] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kNB / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double ad = Lb[16 * wave + (lane & 15)][kk];
+      const double ar = Lr[16 * wave + (lane & 15)][kk];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double bv = Lb[16 * t + (lane & 15)][kk];
+        dacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ad, bv, dacc[t], 0, 0, 0);
+        racc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv, racc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (upd) {
+    // MFMA result layout: row 4 r + (lane >> 4), column lane & 15 of tile t
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Lb[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = dacc[t][r];
+        Lr[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = racc[t][r];
+      }
+    __syncthreads();
+  }
   double d[16];
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int j = q + 4 * u;
-    d[u] = (i < nb && j <= i) ? Abb[(int64_t)i * lda + j] : (i == j ? 1.0 : 0.0);
+    d[u] = (i < nb && j <= i) ? Abb[(int64_t)i * lda + j] - (upd ? Lb[i][j] : 0.0)
+                              : (i == j ? 1.0 : 0.0);
   }
   bool bad = false;
 #pragma unroll
@@ -584,7 +632,7 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int j = q + 4 * u;
-    x[u] = j < nb ? Ar[j] : 0.0;
+    x[u] = j < nb ? Ar[j] - (upd ? Lr[i][j] : 0.0) : 0.0;
   }
 #define GG_TRSM_STEP(J, jq_)                                                         \
   do {                                                                               \
@@ -690,6 +738,24 @@ __global__ __launch_bounds__(256) void trsv_chain_kernel(int n, const double* __
   if (tid == 0) {
     if (!ok) *status = 2;
     __hip_atomic_store(&flags[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// dst[c][r] = src[r][c] (rows x cols -> cols x rows), 32 x 32 LDS tiles
+__global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict__ src,
+                                                        int64_t lds, int rows, int cols,
+                                                        double* __restrict__ dst, int64_t ldd) {
+  __shared__ double tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < rows && c < cols) ? src[(int64_t)r * lds + c] : 0.0;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (c < cols && r < rows) dst[(int64_t)c * ldd + r] = tile[tx][k];
   }
 }
 
@@ -842,6 +908,16 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipStreamWaitEvent(cs, e0, 0));
       GG_HIP(hipStreamWaitEvent(ws, e0, 0));
     }
+    // two transposed-panel buffers (kPanel x ldt each), stream-ordered
+    const int64_t ldt = (n + 1) & ~1;   // even: 16-byte aligned rows for the DMA
+    double* lt_buf = nullptr;
+    if (n > kPanel) GG_HIP(hipMallocAsync(&lt_buf, 2 * (size_t)kPanel * ldt * sizeof(double), s));
+    if (lookahead && lt_buf) {
+      hipEvent_t ea = new_event();   // the allocation is ordered on s
+      GG_HIP(hipEventRecord(ea, s));
+      GG_HIP(hipStreamWaitEvent(cs, ea, 0));
+      GG_HIP(hipStreamWaitEvent(ws, ea, 0));
+    }
     for (int P0 = 0; P0 < n; P0 += kPanel) {
       const int pend = std::min(n, P0 + kPanel);
       for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
@@ -850,22 +926,30 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         const int rest = n - k0 - nb;
         double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
         const int grid = std::max(1, (int)gg::ceil_div(rest, gg::kNB));
+        // the block's update by the panel's earlier blocks is left-looking,
+        // inside the same launch (no in-panel GEMM)
         hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n,
-                           k0, nb, Wk, status, arrived + b);
+                           k0, nb, P0, Wk, status, arrived + b);
         GG_LAUNCH_CHECK();
-        const int pw = pend - (k0 + nb);   // panel columns right of this block
-        if (rest > 0 && pw > 0) {
-          const double* A21 = A_dev + (int64_t)(k0 + nb) * lda + k0;
-          double* A22 = A_dev + (int64_t)(k0 + nb) * lda + (k0 + nb);
-          gg::gemm(false, true, rest, pw, nb, -1.0, A21, lda, A21, lda, 1.0, A22, lda, 1, cs);
-        }
+        (void)rest;
       }
       if (pend >= n) break;
       const int nend = std::min(n, pend + kPanel);
-      const double* Lp = A_dev + (int64_t)pend * lda + P0;   // L[pend:, P0:pend]
+      const int pw = pend - P0;
+      // the panel's rows below it, transposed (k-major, pw x (n - pend)) into
+      // one of two buffers (panel P reuses the buffer of P - 2, whose wide
+      // update cs already waited for), so both updates below are TN products
+      // on the LDS-DMA Gram kernel instead of NT register-staged GEMMs
+      double* LT = lt_buf + (int64_t)((P0 / kPanel) & 1) * kPanel * ldt;
+      {
+        dim3 tg((unsigned)gg::ceil_div(pw, 32), (unsigned)gg::ceil_div(n - pend, 32));
+        hipLaunchKernelGGL(gg::transpose_kernel, tg, dim3(256), 0, cs,
+                           A_dev + (int64_t)pend * lda + P0, lda, n - pend, pw, LT, ldt);
+        GG_LAUNCH_CHECK();
+      }
       // narrow: A[pend:, pend:nend] -= L[pend:, P] L[pend:nend, P]^T (lower)
       if (ev_wide) GG_HIP(hipStreamWaitEvent(cs, ev_wide, 0));
-      gg::gemm(false, true, n - pend, nend - pend, pend - P0, -1.0, Lp, lda, Lp, lda, 1.0,
+      gg::gemm(true, false, n - pend, nend - pend, pw, -1.0, LT, ldt, LT, ldt, 1.0,
                A_dev + (int64_t)pend * lda + pend, lda, 1, cs);
       if (nend < n) {
         // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on ws
@@ -874,8 +958,8 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
           GG_HIP(hipEventRecord(ef, cs));
           GG_HIP(hipStreamWaitEvent(ws, ef, 0));
         }
-        const double* Lw = A_dev + (int64_t)nend * lda + P0;
-        gg::gemm(false, true, n - nend, n - nend, pend - P0, -1.0, Lw, lda, Lw, lda, 1.0,
+        const double* Lw = LT + (nend - pend);
+        gg::gemm(true, false, n - nend, n - nend, pw, -1.0, Lw, ldt, Lw, ldt, 1.0,
                  A_dev + (int64_t)nend * lda + nend, lda, 1, ws);
         if (lookahead) {
           ev_wide = new_event();
@@ -893,6 +977,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipStreamWaitEvent(s, ec, 0));
       GG_HIP(hipStreamWaitEvent(s, ew, 0));
     }
+    if (lt_buf) GG_HIP(hipFreeAsync(lt_buf, s));
     hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
     GG_LAUNCH_CHECK();
     int st = 0;

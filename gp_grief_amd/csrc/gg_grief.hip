@@ -114,7 +114,11 @@ constexpr int kMaxDim = 64;
 // kR kPhiCols), so each Phi element is d LDS loads and d multiplies: the
 // kernel is bound by the Phi store.  Transposed (p x n): the kR x 256 tile
 // goes through LDS so each eigenfunction row is stored as a kR-long run.
-template <int kR, bool kT>
+// kD > 0: d == kD known at compile time -- each thread keeps its d table
+// columns in registers, so an element is d LDS loads + d multiplies (kD == 0:
+// any d <= kMaxDim, indices re-read from LDS).  Row-major Phi is written with
+// non-temporal stores (8 n p bytes stream past the caches).
+template <int kR, bool kT, int kD>
 __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
     const double* __restrict__ Ltab, const double* __restrict__ Stab, int U, int64_t n,
     const int* __restrict__ cidx, int d, const double* __restrict__ log_lam, int p,
@@ -129,18 +133,29 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
   const int rows = (int)min<int64_t>(kR, n - a0);
   for (int e = threadIdx.x; e < rows * U; e += blockDim.x)
     sT[e] = Stab[a0 * U + e] * exp(Ltab[a0 * U + e]);
-  if (j < p)
+  if (kD == 0 && j < p)
     for (int f = 0; f < d; ++f) sC[f * kPhiCols + threadIdx.x] = cidx[(int64_t)j * d + f];
+  int creg[kD > 0 ? kD : 1];
+  if (kD > 0) {
+#pragma unroll
+    for (int f = 0; f < kD; ++f) creg[f] = j < p ? cidx[(int64_t)j * kD + f] : 0;
+  }
   __syncthreads();
   if (j < p) {
     const double sc = exp(-0.5 * log_lam[j]);
     for (int r = 0; r < rows; ++r) {
       double v = sc;
-      for (int f = 0; f < d; ++f) v *= sT[r * U + sC[f * kPhiCols + threadIdx.x]];
+      const double* tr = sT + r * U;
+      if (kD > 0) {
+#pragma unroll
+        for (int f = 0; f < kD; ++f) v *= tr[creg[f]];
+      } else {
+        for (int f = 0; f < d; ++f) v *= tr[sC[f * kPhiCols + threadIdx.x]];
+      }
       if (kT)
         sO[threadIdx.x * (kR + 1) + r] = v;
       else
-        Phi[(a0 + r) * p + j] = v;
+        __builtin_nontemporal_store(v, Phi + (a0 + r) * p + j);
     }
   }
   if (kT) {
@@ -150,6 +165,37 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
       const int jj = e / kR, r = e - jj * kR;
       if (r < rows) Phi[(int64_t)(j0 + jj) * n + a0 + r] = sO[jj * (kR + 1) + r];
     }
+  }
+}
+
+template <int kR, bool kT, int kD>
+static void launch_phi(dim3 grid, size_t lds, hipStream_t s, const double* L, const double* S,
+                       int U, int64_t n, const int* cidx, int d, const double* ll, int p,
+                       double* phi) {
+  static bool attr = false;
+  if (!attr) {
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&grief_phi_kernel<kR, kT, kD>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((grief_phi_kernel<kR, kT, kD>), grid, dim3(kPhiCols), lds, s, L, S, U, n,
+                     cidx, d, ll, p, phi);
+}
+
+template <int kR, bool kT>
+static void launch_phi_d(dim3 grid, size_t lds, hipStream_t s, const double* L, const double* S,
+                         int U, int64_t n, const int* cidx, int d, const double* ll, int p,
+                         double* phi) {
+  switch (d) {
+    case 1: launch_phi<kR, kT, 1>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 2: launch_phi<kR, kT, 2>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 3: launch_phi<kR, kT, 3>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 4: launch_phi<kR, kT, 4>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 5: launch_phi<kR, kT, 5>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 6: launch_phi<kR, kT, 6>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 7: launch_phi<kR, kT, 7>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    case 8: launch_phi<kR, kT, 8>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
+    default: launch_phi<kR, kT, 0>(grid, lds, s, L, S, U, n, cidx, d, ll, p, phi); break;
   }
 }
 
@@ -235,25 +281,13 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
                        (transposed ? (size_t)gg::kPhiCols * (kr + 1) * sizeof(double) : 0) +
                        (size_t)d * gg::kPhiCols * sizeof(int);
     GG_REQUIRE(lds <= 160 * 1024, GG_ERR_VALUE, "too many selected eigenvector rows");
-    static bool attr = false;
-    if (!attr) {
-      GG_HIP(hipFuncSetAttribute(
-          reinterpret_cast<const void*>(gg::grief_phi_kernel<gg::kPhiRows, false>),
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      GG_HIP(hipFuncSetAttribute(
-          reinterpret_cast<const void*>(gg::grief_phi_kernel<gg::kPhiRowsT, true>),
-          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
     dim3 grid((unsigned)gg::ceil_div(n, kr), (unsigned)gg::ceil_div(p, gg::kPhiCols));
     if (transposed)
-      hipLaunchKernelGGL((gg::grief_phi_kernel<gg::kPhiRowsT, true>), grid, dim3(gg::kPhiCols),
-                         lds, gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
-                         log_lam_dev, p, phi_dev);
+      gg::launch_phi_d<gg::kPhiRowsT, true>(grid, lds, gg::as_stream(stream), ltab_dev,
+                                            stab_dev, U, n, cidx_dev, d, log_lam_dev, p, phi_dev);
     else
-      hipLaunchKernelGGL((gg::grief_phi_kernel<gg::kPhiRows, false>), grid, dim3(gg::kPhiCols),
-                         lds, gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev, d,
-                         log_lam_dev, p, phi_dev);
+      gg::launch_phi_d<gg::kPhiRows, false>(grid, lds, gg::as_stream(stream), ltab_dev,
+                                            stab_dev, U, n, cidx_dev, d, log_lam_dev, p, phi_dev);
     GG_LAUNCH_CHECK();
   });
 }
