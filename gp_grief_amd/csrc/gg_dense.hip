@@ -477,8 +477,8 @@ __device__ __forceinline__ double quad_sum(double v) {
 //   L_bb = chol(A[k0:k0+nb, k0:k0+nb])              (every workgroup, in LDS)
 //   L[rows, k0:k0+nb] = A[rows, k0:k0+nb] L_bb^-T    (workgroup b: 64 rows
 //                                                     k0 + nb + 64 b ...)
-// The last workgroup to arrive also stores L_bb and W = L_bb^-1 (ld kNB) for
-// gg_potrs.  The 64 x 64 factor is cheap enough to repeat in every workgroup,
+// The last workgroup to arrive also stores L_bb (W = L_bb^-1 for gg_potrs is
+// formed after the factorisation, potrf_winv_kernel).  The 64 x 64 factor is cheap enough to repeat in every workgroup,
 // so a block step is ONE launch with no dependency between its workgroups.
 // Thread t owns row i = t / 4 and the columns j = (t & 3) + 4 u, u < 16, of
 // the block in registers (factor: D; TRSM: its row of the panel).  Every loop
@@ -491,7 +491,6 @@ __device__ __forceinline__ double quad_sum(double v) {
 // Padding rows / columns >= nb form an identity block (no effect on < nb).
 __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
                                                            int n, int k0, int nb, int P0,
-                                                           double* __restrict__ W,
                                                            int* __restrict__ status,
                                                            int* __restrict__ arrived) {
   __shared__ double Lf[kNB][kNB + 1];
@@ -598,31 +597,6 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
       const int j = q + 4 * u;
       if (i < nb && j <= i) Abb[(int64_t)i * lda + j] = d[u];
     }
-    // W = L^-1: column c = i by the four threads of the quad: the sum over
-    // s < r splits by s mod 4 (W[s][c] = 0 for s < c), a quad sum reduces it,
-    // and the owner (s = r mod 4) keeps W[r][c] in w[r >> 2]
-    const int c = i;
-    double w[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) w[u] = 0.0;
-#pragma unroll
-    for (int r = 0; r < kNB; ++r) {
-      double sacc = 0.0;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        if (4 * u >= r) continue;                 // s >= r for every q
-        const double t = fma(Lf[r][q + 4 * u], w[u], sacc);
-        sacc = (4 * u + 3 < r) ? t : (q + 4 * u < r ? t : sacc);
-      }
-      sacc = quad_sum(sacc);
-      const double wr = r < c ? 0.0 : ((r == c ? 1.0 : 0.0) - sacc) * invd[r];
-      w[r >> 2] = (q == (r & 3)) ? wr : w[r >> 2];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int r = q + 4 * u;
-      W[(int64_t)r * kNB + c] = (r < nb && c < nb && c <= r) ? w[u] : 0.0;
-    }
   }
   // ---- TRSM for this workgroup's 64 rows below the block
   const int64_t row = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB + i;
@@ -658,6 +632,50 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
   for (int u = 0; u < 16; ++u) {
     const int j = q + 4 * u;
     if (j < nb) Ar[j] = x[u];
+  }
+}
+
+// W_b = L_bb^-1 for every 64-column diagonal block (gg_potrs's diagonal
+// solves), one workgroup per block, after the factorisation (off the block
+// chain).  Column c = i by the four threads of the quad: the sum over s < r
+// splits by s mod 4 (W[s][c] = 0 for s < c), a quad sum reduces it, and the
+// owner (s = r mod 4) keeps W[r][c] in w[r >> 2].
+__global__ __launch_bounds__(256) void potrf_winv_kernel(const double* __restrict__ A,
+                                                         int64_t lda, int n,
+                                                         double* __restrict__ Wall) {
+  __shared__ double Lf[kNB][kNB + 1];
+  __shared__ double invd[kNB];
+  const int b = blockIdx.x, k0 = b * kNB, nb = min(kNB, n - k0);
+  const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
+  for (int e = tid; e < kNB * kNB; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    Lf[r][c] = (r < nb && c <= r) ? A[(int64_t)(k0 + r) * lda + k0 + c] : (r == c ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  if (tid < kNB) invd[tid] = 1.0 / Lf[tid][tid];
+  __syncthreads();
+  const int c = i;
+  double w[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) w[u] = 0.0;
+#pragma unroll
+  for (int r = 0; r < kNB; ++r) {
+    double sacc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (4 * u >= r) continue;                 // s >= r for every q
+      const double t = fma(Lf[r][q + 4 * u], w[u], sacc);
+      sacc = (4 * u + 3 < r) ? t : (q + 4 * u < r ? t : sacc);
+    }
+    sacc = quad_sum(sacc);
+    const double wr = r < c ? 0.0 : ((r == c ? 1.0 : 0.0) - sacc) * invd[r];
+    w[r >> 2] = (q == (r & 3)) ? wr : w[r >> 2];
+  }
+  double* W = Wall + (int64_t)b * kNB * kNB;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int r = q + 4 * u;
+    W[(int64_t)r * kNB + c] = (r < nb && c < nb && c <= r) ? w[u] : 0.0;
   }
 }
 
@@ -924,12 +942,11 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         const int b = k0 / gg::kNB;
         const int nb = std::min(gg::kNB, n - k0);
         const int rest = n - k0 - nb;
-        double* Wk = winv_dev + (int64_t)b * gg::kNB * gg::kNB;
         const int grid = std::max(1, (int)gg::ceil_div(rest, gg::kNB));
         // the block's update by the panel's earlier blocks is left-looking,
         // inside the same launch (no in-panel GEMM)
         hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n,
-                           k0, nb, P0, Wk, status, arrived + b);
+                           k0, nb, P0, status, arrived + b);
         GG_LAUNCH_CHECK();
         (void)rest;
       }
@@ -978,6 +995,9 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipStreamWaitEvent(s, ew, 0));
     }
     if (lt_buf) GG_HIP(hipFreeAsync(lt_buf, s));
+    hipLaunchKernelGGL(gg::potrf_winv_kernel, dim3(nblk), dim3(256), 0, s, A_dev, lda, n,
+                       winv_dev);
+    GG_LAUNCH_CHECK();
     hipLaunchKernelGGL(gg::diag_logsum_kernel, dim3(1), dim3(1024), 0, s, A_dev, lda, n, ld);
     GG_LAUNCH_CHECK();
     int st = 0;
