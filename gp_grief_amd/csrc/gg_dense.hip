@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -146,20 +147,18 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
 // instruction), so fragment reads stay conflict-free.  Needs M, N, lda, ldb
 // even and 16-byte aligned A, B (the host checks).  Rows k >= kend of the
 // last stage are clamped reads, zeroed in the A fragment.
-template <int kBKg, int kNSg, int kMinWg>
-__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
+// One 128 x 128 output tile (m0, n0) over k in [kbeg, kbeg + kchunk) -- the
+// body of both TN kernels below.
+template <int kBKg, int kNSg>
+__device__ __forceinline__ void gemm_tn_glds_tile(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
     const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
-    int kchunk, double* __restrict__ partial) {
+    int kchunk, double* __restrict__ partial, int m0, int n0, int kz, double* gl) {
   constexpr int kStageD = 2 * kBKg * kLdT;       // doubles per stage (A then B)
   constexpr int kPerWave = kBKg / 4;             // k-rows of A (and of B) per wave
   static_assert(kBKg % 4 == 0 && kGemmThreads == 256, "four waves share a stage's k-rows");
   constexpr int kInstr = 2 * kPerWave;           // DMA instructions per wave per stage
-  extern __shared__ __attribute__((aligned(16))) double gl[];
-  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
-  if (uplo == 1 && n0 > m0 + kBM - 1) return;
-  if (uplo == 2 && m0 > n0 + kBN - 1) return;
-  const int kbeg = blockIdx.z * kchunk;
+  const int kbeg = kz * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
@@ -225,7 +224,7 @@ __global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
   }
-  double* P = partial ? partial + (int64_t)blockIdx.z * M * N : nullptr;
+  double* P = partial ? partial + (int64_t)kz * M * N : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -245,6 +244,46 @@ __global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
           *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
         }
       }
+}
+
+template <int kBKg, int kNSg, int kMinWg>
+__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) double gl[];
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+  if (uplo == 1 && n0 > m0 + kBM - 1) return;
+  if (uplo == 2 && m0 > n0 + kBN - 1) return;
+  gemm_tn_glds_tile<kBKg, kNSg>(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk,
+                                partial, m0, n0, blockIdx.z, gl);
+}
+
+// Persistent, XCD-grouped variant: the grid is the resident slot count (a
+// multiple of 8); workgroup g works on XCD g % 8 (round-robin dispatch), and
+// in round r the XCD's slots take the contiguous range [r G + x S, r G +
+// (x + 1) S) of a host-built tile order (compact supertiles of the valid
+// tiles).  All slots run the same k-loop length, so the workgroups resident
+// on an XCD stream the few A / B panels of their supertile in near lockstep
+// and share them in that XCD's L2 (the launch-order grid streams ~one panel
+// per workgroup: 13 % L2 hits on the C5 Gram).
+template <int kBKg, int kNSg, int kMinWg>
+__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_pers_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial, const int* __restrict__ tiles, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) double gl[];
+  const int G = gridDim.x, S = G / 8;
+  const int g = blockIdx.x, x = g & 7, slot = g >> 3;
+  for (int base = 0; base < ntiles; base += G) {
+    const int t = base + x * S + slot;
+    if (t < ntiles) {
+      const int mb = tiles[2 * t], nb = tiles[2 * t + 1];
+      gemm_tn_glds_tile<kBKg, kNSg>(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo,
+                                    kchunk, partial, mb * kBM, nb * kBN, blockIdx.z, gl);
+    }
+    __syncthreads();   // LDS stages are reused by the next tile
+  }
 }
 
 template <int kBKg, int kNSg>
@@ -282,6 +321,68 @@ static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alph
   const size_t lds = tn_glds_lds<BK, NS>();
   hipLaunchKernelGGL((gemm_tn_glds_kernel<BK, NS, MW>), grid, dim3(kGemmThreads), lds, s, M, N,
                      K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
+}
+
+// Tile order for gemm_tn_glds_pers_kernel (device int pairs (mb, nb)):
+// supertiles of 8 m-blocks x 12 n-blocks, row-major, the valid tiles of each
+// row-major inside it.  Built once per (device, grid shape, uplo) and kept.
+static const int* tn_tile_order(int gm, int gn, int uplo, int* ntiles, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, int, int, int>, std::pair<int*, int>> cache;
+  int dev = 0;
+  GG_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_tuple(dev, gm, gn, uplo);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    *ntiles = it->second.second;
+    return it->second.first;
+  }
+  constexpr int SM = 8, SN = 12;
+  std::vector<int> order;
+  for (int sm = 0; sm < gm; sm += SM)
+    for (int sn = 0; sn < gn; sn += SN)
+      for (int mb = sm; mb < std::min(gm, sm + SM); ++mb)
+        for (int nb = sn; nb < std::min(gn, sn + SN); ++nb) {
+          const int m0 = mb * kBM, n0 = nb * kBN;
+          if (uplo == 1 && n0 > m0 + kBM - 1) continue;
+          if (uplo == 2 && m0 > n0 + kBN - 1) continue;
+          order.push_back(mb);
+          order.push_back(nb);
+        }
+  int* d = nullptr;
+  GG_HIP(hipMalloc(&d, std::max<size_t>(order.size(), 2) * sizeof(int)));
+  GG_HIP(hipMemcpyAsync(d, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  GG_HIP(hipStreamSynchronize(s));
+  const int nt = (int)(order.size() / 2);
+  cache[key] = {d, nt};
+  *ntiles = nt;
+  return d;
+}
+
+template <int BK, int NS, int MW>
+static void launch_tn_pers(dim3 grid, hipStream_t s, int M, int N, int K, double alpha,
+                           const double* A, int64_t lda, const double* B, int64_t ldb,
+                           double beta, double* C, int64_t ldc, int uplo, int kchunk,
+                           double* part) {
+  static bool attr = false;
+  const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_pers_kernel<BK, NS, MW>);
+  if (!attr) {
+    GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)tn_glds_lds<BK, NS>()));
+    attr = true;
+  }
+  int ntiles = 0;
+  const int* tiles = tn_tile_order((int)grid.y, (int)grid.x, uplo, &ntiles, s);
+  int cus = 0, dev = 0;
+  GG_HIP(hipGetDevice(&dev));
+  GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  int G = std::min(ntiles, cus * MW);
+  G = std::max(8, G - G % 8);
+  const size_t lds = tn_glds_lds<BK, NS>();
+  hipLaunchKernelGGL((gemm_tn_glds_pers_kernel<BK, NS, MW>), dim3(G, 1, grid.z),
+                     dim3(kGemmThreads), lds, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                     uplo, kchunk, part, tiles, ntiles);
 }
 
 // TN-GEMM variant (A/B knob, read per call): GG_GEMM_TN=0 register-staged
@@ -332,6 +433,11 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
       case 2: launch_tn<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
       case 3: launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
       case 4: launch_tn<16, 3, 1>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 6: launch_tn_pers<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 8: launch_tn<4, 4, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 9: launch_tn<4, 3, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 10: launch_tn_pers<4, 4, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 7: launch_tn_pers<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
       default: launch_tn<8, 4, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
     }
     GG_LAUNCH_CHECK();
