@@ -208,20 +208,32 @@ __device__ __forceinline__ void gemm_tn_glds_tile(
     const double* a_s = gl + (g % kNSg) * kStageD;
     const double* b_s = a_s + kBKg * kLdT;
     const int krem = kend - (kbeg + g * kBKg);   // valid k-rows in this stage
-#pragma unroll
-    for (int s = 0; s < kBKg / 4; ++s) {
-      const int kk = 4 * s + (lane >> 4);
+    // fragments of k-step s (the tail mask only in the last, partial stage:
+    // a uniform branch, so full stages carry no per-fragment select)
+    auto frag = [&](int s_, double (&af)[4], double (&bf)[4], bool masked) {
+      const int kk = 4 * s_ + (lane >> 4);
       const int kr = kk * kLdT + (lane & 15);
-      double af[4], bf[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = kk < krem ? a_s[kr + wm + 16 * i] : 0.0;
+      for (int i = 0; i < 4; ++i) {
+        af[i] = a_s[kr + wm + 16 * i];
+        if (masked && kk >= krem) af[i] = 0.0;
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf[j] = b_s[kr + wn + 16 * j];
+    };
+    auto mma = [&](const double (&af)[4], const double (&bf)[4]) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
+    };
+    const bool full = krem >= kBKg;
+#pragma unroll
+    for (int s = 0; s < kBKg / 4; ++s) {
+      double af[4], bf[4];
+      frag(s, af, bf, !full);
+      mma(af, bf);
     }
   }
   double* P = partial ? partial + (int64_t)kz * M * N : nullptr;
@@ -883,6 +895,137 @@ __global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict
   }
 }
 
+// Triangular solve with many right-hand sides as one chained launch per
+// direction: workgroup (b, j) computes the 64 x 64 block X[b, j] (block row b
+// of the solution, column chunk j of the right-hand sides).  Linear ids run
+// b-major in dependency order (forward b = 0.., backward b = nblk-1..), so
+// every block a workgroup waits on belongs to an earlier-dispatched one.  Per
+// dependency block c: L's 64 x 64 block is staged in LDS first (forward
+// L[b, c]; backward L[c, b], read transposed), then the flag of X[c, j] is
+// polled (agent-scope acquire, bounded spin) and X[c, j] staged; each wave
+// accumulates its 16 rows x 64 columns on MFMA.  Then X[b, j] = W_b (B - acc)
+// (forward; W_b^T backward) -- a second MFMA product -- is stored and the
+// flag released.  tri (forward only): the right-hand side is lower
+// triangular with 64-row blocks (the identity), so X[b, j] = 0 for b < j and
+// only c >= j contribute.
+__global__ __launch_bounds__(256) void trsm_chain_kernel(int n, int r, const double* __restrict__ L,
+                                                         int64_t lda,
+                                                         const double* __restrict__ Winv,
+                                                         double* Bm, int64_t ldb, int trans,
+                                                         int tri, int* flags,
+                                                         int* __restrict__ status) {
+  __shared__ double Ls[kNB][kNB + 1];
+  __shared__ double Xs[kNB][kNB + 1];
+  __shared__ int ok;
+  const int nblk = (n + kNB - 1) / kNB, nch = (r + kNB - 1) / kNB;
+  const int order = (int)(blockIdx.x / nch), j = (int)(blockIdx.x % nch);
+  const int b = trans ? nblk - 1 - order : order;
+  const int k0 = b * kNB, nb = min(kNB, n - k0);
+  const int j0 = j * kNB, cw = min(kNB, r - j0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) ok = 1;
+  int* myflag = flags + (int64_t)b * nch + j;
+  if (tri && b < j) {          // X[b, j] = 0 (lower-triangular result)
+    for (int e = tid; e < nb * cw; e += 256)
+      Bm[(int64_t)(k0 + e / cw) * ldb + j0 + e % cw] = 0.0;
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(myflag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  d4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  const int cfirst = trans ? nblk - 1 : (tri ? j : 0);
+  const int ndep = trans ? nblk - 1 - b : b - cfirst;
+  for (int t = 0; t < ndep; ++t) {
+    const int c = trans ? nblk - 1 - t : cfirst + t;
+    const int c0 = c * kNB, ncb = min(kNB, n - c0);
+    __syncthreads();   // the previous block's LDS reads are done
+    for (int e = tid; e < kNB * kNB; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      // Ls[i][k]: row i of block b, column k of block c (the A operand)
+      double v = 0.0;
+      if (!trans) {
+        if (rr < nb && cc < ncb) v = L[(int64_t)(k0 + rr) * lda + c0 + cc];
+        Ls[rr][cc] = v;
+      } else {
+        // L^T[b-row i][c-col k] = L[c0 + k][k0 + i]: coalesced over i
+        if (rr < ncb && cc < nb) v = L[(int64_t)(c0 + rr) * lda + k0 + cc];
+        Ls[cc][rr] = v;
+      }
+    }
+    if (tid == 0) {
+      int spin = 0;
+      while (__hip_atomic_load(&flags[(int64_t)c * nch + j], __ATOMIC_ACQUIRE,
+                               __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spin > kTrsvSpin) {
+          ok = 0;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (!ok) break;
+    for (int e = tid; e < kNB * kNB; e += 256) {
+      const int rr = e >> 6, cc = e & 63;
+      Xs[rr][cc] = (rr < ncb && cc < cw) ? Bm[(int64_t)(c0 + rr) * ldb + j0 + cc] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < kNB / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a = Ls[16 * wave + (lane & 15)][kk];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+        acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[kk][16 * tt + (lane & 15)], acc[tt],
+                                                      0, 0, 0);
+    }
+  }
+  // rhs = B[b, j] - acc  (into Xs), W_b (or W_b^T) into Ls
+  __syncthreads();
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = 16 * wave + 4 * q + (lane >> 4), cc = 16 * tt + (lane & 15);
+      const double bv = (rr < nb && cc < cw) ? Bm[(int64_t)(k0 + rr) * ldb + j0 + cc] : 0.0;
+      Xs[rr][cc] = bv - acc[tt][q];
+    }
+  const double* W = Winv + (int64_t)b * kNB * kNB;
+  for (int e = tid; e < kNB * kNB; e += 256) {
+    const int rr = e >> 6, cc = e & 63;
+    if (!trans) Ls[rr][cc] = W[e];
+    else Ls[cc][rr] = W[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) acc[tt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < kNB / 4; ++ks) {
+    const int kk = 4 * ks + (lane >> 4);
+    const double a = Ls[16 * wave + (lane & 15)][kk];
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+      acc[tt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Xs[kk][16 * tt + (lane & 15)], acc[tt],
+                                                    0, 0, 0);
+  }
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = 16 * wave + 4 * q + (lane >> 4), cc = 16 * tt + (lane & 15);
+      if (rr < nb && cc < cw) Bm[(int64_t)(k0 + rr) * ldb + j0 + cc] = acc[tt][q];
+    }
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) {
+    if (!ok) *status = 2;
+    __hip_atomic_store(myflag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += log(A[(int64_t)i * lda + i]);
@@ -1150,6 +1293,32 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
       if (which & 2)
         hipLaunchKernelGGL(gg::trsv_chain_kernel<true>, dim3(nblk), dim3(256), 0, s, n, L_dev,
                            lda, winv_dev, B_dev, flags + nblk, st);
+      GG_LAUNCH_CHECK();
+      int hst = 0;
+      GG_HIP(hipMemcpyAsync(&hst, st, sizeof(int), hipMemcpyDeviceToHost, s));
+      GG_HIP(hipFreeAsync(flags, s));
+      GG_HIP(hipStreamSynchronize(s));
+      GG_REQUIRE(hst == 0, GG_ERR_RUNTIME, "chained triangular solve timed out");
+      return;
+    }
+    // several right-hand sides: one chained MFMA launch per direction
+    // (trsm_chain_kernel) instead of a GEMM pair per block row
+    // (a triangular right-hand side -- L^-1 itself -- keeps the blocked path
+    // past 100 blocks, where the two measure the same: 26-27 ms at n = 1e4)
+    if (r > 1 && !(ch != nullptr && atoi(ch) == 0) && !(tri && nblk > 100)) {
+      const int nch = (int)gg::ceil_div(r, gg::kNB);
+      const size_t nflags = (size_t)nblk * nch;
+      int* flags = nullptr;
+      GG_HIP(hipMallocAsync(&flags, (2 * nflags + 1) * sizeof(int), s));
+      GG_HIP(hipMemsetAsync(flags, 0, (2 * nflags + 1) * sizeof(int), s));
+      int* st = flags + 2 * nflags;
+      const unsigned grid = (unsigned)((int64_t)nblk * nch);
+      if (which & 1)
+        hipLaunchKernelGGL(gg::trsm_chain_kernel, dim3(grid), dim3(256), 0, s, n, r, L_dev, lda,
+                           winv_dev, B_dev, ldb, 0, tri ? 1 : 0, flags, st);
+      if (which & 2)
+        hipLaunchKernelGGL(gg::trsm_chain_kernel, dim3(grid), dim3(256), 0, s, n, r, L_dev, lda,
+                           winv_dev, B_dev, ldb, 1, 0, flags + nflags, st);
       GG_LAUNCH_CHECK();
       int hst = 0;
       GG_HIP(hipMemcpyAsync(&hst, st, sizeof(int), hipMemcpyDeviceToHost, s));
