@@ -206,6 +206,15 @@ __global__ __launch_bounds__(kEigThreads) void jacobi_kernel(
 // A / Z live in LDS (row stride m + 1) up to kLdsMaxM, else in the HBM
 // scratch (L2-resident).
 constexpr int kTqThreads = 512;
+constexpr int kTqWaves = kTqThreads / 64;
+
+// Bytes of LDS ahead of A in tridiag_ql_kernel: d, e, tau, v, pw, cs, sn
+// (m each), red (16), junk (64), the per-wave partial sums of the column
+// reductions (kTqWaves x m; in the HBM scratch when A is), rank (m ints).
+__host__ __device__ inline int64_t tq_head_bytes(int64_t m, bool lds_a) {
+  return ((((int64_t)7 + (lds_a ? kTqWaves : 0)) * m + 80) * (int64_t)sizeof(double) +
+          m * (int64_t)sizeof(int) + 15) & ~int64_t(15);
+}
 
 __device__ __forceinline__ double tq_block_sum(double v, double* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -219,12 +228,27 @@ __device__ __forceinline__ double tq_block_sum(double v, double* red) {
   return s;
 }
 
-// lanes per row / column for an L-long reduction with nt threads: the largest
-// power of two <= nt / L, at most a wave (groups stay inside one wave)
-__device__ __forceinline__ int tq_group(int L, int nt) {
-  int g = 1;
-  while (g < 64 && 2 * g * L <= nt) g *= 2;
-  return g;
+// Per-wave partial column sums psc[w * ldp + c] = sum over rows r = w, w + nw,
+// ... < L of v[r] M[r * ld + c] (lanes over columns: consecutive addresses)
+__device__ __forceinline__ void tq_colsum(const double* __restrict__ M, int ld,
+                                          const double* __restrict__ v, int L,
+                                          double* __restrict__ psc, int ldp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c0 = 0; c0 < L; c0 += 64) {
+    const int c = c0 + lane;
+    if (c >= L) break;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int r = wave;
+    for (; r + 3 * nw < L; r += 4 * nw) {
+      const double* Mr = M + (int64_t)r * ld + c;
+      s0 = fma(v[r], Mr[0], s0);
+      s1 = fma(v[r + nw], Mr[(int64_t)nw * ld], s1);
+      s2 = fma(v[r + 2 * nw], Mr[(int64_t)2 * nw * ld], s2);
+      s3 = fma(v[r + 3 * nw], Mr[(int64_t)3 * nw * ld], s3);
+    }
+    for (; r < L; r += nw) s0 = fma(v[r], M[(int64_t)r * ld + c], s0);
+    psc[wave * ldp + c] = (s0 + s1) + (s2 + s3);
+  }
 }
 
 // Eigenvalues of the symmetric tridiagonal (d, e[0..m-2]) by multisection on
@@ -301,10 +325,11 @@ __device__ void tq_bisect(const double* __restrict__ d, const double* __restrict
 }
 
 // kMode 0: full decomposition (phases 1-4).  kMode 1: eigenvalues only, by
-// bisection on the tridiagonal (phases 1, 2, then tq_bisect): Z goes to Qout,
-// the tridiagonal (d, e) to work + work_offs[f] + m * m, the eigenvalues
-// (ascending) to lam_out -- the input of tridiag_invit_kernel, which computes
-// selected eigenvectors y of the tridiagonal (the eigenvectors are Z y).
+// bisection on the tridiagonal (phase 1, then tq_bisect): the Householder
+// reflectors go to Qout (as rows), (d, e, tau) to work + work_offs[f] + m * m,
+// the eigenvalues (ascending) to lam_out -- the input of tridiag_invit_kernel
+// (selected eigenvectors y of the tridiagonal) and tridiag_backtransform_kernel
+// (the eigenvectors of A, Z y = H_0 (H_1 (... H_{m-3} y)), without forming Z).
 template <bool kLds, int kMode>
 __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     const int64_t* __restrict__ dims, const int64_t* __restrict__ offs,
@@ -333,19 +358,22 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   double* sn = cs + m;
   double* red = sn + m;
   double* junk = red + 16;   // 64 per-lane dummy slots (wave 0's chain stores)
-  int* rank = reinterpret_cast<int*>(junk + 64);
+  // per-wave partial column sums (wave w: psc[w * m + c])
+  double* psc = kLds ? junk + 64 : work + work_offs[f] + (int64_t)m * m + 2 * m;
+  int* rank = reinterpret_cast<int*>(junk + 64 + (kLds ? kTqWaves * m : 0));
   __shared__ int bad;
-  const int64_t head = (((int64_t)7 * m + 80) * sizeof(double) + (int64_t)m * sizeof(int) + 15) &
-                       ~int64_t(15);
+  const int64_t head = tq_head_bytes(m, kLds);
   const int ld = kLds ? m + 1 : m;
   double* A = kLds ? reinterpret_cast<double*>(tq_lds + head) : work + work_offs[f];
   const double* Asrc = Ain + offs[f];
   const int tid = threadIdx.x, nt = blockDim.x;
+  // the L x L loops: wave w takes rows w, w + nw, ..., its lanes the columns
+  // (consecutive LDS addresses, no index division)
+  const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   if (tid == 0) bad = 0;
-  for (int64_t i = tid; i < (int64_t)m * m; i += nt) {
-    const int r = (int)(i / m), c = (int)(i % m);
-    A[(int64_t)r * ld + c] = 0.5 * (Asrc[i] + Asrc[(int64_t)c * m + r]);
-  }
+  for (int r = wave; r < m; r += nw)
+    for (int c = lane; c < m; c += 64)
+      A[(int64_t)r * ld + c] = 0.5 * (Asrc[(int64_t)r * m + c] + Asrc[(int64_t)c * m + r]);
   __syncthreads();
 
   // ---- 1. tridiagonalisation
@@ -375,30 +403,42 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     }
     __syncthreads();
     if (ti != 0.0) {
-      // p = tau A22 v: a group of tpr lanes per row (strided columns, then a
-      // shuffle reduction inside the group)
-      const int tpr = tq_group(L, nt);
+      // p = tau A22 v as column sums (A22 is symmetric): per-wave partials
+      // over its rows, then one thread per column adds the kTqWaves partials
+      tq_colsum(A + (int64_t)r0 * ld + r0, ld, v, L, psc, m);
+      __syncthreads();
       double pv = 0.0;
-      for (int t0 = tid / tpr; t0 < L; t0 += nt / tpr) {
-        const double* Ar = A + (int64_t)(r0 + t0) * ld + r0;
+      for (int t = tid; t < L; t += nt) {
         double s = 0.0;
-        for (int c = tid % tpr; c < L; c += tpr) s = fma(Ar[c], v[c], s);
-        for (int off = tpr >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        for (int w = 0; w < nw; ++w) s += psc[w * m + t];
         s *= ti;
-        if (tid % tpr == 0) {
-          pw[t0] = s;
-          pv = fma(s, v[t0], pv);
-        }
+        pw[t] = s;
+        pv = fma(s, v[t], pv);
       }
       const double ptv = tq_block_sum(pv, red);
       const double k = 0.5 * ti * ptv;
       for (int t = tid; t < L; t += nt) pw[t] -= k * v[t];   // w
       __syncthreads();
-      // A22 -= v w^T + w v^T
-      for (int64_t q = tid; q < (int64_t)L * L; q += nt) {
-        const int r = (int)(q / L), c = (int)(q - (int64_t)r * L);
-        double* a = A + (int64_t)(r0 + r) * ld + r0 + c;
-        *a -= v[r] * pw[c] + pw[r] * v[c];
+      // A22 -= v w^T + w v^T (four rows' loads issued before their stores:
+      // the LDS accesses may alias, so the compiler keeps program order)
+      for (int c = lane; c < L; c += 64) {
+        const double pc = pw[c], vc = v[c];
+        double* a = A + (int64_t)r0 * ld + r0 + c;
+        int r = wave;
+        for (; r + 3 * nw < L; r += 4 * nw) {
+          double* a0 = a + (int64_t)r * ld;
+          double* a1 = a0 + (int64_t)nw * ld;
+          double* a2 = a1 + (int64_t)nw * ld;
+          double* a3 = a2 + (int64_t)nw * ld;
+          const double x0 = *a0, x1 = *a1, x2 = *a2, x3 = *a3;
+          const double v0 = v[r], v1 = v[r + nw], v2 = v[r + 2 * nw], v3 = v[r + 3 * nw];
+          const double w0 = pw[r], w1 = pw[r + nw], w2 = pw[r + 2 * nw], w3 = pw[r + 3 * nw];
+          *a0 = x0 - (v0 * pc + w0 * vc);
+          *a1 = x1 - (v1 * pc + w1 * vc);
+          *a2 = x2 - (v2 * pc + w2 * vc);
+          *a3 = x3 - (v3 * pc + w3 * vc);
+        }
+        for (; r < L; r += nw) a[(int64_t)r * ld] -= v[r] * pc + pw[r] * vc;
       }
     }
     // keep v (below its implicit unit head) in A[r0+1:, i] for step 2
@@ -417,6 +457,27 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   __syncthreads();
 
   stamp(1);
+  if (kMode == 1) {
+    // the reflectors out as rows (row i = v_i: 1 at column i + 1, A[r][i]
+    // for r > i + 1, zeros elsewhere; rows m - 2, m - 1 have none), tau and
+    // (d, e) to the work tail, eigenvalues by bisection.  The psc partials
+    // (HBM variant) overlap the tau slot: both loops above ended in a barrier.
+    double* R = Qout + offs[f];
+    for (int r = wave; r < m; r += nw)
+      for (int c = lane; c < m; c += 64)
+        R[(int64_t)r * m + c] = (r + 2 >= m || c <= r) ? 0.0
+                                : (c == r + 1 ? 1.0 : A[(int64_t)c * ld + r]);
+    double* de = work + work_offs[f] + (int64_t)m * m;
+    for (int i = tid; i < m; i += nt) {
+      de[i] = d[i];
+      de[m + i] = e[i];
+      de[2 * m + i] = i + 2 < m ? tau[i] : 0.0;
+    }
+    tq_bisect(d, e, v, red, m, lam_out + lam_offs[f]);
+    if (tid == 0) status[f] = 0;
+    stamp(3);
+    return;
+  }
   // ---- 2. Z = H_0 H_1 ... H_{m-3}, backwards, into the same storage.  The
   // reflector vectors sit in the strictly-lower columns 0..m-3, below the
   // subdiagonal; Z's block for step i touches rows/cols > i only, and column
@@ -439,19 +500,32 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
     __syncthreads();
     const double ti = tau[i];
     if (ti != 0.0) {
-      // u[c] = tau sum_r v[r] Z[r0 + r][r0 + c]  (a lane group per column)
-      const int tpc = tq_group(L, nt);
-      for (int t0 = tid / tpc; t0 < L; t0 += nt / tpc) {
+      // u[c] = tau sum_r v[r] Z[r0 + r][r0 + c]: per-wave column partials
+      tq_colsum(A + (int64_t)r0 * ld + r0, ld, v, L, psc, m);
+      __syncthreads();
+      for (int t = tid; t < L; t += nt) {
         double s = 0.0;
-        for (int r = tid % tpc; r < L; r += tpc)
-          s = fma(v[r], A[(int64_t)(r0 + r) * ld + r0 + t0], s);
-        for (int off = tpc >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (tid % tpc == 0) pw[t0] = ti * s;
+        for (int w = 0; w < nw; ++w) s += psc[w * m + t];
+        pw[t] = ti * s;
       }
       __syncthreads();
-      for (int64_t q = tid; q < (int64_t)L * L; q += nt) {
-        const int r = (int)(q / L), c = (int)(q - (int64_t)r * L);
-        A[(int64_t)(r0 + r) * ld + r0 + c] -= v[r] * pw[c];
+      for (int c = lane; c < L; c += 64) {
+        const double pc = pw[c];
+        double* z = A + (int64_t)r0 * ld + r0 + c;
+        int r = wave;
+        for (; r + 3 * nw < L; r += 4 * nw) {
+          double* z0 = z + (int64_t)r * ld;
+          double* z1 = z0 + (int64_t)nw * ld;
+          double* z2 = z1 + (int64_t)nw * ld;
+          double* z3 = z2 + (int64_t)nw * ld;
+          const double x0 = *z0, x1 = *z1, x2 = *z2, x3 = *z3;
+          const double v0 = v[r], v1 = v[r + nw], v2 = v[r + 2 * nw], v3 = v[r + 3 * nw];
+          *z0 = x0 - v0 * pc;
+          *z1 = x1 - v1 * pc;
+          *z2 = x2 - v2 * pc;
+          *z3 = x3 - v3 * pc;
+        }
+        for (; r < L; r += nw) z[(int64_t)r * ld] -= v[r] * pc;
       }
     }
     __syncthreads();
@@ -464,23 +538,6 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   __syncthreads();
 
   stamp(2);
-  if (kMode == 1) {
-    // Z out (row-major), (d, e) to the work tail, eigenvalues by bisection
-    double* Q = Qout + offs[f];
-    for (int64_t q = tid; q < (int64_t)m * m; q += nt) {
-      const int r = (int)(q / m), c = (int)(q % m);
-      Q[q] = A[(int64_t)r * ld + c];
-    }
-    double* de = work + work_offs[f] + (int64_t)m * m;
-    for (int i = tid; i < m; i += nt) {
-      de[i] = d[i];
-      de[m + i] = e[i];
-    }
-    tq_bisect(d, e, v, red, m, lam_out + lam_offs[f]);
-    if (tid == 0) status[f] = 0;
-    stamp(3);
-    return;
-  }
   // ---- 3. implicit QL (tql2 / tqli) on (d, e) accumulating into Z's columns.
   // Wave 0 owns (d, e): it finds the next split point (ballot over its
   // lanes) and runs the sweep's scalar rotation chain (every lane computes
@@ -489,7 +546,6 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   // their rows of Z -- the chains pipeline against the Z updates, one
   // barrier per sweep.
   const double eps = 2.220446049250313e-16;
-  const int lane = tid & 63, wave = tid >> 6;
   __shared__ int lo_b[2], hi_b[2], ql_done;
   if (tid == 0) {
     ql_done = 0;
@@ -665,10 +721,8 @@ __global__ __launch_bounds__(kTqThreads) void tridiag_ql_kernel(
   double* Q = Qout + offs[f];
   double* lam = lam_out + lam_offs[f];
   for (int i = tid; i < m; i += nt) lam[rank[i]] = d[i];
-  for (int64_t q = tid; q < (int64_t)m * m; q += nt) {
-    const int r = (int)(q / m), c = (int)(q % m);
-    Q[(int64_t)r * m + rank[c]] = A[(int64_t)r * ld + c];
-  }
+  for (int r = wave; r < m; r += nw)
+    for (int c = lane; c < m; c += 64) Q[(int64_t)r * m + rank[c]] = A[(int64_t)r * ld + c];
   if (tid == 0) status[f] = bad;
   stamp(4);
 }
@@ -787,6 +841,56 @@ __global__ __launch_bounds__(kInvThreads) void tridiag_invit_kernel(
   for (int i = 0; i < m; ++i) yo[i] = at(5, i) * sc;
 }
 
+// Eigenvectors of A from those of its tridiagonal: y <- H_i y = y - tau_i
+// (v_i . y) v_i for i = m - 3 .. 0, in place on rows of Y.  One workgroup per
+// (factor, up to kBtWaves rows), one wave per row (its y in LDS, lanes over
+// the row, a shuffle reduction per reflector); the reflector rows are staged
+// through LDS in chunks of ch rows shared by the waves.  Work per row: m^2
+// FMAs in m - 2 dependent steps, against forming Z (m^3 / 3 behind barriers)
+// and the GEMM Y Z^T it replaces.
+constexpr int kBtWaves = 8;
+
+__global__ __launch_bounds__(kBtWaves * 64) void tridiag_backtransform_kernel(
+    const int* __restrict__ job_f, const int* __restrict__ job_r0, const int* __restrict__ job_n,
+    const int64_t* __restrict__ dims, const int64_t* __restrict__ tau_offs,
+    const int64_t* __restrict__ r_offs, const int64_t* __restrict__ y_offs,
+    const double* __restrict__ work, const double* __restrict__ R, double* Y, int ch) {
+  extern __shared__ __attribute__((aligned(16))) double bt[];
+  const int job = blockIdx.x;
+  const int f = job_f[job];
+  const int m = (int)dims[f];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool act = wave < job_n[job];
+  const double* tau = work + tau_offs[f];
+  const double* Rf = R + r_offs[f];
+  double* yrow = Y + y_offs[f] + (int64_t)(job_r0[job] + (act ? wave : 0)) * m;
+  double* yw = bt + wave * m;
+  double* rc = bt + kBtWaves * m;
+  if (act)
+    for (int c = lane; c < m; c += 64) yw[c] = yrow[c];
+  for (int hi = m - 3; hi >= 0; hi -= ch) {
+    const int lo = hi - ch + 1 > 0 ? hi - ch + 1 : 0;
+    __syncthreads();   // the previous chunk is consumed
+    for (int i = lo + wave; i <= hi; i += kBtWaves)
+      for (int c = lane; c < m; c += 64) rc[(int64_t)(i - lo) * m + c] = Rf[(int64_t)i * m + c];
+    __syncthreads();
+    if (!act) continue;
+    for (int i = hi; i >= lo; --i) {
+      const double ti = tau[i];
+      if (ti == 0.0) continue;
+      const double* v = rc + (int64_t)(i - lo) * m;
+      double s = 0.0;
+      for (int c = i + 1 + lane; c < m; c += 64) s = fma(v[c], yw[c], s);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      s *= ti;
+      for (int c = i + 1 + lane; c < m; c += 64) yw[c] = fma(-s, v[c], yw[c]);
+    }
+  }
+  if (act)
+    for (int c = lane; c < m; c += 64) yrow[c] = yw[c];
+}
+
 // Orthonormalise the rows of V (k x m, row-major) in place by classical
 // Gram-Schmidt applied twice ("CGS2"), last row first: row v loses its
 // components along rows v+1 .. k-1, twice, then is normalised.  One workgroup
@@ -849,9 +953,10 @@ __global__ __launch_bounds__(kOrthoThreads) void rows_orthonormalize_kernel(
   }
 }
 
-// work doubles per factor: the HBM copy of A / Z (m x m) and, for the
-// eigenvalue-only mode, the tridiagonal (d, e) after it
-inline int64_t eig_work_per(int64_t m) { return std::max(2 * m * m, m * m + 2 * m); }
+// work doubles per factor: the HBM copy of A / Z (m x m), then (d, e, tau)
+// of the eigenvalue-only mode or the HBM variant's column partials
+// (kTqWaves m; the two are never live together), or Jacobi's 2 m^2
+inline int64_t eig_work_per(int64_t m) { return std::max(2 * m * m, m * m + (2 + kTqWaves) * m); }
 
 }  // namespace gg
 
@@ -905,8 +1010,7 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
       GG_HIP(hipMemsetAsync(dstamps, 0, 8 * 64 * sizeof(long long) * count, s));
     }
     if (!jacobi) {
-      const int64_t head = (((int64_t)7 * mmax + 80) * sizeof(double) +
-                            (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
+      const int64_t head = gg::tq_head_bytes(mmax, lds_a);
       const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
       const int iters = std::max(30, max_sweeps);
       if (lds_a) {
@@ -989,8 +1093,7 @@ int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double*
                           hipMemcpyHostToDevice, s));
     int* dstatus = reinterpret_cast<int*>(dmeta + 4 * count);
     const bool lds_a = mmax <= gg::kLdsMaxM;
-    const int64_t head = (((int64_t)7 * mmax + 80) * sizeof(double) +
-                          (int64_t)mmax * sizeof(int) + 15) & ~int64_t(15);
+    const int64_t head = gg::tq_head_bytes(mmax, lds_a);
     const int64_t lds = head + (lds_a ? (int64_t)mmax * (mmax + 1) * sizeof(double) : 0);
     if (lds_a) {
       GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_ql_kernel<true, 1>),
@@ -1010,15 +1113,16 @@ int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double*
   });
 }
 
-int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_dev,
-                               int64_t work_elems, const double* lam_dev, const int* nsel,
-                               const int* sel, double* Y_dev, gg_stream stream) {
+int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* R_dev,
+                               const double* work_dev, int64_t work_elems, const double* lam_dev,
+                               const int* nsel, const int* sel, double* Y_dev, gg_stream stream) {
   return gg::guard([&] {
-    GG_REQUIRE(count >= 1 && m && work_dev && lam_dev && nsel && sel && Y_dev, GG_ERR_VALUE,
-               "bad argument");
-    // per factor: m, (d, e) offset, lambda offset, selection offset, Y offset
-    std::vector<int64_t> fm(5 * (size_t)count);
-    int64_t woff = 0, loff = 0, soff = 0, yoff = 0;
+    GG_REQUIRE(count >= 1 && m && R_dev && work_dev && lam_dev && nsel && sel && Y_dev,
+               GG_ERR_VALUE, "bad argument");
+    // per factor: m, (d, e) offset, lambda offset, selection offset, Y offset,
+    // tau offset, reflector offset
+    std::vector<int64_t> fm(7 * (size_t)count);
+    int64_t woff = 0, loff = 0, soff = 0, yoff = 0, roff = 0;
     int mmax = 1;
     for (int i = 0; i < count; ++i) {
       GG_REQUIRE(m[i] >= 1 && m[i] <= 2048 && nsel[i] >= 0 && nsel[i] <= m[i], GG_ERR_VALUE,
@@ -1031,6 +1135,9 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_d
       fm[2 * count + i] = loff;
       fm[3 * count + i] = soff;
       fm[4 * count + i] = yoff;
+      fm[5 * count + i] = woff + m[i] * m[i] + 2 * m[i];
+      fm[6 * count + i] = roff;
+      roff += m[i] * m[i];
       woff += gg::eig_work_per(m[i]);
       loff += m[i];
       soff += nsel[i];
@@ -1050,8 +1157,18 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_d
         jn.push_back(std::min(B, nsel[i] - k));
       }
     const int njobs = (int)jf.size();
+    // back-transform jobs: up to kBtWaves rows of one factor
+    std::vector<int> bf, br, bn;
+    for (int i = 0; i < count; ++i)
+      for (int k = 0; k < nsel[i]; k += gg::kBtWaves) {
+        bf.push_back(i);
+        br.push_back(k);
+        bn.push_back(std::min(gg::kBtWaves, nsel[i] - k));
+      }
+    const int nbt = (int)bf.size();
     // one device block: int64 factor table, then int job tables and selection
-    const size_t bytes = fm.size() * sizeof(int64_t) + (3 * (size_t)njobs + soff) * sizeof(int);
+    const size_t bytes =
+        fm.size() * sizeof(int64_t) + (3 * (size_t)njobs + soff + 3 * (size_t)nbt) * sizeof(int);
     hipStream_t s = gg::as_stream(stream);
     unsigned char* dbuf = nullptr;
     GG_HIP(hipMallocAsync(&dbuf, bytes, s));
@@ -1062,6 +1179,10 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_d
     memcpy(ip + njobs, js.data(), njobs * sizeof(int));
     memcpy(ip + 2 * njobs, jn.data(), njobs * sizeof(int));
     memcpy(ip + 3 * njobs, sel, soff * sizeof(int));
+    int* bp = ip + 3 * njobs + soff;
+    memcpy(bp, bf.data(), nbt * sizeof(int));
+    memcpy(bp + nbt, br.data(), nbt * sizeof(int));
+    memcpy(bp + 2 * nbt, bn.data(), nbt * sizeof(int));
     GG_HIP(hipMemcpyAsync(dbuf, hbuf.data(), bytes, hipMemcpyHostToDevice, s));
     const int64_t* dfm = reinterpret_cast<const int64_t*>(dbuf);
     const int* dip = reinterpret_cast<const int*>(dbuf + fm.size() * sizeof(int64_t));
@@ -1072,6 +1193,17 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_d
                        dip + njobs, dip + 2 * njobs, dfm, dfm + count, work_dev, lam_dev,
                        dfm + 2 * count, dip + 3 * njobs, dfm + 3 * count, dfm + 4 * count, Y_dev,
                        B);
+    GG_LAUNCH_CHECK();
+    // reflector rows staged per chunk: kBtWaves y rows + ch reflector rows of
+    // LDS (at most 144 KB)
+    const int ch = std::max(1, std::min(64, 18432 / mmax - gg::kBtWaves));
+    const size_t bt_lds = (size_t)(gg::kBtWaves + ch) * mmax * sizeof(double);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&gg::tridiag_backtransform_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bt_lds));
+    const int* dbp = dip + 3 * njobs + soff;
+    hipLaunchKernelGGL(gg::tridiag_backtransform_kernel, dim3(nbt), dim3(gg::kBtWaves * 64),
+                       bt_lds, s, dbp, dbp + nbt, dbp + 2 * nbt, dfm, dfm + 5 * count,
+                       dfm + 6 * count, dfm + 4 * count, work_dev, R_dev, Y_dev, ch);
     GG_LAUNCH_CHECK();
     GG_HIP(hipFreeAsync(dbuf, s));
   });

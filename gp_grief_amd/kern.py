@@ -429,7 +429,7 @@ class GriefKernel(GridKernel):
         eigenvalue enters the selection, but Phi needs only the eigenvectors of
         the selected indices: on a cache miss the factors are tridiagonalised,
         their eigenvalues found by bisection, and only the selected
-        eigenvectors computed (inverse iteration + one GEMM) -- unless a
+        eigenvectors computed (inverse iteration + the reflectors) -- unless a
         selected eigenvalue is not separated from its neighbours (relative gap
         below _SUBSET_GAP), then the full QL decomposition is used.  With
         opt_kernel_params the finite-difference gradient compares LMLs of

@@ -72,7 +72,7 @@ SIGNATURES = {
     "gg_sym_eig_work_elems": [ctypes.c_int, _c_i64p, _c_i64p],
     "gg_sym_eig_tridiag": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
                            _vp],
-    "gg_sym_eig_tridiag_vectors": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_int64, _c_dp,
+    "gg_sym_eig_tridiag_vectors": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, ctypes.c_int64, _c_dp,
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                    _c_dp, _vp],
     "gg_rows_orthonormalize": [ctypes.c_int, _c_i64p, _c_i64p, _c_dp, _vp],

@@ -160,13 +160,13 @@ def device_sym_eig_tridiag(factors):
             raise AssertionError("factor must be square")
     m = [f.shape[0] for f in mats]
     A = dev.to_device(np.concatenate([f.reshape(-1) for f in mats]))
-    Z = dev.empty(A.numel())
+    R = dev.empty(A.numel())
     lam = dev.empty(sum(m))
     marr = native.i64_array(m)
     we = ctypes.c_int64()
     native.check(L.gg_sym_eig_work_elems(len(m), marr, ctypes.byref(we)))
     work = dev.empty(max(we.value, 1))
-    native.check(L.gg_sym_eig_tridiag(len(m), marr, native.dptr(A), native.dptr(Z),
+    native.check(L.gg_sym_eig_tridiag(len(m), marr, native.dptr(A), native.dptr(R),
                                       native.dptr(lam), native.dptr(work), we.value,
                                       native.stream_ptr()), "gg_sym_eig_tridiag")
     lh = dev.to_host(lam)
@@ -174,16 +174,16 @@ def device_sym_eig_tridiag(factors):
     for mi in m:
         out.append(lh[o:o + mi].copy())
         o += mi
-    return out, dict(m=m, Z=Z, lam=lam, work=work, work_elems=we.value)
+    return out, dict(m=m, R=R, lam=lam, work=work, work_elems=we.value)
 
 
 def device_sym_eig_tridiag_vectors(handle, selections):
     """Unit eigenvectors of the selected (ascending-order) indices per factor as
     device tensors V_f (len(sel_f) x m_f; row k = eigenvector sel_f[k], i.e.
-    the rows Q_f^T[sel_f, :]): inverse iteration on the tridiagonal, then
-    V_f = Y_f Z_f^T on the MFMA GEMM and a re-orthonormalisation of the rows
-    (gg_rows_orthonormalize) so they are orthonormal to ~eps."""
-    from . import dense
+    the rows Q_f^T[sel_f, :]): inverse iteration on the tridiagonal, the
+    Householder reflectors applied to each vector in place (Z is never formed),
+    then a re-orthonormalisation of the rows (gg_rows_orthonormalize) so they
+    are orthonormal to ~eps."""
     L = native.lib()
     m = handle["m"]
     assert len(selections) == len(m)
@@ -191,23 +191,16 @@ def device_sym_eig_tridiag_vectors(handle, selections):
     nsel = (ctypes.c_int * len(m))(*[int(s.size) for s in sel])
     flat = np.concatenate(sel) if sum(s.size for s in sel) else np.zeros(0, dtype=np.int64)
     carr = (ctypes.c_int * max(flat.size, 1))(*[int(v) for v in flat])
-    Y = dev.empty(max(sum(int(s.size) * mi for s, mi in zip(sel, m)), 1))
-    native.check(L.gg_sym_eig_tridiag_vectors(
-        len(m), native.i64_array(m), native.dptr(handle["work"]), handle["work_elems"],
-        native.dptr(handle["lam"]), nsel, carr, native.dptr(Y), native.stream_ptr()),
-        "gg_sym_eig_tridiag_vectors")
     V = dev.empty(max(sum(int(s.size) * mi for s, mi in zip(sel, m)), 1))
-    out, oy, oz = [], 0, 0
+    native.check(L.gg_sym_eig_tridiag_vectors(
+        len(m), native.i64_array(m), native.dptr(handle["R"]), native.dptr(handle["work"]),
+        handle["work_elems"], native.dptr(handle["lam"]), nsel, carr, native.dptr(V),
+        native.stream_ptr()), "gg_sym_eig_tridiag_vectors")
+    out, oy = [], 0
     for s, mi in zip(sel, m):
         k = int(s.size)
-        Yf = Y[oy:oy + k * mi].view(k, mi)
-        Zf = handle["Z"][oz:oz + mi * mi].view(mi, mi)
-        Vf = V[oy:oy + k * mi].view(k, mi)
-        if k:
-            dense.matmul(Yf, Zf, tb=True, C=Vf)
-        out.append(Vf)
+        out.append(V[oy:oy + k * mi].view(k, mi))
         oy += k * mi
-        oz += mi * mi
     # inverse iteration leaves neighbours ~eps ||T|| / gap from orthogonal:
     # classical Gram-Schmidt twice, largest eigenvalue (last row) first
     native.check(L.gg_rows_orthonormalize(len(m), native.i64_array([int(s.size) for s in sel]),

@@ -150,20 +150,23 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
 int gg_sym_eig_work_elems(int count, const int64_t* m, int64_t* elems);
 /* Subset path (GRIEF setup, grief_kernel.py:168-190 needs every eigenvalue but
  * only the eigenvectors of the selected indices):
- *   gg_sym_eig_tridiag: Householder tridiagonalisation A = Z T Z^T; Z_dev gets
- *     Z (row-major, like Q_dev), lam_dev the eigenvalues of T (= of A,
- *     ascending) by bisection; T is kept in work_dev (gg_sym_eig_work_elems).
+ *   gg_sym_eig_tridiag: Householder tridiagonalisation A = Z T Z^T,
+ *     Z = H_0 ... H_{m-3}; R_dev gets the reflectors as rows (m[i] x m[i]
+ *     blocks laid out like Q_dev), lam_dev the eigenvalues of T (= of A,
+ *     ascending) by bisection; T and the reflector scales stay in work_dev
+ *     (gg_sym_eig_work_elems).
  *   gg_sym_eig_tridiag_vectors: for factor i the nsel[i] eigenvalue indices
  *     sel (host, concatenated over factors) -> unit eigenvectors y of T by
- *     inverse iteration, rows of Y_dev (concatenated nsel[i] x m[i] blocks);
- *     the eigenvectors of A are Z y (one GEMM).  Valid when every selected
- *     eigenvalue is separated from its neighbours (the caller checks; no
- *     cluster reorthogonalisation).                                           */
-int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double* Z_dev,
+ *     inverse iteration, then the reflectors applied (Z y): rows of Y_dev
+ *     (concatenated nsel[i] x m[i] blocks) are the eigenvectors of A.  Valid
+ *     when every selected eigenvalue is separated from its neighbours (the
+ *     caller checks; no cluster reorthogonalisation).                         */
+int gg_sym_eig_tridiag(int count, const int64_t* m, const double* A_dev, double* R_dev,
                        double* lam_dev, double* work_dev, int64_t work_elems, gg_stream stream);
-int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* work_dev,
-                               int64_t work_elems, const double* lam_dev, const int* nsel,
-                               const int* sel, double* Y_dev, gg_stream stream);
+int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* R_dev,
+                               const double* work_dev, int64_t work_elems,
+                               const double* lam_dev, const int* nsel, const int* sel,
+                               double* Y_dev, gg_stream stream);
 /* Rows of each k[i] x m[i] block of V_dev (concatenated, row-major)
  * orthonormalised in place (classical Gram-Schmidt twice, last row first). */
 int gg_rows_orthonormalize(int count, const int64_t* k, const int64_t* m, double* V_dev,
