@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 2, session zh: checkpoint after the potrf, subset-eigvec and TN-Gram commits -- the whole GPU suite, smoke(), the default
+# bench (with its CPU baseline) and a kernel-trace profile of the bench.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+O=gpurun_out/r02zh
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+tail -3 $O/pytest_gpu.log
+[ $rc -eq 0 ] || { grep -E "^E |FAILED" $O/pytest_gpu.log | head -20; exit $rc; }
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
+python -c "import json; d=json.load(open('$O/bench.json')); print(d['value'], d['ms_per_step'], [round(v,2) for v in d['mode_product_ms_by_position']], d['roofline']['frac'], d['roofline']['traffic'], d['cpu_baseline']['value'])"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_bench -o run -- python -u bench.py --steps 10 --warmup 2 --cpu-baseline off > $O/bench_prof.json 2> $O/bench_prof.err || { tail -5 $O/bench_prof.err; exit 1; }
+echo done
