@@ -31,18 +31,23 @@ constexpr int kLoadPerT = kBM * kBK / kGemmThreads;  // 8 doubles of A and of B 
 // TA: A stored K x M (lda) ; else M x K.   TB: B stored N x K (ldb) ; else K x N.
 // uplo 1: only C[i][j] with i >= j is written (lower), 2: i <= j (upper).
 // partial != nullptr: split-K; block z writes its raw sum to partial + z*M*N.
+// tri (triangular operands, entries outside the triangle are read as zero and
+// never loaded, so the k-loop skips the zero blocks; gg_trtri):
+//   tri & 1: op(B) lower triangular (op(B)[k][n] = 0 for k < n): k >= n0;
+//   tri & 2: op(A) lower triangular (op(A)[m][k] = 0 for k > m): k < m0 + kBM.
+// One 128 x 128 tile (m0, n0) over k in [kbeg, kend); P: the split-K slab
+// (raw sums) or nullptr (C = alpha acc + beta C).  Body of gemm_kernel and of
+// trtri_level_kernel.
 template <bool TA, bool TB>
-__global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
-    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
-    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
-    int kchunk, double* __restrict__ partial) {
+__device__ __forceinline__ void gemm_tile(int M, int N, double alpha,
+                                          const double* __restrict__ A, int64_t lda,
+                                          const double* __restrict__ B, int64_t ldb, double beta,
+                                          double* C, int64_t ldc, int uplo, int m0, int n0,
+                                          int kbeg, int kend, double* __restrict__ P, int tri) {
   __shared__ __attribute__((aligned(16))) double sA[2][kBK * kLdT];
   __shared__ __attribute__((aligned(16))) double sB[2][kBK * kLdT];
-  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
-  if (uplo == 1 && n0 > m0 + kBM - 1) return;
-  if (uplo == 2 && m0 > n0 + kBN - 1) return;
-  const int kbeg = blockIdx.z * kchunk;
-  const int kend = min(K, kbeg + kchunk);
+  if (tri & 1) kbeg = max(kbeg, n0 - n0 % kBK);
+  if (tri & 2) kend = min(kend, m0 + kBM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
@@ -55,13 +60,15 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
       if (TA) { ki = e / kBM; mi = e % kBM; } else { mi = e / kBK; ki = e % kBK; }
       const int gm = m0 + mi, gk = k0 + ki;
       double v = 0.0;
-      if (gm < M && gk < kend) v = TA ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
+      if (gm < M && gk < kend && (!(tri & 2) || gk <= gm))
+        v = TA ? A[(int64_t)gk * lda + gm] : A[(int64_t)gm * lda + gk];
       ra[u] = v;
       int ni, kj;
       if (TB) { ni = e / kBK; kj = e % kBK; } else { kj = e / kBN; ni = e % kBN; }
       const int gn = n0 + ni, gk2 = k0 + kj;
       double w = 0.0;
-      if (gn < N && gk2 < kend) w = TB ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn];
+      if (gn < N && gk2 < kend && (!(tri & 1) || gk2 >= gn))
+        w = TB ? B[(int64_t)gn * ldb + gk2] : B[(int64_t)gk2 * ldb + gn];
       rb[u] = w;
     }
   };
@@ -114,7 +121,6 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
   }
 
   // f64 C/D layout: lane holds D[(lane>>4) + 4r][lane & 15]
-  double* P = partial ? partial + (int64_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -134,6 +140,20 @@ __global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
           *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
         }
       }
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(kGemmThreads, 2) void gemm_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial, int tri = 0) {
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+  if (uplo == 1 && n0 > m0 + kBM - 1) return;
+  if (uplo == 2 && m0 > n0 + kBN - 1) return;
+  const int kbeg = blockIdx.z * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  double* P = partial ? partial + (int64_t)blockIdx.z * M * N : nullptr;
+  gemm_tile<TA, TB>(M, N, alpha, A, lda, B, ldb, beta, C, ldc, uplo, m0, n0, kbeg, kend, P, tri);
 }
 
 // TN GEMM for Gram-type products C = alpha A^T B (+ beta C), A: K x M and
@@ -568,18 +588,46 @@ static int splitk_factor(int M, int N, int K) {
   return (int)ceil_div(std::max(K, 1), kchunk);
 }
 
+static bool tn_dma_shape(bool ta, bool tb, int M, int N) {
+  return ta && !tb && gemm_tn_variant() > 0 && M >= 2 && N >= 2 && (M % 2) == 0 && (N % 2) == 0;
+}
+
+// Split-K for the TN LDS-DMA kernel (the Gram A = Phi^T Phi, n >> p).  All
+// tiles have the same k-length, so with one tile per workgroup they finish in
+// rounds of 768 (3 per CU), and the C4 Gram (820 lower-triangle tiles) runs a
+// full round plus a round of 52.  Splitting K by S = 8 (units of 1/8 of a
+// tile's k-loop, partial sums reduced by splitk_reduce_kernel) measured
+// (profiles/r02_zk_gram_splitk.jsonl, n = 1e5):
+//   p = 1000  14.95 -> 3.35 ms, p = 5000  53.1 -> 47.3 ms,
+//   p = 10^4 192.2 -> 172.6 ms,
+// flat from S = 8 to 32 at every shape (S = 2 / 4 gave 188.7 / 179.3 ms at
+// p = 10^4).  The partial slabs are capped at 8 GB.
+// GG_GEMM_SPLITK=S forces S (A/B).
+static int tn_splitk(int M, int N, int K, int uplo) {
+  (void)uplo;
+  if (K < 4096) return 1;
+  const int64_t cap_k = std::max<int64_t>(1, K / (64 * kBK));
+  const char* e = getenv("GG_GEMM_SPLITK");
+  if (e != nullptr) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), cap_k));
+  const int64_t cap_mem = std::max<int64_t>(1, (int64_t)1e9 / ((int64_t)M * N));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(8, std::min(cap_k, cap_mem)));
+}
+
+// the split gemm() will use for this call (given an unlimited workspace)
+static int choose_splitk(bool ta, bool tb, int M, int N, int K, int uplo) {
+  if (tn_dma_shape(ta, tb, M, N) && K >= 4096) return tn_splitk(M, N, K, uplo);
+  return splitk_factor(M, N, K);
+}
+
 void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, int64_t lda,
           const double* B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
-          hipStream_t s, double* splitk_buf = nullptr, int64_t splitk_elems = 0) {
+          hipStream_t s, double* splitk_buf = nullptr, int64_t splitk_elems = 0, int tri = 0) {
   if (M <= 0 || N <= 0) return;
   const int gm = (int)ceil_div(M, kBM), gn = (int)ceil_div(N, kBN);
   int S = 1;
   if (splitk_buf != nullptr && K > 4 * kBK) {
-    const int64_t tiles = (int64_t)gm * gn;
-    const int64_t want = std::max<int64_t>(1, 512 / std::max<int64_t>(tiles, 1));
     const int64_t cap_mem = std::max<int64_t>(1, splitk_elems / ((int64_t)M * N));
-    const int64_t cap_k = std::max<int64_t>(1, K / (4 * kBK));
-    S = (int)std::min(std::min(want, cap_mem), std::min<int64_t>(cap_k, 64));
+    S = (int)std::min<int64_t>(choose_splitk(ta, tb, M, N, K, uplo), cap_mem);
   }
   const int kchunk = (int)(ceil_div(ceil_div(std::max(K, 1), S), kBK) * kBK);
   S = (int)ceil_div(std::max(K, 1), kchunk);
@@ -588,7 +636,7 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
   // TN with even shapes and 16-byte aligned operands: the LDS-DMA kernel
   // (GG_GEMM_TN selects its stage shape for A/B; 0 = the register-staged one)
   const int tnv = gemm_tn_variant();
-  if (ta && !tb && tnv > 0 && M >= 2 && N >= 2 && (M % 2) == 0 && (N % 2) == 0 &&
+  if (tri == 0 && tn_dma_shape(ta, tb, M, N) &&
       (lda % 2) == 0 && (ldb % 2) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
       ((reinterpret_cast<uintptr_t>(B) & 15) == 0)) {
     switch (tnv) {
@@ -618,7 +666,7 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
   }
 #define GG_GEMM_LAUNCH(TA_, TB_)                                                              \
   hipLaunchKernelGGL((gemm_kernel<TA_, TB_>), grid, dim3(kGemmThreads), 0, s, M, N, K, alpha, \
-                     A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part)
+                     A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part, tri)
   if (ta && tb) GG_GEMM_LAUNCH(true, true);
   else if (ta) GG_GEMM_LAUNCH(true, false);
   else if (tb) GG_GEMM_LAUNCH(false, true);
@@ -1180,6 +1228,56 @@ __global__ __launch_bounds__(256) void trsm_chain_kernel(int n, int r, const dou
   }
 }
 
+// X's 64 x 64 diagonal blocks = the W_b = L_bb^-1 gg_potrf formed (lower,
+// zero above), one workgroup per block (gg_trtri's leaves).
+__global__ __launch_bounds__(256) void trtri_leaves_kernel(int n, const double* __restrict__ Wall,
+                                                           double* __restrict__ X, int64_t ldx) {
+  const int b = blockIdx.x, k0 = b * kNB, nb = min(kNB, n - k0);
+  const double* W = Wall + (int64_t)b * kNB * kNB;
+  for (int e = threadIdx.x; e < kNB * kNB; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    if (r < nb && c < nb) X[(int64_t)(k0 + r) * ldx + k0 + c] = W[e];
+  }
+}
+
+// X = L^-1 by the recursive split of LAPACK's trtri, for a diagonal block
+// [o, o + n) of the factor (n1 = its first half in whole 64-blocks):
+//   [L11   0 ]^-1   [ X11            0  ]
+//   [L21  L22]    = [ -X22 L21 X11   X22 ],   X11 = L11^-1, X22 = L22^-1
+// The leaves (64 x 64) are gg_potrf's W_b.  Every node of one tree level is
+// independent, so a level is two launches (grid z = node): phase 0
+// T = L21 X11 (X11 lower: tri 1), phase 1 X21 = -X22 T (X22 lower: tri 2),
+// each skipping the zero k-blocks of its triangular operand -- ~p^3 / 3 FLOP
+// on the MFMA GEMM in 2 log2(p / 64) launches.  nodes: (o, n1, n2, T offset).
+template <int PH>
+__global__ __launch_bounds__(kGemmThreads, 2) void trtri_level_kernel(
+    const double* __restrict__ L, int64_t ldl, double* X, int64_t ldx, double* T,
+    const int64_t* __restrict__ nodes) {
+  const int64_t* nd = nodes + 4 * blockIdx.z;
+  const int o = (int)nd[0], n1 = (int)nd[1], n2 = (int)nd[2];
+  double* Tn = T + nd[3];
+  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * kBN;
+  if (m0 >= n2 || n0 >= n1) return;
+  if (PH == 0)
+    gemm_tile<false, false>(n2, n1, 1.0, L + (int64_t)(o + n1) * ldl + o, ldl,
+                            X + (int64_t)o * ldx + o, ldx, 0.0, Tn, n1, 0, m0, n0, 0, n1,
+                            nullptr, 1);
+  else
+    gemm_tile<false, false>(n2, n1, -1.0, X + (int64_t)(o + n1) * ldx + o + n1, ldx, Tn, n1,
+                            0.0, X + (int64_t)(o + n1) * ldx + o, ldx, 0, m0, n0, 0, n2,
+                            nullptr, 2);
+}
+
+static void trtri_tree(int o, int n, int depth, std::vector<std::vector<int64_t>>& levels) {
+  if (n <= kNB) return;
+  const int nblk = (int)ceil_div(n, kNB);
+  const int n1 = (nblk / 2) * kNB, n2 = n - n1;
+  if ((int)levels.size() <= depth) levels.resize(depth + 1);
+  levels[depth].insert(levels[depth].end(), {(int64_t)o, (int64_t)n1, (int64_t)n2, 0});
+  trtri_tree(o, n1, depth + 1, levels);
+  trtri_tree(o + n1, n2, depth + 1, levels);
+}
+
 __global__ void diag_logsum_kernel(const double* A, int64_t lda, int n, double* out) {
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) s += log(A[(int64_t)i * lda + i]);
@@ -1239,6 +1337,18 @@ int gg_gemm_splitk_elems(int M, int N, int K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(elems != nullptr && M >= 0 && N >= 0 && K >= 0, GG_ERR_VALUE, "bad argument");
     const int S = (M > 0 && N > 0) ? gg::splitk_factor(M, N, K) : 1;
+    *elems = S > 1 ? (int64_t)S * M * N : 0;
+  });
+}
+
+int gg_gemm_workspace_elems(int trans_a, int trans_b, int M, int N, int K, int uplo,
+                            int64_t* elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(elems != nullptr && M >= 0 && N >= 0 && K >= 0 && uplo >= 0 && uplo <= 2,
+               GG_ERR_VALUE, "bad argument");
+    const int S = (M > 0 && N > 0 && K > 4 * gg::kBK)
+                      ? gg::choose_splitk(trans_a != 0, trans_b != 0, M, N, K, uplo)
+                      : 1;
     *elems = S > 1 ? (int64_t)S * M * N : 0;
   });
 }
@@ -1511,6 +1621,74 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
                    B_dev, ldb, 0, s);
       }
     }
+  });
+}
+
+int gg_trtri(int n, const double* L_dev, int64_t lda, const double* winv_dev, double* X_dev,
+             int64_t ldx, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(n >= 1 && L_dev && winv_dev && X_dev && lda >= n && ldx >= n, GG_ERR_VALUE,
+               "bad argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nblk = (int)gg::ceil_div(n, gg::kNB);
+    hipLaunchKernelGGL(gg::trtri_leaves_kernel, dim3(nblk), dim3(256), 0, s, n, winv_dev, X_dev,
+                       ldx);
+    GG_LAUNCH_CHECK();
+    if (nblk == 1) return;
+    // the level tables depend only on n: built once per (device, n), kept
+    struct Plan {
+      std::vector<std::vector<int64_t>> levels;
+      int64_t* dtab = nullptr;
+      int64_t tmax = 0;
+    };
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, Plan> plans;
+    int dev = 0;
+    GG_HIP(hipGetDevice(&dev));
+    std::unique_lock<std::mutex> lk(mu);
+    Plan& pl = plans[{dev, n}];
+    if (pl.dtab == nullptr) {
+      gg::trtri_tree(0, n, 0, pl.levels);
+      // T offsets per level (the nodes of a level share one scratch)
+      std::vector<int64_t> tab;
+      for (auto& lv : pl.levels) {
+        int64_t off = 0;
+        for (size_t i = 0; i < lv.size(); i += 4) {
+          lv[i + 3] = off;
+          off += lv[i + 1] * lv[i + 2];
+        }
+        pl.tmax = std::max(pl.tmax, off);
+        tab.insert(tab.end(), lv.begin(), lv.end());
+      }
+      GG_HIP(hipMalloc(reinterpret_cast<void**>(&pl.dtab), tab.size() * sizeof(int64_t)));
+      GG_HIP(hipMemcpy(pl.dtab, tab.data(), tab.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
+    lk.unlock();
+    const auto& levels = pl.levels;
+    const int64_t* dtab = pl.dtab;
+    double* T = nullptr;
+    GG_HIP(hipMallocAsync(&T, (size_t)pl.tmax * sizeof(double), s));
+    // deepest level first: a node's halves are finished before it runs
+    std::vector<int64_t> base(levels.size(), 0);
+    for (size_t l = 1; l < levels.size(); ++l) base[l] = base[l - 1] + (int64_t)levels[l - 1].size();
+    for (int l = (int)levels.size() - 1; l >= 0; --l) {
+      const auto& lv = levels[l];
+      const int nodes = (int)(lv.size() / 4);
+      int mx1 = 0, mx2 = 0;
+      for (int i = 0; i < nodes; ++i) {
+        mx1 = std::max(mx1, (int)lv[4 * i + 1]);
+        mx2 = std::max(mx2, (int)lv[4 * i + 2]);
+      }
+      const dim3 grid((unsigned)gg::ceil_div(mx1, gg::kBN), (unsigned)gg::ceil_div(mx2, gg::kBM),
+                      (unsigned)nodes);
+      hipLaunchKernelGGL(gg::trtri_level_kernel<0>, grid, dim3(gg::kGemmThreads), 0, s, L_dev, lda,
+                         X_dev, ldx, T, dtab + base[l]);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::trtri_level_kernel<1>, grid, dim3(gg::kGemmThreads), 0, s, L_dev, lda,
+                         X_dev, ldx, T, dtab + base[l]);
+      GG_LAUNCH_CHECK();
+    }
+    GG_HIP(hipFreeAsync(T, s));
   });
 }
 

@@ -29,11 +29,12 @@ def matmul(A, B, ta=False, tb=False, alpha=1.0, beta=0.0, C=None, uplo=0, splitk
         beta = 0.0
     work = None
     welems = 0
-    if splitk and K >= 4096 and M * N <= (1 << 26):
-        # exactly the slabs gg_gemm will use (none when the tile grid alone
-        # fills the GPU): no oversized, never-touched workspace
+    if splitk and K >= 4096:
+        # exactly the slabs gg_gemm will use for this call (none when the tile
+        # grid alone fills the GPU evenly): no oversized, never-touched workspace
         need = ctypes.c_int64()
-        native.check(_lib().gg_gemm_splitk_elems(int(M), int(N), int(K), ctypes.byref(need)))
+        native.check(_lib().gg_gemm_workspace_elems(int(ta), int(tb), int(M), int(N), int(K),
+                                                    int(uplo), ctypes.byref(need)))
         welems = need.value
         work = dev.empty(welems) if welems > 0 else None
     native.check(_lib().gg_gemm(int(ta), int(tb), int(M), int(N), int(K), float(alpha),
@@ -96,11 +97,17 @@ class Cholesky(object):
         del t
         return X
 
+    def inverse(self):
+        """L^-1 (lower; the strict upper triangle is zero), gg_trtri."""
+        t = dev.torch()
+        X = t.zeros((self.n, self.n), dtype=t.float64, device=self.L.device)
+        native.check(_lib().gg_trtri(self.n, native.dptr(self.L), self.n, native.dptr(self.winv),
+                                     native.dptr(X), self.n, native.stream_ptr()), "gg_trtri")
+        return X
+
     def inverse_diag(self):
         """diag(P^-1) = column sums of squares of L^-1."""
-        t = dev.torch()
-        I = t.eye(self.n, dtype=t.float64, device=self.L.device)
-        Linv = self.solve(I, which=5)
+        Linv = self.inverse()
         out = dev.empty(self.n)
         native.check(_lib().gg_colsumsq_lower(self.n, native.dptr(Linv), self.n,
                                               native.dptr(out), native.stream_ptr()))

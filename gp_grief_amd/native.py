@@ -91,6 +91,8 @@ SIGNATURES = {
                 ctypes.c_double, _c_dp, ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_double,
                 _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
     "gg_gemm_splitk_elems": [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_i64p],
+    "gg_gemm_workspace_elems": [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, _c_i64p],
     "gg_expand_skc": [_c_dp, ctypes.c_int, ctypes.c_int64, _c_dp, ctypes.c_int, ctypes.c_int,
                       ctypes.c_int, _c_dp, _c_dp, _vp],
     "gg_gemv": [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _c_dp,
@@ -102,6 +104,7 @@ SIGNATURES = {
                  _vp],
     "gg_potrs": [ctypes.c_int, ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _c_dp,
                  ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
+    "gg_trtri": [ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _c_dp, ctypes.c_int64, _vp],
     "gg_colsumsq_lower": [ctypes.c_int, _c_dp, ctypes.c_int64, _c_dp, _vp],
     "gg_kron_dist_create": [ctypes.c_int, _c_i64p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],

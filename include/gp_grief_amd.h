@@ -216,6 +216,10 @@ int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const d
             int64_t ldc, int uplo, double* splitk_dev, int64_t splitk_elems, gg_stream stream);
 /* splitk_dev elements gg_gemm uses for this shape (0: it will not split K).  */
 int gg_gemm_splitk_elems(int M, int N, int K, int64_t* elems);
+/* The same for the exact call (transposes and uplo known): the TN kernel
+   splits K when its tiles quantise badly onto the resident slots.           */
+int gg_gemm_workspace_elems(int trans_a, int trans_b, int M, int N, int K, int uplo,
+                            int64_t* elems);
 /* y = alpha op(A) x + beta y, A: rows x cols row-major (Phi^T y, Phi v).    */
 int gg_gemv(int trans, int64_t rows, int cols, double alpha, const double* A_dev, int64_t lda,
             const double* x_dev, double beta, double* y_dev, double* work_dev,
@@ -235,6 +239,12 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
  * tmp_dev: 64 * r doubles.                                                   */
 int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_dev,
              double* B_dev, int64_t ldb, int which, double* tmp_dev, gg_stream stream);
+/* X = L^-1 (lower; entries above the diagonal untouched) from gg_potrf's
+ * factor and winv_dev, by recursive halving on the MFMA GEMM.  Replaces the
+ * reference's cho_solve(P, I) for the adjoint gradient's diag(P^-1)
+ * (gp_grief_model.py:228-235).                                               */
+int gg_trtri(int n, const double* L_dev, int64_t lda, const double* winv_dev, double* X_dev,
+             int64_t ldx, gg_stream stream);
 /* out[j] = sum_{i >= j} M[i][j]^2 (diag of P^-1 from M = L^-1).              */
 int gg_colsumsq_lower(int n, const double* M_dev, int64_t ld, double* out_dev,
                       gg_stream stream);

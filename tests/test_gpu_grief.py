@@ -88,6 +88,47 @@ def test_gemm_triangle(gg):
     assert np.all(np.triu(Ch, 1) == 0)
 
 
+@pytest.mark.parametrize("S", ["2", "3", "8"])
+@pytest.mark.parametrize("uplo", [0, 1])
+def test_gemm_tn_splitk(gg, monkeypatch, S, uplo):
+    """The TN kernel split over K (GG_GEMM_SPLITK forces S): partial slabs +
+    reduce, with alpha / beta and the lower-triangle mode of the Gram."""
+    import ctypes
+    import torch
+    from gp_grief_amd import dense, native
+    monkeypatch.setenv("GG_GEMM_SPLITK", S)
+    rng = np.random.default_rng(int(S) + 10 * uplo)
+    K, M = 20000, 258
+    R = rng.standard_normal((K, M))
+    C0 = rng.standard_normal((M, M))
+    need = ctypes.c_int64()
+    native.check(native.lib().gg_gemm_workspace_elems(1, 0, M, M, K, uplo, ctypes.byref(need)))
+    assert need.value == int(S) * M * M
+    Rd = torch.from_numpy(R).cuda()
+    C = dense.matmul(Rd, Rd, ta=True, alpha=0.5, beta=-2.0,
+                     C=torch.from_numpy(C0.copy()).cuda(), uplo=uplo).cpu().numpy()
+    ref = 0.5 * R.T.dot(R) - 2.0 * C0
+    if uplo == 1:
+        assert rel(np.tril(C), np.tril(ref)) < 1e-13
+        assert np.array_equal(np.triu(C, 1), np.triu(C0, 1))
+    else:
+        assert rel(C, ref) < 1e-13
+
+
+def test_gemm_tn_splitk_model(gg):
+    """The Gram (K = n >> p) is split 8-way over K (gg_dense.hip tn_splitk);
+    a small-K product is not split."""
+    import ctypes
+    from gp_grief_amd import native
+    need = ctypes.c_int64()
+    native.check(native.lib().gg_gemm_workspace_elems(1, 0, 5000, 5000, 100000, 1,
+                                                      ctypes.byref(need)))
+    assert need.value == 8 * 5000 * 5000
+    native.check(native.lib().gg_gemm_workspace_elems(1, 0, 5000, 5000, 256, 1,
+                                                      ctypes.byref(need)))
+    assert need.value == 0
+
+
 @pytest.mark.parametrize("R,C", [(1, 1), (1000, 37), (100000, 300), (33, 5000)])
 def test_gemv(gg, R, C):
     import torch
@@ -130,6 +171,10 @@ def test_cholesky_solve_logdet(gg, n):
     assert rel(L.T.dot(X2), B) < 1e-12
     Li = ch.solve(torch.eye(n, dtype=torch.float64).cuda(), which=5).cpu().numpy()
     assert rel(np.tril(Li), np.linalg.inv(L)) < 1e-10
+    # recursive triangular inverse (gg_trtri), strict upper triangle untouched
+    Xi = ch.inverse().cpu().numpy()
+    assert rel(Xi, np.linalg.inv(L)) < 1e-10
+    assert np.all(np.triu(Xi, 1) == 0)
 
 
 def test_cholesky_not_spd_raises(gg):
