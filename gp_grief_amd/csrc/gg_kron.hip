@@ -790,9 +790,29 @@ static ModeConfig cfg_glds() {
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
 // cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG
 // epilogue (+ side job when d = 2), 4 fused CG side job
+// GG_MP_PRO selects the fused-CG prologue launch's shape (A/B; p = 200 only):
+// 1 / 3: 12-wave workgroups (one per CU) with 3 / 4 k-steps per chunk,
+// 2: 8-wave workgroups -- wider row segments per workgroup for the prologue's
+// five strided vector passes (tools/hbm_stream_bench.hip: 3R2W in the A
+// pattern at 4.18 / 4.43 / 4.66 TB/s for 4 / 8 / 12 waves in lockstep).
+static int pro_variant() {
+  const char* e = getenv("GG_MP_PRO");
+  return e ? atoi(e) : 0;
+}
+
 template <int JT>
 static ModeConfig config_for(int variant, int cgp) {
   if (cgp == 1) return cfg<JT, 4, 3, 1, 3, 1, 2>();
+  if constexpr (JT == 13) {
+    if (cgp == 2) {
+      switch (pro_variant()) {
+        case 1: return cfg<JT, 12, 3, 2, 1, 1, 2>();
+        case 2: return cfg<JT, 8, 3, 2, 1, 1, 2>();
+        case 3: return cfg<JT, 12, 4, 2, 1, 1, 2>();
+        default: break;
+      }
+    }
+  }
   if (cgp == 2) return cfg<JT, 4, 3, 2, 3, 1, 2>();
   if (cgp == 3) return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
   if (cgp == 4) return cfg<JT, 4, 3, 0, 3, 1, 2, 1>();

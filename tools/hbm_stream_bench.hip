@@ -75,14 +75,18 @@ __global__ __launch_bounds__(256) void stream_kernel(d2* a, d2* b, d2* c, d2* d,
 // wave owns 16 columns b0..b0+15 and walks the q rows four at a time, lane l
 // touching row 4 ks + (l >> 4), column b0 + (l & 15): 8 bytes per lane, four
 // 128-B segments per wave instruction.  3R2W like the CG prologue.
-template <bool NT>
-__global__ __launch_bounds__(256) void apattern_kernel(const double* a, const double* b,
-                                                       const double* c, double* d, double* e,
-                                                       int64_t M, int q, double al) {
+// W waves per workgroup (W x 128 B contiguous per row); SYNC: a workgroup
+// barrier every 12 rows, as the mode product's chunk pipeline has.
+template <bool NT, int W = 4, bool SYNC = false>
+__global__ __launch_bounds__(W * 64) void apattern_kernel(const double* a, const double* b,
+                                                          const double* c, double* d, double* e,
+                                                          int64_t M, int q, double al) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t col = ((int64_t)blockIdx.x * 4 + wave) * 16 + (lane & 15);
-  if (col >= M) return;
+  const int64_t col = ((int64_t)blockIdx.x * W + wave) * 16 + (lane & 15);
+  const bool ok = col < M;
   for (int k = lane >> 4; k < q; k += 4) {
+    if (SYNC && (k >> 2) % 3 == 0) __syncthreads();
+    if (!ok) continue;
     const int64_t o = (int64_t)k * M + col;
     double va, vb, vc;
     if (NT) {
@@ -103,29 +107,29 @@ __global__ __launch_bounds__(256) void apattern_kernel(const double* a, const do
   }
 }
 
-template <bool NT>
+template <bool NT, int W = 4, bool SYNC = false>
 static void run_apattern(double* a, double* b, double* c, double* d, double* e, int64_t n) {
   const int q = 200;
   const int64_t M = n / q;
-  const int grid = (int)((M + 63) / 64);
+  const int grid = (int)((M + 16 * W - 1) / (16 * W));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   for (int w = 0; w < 2; ++w)
-    hipLaunchKernelGGL(apattern_kernel<NT>, dim3(grid), dim3(256), 0, 0, a, b, c, d, e, M, q, 0.5);
+    hipLaunchKernelGGL((apattern_kernel<NT, W, SYNC>), dim3(grid), dim3(64 * W), 0, 0, a, b, c, d, e, M, q, 0.5);
   CK(hipDeviceSynchronize());
   const int reps = 5;
   CK(hipEventRecord(e0, 0));
   for (int r = 0; r < reps; ++r)
-    hipLaunchKernelGGL(apattern_kernel<NT>, dim3(grid), dim3(256), 0, 0, a, b, c, d, e, M, q, 0.5);
+    hipLaunchKernelGGL((apattern_kernel<NT, W, SYNC>), dim3(grid), dim3(64 * W), 0, 0, a, b, c, d, e, M, q, 0.5);
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
   const double gb = (double)(M * q) * 40.0 / 1e9;
-  printf("{\"kind\": \"3R2W-apattern\", \"nt\": %d, \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
-         (int)NT, grid, ms, gb / (ms * 1e-3));
+  printf("{\"kind\": \"3R2W-apattern\", \"nt\": %d, \"waves\": %d, \"sync\": %d, \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
+         (int)NT, W, (int)SYNC, grid, ms, gb / (ms * 1e-3));
   fflush(stdout);
 }
 
@@ -179,15 +183,23 @@ int main() {
   CK(hipMemset(b, 0, bytes));
   CK(hipMemset(c, 0, bytes));
   int cus = 256;
-  for (int g : {cus * 4, cus * 8, cus * 16, cus * 64}) {
-    all_kinds<false, 4>(a, b, c, d, e, n2, g, sink);
-    all_kinds<true, 4>(a, b, c, d, e, n2, g, sink);
+  const bool quick = getenv("HBM_QUICK") != nullptr;
+  if (!quick) {
+    for (int g : {cus * 4, cus * 8, cus * 16, cus * 64}) {
+      all_kinds<false, 4>(a, b, c, d, e, n2, g, sink);
+      all_kinds<true, 4>(a, b, c, d, e, n2, g, sink);
+    }
+    all_kinds<false, 1>(a, b, c, d, e, n2, cus * 16, sink);
+    all_kinds<true, 8>(a, b, c, d, e, n2, cus * 8, sink);
   }
-  all_kinds<false, 1>(a, b, c, d, e, n2, cus * 16, sink);
-  all_kinds<true, 8>(a, b, c, d, e, n2, cus * 8, sink);
   // q x M = 200 x M within the 8 GiB buffers
   const int64_t nfit = (bytes / 8) / 200 * 200;
   run_apattern<false>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
   run_apattern<true>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
+  run_apattern<false, 4, true>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
+  run_apattern<false, 8, false>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
+  run_apattern<false, 8, true>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
+  run_apattern<false, 12, true>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
+  run_apattern<false, 16, true>((double*)a, (double*)b, (double*)c, (double*)d, (double*)e, nfit);
   return 0;
 }
