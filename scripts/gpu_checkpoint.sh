@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 2, session zh: checkpoint after the potrf, subset-eigvec and TN-Gram commits -- the whole GPU suite, smoke(), the default
+# Checkpoint on one MI355X: the whole GPU suite, smoke(), the default
 # bench (with its CPU baseline) and a kernel-trace profile of the bench.
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-O=gpurun_out/r02zh
+O=gpurun_out/${1:-checkpoint}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 tail -3 $O/pytest_gpu.log
