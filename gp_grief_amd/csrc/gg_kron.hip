@@ -375,17 +375,28 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
 // epilogue.  kEpi = 2 (fused CG, last mode product): the epilogue also reads r
 // and accumulates r.q and q.q next to p.q (MpFuse::er), a smaller load batch
 // keeping the extra loads within the register budget; side job too (d = 2).
+// kT4 (p = 16 (JT - 1) + r, r <= 8: the last output tile is at most half
+// real): that tile runs as two v_mfma_f64_4x4x4_4b_f64 (cols 16 (JT-1) + 4h +
+// 0..3, h = 0 / 1; 16 cycles each, the same FLOP rate as the 16x16x4 shape,
+// tools/mfma_f64_4x4_bench.hip) instead of one 64-cycle 16x16x4 of which
+// half is padding.  The 4x4x4_4b A operand is the 16x16x4 one (lane 16 k +
+// row, tools/mfma_4x4_layout_probe.hip), its B fragment h holds column
+// 4h + (l & 3) of the tail at lane l for every 4-lane group (Factor::frag4
+// packs JT + 1 fragments per k-step, the last two these), and D lane
+// 16 r + 4 g + c = row 4 g + r, column 4 h + c: one shuffle pass after the
+// k-loop rebuilds the 16x16 layout of acc[JT - 1] for the epilogue.
 template <int JT, int kWaves, int kKC, int CGP, int kMinW, bool kIdent, int kSplit, int kOpt,
-          int kEpi = 0>
+          int kEpi = 0, bool kT4 = false>
 __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int q, int p, int KS, int jt_total, int jt0,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
     const int* __restrict__ skip, OutMap om, MpFuse fz) {
   static_assert(CGP == 0 || kSplit == 1, "the CG prologue needs one wave per element");
+  static_assert(!kT4 || kSplit == 1, "the 4x4 tail needs one wave per strip");
   if (skip != nullptr && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];  // 2 * kKC * JTL * 64
-  constexpr int JTL = JT * kSplit;                        // tiles staged per launch
+  constexpr int JTL = JT * kSplit + (kT4 ? 1 : 0);       // fragments staged per k-step
   constexpr int kThreads = kWaves * 64;
   constexpr int kChunk2 = kKC * JTL * 32;                 // double2 per full chunk
   constexpr int kPerT = (kChunk2 + kThreads - 1) / kThreads;
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   const int wave = threadIdx.x >> 6;
   const int hp = kSplit == 1 ? 0 : wave % kSplit;         // column part of this wave
   const int strip = kSplit == 1 ? wave : wave / kSplit;
-  const int nt = min(JTL, jt_total - jt0);                // real tiles in this launch
+  const int nt = min(JT * kSplit, jt_total - jt0);        // real tiles in this launch
   const int64_t b0 = ((int64_t)blockIdx.x * (kWaves / kSplit) + strip) * 16;
   const int64_t brow = b0 + (lane & 15);
   const bool bvalid = brow < M;
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   d4 acc[JT];
 #pragma unroll
   for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  double t4[2] = {0.0, 0.0};   // kT4: the tail tile's two 4x4x4_4b accumulators
 
   double a_cur[kKC], a_nxt[kKC], r_cur[kKC], r_nxt[kKC], q_cur[kKC], q_nxt[kKC];
   double stx[kPerT], sty[kPerT];
@@ -551,7 +563,12 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
         if (kOpt & 8) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < JT; ++t) {
-          if (kSplit == 1 || hp * JT + t < nt) {
+          if (kT4 && t == JT - 1) {
+            const double b0 = buf[(s * JTL + t) * 64 + lane];
+            const double b1 = buf[(s * JTL + t + 1) * 64 + lane];
+            t4[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a_cur[s], b0, t4[0], 0, 0, 0);
+            t4[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a_cur[s], b1, t4[1], 0, 0, 0);
+          } else if (kSplit == 1 || hp * JT + t < nt) {
             const double b = buf[(s * JTL + hp * JT + t) * 64 + lane];
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_cur[s], b, acc[t], 0, 0, 0);
           }
@@ -576,6 +593,18 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 #undef GG_A_LOAD
 #undef GG_A_MASK
 
+  if (kT4) {
+    // 4x4x4_4b D (lane 16 r + 4 g + c = row 4 g + r, column 4 h + c) -> the
+    // 16x16 layout (lane L, register rho = row 4 rho + (L >> 4), column L & 15)
+    const int cc = lane & 15;
+    const int src0 = 16 * (lane >> 4) + (lane & 3);
+#pragma unroll
+    for (int rho = 0; rho < 4; ++rho) {
+      const double v0 = __shfl(t4[0], src0 + 4 * rho, 64);
+      const double v1 = __shfl(t4[1], src0 + 4 * rho, 64);
+      acc[JT - 1][rho] = cc < 4 ? v0 : cc < 8 ? v1 : 0.0;
+    }
+  }
   mp_finish<JT, kWaves, kSplit, kIdent, kEpi, CGP, false, kEpiBatch, (kOpt & 4) != 0>(
       acc, Y, M, p, jt0, xs, shift, dot_partials, om, fz, rr_acc, b0, hp, lds, blockIdx.x);
 }
@@ -770,6 +799,7 @@ struct ModeConfig {
   size_t lds;                 // dynamic LDS bytes
   bool glds;                  // all-LDS-DMA kernel: needs M even, X 16-B aligned
   int pers;                   // > 0: persistent, at most pers workgroups per CU
+  bool t4 = false;            // reads Factor::frag4 (JT + 1 fragments per k-step)
 };
 
 // JT = output tiles of the launch; a split config gives each wave ceil(JT/2)
@@ -779,6 +809,12 @@ static ModeConfig cfg() {
   return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT, EPI>, W, KC,
                     SPLIT, JW * SPLIT, 2 * (size_t)KC * JW * SPLIT * 64 * sizeof(double), false,
                     0};
+}
+
+template <int JT, int W, int KC, int CGP, int MINW, int OPT, int EPI = 0>
+static ModeConfig cfg_t4() {
+  return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW, true, 1, OPT, EPI, true>, W, KC, 1,
+                    JT + 1, 2 * (size_t)KC * (JT + 1) * 64 * sizeof(double), false, 0, true};
 }
 
 template <int JT, int KC, int NS, int MINW, int EPI = 0, int PERS = 0>
@@ -798,6 +834,23 @@ static ModeConfig cfg_glds() {
 static int pro_variant() {
   const char* e = getenv("GG_MP_PRO");
   return e ? atoi(e) : 0;
+}
+
+// the default shapes with the 4x4x4 tail (kT4), for factors with frag4
+template <int JT>
+static ModeConfig config_t4(int cgp) {
+  if constexpr (JT == 13) {
+    switch (cgp) {
+      case 1: return cfg_t4<JT, 4, 3, 1, 3, 2>();
+      case 2: return cfg_t4<JT, 4, 3, 2, 3, 2>();
+      case 3: return cfg_t4<JT, 4, 3, 0, 3, 2, 2>();
+      case 4: return cfg_t4<JT, 4, 3, 0, 3, 2, 1>();
+      case 5: return cfg_t4<JT, 4, 3, 0, 3, 2, 3>();
+      case 6: return cfg_t4<JT, 4, 3, 0, 3, 2, 4>();
+      default: return cfg_t4<JT, 4, 3, 0, 3, 2>();
+    }
+  }
+  throw Error(GG_ERR_VALUE, "no 4x4-tail kernel for this tile count");
 }
 
 template <int JT>
@@ -883,7 +936,13 @@ struct Factor {
   int64_t p = 0, q = 0;   // as applied: p x q
   int KS = 0, JT = 0;     // k-steps of 4, column tiles of 16
   double* frag = nullptr; // [KS][JT][64] device
+  // [KS][JT + 1][64]: the last tile as the two 4x4x4_4b B fragments
+  // (mode_product_kernel kT4), when that tile is at most half real and the
+  // single-launch kernel has a kT4 instance for JT (t4_supported)
+  double* frag4 = nullptr;
 };
+
+static bool t4_supported(int JT) { return JT == 13; }
 
 static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool transpose,
                            Factor& f) {
@@ -905,6 +964,23 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
       }
   GG_HIP(hipMalloc(&f.frag, h.size() * sizeof(double)));
   GG_HIP(hipMemcpy(f.frag, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (t4_supported(f.JT) && f.p - 16 * (int64_t)(f.JT - 1) <= 8 && getenv("GG_MP_NO_T4") == nullptr) {
+    const int JF = f.JT + 1;
+    std::vector<double> h4(((size_t)f.KS + 8) * JF * 64, 0.0);
+    for (int ks = 0; ks < f.KS; ++ks)
+      for (int jt = 0; jt < JF; ++jt)
+        for (int l = 0; l < 64; ++l) {
+          const int64_t k = (int64_t)ks * 4 + (l >> 4);
+          // tiles < JT - 1 as before; fragment JT - 1 + h: tail column 4h + (l & 3)
+          const int64_t j = jt < f.JT - 1 ? (int64_t)jt * 16 + (l & 15)
+                                          : (int64_t)(f.JT - 1) * 16 + 4 * (jt - (f.JT - 1)) + (l & 3);
+          double v = 0.0;
+          if (k < f.q && j < f.p) v = transpose ? K[k * cols + j] : K[j * cols + k];
+          h4[((size_t)ks * JF + jt) * 64 + l] = v;
+        }
+    GG_HIP(hipMalloc(&f.frag4, h4.size() * sizeof(double)));
+    GG_HIP(hipMemcpy(f.frag4, h4.data(), h4.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
 }
 
 }  // namespace gg
@@ -985,11 +1061,16 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         const bool side = cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
                           (k == 1 || (split_side && k == 2));
         const int epi_kind = !epi ? 0 : cg->ep_out == nullptr ? 3 : cg->ex != nullptr ? 5 : 6;
-        ModeConfig mc = select_kernel(jt, variant, epi ? epi_kind : side ? 4 : pro);
+        const int kind = epi ? epi_kind : side ? 4 : pro;
+        ModeConfig mc = select_kernel(jt, variant, kind);
         const bool with_xs = last && (shift != 0.0 || dot_partials != nullptr);
         if (mc.glds && (M % 2 != 0 || M < 2 || (reinterpret_cast<uintptr_t>(step_src) & 15) ||
                         with_xs))
-          mc = select_kernel(jt, 0, epi ? epi_kind : side ? 4 : pro);
+          mc = select_kernel(jt, 0, kind);
+        // the default shapes take the 4x4x4 tail when the factor has frag4
+        if (f.frag4 != nullptr && jt0 == 0 && jt == f.JT && variant == 0 &&
+            !(kind == 2 && pro_variant() != 0) && jt == 13)
+          mc = config_t4<13>(kind);
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         if (pro) {
@@ -1028,8 +1109,8 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         int64_t grid = nblk;
         if (mc.pers > 0) grid = std::min<int64_t>(nblk, (int64_t)cu_count() * mc.pers);
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
-                           mode_lds_bytes(mc), stream, step_src, dst, f.frag, M, (int)f.q,
-                           (int)f.p, f.KS, f.JT, jt0,
+                           mode_lds_bytes(mc), stream, step_src, dst, mc.t4 ? f.frag4 : f.frag,
+                           M, (int)f.q, (int)f.p, f.KS, mc.t4 ? f.JT + 1 : f.JT, jt0,
                            last && (shift != 0.0 || parts)
                                ? ((cgp == 2 && cg->ep_out == nullptr) ? cg->p_out : x)
                                : nullptr,
@@ -1088,6 +1169,11 @@ static void set_lds_limits() {
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)mode_lds_bytes(mc)));
       }
+  for (int cgp = 0; cgp < 7; ++cgp) {
+    const ModeConfig mc = config_t4<13>(cgp);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)mode_lds_bytes(mc)));
+  }
   done = true;
 }
 
@@ -1131,8 +1217,10 @@ int gg_kron_destroy(gg_kron* K) {
   return gg::guard([&] {
     if (!K) return;
     for (auto* v : {&K->fwd, &K->bwd})
-      for (gg::Factor& f : *v)
+      for (gg::Factor& f : *v) {
         if (f.frag) (void)hipFree(f.frag);
+        if (f.frag4) (void)hipFree(f.frag4);
+      }
     delete K;
   });
 }
@@ -1280,8 +1368,10 @@ int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_ho
 int gg_kron_dist_destroy(gg_kron_dist* D) {
   return gg::guard([&] {
     if (!D) return;
-    for (gg::Factor& f : D->f)
+    for (gg::Factor& f : D->f) {
       if (f.frag) (void)hipFree(f.frag);
+      if (f.frag4) (void)hipFree(f.frag4);
+    }
     for (void* b : D->opened) (void)hipIpcCloseMemHandle(b);
     if (D->peers_recv) (void)hipFree(D->peers_recv);
     if (D->peers_out) (void)hipFree(D->peers_out);

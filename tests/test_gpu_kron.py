@@ -63,6 +63,8 @@ def test_matvec_wrong_shape_raises(gg):
     [(7, 7)], [(1, 1), (3, 3)], [(16, 16), (16, 16)], [(13, 17), (5, 3), (33, 31)],
     [(40, 40)] * 4, [(64, 64)] * 3, [(200, 200)] * 2, [(203, 203), (9, 9)],
     [(300, 300), (20, 20)], [(257, 255), (6, 2)], [(2, 2)] * 12,
+    # last output tile at most half real (p = 193..200): the 4x4x4 tail path
+    [(193, 150), (197, 64)], [(120, 199), (196, 5)], [(200, 7), (5, 5), (194, 194)],
 ])
 def test_matvec_random_vs_oracle(gg, shape):
     rng = np.random.default_rng(len(shape) * 1000 + shape[0][0])
@@ -216,7 +218,8 @@ def _rbf_factors(ms, ell0=0.15):
     return F
 
 
-@pytest.mark.parametrize("ms", [(8, 8, 8, 8), (24, 20, 16), (40, 36), (300, 30)])
+@pytest.mark.parametrize("ms", [(8, 8, 8, 8), (24, 20, 16), (40, 36), (300, 30), (200, 24),
+                                (24, 200)])
 def test_cg_fused_vs_textbook_vs_exact(gg, ms):
     """The fused recurrence (vector updates ride on the mode products, beta
     from the expanded |r - alpha q|^2) converges like scipy's textbook CG:
