@@ -261,12 +261,39 @@ def launch_passes(d, recurrence, fusion=0):
     return passes
 
 
+def launch_kernels(d, recurrence, fusion=0):
+    """The kernel instantiation of each launch position (gg_kron.hip kron_apply
+    selects it per position): positions that share one are one rocprof row."""
+    if d == 1:
+        return ["epilogue"]
+    kinds = ["plain"] * d
+    kinds[0] = "prologue"
+    kinds[d - 1] = "epilogue"
+    if recurrence == "fused" and fusion != 2:
+        kinds[1] = "side"
+        if d >= 4:
+            kinds[2] = "side"
+    return kinds
+
+
+def dominant_group(per_pos, kinds):
+    """Positions of the kernel with the largest total time per iteration (the
+    rocprof-dominant kernel by total time)."""
+    tot = {}
+    for k, t in zip(kinds, per_pos):
+        tot[k] = tot.get(k, 0.0) + t
+    best = max(tot, key=tot.get)
+    return [i for i, k in enumerate(kinds) if k == best], best
+
+
 def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
     flop = 2.0 * n * m                     # one mode product (square factor m)
     passes = launch_passes(d, recurrence, fusion)
-    dom = int(np.argmax(per_pos))          # largest share of the timed region
-    t = per_pos[dom] * 1e-3
-    byts = 8.0 * n * passes[dom]
+    kinds = launch_kernels(d, recurrence, fusion)
+    group, kind = dominant_group(per_pos, kinds)
+    dom = group[0]
+    t = float(np.mean([per_pos[i] for i in group])) * 1e-3   # per-launch average
+    byts = 8.0 * n * float(np.mean([passes[i] for i in group]))
     f_mfma = flop / (FP64_MFMA_PEAK_TFLOPS * 1e12)
     f_hbm = byts / (HBM_PEAK_GBS * 1e9)
     bound = "mfma" if f_mfma >= f_hbm else "hbm"
@@ -282,17 +309,27 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
         "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
         "frac": (f_mfma if bound == "mfma" else f_hbm) / t,
         "traffic": None, "traffic_unit": "bytes per launch",
-        "kernel": "mode product, launch position %d of %d (%s CG, layout %d)"
-                  % (dom, d, recurrence, fusion),
-        "launch_ms": per_pos[dom],
+        "kernel": "mode product, %s kernel (launch position%s %s of %d; %s CG, layout %d)"
+                  % (kind, "s" if len(group) > 1 else "", ", ".join(str(i) for i in group), d,
+                     recurrence, fusion),
+        "selection": "the kernel with the largest total time per iteration (rocprof "
+                     "groups launches by kernel); per-launch averages over its positions",
+        "positions": group,
+        "launch_ms": t * 1e3,
         "launch_ms_source": "HIP events the library records around each launch, on the "
                             "stream it launches on, over the timed iterations",
         "flop_per_launch": flop, "algorithmic_bytes_per_launch": byts,
-        "passes_per_launch": passes[dom],
+        "passes_per_launch": byts / (8.0 * n),
         "frac_mfma": f_mfma / t, "frac_hbm": f_hbm / t,
         "achieved_tflops": tf, "achieved_gbs": gbs,
     }
+    big = int(np.argmax(per_pos))
     extra = {
+        "largest_launch": {"position": big, "launch_ms": per_pos[big],
+                           "passes": passes[big],
+                           "frac_hbm": 8.0 * n * passes[big] / (HBM_PEAK_GBS * 1e9)
+                           / (per_pos[big] * 1e-3),
+                           "frac_mfma": f_mfma / (per_pos[big] * 1e-3)},
         "mode_product_ms_by_position": per_pos,
         "passes_by_position": passes,
         "matvec_ms": 1e3 * mv_s,
@@ -309,19 +346,24 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
     return roof, extra
 
 
-def pmc_traffic(m, d, kernel_position, recurrence):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    passes (tools/pmc_traffic.py) when they were taken on that launch, this
-    workload and a calibration of the kernel's own access pattern; else None."""
+def pmc_traffic(m, d, positions, recurrence, fusion=0):
+    """HBM bytes per launch of the dominant kernel (averaged over its launch
+    positions) from the committed PMC passes (tools/pmc_traffic.py), when they
+    were taken on this workload, recurrence and fusion layout and every launch
+    matched its algorithmic bytes (the counters calibrated on the kernels' own
+    patterns); else None."""
     path = os.path.join(ROOT, "profiles", "r02_pmc_mode_product.json")
     if (m, d) != (200, 4) or not os.path.exists(path):
         return None, None
     rec = json.load(open(path))
-    if rec.get("position") != kernel_position or rec.get("recurrence") != recurrence:
+    if rec.get("recurrence") != recurrence or rec.get("fusion_layout", 0) != fusion:
         return None, None
     if not rec.get("calibrated_on_own_pattern"):
         return None, None
-    return rec["traffic_bytes"], os.path.relpath(path, ROOT)
+    per = {pp["position"]: pp["traffic_bytes"] for pp in rec.get("per_position", [])}
+    if not all(i in per for i in positions):
+        return None, None
+    return float(np.mean([per[i] for i in positions])), os.path.relpath(path, ROOT)
 
 
 # ---------------------------------------------------------------- CPU leg
@@ -449,7 +491,7 @@ def main():
     per_pos = [t / n_mv for t in mode_ms]
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
                                   solver.fusion)
-    traffic, src = pmc_traffic(m, d, int(np.argmax(per_pos)), solver.recurrence)
+    traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
