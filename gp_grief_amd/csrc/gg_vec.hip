@@ -252,50 +252,75 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
 }
 
 // ----------------------------------------------------------- Lanczos kernels
-// w -= beta * v_prev ; partial w.v
-__global__ __launch_bounds__(kVecThreads) void lz_axpy_dot_kernel(
-    double* __restrict__ w, const double* __restrict__ vprev, const double* __restrict__ v,
-    int64_t n, const double* __restrict__ beta_ptr, double* __restrict__ partials) {
-  const double beta = *beta_ptr;
+// ---- fused Lanczos (gg_lanczos_probe).  The Lanczos vectors are kept
+// unnormalised: V holds u with v = sV u, P holds u_prev with v_prev = sP u_prev
+// (lzs[0], lzs[1]).  The matvec Y = K u + shift u has alpha's dot u.Y in its
+// last epilogue (v.Av = sV^2 u.Y), and ONE streaming pass forms
+// w = Av - alpha v - beta v_prev = cy Y + cu u + cp u_prev with |w|^2, in
+// place of Y: 13 passes over N per step instead of 18 (no normalisation pass;
+// the next step's v is w with sV = 1 / beta).  alpha = v.Av: the oracle's
+// v.(Av - beta v_prev) differs by beta v.v_prev, rounding-level while the
+// three-term recurrence keeps local orthogonality.
+// lzs: [0] sV, [1] sP, [2] cy, [3] cu, [4] cp
+__global__ void lz_coef_kernel(double* __restrict__ lzs, const double* __restrict__ dot,
+                               double* __restrict__ alpha_out,
+                               const double* __restrict__ beta_prev) {
+  const double sV = lzs[0], sP = lzs[1];
+  const double a = sV * sV * *dot;
+  *alpha_out = a;
+  lzs[2] = sV;
+  lzs[3] = -a * sV;
+  lzs[4] = -(*beta_prev) * sP;
+}
+
+// w = cy w + cu v + cp p (in place), partial w.w; 16-byte lanes when all
+// three vectors are 16-byte aligned (wide), else 8-byte
+__global__ __launch_bounds__(kVecThreads) void lz_update_kernel(
+    double* __restrict__ w, const double* __restrict__ v, const double* __restrict__ pv,
+    int64_t n, const double* __restrict__ lzs, double* __restrict__ partials, int wide) {
+  const double cy = lzs[2], cu = lzs[3], cp = lzs[4];
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double wi = w[i] - beta * vprev[i];
-    w[i] = wi;
-    acc = fma(wi, v[i], acc);
+  if (!wide) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const double r = fma(cp, pv[i], fma(cu, v[i], cy * w[i]));
+      w[i] = r;
+      acc = fma(r, r, acc);
+    }
+    const double s = block_sum(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
+    return;
+  }
+  const int64_t n2 = n / 2;
+  double2* __restrict__ w2 = reinterpret_cast<double2*>(w);
+  const double2* __restrict__ v2 = reinterpret_cast<const double2*>(v);
+  const double2* __restrict__ p2 = reinterpret_cast<const double2*>(pv);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+    const double2 a = w2[i], b = v2[i], c = p2[i];
+    double2 r;
+    r.x = fma(cp, c.x, fma(cu, b.x, cy * a.x));
+    r.y = fma(cp, c.y, fma(cu, b.y, cy * a.y));
+    w2[i] = r;
+    acc = fma(r.x, r.x, acc);
+    acc = fma(r.y, r.y, acc);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    const double r = fma(cp, pv[i], fma(cu, v[i], cy * w[i]));
+    w[i] = r;
+    acc = fma(r, r, acc);
   }
   const double s = block_sum(acc);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
-// w -= alpha * v ; partial w.w
-__global__ __launch_bounds__(kVecThreads) void lz_axpy_norm_kernel(
-    double* __restrict__ w, const double* __restrict__ v, int64_t n,
-    const double* __restrict__ alpha_ptr, double* __restrict__ partials) {
-  const double alpha = *alpha_ptr;
-  double acc = 0.0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double wi = w[i] - alpha * v[i];
-    w[i] = wi;
-    acc = fma(wi, wi, acc);
-  }
-  const double s = block_sum(acc);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+// beta = sqrt(|w|^2) ; next step: v_prev = v (sP = sV), v = w (sV = 1 / beta)
+__global__ void lz_beta_kernel(double* __restrict__ lzs, double* __restrict__ beta) {
+  const double b = sqrt(*beta);
+  *beta = b;
+  lzs[1] = lzs[0];
+  lzs[0] = b > 0.0 ? 1.0 / b : 0.0;
 }
-
-// out = w / beta
-__global__ __launch_bounds__(kVecThreads) void lz_scale_kernel(const double* __restrict__ w,
-                                                               double* __restrict__ out,
-                                                               int64_t n,
-                                                               const double* __restrict__ beta_ptr) {
-  const double inv = 1.0 / *beta_ptr;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    out[i] = w[i] * inv;
-}
-
-__global__ void sqrt_inplace_kernel(double* v) { *v = sqrt(*v); }
 
 // A[i][j] *= w[i] (mode 0) or /= w[i] (mode 1); square (mode 2): A = A * A
 __global__ __launch_bounds__(kVecThreads) void scale_rows_kernel(double* __restrict__ A,
@@ -825,42 +850,50 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
     GG_REQUIRE(we <= nr, GG_ERR_VALUE, "non-square factors are not supported here");
     hipStream_t s = gg::as_stream(stream);
     const int64_t n = nr;
-    double* P = work_dev;        // v_prev
-    double* V = work_dev + n;    // v
+    double* P = work_dev;        // u_prev (v_prev = sP u_prev)
+    double* V = work_dev + n;    // u      (v = sV u)
     double* W = work_dev + 2 * n;
     double* mvw = work_dev + 3 * n;
-    double* scal = nullptr;      // [2*steps] alphas, betas + partials
     const int nb = gg::vec_blocks(n);
-    GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + gg::kVecBlocks + 1) * sizeof(double), s));
+    const int64_t npart = std::max<int64_t>(gg::kron_partials_needed(K, false), gg::kVecBlocks);
+    // [alphas | betas | partials | zero | dot | lzs(8)]
+    double* scal = nullptr;
+    GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + npart + 10 + 8) * sizeof(double), s));
     double* alphas = scal;
     double* betas = scal + steps;
     double* parts = scal + 2 * steps;
-    double* zero = parts + gg::kVecBlocks;
+    double* zero = parts + npart;
+    double* dot = zero + 1;
+    double* lzs = dot + 1;
+    const double init[2] = {1.0, 0.0};   // sV = 1 (the probe is normalised), sP = 0
     GG_HIP(hipMemsetAsync(zero, 0, sizeof(double), s));
+    GG_HIP(hipMemcpyAsync(lzs, init, sizeof(init), hipMemcpyHostToDevice, s));
     GG_HIP(hipMemsetAsync(P, 0, n * sizeof(double), s));
     hipLaunchKernelGGL(gg::probe_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
     for (int j = 0; j < steps; ++j) {
-      gg::kron_apply(K, false, V, W, shift, mvw, nullptr, nullptr, s, nullptr, nullptr, 0,
-                     nullptr);
+      // W = K u + shift u, and u.W per block of the last mode product
+      int64_t np = 0;
+      gg::kron_apply(K, false, V, W, shift, mvw, parts, nullptr, s, &np, nullptr, 0, nullptr);
+      gg::launch_reduce_to(parts, np, dot, s);
       const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
-      hipLaunchKernelGGL(gg::lz_axpy_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P,
-                         V, n, beta_prev, parts);
+      hipLaunchKernelGGL(gg::lz_coef_kernel, dim3(1), dim3(1), 0, s, lzs, dot, alphas + j,
+                         beta_prev);
       GG_LAUNCH_CHECK();
-      gg::launch_reduce_to(parts, nb, alphas + j, s);
-      hipLaunchKernelGGL(gg::lz_axpy_norm_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, V,
-                         n, alphas + j, parts);
+      const int wide = ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(V) |
+                         reinterpret_cast<uintptr_t>(P)) & 15) == 0;
+      hipLaunchKernelGGL(gg::lz_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, V, P, n,
+                         lzs, parts, wide);
       GG_LAUNCH_CHECK();
       gg::launch_reduce_to(parts, nb, betas + j, s);
-      hipLaunchKernelGGL(gg::sqrt_inplace_kernel, dim3(1), dim3(1), 0, s, betas + j);
+      hipLaunchKernelGGL(gg::lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + j);
       GG_LAUNCH_CHECK();
-      if (j + 1 < steps) {
-        hipLaunchKernelGGL(gg::lz_scale_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, P, n,
-                           betas + j);
-        GG_LAUNCH_CHECK();
-        std::swap(P, V);  // new v_prev = old v ; new v = W / beta (written into old P)
-      }
+      // rotate: u_prev <- u, u <- w, the old u_prev buffer takes the next matvec
+      double* oldP = P;
+      P = V;
+      V = W;
+      W = oldP;
     }
     GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost,
                           s));

@@ -345,6 +345,23 @@ def test_lanczos_matches_oracle(gg):
     np.testing.assert_allclose(b, bo, rtol=1e-7)
 
 
+@pytest.mark.parametrize("ms", [(7, 9, 5), (40, 36), (200, 30)])
+def test_lanczos_fused_vs_oracle(gg, ms):
+    """The fused Lanczos step (alpha from the matvec epilogue, one update pass,
+    unnormalised vectors): odd n (8-byte update lanes), even n, and a
+    p = 200 factor (the 4x4x4-tail kernels), against the oracle's recurrence."""
+    F = _rbf_factors(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    s = 0.03
+    a, b = gg.linalg.lanczos_tridiag(K, s, 20, seed=7, probe=2)
+    zp = oracle.cg.probe_signs(7, 2, n)
+    ao, bo = oracle.lanczos_tridiag(lambda v: oracle.kron_matvec(F, v) + s * v, zp, 20)
+    k = min(a.size, ao.size, 12)   # late steps drift with rounding (loss of orthogonality)
+    np.testing.assert_allclose(a[:k], ao[:k], rtol=1e-8)
+    np.testing.assert_allclose(b[:k - 1], bo[:k - 1], rtol=1e-7)
+
+
 def test_slq_logdet_vs_exact(gg):
     z = golden("grid_gp.npz")
     s = float(z["sigma2"])
