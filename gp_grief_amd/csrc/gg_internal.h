@@ -111,6 +111,11 @@ struct MpFuse {
   // to ep_out, and (layout 2) applies x += alpha p_old to ex when pending
   double* ep_out = nullptr;
   double* ex = nullptr;
+  // Lanczos prologue (CGP = 3, gg_lanczos_probe): X holds the previous
+  // matvec output Y, r the Lanczos vector u, q_old u_prev; the A operand is
+  // w = coef[2] Y + coef[3] u + coef[4] u_prev, stored to p_out (over u_prev,
+  // element-wise in place), its block partial |w|^2 to rr_part
+  const double* coef = nullptr;
 };
 
 // Output address map of a mode product (see gg_kron.hip epilogue):

@@ -291,7 +291,7 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
   // ---- per-workgroup partial sums: p.q (+ r.q, q.q) of the epilogue, r.r of
   // the fused prologue.  The k-loop ended with a barrier: LDS is free.
   const bool want_dot = dot_partials != nullptr;
-  const bool want_rr = CGP == 2 && fz.rr_part != nullptr;
+  const bool want_rr = CGP >= 2 && fz.rr_part != nullptr;
   if (want_dot || want_rr) {
     double v4[4] = {dsum, rqsum, qqsum, rr_acc};
 #pragma unroll
@@ -440,6 +440,9 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   const int64_t achunk = (int64_t)kKC * m4;
   double* __restrict__ Rg = fz.r;
   const double* __restrict__ Qg = fz.q_old;
+  // CGP 3 writes its output over q_old's elements (Pout == q_old, each element
+  // read then written by the same lane): no restrict on that operand
+  const double* Qa = fz.q_old;
   double* Pout = fz.p_out;
 
   // kOpt & 2: the factor chunk goes global -> LDS directly (global_load_lds,
@@ -483,14 +486,14 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
         const int64_t oc_ = o_ < alast ? o_ : alast;                                  \
         a[s_] = X[oc_];                                                               \
         if (CGP) rr[s_] = Rg[oc_];                                                    \
-        if (CGP == 2) qq[s_] = Qg[oc_];                                               \
+        if (CGP >= 2) qq[s_] = CGP == 3 ? Qa[oc_] : Qg[oc_];                          \
         o_ += m4;                                                                     \
       }                                                                               \
     } else {                                                                          \
       _Pragma("unroll") for (int s_ = 0; s_ < kKC; ++s_) {                            \
         a[s_] = X[o_];                                                                \
         if (CGP) rr[s_] = Rg[o_];                                                     \
-        if (CGP == 2) qq[s_] = Qg[o_];                                                \
+        if (CGP >= 2) qq[s_] = CGP == 3 ? Qa[o_] : Qg[o_];                            \
         o_ += m4;                                                                     \
       }                                                                               \
     }                                                                                 \
@@ -502,7 +505,14 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       const int k_ = (ks0_ + s_) * 4 + krow;                                          \
       const bool ok_ = bvalid && k_ < q;                                              \
       double v_ = a[s_];                                                              \
-      if (CGP) {                                                                      \
+      if (CGP == 3) {                                                                 \
+        const int64_t e_ = (int64_t)k_ * M + brow;                                    \
+        v_ = fma(lz_cp, qq[s_], fma(lz_cu, rr[s_], lz_cy * v_));                      \
+        if (ok_) {                                                                    \
+          Pout[e_] = v_;                                                              \
+          rr_acc = fma(v_, v_, rr_acc);                                               \
+        }                                                                             \
+      } else if (CGP) {                                                               \
         double r_ = rr[s_];                                                           \
         const int64_t e_ = (int64_t)k_ * M + brow;                                    \
         if (CGP == 2 && cg_pending) {                                                 \
@@ -528,7 +538,12 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
   double stx[kPerT], sty[kPerT];
   bool cg_first = false, cg_pending = false;
   double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0;
-  if (CGP) {
+  double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
+  if (CGP == 3) {
+    lz_cy = fz.coef[2];
+    lz_cu = fz.coef[3];
+    lz_cp = fz.coef[4];
+  } else if (CGP) {
     cg_first = fz.sc->first != 0;
     cg_beta = fz.sc->beta;
     if (CGP == 2) {
@@ -582,7 +597,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       for (int s = 0; s < kKC; ++s) {
         a_cur[s] = a_nxt[s];
         if (CGP) r_cur[s] = r_nxt[s];
-        if (CGP == 2) q_cur[s] = q_nxt[s];
+        if (CGP >= 2) q_cur[s] = q_nxt[s];
       }
       GG_A_MASK(c + 1, a_cur, r_cur, q_cur);
     }
@@ -825,7 +840,8 @@ static ModeConfig cfg_glds() {
 
 // variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
 // cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG
-// epilogue (+ side job when d = 2), 4 fused CG side job
+// epilogue (+ side job when d = 2), 4 fused CG side job, 5 / 6 fusion layouts
+// 2 / 1 epilogues, 7 Lanczos prologue
 // GG_MP_PRO selects the fused-CG prologue launch's shape (A/B; p = 200 only):
 // 1 / 3: 12-wave workgroups (one per CU) with 3 / 4 k-steps per chunk,
 // 2: 8-wave workgroups -- wider row segments per workgroup for the prologue's
@@ -847,6 +863,7 @@ static ModeConfig config_t4(int cgp) {
       case 4: return cfg_t4<JT, 4, 3, 0, 3, 2, 1>();
       case 5: return cfg_t4<JT, 4, 3, 0, 3, 2, 3>();
       case 6: return cfg_t4<JT, 4, 3, 0, 3, 2, 4>();
+      case 7: return cfg_t4<JT, 4, 3, 3, 3, 2>();
       default: return cfg_t4<JT, 4, 3, 0, 3, 2>();
     }
   }
@@ -856,6 +873,7 @@ static ModeConfig config_t4(int cgp) {
 template <int JT>
 static ModeConfig config_for(int variant, int cgp) {
   if (cgp == 1) return cfg<JT, 4, 3, 1, 3, 1, 2>();
+  if (cgp == 7) return cfg<JT, 4, 3, 3, 3, 1, 2>();   // Lanczos prologue (CGP 3)
   if constexpr (JT == 13) {
     if (cgp == 2) {
       switch (pro_variant()) {
@@ -1020,7 +1038,12 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   const bool square = transpose ? K->square_steps_bwd : K->square_steps_fwd;
   const int64_t n_in = transpose ? K->n_rows : K->n_cols;
   const int64_t max_inter = transpose ? K->max_inter_bwd : K->max_inter_fwd;
-  GG_REQUIRE(x != y, GG_ERR_VALUE, "x and y must not alias");
+  // x == y only for the Lanczos prologue with an even number of square steps:
+  // the first step reads x and writes the scratch, y is first written by the
+  // second step (gg_lanczos_probe)
+  GG_REQUIRE(x != y || (cgp == 3 && cg != nullptr && fs.size() % 2 == 0 &&
+                        (transpose ? K->square_steps_bwd : K->square_steps_fwd)),
+             GG_ERR_VALUE, "x and y must not alias");
   if (shift != 0.0 || dot_partials != nullptr)
     GG_REQUIRE(K->n_rows == K->n_cols, GG_ERR_VALUE, "shift needs a square operator");
   if (cg == nullptr) cgp = 0;
@@ -1053,7 +1076,8 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         MpFuse fz;
         // the fused CG direction update runs once, in the first launch of
         // step 0; the later launches of that step read the updated p
-        const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? cgp : 0;
+        // cgp 3 (Lanczos prologue) is launch kind 7
+        const int pro = (cgp != 0 && k == 0 && jt0 == 0) ? (cgp == 3 ? 7 : cgp) : 0;
         const bool epi = cgp == 2 && last && dot_partials != nullptr;
         // the x side job rides on the second mode product; with d >= 4 the
         // third (also a plain, MFMA-bound one) takes the second half of x
@@ -1077,10 +1101,11 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           fz.r = cg->r;
           fz.sc = cg->sc;
           fz.p_out = pro == 1 ? const_cast<double*>(x) : cg->p_out;
-          if (pro == 2) {
+          if (pro == 2 || pro == 7) {
             fz.q_old = cg->q_old;
             fz.rr_part = cg->rr_part;
           }
+          if (pro == 7) fz.coef = cg->coef;
         }
         if (side) {
           // [off, off + len): all of x, or its half (even split: 16-byte
@@ -1112,7 +1137,8 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
                            mode_lds_bytes(mc), stream, step_src, dst, mc.t4 ? f.frag4 : f.frag,
                            M, (int)f.q, (int)f.p, f.KS, mc.t4 ? f.JT + 1 : f.JT, jt0,
                            last && (shift != 0.0 || parts)
-                               ? ((cgp == 2 && cg->ep_out == nullptr) ? cg->p_out : x)
+                               ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
+                                                                                   : x)
                                : nullptr,
                            shift, parts, skip, OutMap::ident(), fz);
         GG_LAUNCH_CHECK();
@@ -1163,13 +1189,13 @@ static void set_lds_limits() {
   if (done) return;
   for (int v = 0; v < kNumVariants; ++v)
     for (int jt = 1; jt <= kMaxJT; ++jt)
-      for (int cgp = 0; cgp < 7; ++cgp) {
+      for (int cgp = 0; cgp < 8; ++cgp) {
         const ModeConfig mc = select_kernel(jt, v, cgp);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)mode_lds_bytes(mc)));
       }
-  for (int cgp = 0; cgp < 7; ++cgp) {
+  for (int cgp = 0; cgp < 8; ++cgp) {
     const ModeConfig mc = config_t4<13>(cgp);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)mode_lds_bytes(mc)));

@@ -258,7 +258,9 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
 // last epilogue (v.Av = sV^2 u.Y), and ONE streaming pass forms
 // w = Av - alpha v - beta v_prev = cy Y + cu u + cp u_prev with |w|^2, in
 // place of Y: 13 passes over N per step instead of 18 (no normalisation pass;
-// the next step's v is w with sV = 1 / beta).  alpha = v.Av: the oracle's
+// the next step's v is w with sV = 1 / beta).  With an even number of
+// factors that pass is the next matvec's prologue instead (CGP 3 in
+// gg_kron.hip: w is the MFMA operand, written over u_prev).  alpha = v.Av: the oracle's
 // v.(Av - beta v_prev) differs by beta v.v_prev, rounding-level while the
 // three-term recurrence keeps local orthogonality.
 // lzs: [0] sV, [1] sP, [2] cy, [3] cu, [4] cp
@@ -856,13 +858,15 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
     double* mvw = work_dev + 3 * n;
     const int nb = gg::vec_blocks(n);
     const int64_t npart = std::max<int64_t>(gg::kron_partials_needed(K, false), gg::kVecBlocks);
-    // [alphas | betas | partials | zero | dot | lzs(8)]
+    const int64_t nrr = std::max<int64_t>(gg::kron_prologue_blocks(K), 1);
+    // [alphas | betas | partials | |w|^2 partials | zero | dot | lzs(8)]
     double* scal = nullptr;
-    GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + npart + 10 + 8) * sizeof(double), s));
+    GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + npart + nrr + 10 + 8) * sizeof(double), s));
     double* alphas = scal;
     double* betas = scal + steps;
     double* parts = scal + 2 * steps;
-    double* zero = parts + npart;
+    double* rrparts = parts + npart;
+    double* zero = rrparts + nrr;
     double* dot = zero + 1;
     double* lzs = dot + 1;
     const double init[2] = {1.0, 0.0};   // sV = 1 (the probe is normalised), sP = 0
@@ -872,15 +876,8 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
     hipLaunchKernelGGL(gg::probe_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
-    for (int j = 0; j < steps; ++j) {
-      // W = K u + shift u, and u.W per block of the last mode product
-      int64_t np = 0;
-      gg::kron_apply(K, false, V, W, shift, mvw, parts, nullptr, s, &np, nullptr, 0, nullptr);
-      gg::launch_reduce_to(parts, np, dot, s);
-      const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
-      hipLaunchKernelGGL(gg::lz_coef_kernel, dim3(1), dim3(1), 0, s, lzs, dot, alphas + j,
-                         beta_prev);
-      GG_LAUNCH_CHECK();
+    // w = cy W + cu u + cp u_prev in place of W, |w|^2 -> betas[j], scales
+    auto update_beta = [&](int j) {
       const int wide = ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(V) |
                          reinterpret_cast<uintptr_t>(P)) & 15) == 0;
       hipLaunchKernelGGL(gg::lz_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, W, V, P, n,
@@ -889,11 +886,46 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
       gg::launch_reduce_to(parts, nb, betas + j, s);
       hipLaunchKernelGGL(gg::lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + j);
       GG_LAUNCH_CHECK();
-      // rotate: u_prev <- u, u <- w, the old u_prev buffer takes the next matvec
-      double* oldP = P;
-      P = V;
-      V = W;
-      W = oldP;
+    };
+    // The update of step j - 1 rides on step j's first mode product as its
+    // prologue (CGP 3: the MFMA operand is w itself, written over u_prev)
+    // when the chain's first step writes its scratch, not y (an even number
+    // of factors); otherwise it is its own streaming pass.
+    const bool fuse = gg::kron_d(K) % 2 == 0 && getenv("GG_LANCZOS_UNFUSED") == nullptr;
+    for (int j = 0; j < steps; ++j) {
+      int64_t np = 0;
+      if (j == 0 || !fuse) {
+        // W = K u + shift u, and u.W per block of the last mode product
+        gg::kron_apply(K, false, V, W, shift, mvw, parts, nullptr, s, &np, nullptr, 0, nullptr);
+      } else {
+        gg::MpFuse lf;
+        lf.r = V;
+        lf.q_old = P;
+        lf.p_out = P;
+        lf.rr_part = rrparts;
+        lf.coef = lzs;
+        gg::kron_apply(K, false, W, W, shift, mvw, parts, nullptr, s, &np, &lf, 3, nullptr);
+        // |w|^2 of the prologue -> beta_{j-1}; w (now in P) is the new u
+        gg::launch_reduce_to(rrparts, gg::kron_prologue_blocks(K), betas + (j - 1), s);
+        hipLaunchKernelGGL(gg::lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + (j - 1));
+        GG_LAUNCH_CHECK();
+        std::swap(P, V);   // u_prev <- u, u <- w
+      }
+      gg::launch_reduce_to(parts, np, dot, s);
+      const double* beta_prev = (j == 0) ? zero : betas + (j - 1);
+      hipLaunchKernelGGL(gg::lz_coef_kernel, dim3(1), dim3(1), 0, s, lzs, dot, alphas + j,
+                         beta_prev);
+      GG_LAUNCH_CHECK();
+      if (!fuse || j + 1 == steps) {
+        update_beta(j);
+        if (j + 1 < steps) {
+          // rotate: u_prev <- u, u <- w, the old u_prev buffer takes the next matvec
+          double* oldP = P;
+          P = V;
+          V = W;
+          W = oldP;
+        }
+      }
     }
     GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost,
                           s));
