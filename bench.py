@@ -20,8 +20,9 @@ Prints ONE JSON line (rank 0):
                       sequence; fidelity vs the reference in
                       profiles/r02_cpu_fidelity.json) in a textbook CG on the
                       full grid, 1 warm-up + 3 timed iterations, host threads
-  lanczos             (--lanczos K) K steps of device Lanczos on the same
-                      operator, timed with HIP events (SLQ log-det leg of C3)
+  lanczos             (--lanczos K, default 30) K steps of device Lanczos on
+                      the same operator after the CG leg, timed with HIP
+                      events (SLQ log-det leg of C3); not part of `value`
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 200] [--dims 4]
 --gpus N > 1 without a launcher: this process starts
@@ -59,8 +60,9 @@ def parse():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--recurrence", default="fused", choices=["fused", "textbook"])
-    ap.add_argument("--lanczos", type=int, default=0,
-                    help="also time this many device Lanczos steps (one probe)")
+    ap.add_argument("--lanczos", type=int, default=30,
+                    help="also time this many device Lanczos steps (one probe; 0 = off; "
+                         "single GPU only)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "push", "a2a"])
     ap.add_argument("--fusion", type=int, default=None, choices=[0, 1, 2],
                     help="fused-CG layout (gg_cg_set_fusion); default: the library's")
