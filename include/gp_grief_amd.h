@@ -214,7 +214,10 @@ int gg_expand_skc(const double* x_dev, int U, int64_t n, const int* cidx_dev, in
 int gg_gemm(int trans_a, int trans_b, int M, int N, int K, double alpha, const double* A_dev,
             int64_t lda, const double* B_dev, int64_t ldb, double beta, double* C_dev,
             int64_t ldc, int uplo, double* splitk_dev, int64_t splitk_elems, gg_stream stream);
-/* splitk_dev elements gg_gemm uses for this shape (0: it will not split K).  */
+/* splitk_dev elements gg_gemm uses for this shape with the register-staged
+   kernel's rule (0: it will not split K); kept for callers of round 1 --
+   gg_gemm_workspace_elems below knows the transposes and uplo (the TN Gram
+   kernel's own split) and is the one to use.                                 */
 int gg_gemm_splitk_elems(int M, int N, int K, int64_t* elems);
 /* The same for the exact call (transposes and uplo known): the TN kernel
    splits K when its tiles quantise badly onto the resident slots.           */
