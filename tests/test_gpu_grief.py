@@ -145,7 +145,7 @@ def test_gemv(gg, R, C):
 
 
 # ------------------------------------------------------------------ Cholesky
-@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 300, 1000, 2500])
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 129, 300, 1000, 2500, 4099])
 def test_cholesky_solve_logdet(gg, n):
     import torch
     from gp_grief_amd import dense

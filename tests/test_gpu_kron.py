@@ -345,11 +345,13 @@ def test_lanczos_matches_oracle(gg):
     np.testing.assert_allclose(b, bo, rtol=1e-7)
 
 
-@pytest.mark.parametrize("ms", [(7, 9, 5), (40, 36), (200, 30)])
+@pytest.mark.parametrize("ms", [(7, 9, 5), (40, 36), (200, 30), (9, 8, 7, 6), (24, 200)])
 def test_lanczos_fused_vs_oracle(gg, ms):
-    """The fused Lanczos step (alpha from the matvec epilogue, one update pass,
-    unnormalised vectors): odd n (8-byte update lanes), even n, and a
-    p = 200 factor (the 4x4x4-tail kernels), against the oracle's recurrence."""
+    """The fused Lanczos step (alpha from the matvec epilogue, unnormalised
+    vectors; with an even number of factors the update is the next matvec's
+    prologue): d = 3 with odd n (separate update pass, 8-byte lanes), d = 2 / 4
+    (prologue), a p = 200 factor first and last (the 4x4x4-tail kernels),
+    against the oracle's recurrence."""
     F = _rbf_factors(ms)
     K = gg.tensors.KronMatrix(F, sym=True)
     n = int(np.prod(ms))
