@@ -950,19 +950,42 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
 // them with RCCL, and these kernels consume the global values.
 namespace gg {
 
+// q += shift p ; partial p.q -- 16-byte lanes when q and p are 16-byte
+// aligned (wide), else 8-byte
 __global__ __launch_bounds__(kVecThreads) void shift_dot_kernel(double* __restrict__ q,
                                                                 const double* __restrict__ p,
                                                                 int64_t n, double shift,
                                                                 const CgScalars* __restrict__ sc,
-                                                                double* __restrict__ partials) {
+                                                                double* __restrict__ partials,
+                                                                int wide) {
   if (sc->done) return;
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const double pv = p[i];
-    const double v = fma(shift, pv, q[i]);
-    q[i] = v;
-    acc = fma(pv, v, acc);
+  if (wide) {
+    const int64_t n2 = n / 2;
+    double2* q2 = reinterpret_cast<double2*>(q);
+    const double2* p2 = reinterpret_cast<const double2*>(p);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += stride) {
+      const double2 pv = p2[i];
+      double2 v = q2[i];
+      v.x = fma(shift, pv.x, v.x);
+      v.y = fma(shift, pv.y, v.y);
+      q2[i] = v;
+      acc = fma(pv.x, v.x, acc);
+      acc = fma(pv.y, v.y, acc);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {
+      const double v = fma(shift, p[n - 1], q[n - 1]);
+      q[n - 1] = v;
+      acc = fma(p[n - 1], v, acc);
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const double pv = p[i];
+      const double v = fma(shift, pv, q[i]);
+      q[i] = v;
+      acc = fma(pv, v, acc);
+    }
   }
   const double s = block_sum(acc);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
@@ -1068,8 +1091,10 @@ int gg_cgs_shift_dot(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, d
     GG_REQUIRE(c && q_dev && p_dev && out_dev, GG_ERR_VALUE, "NULL argument");
     hipStream_t s = gg::as_stream(stream);
     const int nb = gg::vec_blocks(n);
+    const int wide =
+        ((reinterpret_cast<uintptr_t>(q_dev) | reinterpret_cast<uintptr_t>(p_dev)) & 15) == 0;
     hipLaunchKernelGGL(gg::shift_dot_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, q_dev,
-                       p_dev, n, shift, c->sc, c->partials);
+                       p_dev, n, shift, c->sc, c->partials, wide);
     GG_LAUNCH_CHECK();
     gg::launch_reduce_to(c->partials, nb, out_dev, s);
   });
