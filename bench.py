@@ -99,46 +99,51 @@ def grid_factors(m, d):
     return K, [np.asarray(f, dtype=np.float64) for f in K.K]
 
 
-def grid_rhs_device(m, d, torch, dev, seed=1):
-    """y = sum_i sin(6 xg_i) + 0.1 eps on the grid, built on the device."""
-    g = torch.linspace(0.0, 1.0, m, dtype=torch.float64, device=dev)
-    f = torch.sin(6.0 * g)
-    y = torch.zeros([m] * d, dtype=torch.float64, device=dev)
-    for k in range(d):
-        shape = [1] * d
-        shape[k] = m
-        y += f.reshape(shape)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(seed)
-    y = y.reshape(-1)
-    chunk = 1 << 27
-    for i in range(0, y.numel(), chunk):
-        n = min(chunk, y.numel() - i)
-        y[i:i + n] += 0.1 * torch.randn(n, dtype=torch.float64, device=dev, generator=gen)
+RHS_NOISE = 0.6180339887498949   # golden-ratio increment of the index-based noise
+
+
+def rhs_at(g, m, d, torch):
+    """y[g] = sum_k sin(6 xg[i_k]) + 0.1 eps(g), xg = linspace(0, 1, m), i_k the
+    digits of the global flat index g (C order), eps(g) = 2 frac(g phi) - 1 --
+    a function of the global index alone, so the sharded layouts of every N
+    hold exactly the single-GPU right-hand side."""
+    gd = g.to(torch.float64)
+    eps = 2.0 * torch.frac(gd * RHS_NOISE) - 1.0
+    y = 0.1 * eps
+    rest = g.clone()
+    for _ in range(d):
+        i = torch.remainder(rest, m)
+        y += torch.sin(6.0 * i.to(torch.float64) / (m - 1))
+        rest = torch.div(rest, m, rounding_mode="floor")
     return y
 
 
-def local_rhs(m, d, world, rank, torch, dev, seed=1):
+def grid_rhs_device(m, d, torch, dev):
+    """The 200^4 right-hand side on the device, built in chunks."""
+    n = m ** d
+    y = torch.empty(n, dtype=torch.float64, device=dev)
+    chunk = 1 << 26
+    for i in range(0, n, chunk):
+        k = min(chunk, n - i)
+        y[i:i + k] = rhs_at(torch.arange(i, i + k, dtype=torch.int64, device=dev), m, d, torch)
+    return y
+
+
+def local_rhs(m, d, world, rank, torch, dev):
     """This rank's shard of the same right-hand side, in the sharded layout
-    (m_1, ..., m_{d-1}, a) with a = i_0 - rank * m/world fastest."""
+    (m_1, ..., m_{d-1}, a) with a = i_0 - rank * m/world fastest: local index
+    l = r s0 + a holds the global element g = (rank s0 + a) R + r, R = N / m."""
     s0 = m // world
-    g = torch.linspace(0.0, 1.0, m, dtype=torch.float64, device=dev)
-    f = torch.sin(6.0 * g)
-    y = torch.zeros([m] * (d - 1) + [s0], dtype=torch.float64, device=dev)
-    for k in range(d - 1):
-        shape = [1] * d
-        shape[k] = m
-        y += f.reshape(shape)
-    shape = [1] * d
-    shape[d - 1] = s0
-    y += f[rank * s0:(rank + 1) * s0].reshape(shape)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(seed + 1000 * rank)
-    y = y.reshape(-1)
-    chunk = 1 << 27
-    for i in range(0, y.numel(), chunk):
-        n = min(chunk, y.numel() - i)
-        y[i:i + n] += 0.1 * torch.randn(n, dtype=torch.float64, device=dev, generator=gen)
+    R = m ** (d - 1)
+    nl = R * s0
+    y = torch.empty(nl, dtype=torch.float64, device=dev)
+    chunk = 1 << 26
+    for i in range(0, nl, chunk):
+        k = min(chunk, nl - i)
+        l = torch.arange(i, i + k, dtype=torch.int64, device=dev)
+        r = torch.div(l, s0, rounding_mode="floor")
+        a = l - r * s0
+        y[i:i + k] = rhs_at((rank * s0 + a) * R + r, m, d, torch)
     return y
 
 
@@ -169,7 +174,9 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     mode = os.environ.get("GG_DIST_MODE", a.exchange)
     if mode == "auto":
-        mode = "push" if getattr(eng, "supports_push", False) else "a2a"
+        # the library's default (DistKronCG): RCCL all-to-all; push (peer
+        # stores over xGMI) is opt-in until it has run across devices
+        mode = "a2a"
     # every rank must take the same exchange: a push setup that fails on any
     # rank (IPC mapping of a peer's buffer) sends all ranks to all-to-all
     try:
@@ -202,6 +209,8 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     sync()
     dist.barrier()
     sync()
+    if on_gpu:
+        cg.profile(True)      # HIP events between the phases, on the compute stream
     t0 = time.perf_counter()
     cg.iterate(a.steps)
     sync()
@@ -213,7 +222,16 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     it, done, rho, tol = cg.status()
     assert it == a.warmup + a.steps and np.isfinite(rho), (it, rho)
     n = m ** d
-    return {
+    phases = None
+    if on_gpu:
+        ph = cg.profile_read()
+        cg.profile(False)
+        # max over ranks of each phase's mean per iteration
+        keys = sorted(ph)
+        v = torch.tensor([ph[k] / a.steps for k in keys], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        phases = dict(zip(keys, [float(u) for u in v.tolist()]))
+    res = {
         "metric": METRIC,
         "value": a.steps / dt,
         "unit": "CG iters/s",
@@ -236,6 +254,40 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
                                              "epilogues + 2 RCCL barriers"
                                       if cg.mode == "push" else "2 RCCL all-to-all"))},
     }
+    if phases is not None:
+        res["phase_ms_per_iteration"] = phases
+        res["local_roofline"] = sharded_roofline(phases, n, m, d, world,
+                                                 getattr(eng, "fold_mask", 0))
+    return res
+
+
+def sharded_roofline(phases, n, m, d, world, fold_mask):
+    """Per-rank achieved rates of the two local MFMA phases (DESIGN.md section
+    6): phase 1 = factors 1..d-1 on N/G elements, phase 2 = factor 0 on N/G;
+    a folded factor (centrosymmetric split) does m instead of 2 m FLOP per
+    element.  Bytes: X read + Y written per mode product."""
+    nl = n / world
+
+    def flop(k):
+        return (1.0 if (fold_mask >> k) & 1 else 2.0) * nl * m
+
+    out = {}
+    for name, ks in (("phase1", range(1, d)), ("phase2", [0])):
+        ms = phases.get(name)
+        if not ms:
+            continue
+        f = sum(flop(k) for k in ks)
+        b = 16.0 * nl * len(ks)
+        out[name] = {"ms": ms, "flop": f, "bytes": b,
+                     "tflops": f / (ms * 1e-3) / 1e12, "gbs": b / (ms * 1e-3) / 1e9,
+                     "frac_mfma": f / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+                     "frac_hbm": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    ex = sum(phases.get(k, 0.0) for k in ("exchange1", "exchange2"))
+    out["exchange_ms"] = ex
+    out["exchange_bytes_per_rank"] = 2 * 8.0 * nl * (world - 1) / world
+    if ex > 0:
+        out["exchange_gbs_per_rank"] = out["exchange_bytes_per_rank"] / (ex * 1e-3) / 1e9
+    return out
 
 
 # ---------------------------------------------------------------- roofline

@@ -26,15 +26,14 @@
 //     four 128-B segments per store.  The last step can fuse y += shift * x
 //     and the partial dot x.y (the CG p.q) per workgroup.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
-#include "gg_internal.h"
+#include "gg_mp.h"
 
 namespace gg {
-
-typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int kMaxJT = 16;  // accumulator tiles per launch (<= 256 output columns)
 constexpr int kEpiBatch = 4;  // epilogue tiles whose x loads are issued together
@@ -68,7 +67,6 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
                                           int64_t b0, int hp, double* red, int64_t blk) {
   constexpr int kThreads = kWaves * 64;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
   // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
   // Output address = rowoff(row) + coloff(j): the identity map is row * p + j;
   // the distributed matvec permutes rows / columns into all-to-all order
@@ -288,66 +286,8 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
       }
     }
   }
-  // ---- per-workgroup partial sums: p.q (+ r.q, q.q) of the epilogue, r.r of
-  // the fused prologue.  The k-loop ended with a barrier: LDS is free.
-  const bool want_dot = dot_partials != nullptr;
-  const bool want_rr = CGP >= 2 && fz.rr_part != nullptr;
-  if (want_dot || want_rr) {
-    double v4[4] = {dsum, rqsum, qqsum, rr_acc};
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v4[i] += __shfl_xor(v4[i], off, 64);
-    if (lane == 0)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[4 * wave + i] = v4[i];
-    if (kRaw) {
-      __builtin_amdgcn_s_waitcnt((7 << 4) | 0xC00F);  // lgkmcnt(0) only
-      __builtin_amdgcn_s_barrier();
-    } else {
-      __syncthreads();
-    }
-    if (threadIdx.x < 4) {
-      const int i = threadIdx.x;
-      double s = 0.0;
-#pragma unroll
-      for (int w = 0; w < kWaves; ++w) s += red[4 * w + i];
-      if (i == 0 && want_dot) dot_partials[blk] = s;
-      if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blk] = s;
-      if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blk] = s;
-      if (i == 3 && want_rr) fz.rr_part[blk] = s;
-    }
-  }
-  // ---- side job (fused CG, second mode product): x += alpha p_old over this
-  // workgroup's slice.  The MFMA-bound kernel has HBM headroom; the other
-  // workgroups of the CU keep the matrix cores busy meanwhile.
-  if (kEpi >= 1 && fz.sx != nullptr && fz.sc->pending) {
-    const double al = fz.sc->alpha;
-    const int64_t lo = blk * fz.schunk;
-    const int64_t hi = min(fz.sn, lo + fz.schunk);
-    double* __restrict__ sx = fz.sx;
-    const double* __restrict__ sp = fz.sp;
-    constexpr int kB = 4;
-    int64_t i = lo + 2 * threadIdx.x;
-    for (; i + 2 * kThreads * (kB - 1) + 1 < hi; i += 2 * kThreads * kB) {
-      double2 xv2[kB], pv2[kB];
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        xv2[u] = *reinterpret_cast<const double2*>(sx + i + 2 * kThreads * u);
-        pv2[u] = *reinterpret_cast<const double2*>(sp + i + 2 * kThreads * u);
-      }
-#pragma unroll
-      for (int u = 0; u < kB; ++u) {
-        xv2[u].x += al * pv2[u].x;
-        xv2[u].y += al * pv2[u].y;
-        *reinterpret_cast<double2*>(sx + i + 2 * kThreads * u) = xv2[u];
-      }
-    }
-    for (; i < hi; i += 2 * kThreads) {
-      sx[i] += al * sp[i];
-      if (i + 1 < hi) sx[i + 1] += al * sp[i + 1];
-    }
-  }
+  mp_block_sums<kWaves, CGP, edots, kRaw>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz, red, blk);
+  if (kEpi >= 1) mp_side_job<kThreads>(fz, blk);
 }
 
 // Double-buffered chunk pipeline, one barrier per chunk:
@@ -797,10 +737,6 @@ static constexpr size_t glds_lds_bytes() {
   return ((size_t)NS * (KC * JT * 64 + 4 * KC * 4 * 16) + 16) * sizeof(double);
 }
 
-typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
-                              int, int, const double*, double, double*, const int*, OutMap,
-                              MpFuse);
-
 // Launch configuration of one mode product: waves per workgroup, k-steps per
 // LDS chunk.  The default -- 4-wave workgroups (one wave per SIMD), 3 k-steps
 // per chunk, three independent workgroups per CU, factor chunks staged by
@@ -958,6 +894,10 @@ struct Factor {
   // (mode_product_kernel kT4), when that tile is at most half real and the
   // single-launch kernel has a kT4 instance for JT (t4_supported)
   double* frag4 = nullptr;
+  // centrosymmetric split (mode_product_fold_kernel): [fKS + 8][2 fFH][64],
+  // fJT 16-wide tiles per half, the last as fTT 4x4x4_4b fragments if fTT > 0
+  double* ffrag = nullptr;
+  int fKS = 0, fJT = 0, fTT = 0;
 };
 
 static bool t4_supported(int JT) { return JT == 13; }
@@ -999,6 +939,67 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
     GG_HIP(hipMalloc(&f.frag4, h4.size() * sizeof(double)));
     GG_HIP(hipMemcpy(f.frag4, h4.data(), h4.size() * sizeof(double), hipMemcpyHostToDevice));
   }
+}
+
+// the centrosymmetric split (mode_product_fold_kernel) for square factors
+static int fold_min_size() {
+  const char* e = getenv("GG_KRON_FOLD_MIN");
+  const int v = e ? atoi(e) : 48;
+  return v < 8 ? 8 : v;   // h >= 4: the kernel's unclamped row walk stays in bounds
+}
+static bool fold_enabled() {
+  const char* e = getenv("GG_KRON_FOLD");
+  return !(e && atoi(e) == 0);
+}
+// tail fragments of a half of hS columns in JT tiles (even m, JT >= 4 only:
+// the instantiated shapes)
+static int fold_tail(int64_t m, int JT) {
+  if (m % 2 != 0 || JT < 4 || getenv("GG_MP_NO_T4") != nullptr) return 0;
+  const int64_t r = (m - m / 2) - 16 * (int64_t)(JT - 1);
+  return r <= 4 ? 1 : r <= 8 ? 2 : 0;
+}
+
+static void pack_fold(const double* K, int64_t m, bool transpose, Factor& f) {
+  if (!fold_enabled() || m < fold_min_size() || m > 256) return;
+  auto F = [&](int64_t j, int64_t i) { return transpose ? K[i * m + j] : K[j * m + i]; };
+  double amax = 0.0, dmax = 0.0;
+  for (int64_t j = 0; j < m; ++j)
+    for (int64_t i = 0; i < m; ++i) {
+      amax = std::max(amax, std::fabs(F(j, i)));
+      dmax = std::max(dmax, std::fabs(F(j, i) - F(m - 1 - j, m - 1 - i)));
+    }
+  if (!(dmax <= 16.0 * 2.220446049250313e-16 * amax) || !(amax > 0.0)) return;
+  // the centrosymmetric part (F + J F J) / 2
+  auto Fc = [&](int64_t j, int64_t i) { return 0.5 * (F(j, i) + F(m - 1 - j, m - 1 - i)); };
+  const int64_t h = m / 2, hS = m - h;
+  const int JT = (int)ceil_div(hS, 16);
+  const int TT = fold_tail(m, JT);
+  const int FH = JT - (TT > 0 ? 1 : 0) + TT;   // fragments per half and k-step
+  const int JF = 2 * FH;
+  const int KS = (int)ceil_div(hS, 4);
+  std::vector<double> hb(((size_t)KS + 8) * JF * 64, 0.0);
+  for (int ks = 0; ks < KS; ++ks)
+    for (int fr = 0; fr < JF; ++fr)
+      for (int l = 0; l < 64; ++l) {
+        const int64_t k = (int64_t)ks * 4 + (l >> 4);   // i'
+        const bool odd_half = fr >= FH;
+        const int t = odd_half ? fr - FH : fr;
+        const int64_t j = (TT > 0 && t >= JT - 1)
+                              ? 16 * (int64_t)(JT - 1) + 4 * (t - (JT - 1)) + (l & 3)
+                              : 16 * (int64_t)t + (l & 15);   // j'
+        double v = 0.0;
+        if (!odd_half) {
+          if (j < hS && k < hS) v = k < h ? 0.5 * (Fc(j, k) + Fc(j, m - 1 - k)) : Fc(j, k);
+        } else if (j < h && k < h) {
+          v = 0.5 * (Fc(j, k) - Fc(j, m - 1 - k));
+        }
+        hb[((size_t)ks * JF + fr) * 64 + l] = v;
+      }
+  GG_HIP(hipMalloc(&f.ffrag, hb.size() * sizeof(double)));
+  GG_HIP(hipMemcpy(f.ffrag, hb.data(), hb.size() * sizeof(double), hipMemcpyHostToDevice));
+  f.fKS = KS;
+  f.fJT = JT;
+  f.fTT = TT;
 }
 
 }  // namespace gg
@@ -1095,6 +1096,13 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         if (f.frag4 != nullptr && jt0 == 0 && jt == f.JT && variant == 0 &&
             !(kind == 2 && pro_variant() != 0) && jt == 13)
           mc = config_t4<13>(kind);
+        // centrosymmetric factors: the even/odd split (half the MFMA work)
+        const bool fold = f.ffrag != nullptr && jt0 == 0 && variant == 0 && fold_kind(kind) &&
+                          !(pro && last) && !(kind == 2 && pro_variant() != 0);
+        if (fold) {
+          const FoldConfig fc = select_fold(f.fJT, f.fTT, kind);
+          mc = ModeConfig{fc.fn, 4, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
+        }
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
         if (pro) {
@@ -1134,8 +1142,9 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         int64_t grid = nblk;
         if (mc.pers > 0) grid = std::min<int64_t>(nblk, (int64_t)cu_count() * mc.pers);
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
-                           mode_lds_bytes(mc), stream, step_src, dst, mc.t4 ? f.frag4 : f.frag,
-                           M, (int)f.q, (int)f.p, f.KS, mc.t4 ? f.JT + 1 : f.JT, jt0,
+                           mode_lds_bytes(mc), stream, step_src, dst,
+                           fold ? f.ffrag : mc.t4 ? f.frag4 : f.frag, M, (int)f.q, (int)f.p,
+                           fold ? f.fKS : f.KS, fold ? mc.jtl : mc.t4 ? f.JT + 1 : f.JT, jt0,
                            last && (shift != 0.0 || parts)
                                ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
                                                                                    : x)
@@ -1200,6 +1209,7 @@ static void set_lds_limits() {
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)mode_lds_bytes(mc)));
   }
+  set_fold_lds_limits();
   done = true;
 }
 
@@ -1228,6 +1238,10 @@ int gg_kron_create(int d, const int64_t* rows, const int64_t* cols,
       for (int k = 0; k < d; ++k) {
         gg::pack_fragments(factors_host[k], rows[k], cols[k], false, K->fwd[k]);
         gg::pack_fragments(factors_host[k], rows[k], cols[k], true, K->bwd[k]);
+        if (rows[k] == cols[k]) {
+          gg::pack_fold(factors_host[k], rows[k], false, K->fwd[k]);
+          gg::pack_fold(factors_host[k], rows[k], true, K->bwd[k]);
+        }
       }
       gg::plan_sizes(K->fwd, K->n_cols, K->max_inter_fwd, K->square_steps_fwd);
       gg::plan_sizes(K->bwd, K->n_rows, K->max_inter_bwd, K->square_steps_bwd);
@@ -1246,6 +1260,7 @@ int gg_kron_destroy(gg_kron* K) {
       for (gg::Factor& f : *v) {
         if (f.frag) (void)hipFree(f.frag);
         if (f.frag4) (void)hipFree(f.frag4);
+        if (f.ffrag) (void)hipFree(f.ffrag);
       }
     delete K;
   });
@@ -1258,6 +1273,17 @@ int gg_kron_shape(const gg_kron* K, int transpose, int64_t* n_out, int64_t* n_in
     if (n_out) *n_out = transpose ? K->n_cols : K->n_rows;
     if (n_in) *n_in = transpose ? K->n_rows : K->n_cols;
     if (work_elems) *work_elems = gg::kron_work_elems(K, transpose != 0);
+  });
+}
+
+int gg_kron_fold_mask(const gg_kron* K, int transpose, int64_t* mask) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && mask != nullptr, GG_ERR_VALUE, "NULL argument");
+    const std::vector<gg::Factor>& fs = transpose ? K->bwd : K->fwd;
+    int64_t v = 0;
+    for (size_t k = 0; k < fs.size(); ++k)
+      if (fs[k].ffrag != nullptr) v |= (int64_t)1 << k;
+    *mask = v;
   });
 }
 

@@ -1,0 +1,429 @@
+// Centrosymmetric Kronecker factors on MI355X: the mode product of
+// gg_kron.hip with the factor's even/odd split, half the FP64 MFMA work.
+//
+// Reference: KronMatrix.kronvec_prod, gp_grief/tensors/kron_matrix.py:52-97
+// (each factor applied by BLAS3 dsymm/dgemm); the split is an execution
+// detail of that product.
+#include "gg_mp.h"
+
+namespace gg {
+
+// ---------------------------------------------------------------------------
+// Centrosymmetric factors: the even/odd split, half the MFMA work.
+//
+// A square factor F (m x m) with J F J = F (J reverses the index order) --
+// every stationary kernel (RBF, Matern, ...) on an evenly spaced grid, i.e.
+// every GridKernel.cov_grid factor on InducingGrid / linspace points -- maps
+// the even and odd parts of its input to the even and odd parts of its output.
+// With h = m / 2, hS = m - h (= h + 1 for odd m), for i', j' < h:
+//   u[i'] = x[i'] + x[m-1-i'],   v[i'] = x[i'] - x[m-1-i']     (u[h] = x[h])
+//   S = Es u (hS x hS),  T = Ea v (h x h),
+//   Es[j'][i'] = (F[j'][i'] + F[j'][m-1-i']) / 2,  Es[j'][h] = F[j'][h],
+//   Ea[j'][i'] = (F[j'][i'] - F[j'][m-1-i']) / 2,
+//   y[j'] = S[j'] + T[j'],   y[m-1-j'] = S[j'] - T[j']         (y[h] = S[h])
+// so one mode product is two half-size GEMMs: m^2 instead of 2 m^2 FLOP per
+// column of X, the same HBM bytes -- at m = 200 in FP64 the mode product moves
+// from the MFMA roof to the HBM roof.  The host packs Es / Ea from the
+// centrosymmetric part (F + J F J) / 2, accepted when max |F - J F J| <= 16 eps
+// max |F| (the dense product's own rounding is m eps); Factor::fold.
+//
+// Same work decomposition as mode_product_kernel: a wave owns 16 rows b of
+// Y and every output column; lane l's A operand at k-step s is built from
+// X[i'][b] and X[m-1-i'][b], i' = 4 s + (l >> 4) -- two 128-B row segments per
+// wave instruction, rows i' ascending and m-1-i' descending -- and the S
+// accumulators take u, the T accumulators v.  Per k-step the fragments are
+// [S tiles][S 4x4 tail][T tiles][T 4x4 tail] (FS + FA of them), staged by
+// global_load_lds, double-buffered, one barrier per chunk.  JS / JA: 16-wide
+// tiles of S / T; TS / TA > 0: that half's last tile (at most 4 TS real
+// columns) runs as TS v_mfma_f64_4x4x4_4b_f64 (see kT4 above).
+// The CG / Lanczos prologues (CGP) update both elements a lane loads and
+// write both back; the epilogue stores S + T at column j' and S - T at m-1-j'
+// (+ shift * x and the CG partial dots, kEpi as mode_product_kernel).
+template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi>
+__global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
+    const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
+    int64_t M, int m, int, int KS, int, int,
+    const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
+    const int* __restrict__ skip, OutMap, MpFuse fz) {
+  constexpr int kWaves = 4;
+  constexpr int kThreads = 256;
+  constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;   // S fragments per k-step
+  constexpr int FA = JA - (TA > 0 ? 1 : 0) + TA;   // T fragments per k-step
+  constexpr int JF = FS + FA;
+  constexpr int kChunk2 = kKC * JF * 32;           // double2 per chunk
+  constexpr int kPerT = (kChunk2 + kThreads - 1) / kThreads;
+  constexpr int kBuf = kKC * JF * 64;              // doubles per LDS buffer
+  constexpr bool edots = kEpi >= 2;
+  if (skip != nullptr && *skip) return;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int h = m >> 1;
+  const int hS = m - h;
+  const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wave) * 16;
+  const int64_t brow = b0 + (lane & 15);
+  const bool bvalid = brow < M;
+  const int64_t bclamp = bvalid ? brow : M - 1;
+  const int krow = lane >> 4;
+  const int nchunks = (KS + kKC - 1) / kKC;
+
+  // B staging: a chunk is kKC * JF * 64 contiguous doubles (8 zero k-steps of
+  // padding after the last, so a partial last chunk stays in bounds)
+  const int64_t bchunk = (int64_t)kBuf;
+  int boff[kPerT];
+  bool bfull[kPerT];
+#pragma unroll
+  for (int u = 0; u < kPerT; ++u) {
+    const int i = threadIdx.x + u * kThreads;
+    bfull[u] = i < kChunk2;
+    boff[u] = 2 * (i < kChunk2 ? i : kChunk2 - 1);
+  }
+  // A operand rows: lo = i' ascending from krow, hi = m-1-i' descending
+  const int64_t m4 = 4 * M;
+  const int64_t lo0 = (int64_t)krow * M + bclamp;
+  const int64_t hi0 = (int64_t)(m - 1 - krow) * M + bclamp;
+  const int64_t alast = (int64_t)(m - 1) * M + bclamp;
+  const int64_t achunk = (int64_t)kKC * m4;
+  double* __restrict__ Rg = fz.r;
+  const double* Qa = fz.q_old;   // CGP 3 writes over q_old (same lane): no restrict
+  double* Pout = fz.p_out;
+
+  bool cg_first = false, cg_pending = false;
+  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0;
+  double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
+  if (CGP == 3) {
+    lz_cy = fz.coef[2];
+    lz_cu = fz.coef[3];
+    lz_cp = fz.coef[4];
+  } else if (CGP) {
+    cg_first = fz.sc->first != 0;
+    cg_beta = fz.sc->beta;
+    if (CGP == 2) {
+      cg_pending = fz.sc->pending != 0;
+      cg_alpha = fz.sc->alpha;
+    }
+  }
+
+  auto stage = [&](int c) {
+    const double* cb = Bf + (int64_t)c * bchunk;
+    double* dstb = lds + (c & 1) * kBuf + wave * 128;
+#pragma unroll
+    for (int u = 0; u < kPerT; ++u)
+      if (bfull[u])
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(cb + boff[u]),
+            (__attribute__((address_space(3))) void*)(dstb + u * kThreads * 2), 16, 0, 0);
+  };
+  // raw loads of chunk c: [0] = row i', [1] = row m-1-i' (only the last
+  // chunk can step past the rows: clamp there, masked when consumed)
+  auto aload = [&](int c, double (&a)[2][kKC], double (&r)[2][kKC], double (&q)[2][kKC]) {
+    int64_t ol = lo0 + (int64_t)c * achunk;
+    int64_t oh = hi0 - (int64_t)c * achunk;
+    const bool last = c == nchunks - 1;
+#pragma unroll
+    for (int s = 0; s < kKC; ++s) {
+      const int64_t l_ = last ? (ol < alast ? ol : alast) : ol;
+      const int64_t h_ = last ? (oh > bclamp ? oh : bclamp) : oh;
+      a[0][s] = X[l_];
+      a[1][s] = X[h_];
+      if (CGP) {
+        r[0][s] = Rg[l_];
+        r[1][s] = Rg[h_];
+      }
+      if (CGP >= 2) {
+        q[0][s] = Qa[l_];
+        q[1][s] = Qa[h_];
+      }
+      ol += m4;
+      oh -= m4;
+    }
+  };
+  // one element of the CG / Lanczos prologue (mode_product_kernel GG_A_MASK)
+  auto upd = [&](double v, double r, double q, bool ok, int64_t e) -> double {
+    if (CGP == 3) {
+      v = fma(lz_cp, q, fma(lz_cu, r, lz_cy * v));
+      if (ok) {
+        Pout[e] = v;
+        rr_acc = fma(v, v, rr_acc);
+      }
+    } else if (CGP) {
+      if (CGP == 2 && cg_pending) {
+        r = r - cg_alpha * q;
+        if (ok) {
+          Rg[e] = r;
+          rr_acc = fma(r, r, rr_acc);
+        }
+      }
+      v = cg_first ? r : fma(cg_beta, v, r);
+      if (Pout != nullptr && ok) Pout[e] = v;
+    }
+    return v;
+  };
+  // raw (row i', row m-1-i') -> (u, v) in place
+  auto amask = [&](int c, double (&a)[2][kKC], double (&r)[2][kKC], double (&q)[2][kKC]) {
+#pragma unroll
+    for (int s = 0; s < kKC; ++s) {
+      const int k = (c * kKC + s) * 4 + krow;
+      const bool okl = bvalid && k < hS;
+      const bool okh = bvalid && k < h;   // a distinct mirrored row
+      double xl = a[0][s], xh = a[1][s];
+      if (CGP) {
+        xl = upd(xl, r[0][s], q[0][s], okl, (int64_t)k * M + brow);
+        xh = upd(xh, r[1][s], q[1][s], okh, (int64_t)(m - 1 - k) * M + brow);
+      }
+      a[0][s] = okl ? (okh ? xl + xh : xl) : 0.0;
+      a[1][s] = okh ? xl - xh : 0.0;
+    }
+  };
+
+  d4 accs[JS], acca[JA];
+#pragma unroll
+  for (int t = 0; t < JS; ++t) accs[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < JA; ++t) acca[t] = d4{0.0, 0.0, 0.0, 0.0};
+  double t4s[TS > 0 ? TS : 1], t4a[TA > 0 ? TA : 1];
+#pragma unroll
+  for (int i = 0; i < (TS > 0 ? TS : 1); ++i) t4s[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < (TA > 0 ? TA : 1); ++i) t4a[i] = 0.0;
+
+  double a_cur[2][kKC], a_nxt[2][kKC], r_cur[2][kKC], r_nxt[2][kKC], q_cur[2][kKC],
+      q_nxt[2][kKC];
+  stage(0);
+  aload(0, a_cur, r_cur, q_cur);
+  amask(0, a_cur, r_cur, q_cur);
+  __syncthreads();
+
+  for (int c = 0; c < nchunks; ++c) {
+    const bool more = c + 1 < nchunks;
+    const int kcn = min(kKC, KS - c * kKC);
+    const double* buf = lds + (c & 1) * kBuf + lane;
+#pragma unroll
+    for (int s = 0; s < kKC; ++s) {
+      if (s == 1 || (kKC == 1 && s == 0)) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) {
+          stage(c + 1);
+          aload(c + 1, a_nxt, r_nxt, q_nxt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (s < kcn) {
+        const double* bs = buf + s * JF * 64;
+        const double au = a_cur[0][s], av = a_cur[1][s];
+#pragma unroll
+        for (int t = 0; t < JS; ++t) {
+          if (TS > 0 && t == JS - 1) {
+#pragma unroll
+            for (int i = 0; i < (TS > 0 ? TS : 1); ++i)
+              t4s[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(au, bs[(t + i) * 64], t4s[i], 0, 0, 0);
+          } else {
+            accs[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bs[t * 64], accs[t], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < JA; ++t) {
+          if (TA > 0 && t == JA - 1) {
+#pragma unroll
+            for (int i = 0; i < (TA > 0 ? TA : 1); ++i)
+              t4a[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bs[(FS + t + i) * 64], t4a[i], 0, 0,
+                                                          0);
+          } else {
+            acca[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bs[(FS + t) * 64], acca[t], 0, 0, 0);
+          }
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int s = 0; s < kKC; ++s)
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          a_cur[w][s] = a_nxt[w][s];
+          if (CGP) r_cur[w][s] = r_nxt[w][s];
+          if (CGP >= 2) q_cur[w][s] = q_nxt[w][s];
+        }
+      amask(c + 1, a_cur, r_cur, q_cur);
+    }
+    __syncthreads();
+  }
+
+  // 4x4x4_4b tails -> the 16x16 layout (see mode_product_kernel kT4)
+  {
+    const int cc = lane & 15;
+    const int src0 = 16 * (lane >> 4) + (lane & 3);
+    if (TS > 0) {
+#pragma unroll
+      for (int rho = 0; rho < 4; ++rho) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < (TS > 0 ? TS : 1); ++i) {
+          const double w = __shfl(t4s[i], src0 + 4 * rho, 64);
+          if ((cc >> 2) == i) v = w;
+        }
+        accs[JS - 1][rho] = v;
+      }
+    }
+    if (TA > 0) {
+#pragma unroll
+      for (int rho = 0; rho < 4; ++rho) {
+        double v = 0.0;
+#pragma unroll
+        for (int i = 0; i < (TA > 0 ? TA : 1); ++i) {
+          const double w = __shfl(t4a[i], src0 + 4 * rho, 64);
+          if ((cc >> 2) == i) v = w;
+        }
+        acca[JA - 1][rho] = v;
+      }
+    }
+  }
+
+  // ---- epilogue: D[b][j'] at lane (j' & 15), register r = row 4 r + (l >> 4).
+  // Half-tile e = 2 t + w: w = 0 stores S + T at column j' = 16 t + (l & 15)
+  // (valid below hS), w = 1 stores S - T at m-1-j' (valid below h).  The wave's
+  // 16 x m output block is contiguous: SGPR base + 32-bit lane byte offset.
+  const int col = lane & 15;
+  const int64_t b0u = (int64_t)__builtin_amdgcn_readfirstlane((int)b0) |
+                      ((int64_t)__builtin_amdgcn_readfirstlane((int)(b0 >> 32)) << 32);
+  const int rows_left = (int)min<int64_t>(16, M - b0u);
+  char* ybase = reinterpret_cast<char*>(Y + b0u * m);
+  auto jcol = [&](int e) -> int {
+    const int j = (e >> 1) * 16 + col;
+    return (e & 1) ? m - 1 - j : j;
+  };
+  auto col_ok = [&](int e) -> bool {
+    const int j = (e >> 1) * 16 + col;
+    return (e & 1) ? j < h : j < hS;
+  };
+  auto boff_of = [&](int r, int e) -> uint32_t {
+    return (uint32_t)(((lane >> 4) + 4 * r) * m + jcol(e)) * 8u;
+  };
+  auto value = [&](int e, int r) -> double {
+    const int t = e >> 1;
+    const double sv = accs[t][r];
+    const double tv = t < JA ? acca[t < JA ? t : 0][r] : 0.0;
+    return (e & 1) ? sv - tv : sv + tv;
+  };
+  double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
+  if (xs == nullptr) {
+#pragma unroll
+    for (int e = 0; e < 2 * JS; ++e) {
+      const bool cok = col_ok(e);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (cok && (lane >> 4) + 4 * r < rows_left)
+          *reinterpret_cast<double*>(ybase + boff_of(r, e)) = value(e, r);
+    }
+  } else {
+    // shift / dots: the loads of half-tile e + 1 are issued before e's stores
+    // (CDNA4 retires vmcnt in order and stores count)
+    const double* __restrict__ er = fz.er;
+    const char* xbase = reinterpret_cast<const char*>(xs + b0u * m);
+    const char* ebase = edots ? reinterpret_cast<const char*>(er + b0u * m) : nullptr;
+    double xv[2][4], ev[2][4];
+    auto load_e = [&](int e, double (&xo)[4], double (&eo)[4]) {
+      const bool cok = col_ok(e);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = cok && (lane >> 4) + 4 * r < rows_left;
+        const uint32_t o = boff_of(r, e);
+        xo[r] = ok ? *reinterpret_cast<const double*>(xbase + o) : 0.0;
+        eo[r] = (ok && edots) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
+      }
+    };
+    load_e(0, xv[0], ev[0]);
+#pragma unroll
+    for (int e = 0; e < 2 * JS; ++e) {
+      const int cb = e & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      if (e + 1 < 2 * JS) load_e(e + 1, xv[cb ^ 1], ev[cb ^ 1]);
+      const bool cok = col_ok(e);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (cok && (lane >> 4) + 4 * r < rows_left) {
+          const double pv = xv[cb][r];
+          const double v = fma(shift, pv, value(e, r));
+          dsum = fma(pv, v, dsum);
+          if (edots) {
+            rqsum = fma(ev[cb][r], v, rqsum);
+            qqsum = fma(v, v, qqsum);
+          }
+          *reinterpret_cast<double*>(ybase + boff_of(r, e)) = v;
+        }
+      }
+    }
+  }
+  mp_block_sums<kWaves, CGP, edots, false>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz, lds,
+                                           blockIdx.x);
+  if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
+}
+
+// kind (kron_apply's launch kind) -> the folded kernel; kinds 5 / 6 (fusion
+// layouts 1 / 2) and the tuning variants stay on mode_product_kernel
+bool fold_kind(int kind) {
+  return kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 4 || kind == 7;
+}
+
+template <int JT, int TT, int KIND>
+static FoldConfig cfg_fold() {
+  constexpr int CGP = KIND == 1 ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
+  constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : 0;
+  constexpr int KC = CGP ? 2 : 3;
+  constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI>, KC, JF,
+                    2 * (size_t)KC * JF * 64 * sizeof(double)};
+}
+
+template <int JT, int TT>
+static FoldConfig fold_by_kind(int kind) {
+  switch (kind) {
+    case 1: return cfg_fold<JT, TT, 1>();
+    case 2: return cfg_fold<JT, TT, 2>();
+    case 3: return cfg_fold<JT, TT, 3>();
+    case 4: return cfg_fold<JT, TT, 4>();
+    case 7: return cfg_fold<JT, TT, 7>();
+    default: return cfg_fold<JT, TT, 0>();
+  }
+}
+
+FoldConfig select_fold(int JT, int TT, int kind) {
+  if (TT == 0) {
+    switch (JT) {
+      case 1: return fold_by_kind<1, 0>(kind);
+      case 2: return fold_by_kind<2, 0>(kind);
+      case 3: return fold_by_kind<3, 0>(kind);
+      case 4: return fold_by_kind<4, 0>(kind);
+      case 5: return fold_by_kind<5, 0>(kind);
+      case 6: return fold_by_kind<6, 0>(kind);
+      case 7: return fold_by_kind<7, 0>(kind);
+      case 8: return fold_by_kind<8, 0>(kind);
+      default: break;
+    }
+  } else if (TT == 1 || TT == 2) {
+    switch (JT) {
+      case 4: return TT == 1 ? fold_by_kind<4, 1>(kind) : fold_by_kind<4, 2>(kind);
+      case 5: return TT == 1 ? fold_by_kind<5, 1>(kind) : fold_by_kind<5, 2>(kind);
+      case 6: return TT == 1 ? fold_by_kind<6, 1>(kind) : fold_by_kind<6, 2>(kind);
+      case 7: return TT == 1 ? fold_by_kind<7, 1>(kind) : fold_by_kind<7, 2>(kind);
+      case 8: return TT == 1 ? fold_by_kind<8, 1>(kind) : fold_by_kind<8, 2>(kind);
+      default: break;
+    }
+  }
+  throw Error(GG_ERR_VALUE, "no folded kernel for this factor shape");
+}
+
+void set_fold_lds_limits() {
+  for (int jt = 1; jt <= 8; ++jt)
+    for (int tt = 0; tt <= 2; ++tt) {
+      if (tt > 0 && jt < 4) continue;
+      for (int kind = 0; kind < 8; ++kind) {
+        if (!fold_kind(kind)) continue;
+        const FoldConfig fc = select_fold(jt, tt, kind);
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+      }
+    }
+}
+
+}  // namespace gg

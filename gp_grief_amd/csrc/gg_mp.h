@@ -1,0 +1,97 @@
+// Device helpers shared by the mode-product kernels (gg_kron.hip,
+// gg_kron_fold.hip) and the folded-kernel launch table.  Internal.
+#pragma once
+
+#include "gg_internal.h"
+
+namespace gg {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, int, int, int,
+                              int, int, const double*, double, double*, const int*, OutMap,
+                              MpFuse);
+
+// Per-workgroup partial sums of a mode product: p.q (+ r.q, q.q when edots)
+// of the epilogue, r.r (or |w|^2) of the fused prologue.  Called after the
+// k-loop's last barrier (LDS is free); red: 4 * kWaves doubles of LDS.
+template <int kWaves, int CGP, bool edots, bool kRaw>
+__device__ __forceinline__ void mp_block_sums(double dsum, double rqsum, double qqsum,
+                                              double rr_acc, double* __restrict__ dot_partials,
+                                              const MpFuse& fz, double* red, int64_t blk) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const bool want_dot = dot_partials != nullptr;
+  const bool want_rr = CGP >= 2 && fz.rr_part != nullptr;
+  if (!(want_dot || want_rr)) return;
+  double v4[4] = {dsum, rqsum, qqsum, rr_acc};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v4[i] += __shfl_xor(v4[i], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[4 * wave + i] = v4[i];
+  if (kRaw) {
+    __builtin_amdgcn_s_waitcnt((7 << 4) | 0xC00F);  // lgkmcnt(0) only
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) {
+    const int i = threadIdx.x;
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += red[4 * w + i];
+    if (i == 0 && want_dot) dot_partials[blk] = s;
+    if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blk] = s;
+    if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blk] = s;
+    if (i == 3 && want_rr) fz.rr_part[blk] = s;
+  }
+}
+
+// Side job (fused CG, second / third mode product): x += alpha p_old over
+// this workgroup's slice, 16-byte lanes.  The mode product has HBM headroom;
+// the other workgroups of the CU keep the matrix cores busy meanwhile.
+template <int kThreads>
+__device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
+  if (fz.sx == nullptr || !fz.sc->pending) return;
+  const double al = fz.sc->alpha;
+  const int64_t lo = blk * fz.schunk;
+  const int64_t hi = min(fz.sn, lo + fz.schunk);
+  double* __restrict__ sx = fz.sx;
+  const double* __restrict__ sp = fz.sp;
+  constexpr int kB = 4;
+  int64_t i = lo + 2 * threadIdx.x;
+  for (; i + 2 * kThreads * (kB - 1) + 1 < hi; i += 2 * kThreads * kB) {
+    double2 xv2[kB], pv2[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      xv2[u] = *reinterpret_cast<const double2*>(sx + i + 2 * kThreads * u);
+      pv2[u] = *reinterpret_cast<const double2*>(sp + i + 2 * kThreads * u);
+    }
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      xv2[u].x += al * pv2[u].x;
+      xv2[u].y += al * pv2[u].y;
+      *reinterpret_cast<double2*>(sx + i + 2 * kThreads * u) = xv2[u];
+    }
+  }
+  for (; i < hi; i += 2 * kThreads) {
+    sx[i] += al * sp[i];
+    if (i + 1 < hi) sx[i + 1] += al * sp[i + 1];
+  }
+}
+
+// The folded (centrosymmetric) mode product, gg_kron_fold.hip: one kernel per
+// (tiles per half JT, 4x4 tail fragments TT, kron_apply launch kind)
+struct FoldConfig {
+  mode_kernel_t fn;
+  int kc, jf;     // k-steps per LDS chunk, fragments per k-step (both halves)
+  size_t lds;     // dynamic LDS bytes
+};
+bool fold_kind(int kind);
+FoldConfig select_fold(int JT, int TT, int kind);
+void set_fold_lds_limits();
+
+}  // namespace gg

@@ -270,21 +270,56 @@ class DistKronCG(object):
         else:
             self.q, self.recv = engine.empty(), engine.empty()
         self.x = None
+        self._prof = None
+
+    # ---- per-phase timing (GPU engines): HIP events on the compute stream;
+    # a collective's time is what the compute stream waits for it
+    def profile(self, enable):
+        self._prof = [] if enable else None
+
+    def _mark(self, name):
+        if self._prof is not None:
+            import torch
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._prof.append((name, e))
+
+    def profile_read(self):
+        """ms per phase name summed over the profiled iterations (the interval
+        ending at each mark is charged to that mark's phase)."""
+        import torch
+        torch.cuda.synchronize()
+        out = {}
+        ev = self._prof or []
+        for (_, e0), (n1, e1) in zip(ev[:-1], ev[1:]):
+            if n1 == "start":
+                continue
+            out[n1] = out.get(n1, 0.0) + e0.elapsed_time(e1)
+        return out
 
     def _allreduce(self):
         self.x_ex.all_reduce(self.e.reduce_buffer())
+        self._mark("allreduce")
 
     def _matvec_into_q(self, x, fuse_cg):
         if self.mode == "push":
             self.e.phase1_push(x, self.send, r=self.r if fuse_cg else None)
+            self._mark("phase1")
             self.x_ex.barrier()   # every rank's chunks have landed in every recv
+            self._mark("exchange1")
             self.e.phase2_push()
+            self._mark("phase2")
             self.x_ex.barrier()   # every rank's q is complete
+            self._mark("exchange2")
         else:
             self.e.phase1(x, self.send, r=self.r if fuse_cg else None)
+            self._mark("phase1")
             self.x_ex.all_to_all(self.recv, self.send)
+            self._mark("exchange1")
             self.e.phase2(self.recv, self.send)
+            self._mark("phase2")
             self.x_ex.all_to_all(self.q, self.send)
+            self._mark("exchange2")
 
     def apply(self, x, y, fuse_cg=False):
         """y = K x (no shift) for local shards; fuse_cg: x <- beta x + r first."""
@@ -302,13 +337,17 @@ class DistKronCG(object):
 
     def iterate(self, n_iter):
         for _ in range(int(n_iter)):
+            self._mark("start")
             self._matvec_into_q(self.p, fuse_cg=True)        # p = r + beta p ; q = K p
             self.e.shift_dot(self.q, self.p, self.shift)     # q += s p ; local p.q
+            self._mark("vector")
             self._allreduce()
             self.e.cg_alpha()
             self.e.cg_update(self.x, self.r, self.p, self.q)  # x, r ; local r.r
+            self._mark("vector")
             self._allreduce()
             self.e.cg_rho()
+            self._mark("scalars")
 
     def status(self):
         return self.e.cg_status()

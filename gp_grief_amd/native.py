@@ -40,6 +40,7 @@ SIGNATURES = {
                        ctypes.POINTER(ctypes.c_void_p)],
     "gg_kron_destroy": [_vp],
     "gg_kron_shape": [_vp, ctypes.c_int, _c_i64p, _c_i64p, _c_i64p],
+    "gg_kron_fold_mask": [_vp, ctypes.c_int, _c_i64p],
     "gg_kron_matvec": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_double, _c_dp, _vp],
     "gg_kron_diag_scale": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double, ctypes.c_int, _c_dp,
                            _c_dp, _vp],

@@ -62,6 +62,13 @@ class _DeviceKron(object):
                                                 ctypes.byref(b), ctypes.byref(w)))
         return a.value, b.value, w.value
 
+    def fold_mask(self, transpose=False):
+        """Bit k set: factor k runs through the centrosymmetric even/odd split
+        (gg_kron_fold_mask; half the MFMA work)."""
+        v = ctypes.c_int64()
+        native.check(native.lib().gg_kron_fold_mask(self.h, int(transpose), ctypes.byref(v)))
+        return v.value
+
     def work(self, transpose):
         key = bool(transpose)
         if key not in self._work:

@@ -56,6 +56,14 @@ int gg_kron_destroy(gg_kron* K);
  * float64 elements of the `work_dev` scratch gg_kron_matvec needs.          */
 int gg_kron_shape(const gg_kron* K, int transpose, int64_t* n_out, int64_t* n_in,
                   int64_t* work_elems);
+/* Bit k of *mask is set when factor k of the operator (of K^T if transpose)
+ * is applied through the centrosymmetric even/odd split: square factors with
+ * max |F - J F J| <= 16 eps max |F| (J = index reversal; every stationary
+ * kernel on an evenly spaced grid), m >= GG_KRON_FOLD_MIN (default 48),
+ * unless GG_KRON_FOLD=0 at gg_kron_create.  Half the MFMA work of the dense
+ * factor, same result up to rounding.  No
+ * reference counterpart: an execution detail of kron_matrix.py:52-97.     */
+int gg_kron_fold_mask(const gg_kron* K, int transpose, int64_t* mask);
 
 /* y = (K_0 (x) ... (x) K_{d-1})^{T?} x + shift * x
  * KronMatrix.kronvec_prod / __mul__ / .T     kron_matrix.py:52-102, 203-213

@@ -148,6 +148,16 @@ class ThreadExchange(object):
         self.bar.wait()
 
 
+def bind_device(rank):
+    """One GPU per rank when the box has several (rank % device count), so
+    the process tests run cross-device -- peer stores and RCCL over xGMI --
+    on any multi-GPU node; on one GPU every rank shares cuda:0."""
+    n = torch.cuda.device_count()
+    if n > 0:
+        torch.cuda.set_device(rank % n)
+    return rank % n if n > 0 else None
+
+
 def run_threads(world, fn):
     """Run fn(rank) in `world` threads; re-raise the first failure."""
     errs = [None] * world

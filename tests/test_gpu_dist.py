@@ -74,9 +74,10 @@ def _ipc_worker(rank, world, port, m, d, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
+    from dist_helpers import bind_device, reference_factors
+    bind_device(rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from gp_grief_amd.distributed import DistKronCG, HipEngine, TorchExchange, scatter_global
-    from dist_helpers import reference_factors
     F = reference_factors(m, d)
     xg = np.random.default_rng(11).standard_normal(m ** d)
     eng = HipEngine(F, world, rank)

@@ -1,0 +1,180 @@
+"""The centrosymmetric even/odd split of the Kronecker mode product on the MI355X.
+
+Every stationary kernel on an evenly spaced grid gives a factor F with
+J F J = F (J reverses the index order); gg_kron_create then packs the two
+half-size blocks Es / Ea and the mode product runs as two h x h GEMMs
+(mode_product_fold_kernel).  The product it computes is
+the reference's KronMatrix.kronvec_prod (gp_grief/tensors/kron_matrix.py:52-97)
+up to rounding: these tests hold it to the oracle's dense product at 1e-13
+relative (one GEMM chain) and to the unfolded device kernel, for every launch
+kind the CG / Lanczos drivers use (plain, textbook / fused / Lanczos
+prologues, side job, fused epilogue), even and odd m, the 4x4x4 tails, and
+partial row strips.  GG_KRON_FOLD_MIN=8 lets small factors take the split.
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def gg(gpu):
+    import gp_grief_amd
+    return gp_grief_amd
+
+
+@pytest.fixture
+def fold_small(monkeypatch):
+    monkeypatch.setenv("GG_KRON_FOLD_MIN", "8")
+    monkeypatch.delenv("GG_KRON_FOLD", raising=False)
+
+
+def grid_factor(m, ell=0.15, kind="RBF"):
+    g = np.linspace(0.0, 1.0, m)
+    return oracle.cov_1d(kind, g, g, 1.0, ell) + 1e-12 * np.eye(m)
+
+
+def kron(gg, F):
+    return gg.tensors.KronMatrix(F, sym=True)
+
+
+def fold_mask(K, transpose=False):
+    return K._device().fold_mask(transpose)
+
+
+# m: even / odd, below / at / above a 16-column tile, the 4x4x4 tails (even m
+# with a last half-tile of 1..8 columns: 200, 230, 100), the 256 limit
+MS = [8, 9, 16, 17, 31, 32, 33, 47, 64, 65, 97, 100, 127, 128, 129, 199, 200, 201, 230, 255,
+      256]
+
+
+@pytest.mark.parametrize("m", MS)
+def test_fold_matvec_vs_oracle(gg, fold_small, m):
+    """[F_m, B_7, F_m]: the split on the first and the last mode product
+    (7 < 8 stays dense), forward and transposed, vs the dense oracle and
+    vs the unfolded kernel."""
+    F = [grid_factor(m, 0.12), grid_factor(7, 0.3), grid_factor(m, 0.2, "Matern52")]
+    K = kron(gg, F)
+    assert fold_mask(K) == 0b101 and fold_mask(K, True) == 0b101
+    n = 7 * m * m
+    x = np.random.default_rng(m).standard_normal((n, 1))
+    y = K * x
+    ref = oracle.kron_matvec(F, x[:, 0])
+    assert rel(y, ref) < 1e-13
+    assert rel(K.T * x, ref) < 1e-13   # symmetric factors: K^T = K
+
+
+def test_fold_matches_unfolded_kernel(gg, monkeypatch):
+    F = [grid_factor(200, 0.1), grid_factor(64, 0.11), grid_factor(49, 0.3)]
+    x = np.random.default_rng(0).standard_normal((200 * 64 * 49, 1))
+    monkeypatch.setenv("GG_KRON_FOLD", "0")
+    K0 = kron(gg, F)
+    assert fold_mask(K0) == 0
+    y0 = K0 * x
+    monkeypatch.delenv("GG_KRON_FOLD")
+    K1 = kron(gg, F)
+    assert fold_mask(K1) == 0b111   # default GG_KRON_FOLD_MIN = 48
+    y1 = K1 * x
+    assert rel(y1, y0) < 1e-14
+    assert rel(y1, oracle.kron_matvec(F, x[:, 0])) < 1e-13
+
+
+def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
+    """A centrosymmetric but non-symmetric factor: the transposed operator's
+    split is packed from F^T."""
+    rng = np.random.default_rng(4)
+    C = rng.standard_normal((37, 37))
+    Fc = C + C[::-1, ::-1]
+    F = [Fc, grid_factor(12)]
+    K = gg.tensors.KronMatrix(F)
+    assert fold_mask(K) == 0b11 and fold_mask(K, True) == 0b11
+    x = rng.standard_normal((37 * 12, 1))
+    assert rel(K * x, oracle.kron_matvec(F, x[:, 0])) < 1e-13
+    FT = [f.T for f in F]
+    assert rel(K.T * x, oracle.kron_matvec(FT, x[:, 0])) < 1e-13
+
+
+def test_fold_not_taken(gg, fold_small):
+    """Random SPD factors, a grid factor perturbed above the 16 eps test, and
+    non-square factors stay on the dense kernel."""
+    rng = np.random.default_rng(2)
+    A = rng.standard_normal((40, 40))
+    G = grid_factor(40)
+    Gp = G.copy()
+    Gp[3, 5] += 1e-13
+    Gp[5, 3] += 1e-13
+    F = [A.dot(A.T) / 40 + np.eye(40), Gp, rng.standard_normal((30, 20))]
+    K = gg.tensors.KronMatrix(F)
+    assert fold_mask(K) == 0
+    x = rng.standard_normal((40 * 40 * 20, 1))
+    assert rel(K * x, oracle.kron_matvec(F, x[:, 0])) < 1e-13
+
+
+@pytest.mark.parametrize("ms", [(24, 20, 16, 18), (200, 24), (24, 200), (40, 36, 10)])
+def test_fold_cg_fused_and_textbook(gg, fold_small, ms):
+    """Every CG launch kind on folded factors (prologue, side job, fused
+    epilogue; textbook prologue + shift / p.q epilogue) vs the exact solve."""
+    F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate(ms)]
+    K = kron(gg, F)
+    assert fold_mask(K) == sum(1 << k for k, m in enumerate(ms) if m >= 8)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(3).standard_normal((n, 1))
+    s = 0.05
+    xf, inf = gg.linalg.cg(K, b, shift=s, rtol=1e-10, recurrence="fused")
+    itf = gg.linalg.cg.last.iters
+    xt, intb = gg.linalg.cg(K, b, shift=s, rtol=1e-10, recurrence="textbook")
+    assert inf == 0 and intb == 0
+    xo, _, ito = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + s * v, b[:, 0], rtol=1e-10)
+    assert abs(itf - ito) <= max(3, 0.05 * ito), (itf, ito)
+    Q, lam = oracle.factor_eigh(F)
+    ex = oracle.solve_schur(Q, oracle.kron_expand(lam), b[:, 0], s)
+    assert rel(xf, ex) < 1e-8 and rel(xt, ex) < 1e-8
+    res = b[:, 0] - (oracle.kron_matvec(F, xf[:, 0]) + s * xf[:, 0])
+    assert np.linalg.norm(res) < 2e-10 * np.linalg.norm(b)
+
+
+def test_fold_cg_odd_n_textbook(gg, fold_small):
+    F = [grid_factor(m) for m in (17, 13, 9)]
+    K = kron(gg, F)
+    assert fold_mask(K) == 0b111
+    b = np.random.default_rng(8).standard_normal((17 * 13 * 9, 1))
+    x, info = gg.linalg.cg(K, b, shift=0.1, rtol=1e-10)
+    assert info == 0 and gg.linalg.KronCG(K, 0.1).recurrence == "textbook"
+    Q, lam = oracle.factor_eigh(F)
+    assert rel(x, oracle.solve_schur(Q, oracle.kron_expand(lam), b[:, 0], 0.1)) < 1e-8
+
+
+@pytest.mark.parametrize("ms", [(20, 18, 16, 12), (200, 30), (9, 8, 7)])
+def test_fold_lanczos_vs_oracle(gg, fold_small, ms):
+    """Fused Lanczos on folded factors: the CGP 3 prologue (even d) and the
+    separate update pass (odd d)."""
+    F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate(ms)]
+    K = kron(gg, F)
+    n = int(np.prod(ms))
+    s = 0.03
+    a, b = gg.linalg.lanczos_tridiag(K, s, 20, seed=7, probe=2)
+    zp = oracle.cg.probe_signs(7, 2, n)
+    ao, bo = oracle.lanczos_tridiag(lambda v: oracle.kron_matvec(F, v) + s * v, zp, 20)
+    k = min(a.size, ao.size, 12)
+    np.testing.assert_allclose(a[:k], ao[:k], rtol=1e-8)
+    np.testing.assert_allclose(b[:k - 1], bo[:k - 1], rtol=1e-7)
+
+
+def test_fold_partial_strips(gg, fold_small):
+    """Row counts M that are not multiples of the 64-row workgroup or the
+    16-row wave strip, on every position."""
+    F = [grid_factor(33), grid_factor(11), grid_factor(9)]
+    K = kron(gg, F)
+    assert fold_mask(K) == 0b111
+    x = np.random.default_rng(1).standard_normal((33 * 11 * 9, 1))
+    assert rel(K * x, oracle.kron_matvec(F, x[:, 0])) < 1e-13
+    y = K._device().matvec(gg.device.to_device(x[:, 0]), shift=0.7)
+    assert rel(y.cpu().numpy(), oracle.kron_matvec(F, x[:, 0]) + 0.7 * x[:, 0]) < 1e-13

@@ -70,12 +70,16 @@ def _free_port():
 
 
 def _grief_rank(rank, world, port, case, solver, out_dir):
-    """One process per rank (all on cuda:0 here; on a node, one GPU each):
-    GPGriefModel(comm=TorchExchange()) over a real torch.distributed group."""
+    """One process per rank (one GPU each on a multi-GPU node, all on cuda:0
+    on one GPU): GPGriefModel(comm=TorchExchange()) over a real
+    torch.distributed group."""
     import os
     import sys
     from conftest import ROOT
     sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from dist_helpers import bind_device
+    bind_device(rank)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
