@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--exchange", default="auto", choices=["auto", "push", "a2a"])
     ap.add_argument("--fusion", type=int, default=None, choices=[0, 1, 2],
                     help="fused-CG layout (gg_cg_set_fusion); default: the library's")
+    ap.add_argument("--grief", default="C2,C5",
+                    help="P2 GRIEF fits timed after the CG leg (bench_grief configs, "
+                         "comma-separated; 'off' = none); not part of `value`")
     return ap.parse_args()
 
 
@@ -340,12 +343,16 @@ def dominant_group(per_pos, kinds):
     return [i for i, k in enumerate(kinds) if k == best], best
 
 
-def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
-    flop = 2.0 * n * m                     # one mode product (square factor m)
+def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0):
+    """fold_mask bit k: mode product k runs on the centrosymmetric split
+    (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
+    the roofline prices the work the kernel actually does."""
+    flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
     passes = launch_passes(d, recurrence, fusion)
     kinds = launch_kernels(d, recurrence, fusion)
     group, kind = dominant_group(per_pos, kinds)
     dom = group[0]
+    flop = flops[dom]
     t = float(np.mean([per_pos[i] for i in group])) * 1e-3   # per-launch average
     byts = 8.0 * n * float(np.mean([passes[i] for i in group]))
     f_mfma = flop / (FP64_MFMA_PEAK_TFLOPS * 1e12)
@@ -355,7 +362,7 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
     gbs = byts / t / 1e9
     mv_s = sum(per_pos) * 1e-3
     it_bytes = 8.0 * n * sum(passes)
-    floor_it = max(d * f_mfma, it_bytes / (HBM_PEAK_GBS * 1e9))
+    floor_it = max(sum(flops) / (FP64_MFMA_PEAK_TFLOPS * 1e12), it_bytes / (HBM_PEAK_GBS * 1e9))
     roof = {
         "bound": bound,
         "achieved": tf if bound == "mfma" else gbs,
@@ -373,6 +380,9 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
         "launch_ms_source": "HIP events the library records around each launch, on the "
                             "stream it launches on, over the timed iterations",
         "flop_per_launch": flop, "algorithmic_bytes_per_launch": byts,
+        "flop_rule": ("n m MFMA FLOP (centrosymmetric even/odd split: two h x h GEMMs, "
+                      "h = m/2; the dense product is 2 n m)" if (fold_mask >> dom) & 1
+                      else "2 n m (dense factor)"),
         "passes_per_launch": byts / (8.0 * n),
         "frac_mfma": f_mfma / t, "frac_hbm": f_hbm / t,
         "achieved_tflops": tf, "achieved_gbs": gbs,
@@ -387,8 +397,10 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
         "mode_product_ms_by_position": per_pos,
         "passes_by_position": passes,
         "matvec_ms": 1e3 * mv_s,
-        "matvec_tflops": d * flop / mv_s / 1e12,
-        "matvec_frac": d * flop / mv_s / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+        "matvec_tflops": sum(flops) / mv_s / 1e12,
+        "matvec_frac": sum(flops) / mv_s / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+        "matvec_dense_equivalent_tflops": d * 2.0 * n * m / mv_s / 1e12,
+        "fold_mask": fold_mask,
         "matvec_hbm_gbs": 8.0 * n * (2 * d + 1) / mv_s / 1e9,
         "matvec_hbm_frac": 8.0 * n * (2 * d + 1) / mv_s / 1e9 / HBM_PEAK_GBS,
         "iteration_algorithmic_bytes": it_bytes,
@@ -400,36 +412,98 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0):
     return roof, extra
 
 
-def pmc_traffic(m, d, positions, recurrence, fusion=0):
+PMC_JSON = os.path.join("profiles", "r03", "pmc_mode_product.json")
+# the sources that decide the CG mode products' HBM traffic
+KERNEL_SOURCES = ["gp_grief_amd/csrc/gg_kron.hip", "gp_grief_amd/csrc/gg_kron_fold.hip",
+                  "gp_grief_amd/csrc/gg_mp.h", "gp_grief_amd/csrc/gg_internal.h",
+                  "gp_grief_amd/csrc/gg_vec.hip"]
+
+
+def kernel_source_hash():
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
-    positions) from the committed PMC passes (tools/pmc_traffic.py), when they
-    were taken on this workload, recurrence and fusion layout and every launch
-    matched its algorithmic bytes (the counters calibrated on the kernels' own
-    patterns); else None."""
-    path = os.path.join(ROOT, "profiles", "r02_pmc_mode_product.json")
-    if (m, d) != (200, 4) or not os.path.exists(path):
-        return None, None
+    positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
+    when they were taken on this workload, recurrence, fusion layout and fold
+    state, by kernels built from the same sources (sha256 of KERNEL_SOURCES
+    recorded in the JSON), and every launch matched its algorithmic bytes;
+    else (None, reason)."""
+    path = os.path.join(ROOT, PMC_JSON)
+    if (m, d) != (200, 4):
+        return None, "no PMC passes for this workload"
+    if not os.path.exists(path):
+        return None, "no PMC passes committed (%s)" % PMC_JSON
     rec = json.load(open(path))
     if rec.get("recurrence") != recurrence or rec.get("fusion_layout", 0) != fusion:
-        return None, None
+        return None, "PMC passes taken with another recurrence / fusion layout"
+    if rec.get("fold_mask", 0) != fold_mask:
+        return None, "PMC passes taken with another fold state"
+    if rec.get("source_sha256") != kernel_source_hash():
+        return None, "stale: the kernel sources changed since the PMC passes (%s)" % PMC_JSON
     if not rec.get("calibrated_on_own_pattern"):
-        return None, None
+        return None, "PMC bytes did not match the algorithmic bytes of every launch"
     per = {pp["position"]: pp["traffic_bytes"] for pp in rec.get("per_position", [])}
     if not all(i in per for i in positions):
-        return None, None
-    return float(np.mean([per[i] for i in positions])), os.path.relpath(path, ROOT)
+        return None, "PMC passes miss a launch position"
+    return float(np.mean([per[i] for i in positions])), PMC_JSON
 
 
 # ---------------------------------------------------------------- CPU leg
-def cpu_model():
+def _lscpu():
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
-        for line in out.splitlines():
-            if line.startswith("Model name:"):
-                return line.split(":", 1)[1].strip()
+    except Exception:  # noqa: BLE001
+        return {}
+    kv = {}
+    for line in out.splitlines():
+        if ":" in line:
+            k, v = line.split(":", 1)
+            kv[k.strip()] = v.strip()
+    return kv
+
+
+def cpu_model():
+    return _lscpu().get("Model name")
+
+
+def cpu_share():
+    """Host threads the CPU baseline may use on this box, and why: the
+    process's affinity mask, the cgroup CPU quota (cpu.max) and the
+    harness's OMP_NUM_THREADS share, whichever is smallest, beside the
+    machine's physical core count (BASELINE.md section 4 asks for all
+    physical cores; a leased GPU box confines a process to its share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except Exception:  # noqa: BLE001
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    kv = _lscpu()
+    phys = None
+    try:
+        phys = int(kv["Core(s) per socket"]) * int(kv.get("Socket(s)", "1"))
     except Exception:  # noqa: BLE001
         pass
-    return None
+    limits = {"affinity_mask": aff}
+    if quota is not None:
+        limits["cgroup_cpu_quota"] = max(1, int(quota))
+    if omp and omp.isdigit() and int(omp) > 0:
+        limits["OMP_NUM_THREADS"] = int(omp)
+    by = min(limits, key=limits.get)
+    return limits[by], {"affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                        "omp_num_threads": omp, "physical_cores": phys,
+                        "logical_cpus": os.cpu_count(), "limited_by": by}
 
 
 def cpu_baseline(F, sigma2, iters):
@@ -437,7 +511,7 @@ def cpu_baseline(F, sigma2, iters):
     call sequence for the operator (oracle.kron_matvec_dsymm, restating
     kron_matrix.py:74-96), 1 warm-up + `iters` timed iterations."""
     import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads, share = cpu_share()
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(limits=threads)
@@ -460,13 +534,38 @@ def cpu_baseline(F, sigma2, iters):
     return {"value": 1.0 / float(np.mean(timed)), "unit": "CG iters/s", "cores": threads,
             "kind": "port",
             "host_cpu_count": os.cpu_count(), "host_cpu_model": cpu_model(),
+            "cpu_share": share,
             "iteration_s": [float(v) for v in per_it],
             "fidelity": "profiles/r02_cpu_fidelity.json",
             "sample": "textbook CG on the full %d^%d grid, operator = the reference's dsymm "
-                      "sequence restated (oracle.kron_matvec_dsymm), %d threads "
-                      "(OMP_NUM_THREADS: this process's CPU share of the box), 1 warm-up "
+                      "sequence restated (oracle.kron_matvec_dsymm), %d threads (limited by "
+                      "%s; affinity mask %d CPUs, %s physical cores on the host), 1 warm-up "
                       "iteration (%.1f s) + %d timed (mean %.1f s)"
-                      % (m, d, threads, per_it[0], iters, float(np.mean(timed)))}
+                      % (m, d, threads, share["limited_by"], share["affinity_cpus"],
+                         share["physical_cores"], per_it[0], iters, float(np.mean(timed)))}
+
+
+def grief_leg(names, torch, cpu):
+    """P2 beside the headline: one cold GPGriefModel fit per config through the
+    public API, stage-timed with HIP events (bench_grief.run_config: best of
+    2), the Gram's MFMA and the Phi writer's HBM fractions, and for C2 the
+    oracle's NumPy fit (oracle/grief.py) on the host as its CPU baseline."""
+    import bench_grief
+    import gp_grief_amd as gg
+    import gp_grief_amd.grid  # noqa: F401
+    import gp_grief_amd.kern  # noqa: F401
+    import gp_grief_amd.models  # noqa: F401
+    ctx = bench_grief.Ctx(torch, None, 1, 0)
+    out = {}
+    for name in names:
+        r = bench_grief.run_config(gg, ctx, name, 2, cpu and name == "C2", False)
+        keep = {k: r[k] for k in ("fit_ms", "stage_ms", "gram", "phi", "lml") if k in r}
+        keep["workload"] = r["config"]
+        if "cpu_baseline" in r:
+            keep["cpu_baseline"] = r["cpu_baseline"]
+        out[name] = keep
+        torch.cuda.empty_cache()
+    return out
 
 
 def time_lanczos(K, s, steps, torch):
@@ -543,9 +642,11 @@ def main():
 
     ms_per_step = 1e3 * dt / a.steps
     per_pos = [t / n_mv for t in mode_ms]
+    fold_mask = K._device().fold_mask()
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
-                                  solver.fusion)
-    traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0)
+                                  solver.fusion, fold_mask)
+    traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
+                               fold_mask)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -574,6 +675,9 @@ def main():
     if a.lanczos > 0:
         result["lanczos"] = time_lanczos(K, s, a.lanczos, torch)
         torch.cuda.empty_cache()
+    if a.grief != "off":
+        result["grief"] = grief_leg([c.strip() for c in a.grief.split(",") if c.strip()], torch,
+                                    a.cpu_baseline == "auto")
     if a.cpu_baseline == "auto":
         result["cpu_baseline"] = cpu_baseline(F, s, a.cpu_iters)
     print(json.dumps(result), flush=True)

@@ -192,7 +192,8 @@ def cg_leg(gg, ctx, mdl_chol, d, m, kind, p, x, y, s):
 def cpu_fit(d, m, kind, p, x, y, s):
     import oracle
     from oracle.grief import grief_inducing, grief_phi, grief_fit, grief_lml
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    from bench import cpu_share
+    threads, share = cpu_share()
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(limits=threads)
@@ -212,7 +213,7 @@ def cpu_fit(d, m, kind, p, x, y, s):
         ctx.__exit__(None, None, None)
     del oracle
     return {"setup_s": t1 - t0, "phi_s": t2 - t1, "gram_chol_alpha_s": t3 - t2,
-            "fit_s": t3 - t0, "threads": threads, "lml": ll}
+            "fit_s": t3 - t0, "threads": threads, "cpu_share": share, "lml": ll}
 
 
 def run_config(gg, ctx, name, repeats, cpu, with_cg, s=0.01):
@@ -269,7 +270,7 @@ def run_config(gg, ctx, name, repeats, cpu, with_cg, s=0.01):
         gpu_sample_ms = sum(t[k] for k in ("setup", "phi", "gram", "reduce", "chol", "alpha"))
         res["cpu_baseline"] = {
             "value": 1.0 / c["fit_s"], "unit": "fits/s", "cores": c["threads"], "kind": "port",
-            "host_cpu_count": os.cpu_count(),
+            "host_cpu_count": os.cpu_count(), "cpu_share": c["cpu_share"],
             "sample": "oracle/grief.py fit on the first %d of the %d rows (NumPy/OpenBLAS, "
                       "%d threads): setup %.2f s, Phi %.2f s, Gram+chol+alpha %.2f s"
                       % (n_cpu, n, c["threads"], c["setup_s"], c["phi_s"],

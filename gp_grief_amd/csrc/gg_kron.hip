@@ -1366,6 +1366,18 @@ static void dist_step(const Factor& f, const double* X, double* Y, int64_t M, Ou
   if (M <= 0) return;
   GG_REQUIRE(f.JT <= kMaxJT, GG_ERR_VALUE, "sharded operator supports factors up to 256");
   const bool cgp = pro != nullptr;
+  if (f.ffrag != nullptr) {
+    // centrosymmetric factor: the folded kernel (identity epilogue = launch
+    // kinds 0 / 1, mapped = 8 / 9)
+    const int kind = om.identity != 0 ? (cgp ? 1 : 0) : (cgp ? 9 : 8);
+    const FoldConfig fc = select_fold(f.fJT, f.fTT, kind);
+    const int64_t nblk = ceil_div(M, (int64_t)4 * 16);
+    hipLaunchKernelGGL(fc.fn, dim3((unsigned)nblk), dim3(256), fc.lds, s, X, Y, f.ffrag, M,
+                       (int)f.q, (int)f.p, f.fKS, fc.jf, 0, nullptr, 0.0, nullptr,
+                       cgp ? &pro->sc->done : nullptr, om, cgp ? *pro : MpFuse());
+    GG_LAUNCH_CHECK();
+    return;
+  }
   mode_kernel_t fn = select_dist(f.JT, cgp, om.identity != 0);
   static bool attr[2][2][kMaxJT + 1] = {};
   bool& done = attr[cgp][om.identity != 0][f.JT];
@@ -1405,6 +1417,7 @@ int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_ho
       for (int k = 0; k < d; ++k) {
         GG_REQUIRE(m[k] >= 1 && m[k] <= 256, GG_ERR_VALUE, "factor size must be in [1, 256]");
         gg::pack_fragments(factors_host[k], m[k], m[k], false, D->f[k]);
+        gg::pack_fold(factors_host[k], m[k], false, D->f[k]);
         D->n *= m[k];
       }
       D->n_local = D->n / world;
@@ -1423,6 +1436,7 @@ int gg_kron_dist_destroy(gg_kron_dist* D) {
     for (gg::Factor& f : D->f) {
       if (f.frag) (void)hipFree(f.frag);
       if (f.frag4) (void)hipFree(f.frag4);
+      if (f.ffrag) (void)hipFree(f.ffrag);
     }
     for (void* b : D->opened) (void)hipIpcCloseMemHandle(b);
     if (D->peers_recv) (void)hipFree(D->peers_recv);
@@ -1475,6 +1489,16 @@ int gg_kron_dist_set_peers(gg_kron_dist* D, double* own_xbuf, int use_ipc, const
     GG_HIP(hipMalloc(&D->peers_out, G * sizeof(double*)));
     GG_HIP(hipMemcpy(D->peers_recv, recv.data(), G * sizeof(double*), hipMemcpyHostToDevice));
     GG_HIP(hipMemcpy(D->peers_out, out.data(), G * sizeof(double*), hipMemcpyHostToDevice));
+  });
+}
+
+int gg_kron_dist_fold_mask(const gg_kron_dist* D, int64_t* mask) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && mask, GG_ERR_VALUE, "NULL argument");
+    int64_t v = 0;
+    for (size_t k = 0; k < D->f.size(); ++k)
+      if (D->f[k].ffrag != nullptr) v |= (int64_t)1 << k;
+    *mask = v;
   });
 }
 

@@ -39,12 +39,16 @@ namespace gg {
 // The CG / Lanczos prologues (CGP) update both elements a lane loads and
 // write both back; the epilogue stores S + T at column j' and S - T at m-1-j'
 // (+ shift * x and the CG partial dots, kEpi as mode_product_kernel).
-template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi>
+// kMap: the sharded operator's plain-store epilogue through an OutMap
+// (all-to-all chunk order, or peer stores in push mode; mode_product_kernel
+// mp_finish), no shift / dots.
+template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi, bool kMap = false>
 __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int, int KS, int, int,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
-    const int* __restrict__ skip, OutMap, MpFuse fz) {
+    const int* __restrict__ skip, OutMap om, MpFuse fz) {
+  static_assert(!kMap || kEpi == 0, "the mapped epilogue stores only");
   constexpr int kWaves = 4;
   constexpr int kThreads = 256;
   constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;   // S fragments per k-step
@@ -306,7 +310,44 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     return (e & 1) ? sv - tv : sv + tv;
   };
   double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
-  if (xs == nullptr) {
+  if (kMap) {
+    // rows: a = row / mi, h = (row % mi) / cr, br = (row % mi) % cr; columns
+    // grouped by cg (include gg_internal.h OutMap)
+    int64_t rowoff[4];
+    int rowdest[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = b0 + (lane >> 4) + 4 * r;
+      const int64_t a_ = row / om.mi, bi = row - a_ * om.mi;
+      const int64_t hh = bi / om.cr, br = bi - hh * om.cr;
+      rowoff[r] = a_ * om.as + br * om.cg;
+      rowdest[r] = 0;
+      if (om.push == 1) rowdest[r] = (int)hh;
+      else rowoff[r] += hh * om.hs;
+    }
+#pragma unroll
+    for (int e = 0; e < 2 * JS; ++e) {
+      if (!col_ok(e)) continue;
+      const int64_t j = jcol(e);
+      const int64_t jg = j / om.cg;
+      const int64_t co = (j - jg * om.cg) + (om.push == 2 ? 0 : jg * om.gs);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if ((lane >> 4) + 4 * r >= rows_left) continue;
+        const double v = value(e, r);
+        if (om.push != 0) {
+          const int dest = om.push == 1 ? rowdest[r] : (int)jg;
+          om.peers[dest][om.self_off + rowoff[r] + co] = v;
+        } else {
+          Y[rowoff[r] + co] = v;
+        }
+      }
+    }
+    // push: the stores went to other GPUs' HBM over xGMI; release them at
+    // system scope before the kernel ends (mode_product_kernel mp_finish)
+    if (om.push != 0) __threadfence_system();
+    return;
+  } else if (xs == nullptr) {
 #pragma unroll
     for (int e = 0; e < 2 * JS; ++e) {
       const bool cok = col_ok(e);
@@ -365,19 +406,24 @@ bool fold_kind(int kind) {
   return kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 4 || kind == 7;
 }
 
+// KIND: kron_apply's launch kind; 8 / 9: the sharded operator's mapped
+// epilogue without / with the textbook CG prologue (gg_kron_dist_*)
 template <int JT, int TT, int KIND>
 static FoldConfig cfg_fold() {
-  constexpr int CGP = KIND == 1 ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
+  constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
   constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : 0;
+  constexpr bool MAP = KIND >= 8;
   constexpr int KC = CGP ? 2 : 3;
   constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI>, KC, JF,
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI, MAP>, KC, JF,
                     2 * (size_t)KC * JF * 64 * sizeof(double)};
 }
 
 template <int JT, int TT>
 static FoldConfig fold_by_kind(int kind) {
   switch (kind) {
+    case 8: return cfg_fold<JT, TT, 8>();
+    case 9: return cfg_fold<JT, TT, 9>();
     case 1: return cfg_fold<JT, TT, 1>();
     case 2: return cfg_fold<JT, TT, 2>();
     case 3: return cfg_fold<JT, TT, 3>();
@@ -417,8 +463,8 @@ void set_fold_lds_limits() {
   for (int jt = 1; jt <= 8; ++jt)
     for (int tt = 0; tt <= 2; ++tt) {
       if (tt > 0 && jt < 4) continue;
-      for (int kind = 0; kind < 8; ++kind) {
-        if (!fold_kind(kind)) continue;
+      for (int kind = 0; kind < 10; ++kind) {
+        if (!fold_kind(kind) && kind < 8) continue;
         const FoldConfig fc = select_fold(jt, tt, kind);
         GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));

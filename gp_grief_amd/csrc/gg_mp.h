@@ -84,7 +84,8 @@ __device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
 }
 
 // The folded (centrosymmetric) mode product, gg_kron_fold.hip: one kernel per
-// (tiles per half JT, 4x4 tail fragments TT, kron_apply launch kind)
+// (tiles per half JT, 4x4 tail fragments TT, kron_apply launch kind; kinds
+// 8 / 9 = the sharded operator's OutMap epilogue, plain / textbook prologue)
 struct FoldConfig {
   mode_kernel_t fn;
   int kc, jf;     // k-steps per LDS chunk, fragments per k-step (both halves)

@@ -122,6 +122,9 @@ class HipEngine(object):
         nl, we = ctypes.c_int64(), ctypes.c_int64()
         native.check(L.gg_kron_dist_sizes(self.h, ctypes.byref(nl), ctypes.byref(we)))
         self.n_local = nl.value
+        fm = ctypes.c_int64()
+        native.check(L.gg_kron_dist_fold_mask(self.h, ctypes.byref(fm)))
+        self.fold_mask = fm.value   # factors on the centrosymmetric split
         self.work = dev.empty(we.value)
         c = ctypes.c_void_p()
         native.check(L.gg_cgs_create(ctypes.byref(c)), "gg_cgs_create")

@@ -111,6 +111,7 @@ SIGNATURES = {
                             ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)],
     "gg_kron_dist_destroy": [_vp],
     "gg_kron_dist_sizes": [_vp, _c_i64p, _c_i64p],
+    "gg_kron_dist_fold_mask": [_vp, _c_i64p],
     "gg_kron_dist_phase1": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, _vp, _vp],
     "gg_kron_dist_phase2": [_vp, _c_dp, _c_dp, _vp],
     "gg_ipc_handle": [_c_dp, ctypes.c_void_p, _c_i64p],

@@ -292,6 +292,9 @@ int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_ho
                         int rank, gg_kron_dist** out);
 int gg_kron_dist_destroy(gg_kron_dist* D);
 int gg_kron_dist_sizes(const gg_kron_dist* D, int64_t* n_local, int64_t* work_elems);
+/* Bit k set: factor k of the sharded operator runs through the
+ * centrosymmetric even/odd split (as gg_kron_fold_mask).                  */
+int gg_kron_dist_fold_mask(const gg_kron_dist* D, int64_t* mask);
 int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
                         double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
                         gg_stream stream);

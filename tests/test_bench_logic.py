@@ -33,3 +33,62 @@ def test_dominant_group_is_largest_total_not_largest_launch():
     assert roof["bound"] == "mfma"          # 8.1 ms of MFMA > 5.6 ms of HBM at 3.5 passes
     assert extra["largest_launch"]["position"] == 0
     assert 0 < roof["frac"] < 1
+
+
+def test_roofline_folded_launches_are_hbm_bound():
+    """With every factor on the centrosymmetric split the side-job launch
+    executes n m FLOP (4.1 ms of MFMA at 200^4) against 3.5 passes of HBM
+    (5.6 ms): priced against HBM."""
+    per = [15.5, 9.2, 9.3, 11.7]
+    roof, extra = bench.roofline_report(per, 200 ** 4, 200, 4, "fused", 46.5, 0, 0b1111)
+    assert roof["positions"] == [1, 2] and roof["bound"] == "hbm"
+    assert abs(roof["flop_per_launch"] - 200 ** 4 * 200) < 1
+    assert abs(roof["achieved"] - 3.5 * 8 * 200 ** 4 / 9.25e-3 / 1e9) < 1e-6
+    assert extra["fold_mask"] == 0b1111
+    assert abs(extra["matvec_dense_equivalent_tflops"] - 2 * extra["matvec_tflops"]) < 1e-9
+
+
+def test_rhs_identical_in_every_shard_layout():
+    """bench.py's right-hand side is a function of the global index, so the
+    sharded layouts of every N hold the single-GPU vector."""
+    import torch
+    from gp_grief_amd.distributed import scatter_global
+    m, d = 8, 3
+    dev = torch.device("cpu")
+    y = bench.grid_rhs_device(m, d, torch, dev).numpy()
+    assert y.shape == (m ** d,) and abs(y).max() < 3.2
+    for world in (1, 2, 4, 8):
+        for rank in range(world):
+            loc = bench.local_rhs(m, d, world, rank, torch, dev).numpy()
+            ref = scatter_global(y, [m] * d, world, rank)
+            assert (loc == ref).all()
+
+
+def test_pmc_traffic_requires_matching_sources(tmp_path, monkeypatch):
+    import json
+    rec = {"recurrence": "fused", "fusion_layout": 0, "fold_mask": 15,
+           "source_sha256": bench.kernel_source_hash(), "calibrated_on_own_pattern": True,
+           "per_position": [{"position": k, "traffic_bytes": 1e10 * (k + 1)} for k in range(4)]}
+    os.makedirs(tmp_path / "profiles" / "r03")
+    path = tmp_path / bench.PMC_JSON
+    json.dump(rec, open(path, "w"))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    for rel in bench.KERNEL_SOURCES:      # the same sources under the fake root
+        os.makedirs(os.path.dirname(tmp_path / rel), exist_ok=True)
+        with open(os.path.join(ROOT, rel), "rb") as f, open(tmp_path / rel, "wb") as g:
+            g.write(f.read())
+    t, src = bench.pmc_traffic(200, 4, [1, 2], "fused", 0, 15)
+    assert t == 2.5e10 and src == bench.PMC_JSON
+    t, why = bench.pmc_traffic(200, 4, [1, 2], "fused", 0, 0)
+    assert t is None and "fold" in why
+    with open(tmp_path / bench.KERNEL_SOURCES[0], "ab") as g:
+        g.write(b"// changed\n")
+    t, why = bench.pmc_traffic(200, 4, [1, 2], "fused", 0, 15)
+    assert t is None and why.startswith("stale")
+
+
+def test_cpu_share_reports_its_limit():
+    threads, share = bench.cpu_share()
+    assert threads >= 1 and share["limited_by"] in ("affinity_mask", "cgroup_cpu_quota",
+                                                    "OMP_NUM_THREADS")
+    assert threads <= share["affinity_cpus"]

@@ -21,18 +21,27 @@ from dist_helpers import ThreadExchange, reference_factors, run_threads
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("fold", ["dense", "fold"])
 @pytest.mark.parametrize("mode", ["push", "a2a"])
 @pytest.mark.parametrize("world,m,d", [(2, 8, 2), (2, 12, 3), (4, 16, 4), (8, 24, 3),
-                                       (4, 40, 3)])
-def test_sharded_matvec_and_cg_virtual_ranks(gpu, world, m, d, mode):
+                                       (4, 40, 3), (2, 200, 2)])
+def test_sharded_matvec_and_cg_virtual_ranks(gpu, monkeypatch, world, m, d, mode, fold):
+    """fold: every factor on the centrosymmetric split (GG_KRON_FOLD_MIN=8) --
+    identity and OutMap (all-to-all order / peer push) epilogues, with and
+    without the textbook CG prologue; m = 200 with the 4x4x4 tails."""
     import torch
     from gp_grief_amd.distributed import (DistKronCG, HipEngine, gather_global,
                                           scatter_global)
+    if fold == "fold":
+        monkeypatch.setenv("GG_KRON_FOLD_MIN", "8")
+    else:
+        monkeypatch.setenv("GG_KRON_FOLD", "0")
     F = reference_factors(m, d)
     xg = np.random.default_rng(3).standard_normal(m ** d)
     shift = 0.05
     ex = ThreadExchange(world)
     engines = [HipEngine(F, world, g) for g in range(world)]
+    assert engines[0].fold_mask == ((1 << d) - 1 if fold == "fold" else 0)
 
     def body(g):
         ex.bind(g)
@@ -95,12 +104,15 @@ def _ipc_worker(rank, world, port, m, d, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,m,d", [(2, 16, 3), (4, 24, 3)])
-def test_push_exchange_over_ipc_processes(gpu, tmp_path, world, m, d):
-    """One process per rank on the same GPU: exchange buffers shared by IPC
-    handle (gg_ipc_handle / gg_kron_dist_set_peers), barriers over gloo."""
+@pytest.mark.parametrize("world,m,d,fold", [(2, 16, 3, False), (4, 24, 3, True)])
+def test_push_exchange_over_ipc_processes(gpu, tmp_path, monkeypatch, world, m, d, fold):
+    """One process per rank (one GPU each on a multi-GPU node, else all on
+    cuda:0): exchange buffers shared by IPC handle (gg_ipc_handle /
+    gg_kron_dist_set_peers), barriers over gloo; fold: the ranks' factors on
+    the centrosymmetric split (the environment is inherited by the ranks)."""
     import torch.multiprocessing as mp
     from gp_grief_amd.distributed import gather_global
+    monkeypatch.setenv("GG_KRON_FOLD_MIN", "8" if fold else "1000")
     port = _free_port()
     mp.start_processes(_ipc_worker, args=(world, port, m, d, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")

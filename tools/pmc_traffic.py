@@ -63,8 +63,15 @@ def main():
     calib = {"iteration_ratio": tot / (sum(passes) * 8.0 * n),
              "per_position_ratio": [pp["ratio"] for pp in per_pos]}
     dom = per_pos[0]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    fold_mask = sum(1 << k for k, pp in enumerate(per_pos) if "fold" in pp["kernel"])
     res = {
         "position": 0, "recurrence": "fused", "fusion_layout": 0,
+        "fold_mask": fold_mask,
+        # bench.py reuses these counters only for kernels built from the same sources
+        "source_sha256": bench.kernel_source_hash(),
+        "sources": bench.KERNEL_SOURCES,
         "kernel": dom["kernel"], "traffic_bytes": dom["traffic_bytes"],
         "read_bytes": dom["read_bytes"], "write_bytes": dom["write_bytes"],
         "algorithmic_bytes": 6 * 8.0 * n,
