@@ -80,6 +80,12 @@ struct CgScalars {
   double rq, qq;    // fused CG: r.q and q.q of the last matvec
   int repair;       // fused CG: |r - alpha q|^2 cancelled; apply x / r and take the
                     // textbook beta before the next matvec
+  // fused CG with the x update deferred (gg_vec.hip, x_defer): x lags by
+  // xpend steps, x_true = x + sum_{i < xpend} xc[i] xp[i]; the side job folds
+  // both into x when xpend == 2, the closing update whatever is left
+  int xpend;
+  double xc[2];
+  const double* xp[2];
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
@@ -101,6 +107,10 @@ struct MpFuse {
   double* sx = nullptr;
   const double* sp = nullptr;
   int64_t sn = 0, schunk = 0;
+  // x_defer: the side job applies sc->xc / sc->xp (at element offset soff of
+  // the slice) when sc->xpend == 2, instead of alpha p_side when pending
+  int xdefer = 0;
+  int64_t soff = 0;
   // last mode product: partial r.q and q.q next to p.q (fused CG); the three
   // partial arrays are pstride apart
   const double* er = nullptr;

@@ -1124,6 +1124,8 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           fz.sc = cg->sc;
           fz.sx = cg->sx + off;
           fz.sp = cg->sp + off;
+          fz.xdefer = cg->xdefer;
+          fz.soff = off;
           fz.sn = len;
           fz.schunk = 2 * ceil_div(std::max<int64_t>(len, 1), 2 * nblk);
         }

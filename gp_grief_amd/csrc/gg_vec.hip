@@ -122,9 +122,23 @@ __global__ __launch_bounds__(kVecThreads) void cg_xr_update_kernel(
     const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
     double* __restrict__ partials, int need_pending) {
   // need_pending: 0 always, 1 only with a pending fused update, 2 only when
-  // the fused recurrence asked for a repair (cancelled beta)
+  // the fused recurrence asked for a repair (cancelled beta); x == nullptr:
+  // r only (x_defer keeps its own x bookkeeping, cg_x_flush_kernel)
   if (sc->done || (need_pending && !sc->pending)) return;
   if (need_pending == 2 && !sc->repair) return;
+  if (x == nullptr) {
+    const double a = sc->alpha;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      const double rv = r[i] - a * q[i];
+      r[i] = rv;
+      acc = fma(rv, rv, acc);
+    }
+    const double s = block_sum(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
+    return;
+  }
   const double a = sc->alpha;
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -175,6 +189,23 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
   }
 }
 
+// x_defer: fold the deferred steps into x, x += sum_{i < xpend} xc[i] xp[i]
+// (also after convergence: x lags r by up to two steps)
+__global__ __launch_bounds__(kVecThreads) void cg_x_flush_kernel(double* __restrict__ x,
+                                                                 int64_t n,
+                                                                 const CgScalars* __restrict__ sc) {
+  const int k = sc->xpend;
+  if (k <= 0) return;
+  const double c0 = sc->xc[0], c1 = k >= 2 ? sc->xc[1] : 0.0;
+  const double* __restrict__ p0 = sc->xp[0];
+  const double* __restrict__ p1 = k >= 2 ? sc->xp[1] : sc->xp[0];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    x[i] += c0 * p0[i] + c1 * p1[i];
+}
+
+__global__ void cg_x_flushed_kernel(CgScalars* sc) { sc->xpend = 0; }
+
 // Fused recurrence, end of iteration j (after the last mode product):
 //   rho_j = r_j.r_j (partials of the first mode product's prologue, which
 //   applied r_j = r_{j-1} - alpha q_{j-1}), stopping test on it;
@@ -184,9 +215,16 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
 //   r_{j+1}.r_{j+1} replaces it in the next iteration (stopping test, alpha).
 // The x / r updates of iteration j stay pending until the next iteration's
 // first two mode products (or gg_cg_iterate's closing update).
+//
+// x_defer (p_new != nullptr): x is not updated every iteration.  With xpend
+// deferred steps at the start of iteration j (the side job folded both into
+// x if xpend was 2):  xpend 2 or 0 -> 1 pending, (p_j, alpha_j);  xpend 1 ->
+// 2 pending, (p_j, alpha_j) and (p_{j-1}, alpha_{j-1}).  p_new = p_j (this
+// iteration's direction buffer); the host keeps three direction buffers so
+// p_{j-1} survives the next prologue.
 __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     const double* __restrict__ rr_part, int64_t nrr, const double* __restrict__ mv_part,
-    int64_t nmv, int64_t pstride, CgScalars* sc) {
+    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new) {
   if (sc->done) return;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
@@ -212,6 +250,9 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
       if (!(sqrt(rr) >= sc->tol)) {  // converged (or NaN): x_j, r_j are final
         sc->done = 1;
         sc->pending = 0;
+        // x_defer: xpend 2 was folded into x by this iteration's side job;
+        // xpend 1 (alpha_{j-1} p_{j-1}) stays for the closing flush
+        if (p_new != nullptr && sc->xpend == 2) sc->xpend = 0;
         return;
       }
     }
@@ -229,6 +270,17 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     sc->beta = sc->repair ? 0.0 : rt / rho;
     sc->first = 0;
     sc->pending = 1;
+    if (p_new != nullptr) {
+      if (sc->xpend == 1) {
+        sc->xc[1] = sc->xc[0];
+        sc->xp[1] = sc->xp[0];
+        sc->xpend = 2;
+      } else {
+        sc->xpend = 1;
+      }
+      sc->xc[0] = alpha;
+      sc->xp[0] = p_new;
+    }
   }
 }
 
@@ -247,6 +299,7 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->pending = 0;
     sc->alpha = sc->beta = sc->pq = sc->rq = sc->qq = 0.0;
     sc->repair = 0;
+    sc->xpend = 0;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -462,8 +515,10 @@ struct gg_cg {
   int64_t n = 0;
   double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
   double* p2 = nullptr;        // second direction buffer (fused recurrence)
+  double* p3 = nullptr;        // third (x_defer: p_{j-1} outlives the next prologue)
   bool fused = true;           // recurrence: fused (default) or textbook
   int fusion = 0;              // fused layout (gg_cg_set_fusion): 0, 1 or 2
+  bool xdefer = true;          // layout 0: x updated every other iteration
   double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
   double* rr_part = nullptr;   // device, prologue r.r partials (fused)
   int64_t rr_count = 0;
@@ -585,7 +640,8 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
-    *elems = 4 * n + gg::kron_work_elems(K, false);
+    // r, p, q, p2, p3 (x_defer) + the matvec scratch
+    *elems = 5 * n + gg::kron_work_elems(K, false);
   });
 }
 
@@ -604,7 +660,10 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->p = work_dev + nr;
       cg->q = work_dev + 2 * nr;
       cg->p2 = work_dev + 3 * nr;
-      cg->mv_work = work_dev + 4 * nr;
+      cg->p3 = work_dev + 4 * nr;
+      cg->mv_work = work_dev + 5 * nr;
+      const char* xd = getenv("GG_CG_XDEFER");   // A/B knob
+      cg->xdefer = !(xd && atoi(xd) == 0);
       cg->mv_partials = gg::kron_partials_needed(K, false);
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
       GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
@@ -759,12 +818,14 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         ev = cg->events.data() + cg->events_used;
         cg->events_used = need;
       }
+      const bool xdefer = cg->fused && cg->xdefer && cg->fusion == 0;
       if (cg->fused) {
         // repair (no-op unless the last beta cancelled): x += alpha p,
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
-        // pending update
+        // pending update (x_defer: r only, x keeps its deferred steps)
         hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                           cg->x, cg->r, cg->p, cg->q, n, cg->sc, cg->partials, 2);
+                           xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                           cg->partials, 2);
         GG_LAUNCH_CHECK();
         hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
                            (int64_t)nb, cg->sc, 2);
@@ -780,14 +841,25 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.sx = cg->fusion == 2 ? nullptr : cg->x;
         fz.sp = cg->p;
         fz.sn = n;
+        fz.xdefer = xdefer ? 1 : 0;
         fz.er = cg->r;
         fz.pstride = cg->mv_partials;
         gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
                        &cg->sc->done, s, &nparts, &fz, 2, ev);
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
-                           cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc);
+                           cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc,
+                           xdefer ? (const double*)cg->p2 : nullptr);
         GG_LAUNCH_CHECK();
-        std::swap(cg->p, cg->p2);
+        if (xdefer) {
+          // (cur, free, old) <- (free, old, cur): p_j becomes current, p_{j-1}
+          // is kept one more iteration for the deferred x update
+          double* old_ = cg->p3;
+          cg->p3 = cg->p;
+          cg->p = cg->p2;
+          cg->p2 = old_;
+        } else {
+          std::swap(cg->p, cg->p2);
+        }
       } else {
         gg::MpFuse fz;
         fz.r = cg->r;
@@ -812,10 +884,20 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
       }
     }
     if (cg->fused) {
+      const bool xdefer = cg->xdefer && cg->fusion == 0;
       // closing update (no-op unless pending): x += alpha p, r -= alpha q,
-      // rho = r.r, beta, iteration count -- the textbook state
-      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
-                         cg->r, cg->p, cg->q, n, cg->sc, cg->partials, 1);
+      // rho = r.r, beta, iteration count -- the textbook state.  x_defer: the
+      // deferred steps first (also after convergence), then r only
+      if (xdefer) {
+        hipLaunchKernelGGL(gg::cg_x_flush_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
+                           n, cg->sc);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+        GG_LAUNCH_CHECK();
+      }
+      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                         xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc, cg->partials,
+                         1);
       GG_LAUNCH_CHECK();
       hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
                          (int64_t)nb, cg->sc, 1);
