@@ -294,9 +294,12 @@ def sharded_roofline(phases, n, m, d, world, fold_mask):
 
 
 # ---------------------------------------------------------------- roofline
-def launch_passes(d, recurrence, fusion=0):
+def launch_passes(d, recurrence, fusion=0, xdefer=False):
     """Algorithmic 8-byte passes over N of each mode-product launch position of
-    one CG iteration (reads + writes, gg_kron.hip kron_apply / MpFuse)."""
+    one CG iteration (reads + writes, gg_kron.hip kron_apply / MpFuse),
+    averaged over iterations.  xdefer: the x update runs every other
+    iteration as x += c0 p0 + c1 p1 (4 passes per two iterations, 2 per
+    iteration on average instead of 3)."""
     if d == 1:
         return [4] if recurrence == "fused" else [5]
     passes = [2] * d
@@ -305,13 +308,14 @@ def launch_passes(d, recurrence, fusion=0):
         passes[0] += 3 if fusion else 4
         # epilogue: p and r read (shift, p.q, r.q); layouts 1/2 also write p_new
         passes[d - 1] += 3 if fusion else 2
+        xp = 2.0 if (xdefer and fusion != 2) else 3.0
         if fusion == 2:
             passes[d - 1] += 2  # x += alpha p_old in the epilogue (x read + written)
         elif d >= 4:
-            passes[1] += 1.5    # side job x += alpha p_old, first half of x
-            passes[2] += 1.5    # ... second half (gg_kron.hip kron_apply split_side)
+            passes[1] += xp / 2  # side job on the first half of x
+            passes[2] += xp / 2  # ... second half (gg_kron.hip kron_apply split_side)
         else:
-            passes[1] += 3      # side job: x += alpha p_old (x, p_old read; x written)
+            passes[1] += xp      # side job: x update (x, p read; x written)
     else:
         passes[0] += 2          # prologue: r read, p written in place
         passes[d - 1] += 1      # epilogue: p read (shift, p.q)
@@ -343,12 +347,13 @@ def dominant_group(per_pos, kinds):
     return [i for i, k in enumerate(kinds) if k == best], best
 
 
-def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0):
+def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0,
+                    xdefer=False):
     """fold_mask bit k: mode product k runs on the centrosymmetric split
     (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
     the roofline prices the work the kernel actually does."""
     flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
-    passes = launch_passes(d, recurrence, fusion)
+    passes = launch_passes(d, recurrence, fusion, xdefer)
     kinds = launch_kernels(d, recurrence, fusion)
     group, kind = dominant_group(per_pos, kinds)
     dom = group[0]
@@ -428,7 +433,7 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
-def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0):
+def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
     positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
     when they were taken on this workload, recurrence, fusion layout and fold
@@ -445,6 +450,8 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0):
         return None, "PMC passes taken with another recurrence / fusion layout"
     if rec.get("fold_mask", 0) != fold_mask:
         return None, "PMC passes taken with another fold state"
+    if bool(rec.get("x_deferred", False)) != bool(xdefer):
+        return None, "PMC passes taken with another x-update schedule"
     if rec.get("source_sha256") != kernel_source_hash():
         return None, "stale: the kernel sources changed since the PMC passes (%s)" % PMC_JSON
     if not rec.get("calibrated_on_own_pattern"):
@@ -644,9 +651,9 @@ def main():
     per_pos = [t / n_mv for t in mode_ms]
     fold_mask = K._device().fold_mask()
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
-                                  solver.fusion, fold_mask)
+                                  solver.fusion, fold_mask, solver.xdefer)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
-                               fold_mask)
+                               fold_mask, solver.xdefer)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -666,6 +673,8 @@ def main():
                    "grid": m, "dims": d, "sigma2": s, "n": n,
                    "cg_recurrence": solver.recurrence,
                    "cg_fusion_layout": solver.fusion,
+                   "cg_x_deferred": solver.xdefer,
+                   "fold_mask": fold_mask,
                    "parallelism": "single-gpu"},
         "roofline": roof,
     }

@@ -111,6 +111,9 @@ struct MpFuse {
   // the slice) when sc->xpend == 2, instead of alpha p_side when pending
   int xdefer = 0;
   int64_t soff = 0;
+  // output of the first mode product when the ping-pong would put it in y
+  // (odd d): the fused prologue still reads q_old == y in other workgroups
+  double* first_dst = nullptr;
   // last mode product: partial r.q and q.q next to p.q (fused CG); the three
   // partial arrays are pstride apart
   const double* er = nullptr;

@@ -1068,6 +1068,13 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
     } else {
       dst = (k % 2 == 0) ? work : work + max_inter;
     }
+    // the fused CG prologue reads q_old == y across workgroups while the
+    // first mode product writes its output: never into y (odd d)
+    if (k == 0 && k != d - 1 && cgp == 2 && dst == y) {
+      GG_REQUIRE(cg->first_dst != nullptr, GG_ERR_VALUE,
+                 "the fused CG with an odd number of factors needs a first-step scratch");
+      dst = cg->first_dst;
+    }
     const bool last = (k == d - 1);
     const int variant = mode_variant();
     if (M > 0) {

@@ -42,7 +42,11 @@ namespace gg {
 // kMap: the sharded operator's plain-store epilogue through an OutMap
 // (all-to-all chunk order, or peer stores in push mode; mode_product_kernel
 // mp_finish), no shift / dots.
-template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi, bool kMap = false>
+// kOpt (A/B variants, GG_FOLD_VARIANT): bit 0 s_setprio(1) around each
+// k-step's MFMAs; bit 1 issue the next chunk's loads before the first k-step
+// instead of after it.
+template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi, bool kMap = false,
+          int kOpt = 0>
 __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int, int KS, int, int,
@@ -58,6 +62,10 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   constexpr int kPerT = (kChunk2 + kThreads - 1) / kThreads;
   constexpr int kBuf = kKC * JF * 64;              // doubles per LDS buffer
   constexpr bool edots = kEpi >= 2;
+  // kEpi 4: fusion layout 1 -- xs holds p_old, the epilogue recomputes
+  // p_new = r + beta p_old (bitwise the prologue's value) and stores it
+  constexpr bool kRecomp = kEpi == 4;
+  static_assert(kEpi != 3, "fusion layout 2 runs on mode_product_kernel");
   if (skip != nullptr && *skip) return;
   extern __shared__ __attribute__((aligned(16))) double lds[];
 
@@ -205,7 +213,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* buf = lds + (c & 1) * kBuf + lane;
 #pragma unroll
     for (int s = 0; s < kKC; ++s) {
-      if (s == 1 || (kKC == 1 && s == 0)) {
+      if ((kOpt & 2) ? s == 0 : (s == 1 || (kKC == 1 && s == 0))) {
         __builtin_amdgcn_sched_barrier(0);
         if (more) {
           stage(c + 1);
@@ -216,6 +224,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
       if (s < kcn) {
         const double* bs = buf + s * JF * 64;
         const double au = a_cur[0][s], av = a_cur[1][s];
+        if (kOpt & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < JS; ++t) {
           if (TS > 0 && t == JS - 1) {
@@ -237,6 +246,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
             acca[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bs[(FS + t) * 64], acca[t], 0, 0, 0);
           }
         }
+        if (kOpt & 1) __builtin_amdgcn_s_setprio(0);
       }
     }
     if (more) {
@@ -362,6 +372,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* __restrict__ er = fz.er;
     const char* xbase = reinterpret_cast<const char*>(xs + b0u * m);
     const char* ebase = edots ? reinterpret_cast<const char*>(er + b0u * m) : nullptr;
+    char* pbase = kRecomp ? reinterpret_cast<char*>(fz.ep_out + b0u * m) : nullptr;
+    const bool first = kRecomp && fz.sc->first != 0;
+    const double beta = kRecomp ? fz.sc->beta : 0.0;
     double xv[2][4], ev[2][4];
     auto load_e = [&](int e, double (&xo)[4], double (&eo)[4]) {
       const bool cok = col_ok(e);
@@ -383,7 +396,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         if (cok && (lane >> 4) + 4 * r < rows_left) {
-          const double pv = xv[cb][r];
+          double pv = xv[cb][r];
+          if (kRecomp) pv = first ? ev[cb][r] : fma(beta, pv, ev[cb][r]);
           const double v = fma(shift, pv, value(e, r));
           dsum = fma(pv, v, dsum);
           if (edots) {
@@ -391,6 +405,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
             qqsum = fma(v, v, qqsum);
           }
           *reinterpret_cast<double*>(ybase + boff_of(r, e)) = v;
+          if (kRecomp) *reinterpret_cast<double*>(pbase + boff_of(r, e)) = pv;
         }
       }
     }
@@ -400,10 +415,11 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
 }
 
-// kind (kron_apply's launch kind) -> the folded kernel; kinds 5 / 6 (fusion
-// layouts 1 / 2) and the tuning variants stay on mode_product_kernel
+// kind (kron_apply's launch kind) -> the folded kernel; kind 5 (fusion
+// layout 2) and the tuning variants stay on mode_product_kernel
 bool fold_kind(int kind) {
-  return kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 4 || kind == 7;
+  return kind == 0 || kind == 1 || kind == 2 || kind == 3 || kind == 4 || kind == 6 ||
+         kind == 7;
 }
 
 // KIND: kron_apply's launch kind; 8 / 9: the sharded operator's mapped
@@ -411,7 +427,7 @@ bool fold_kind(int kind) {
 template <int JT, int TT, int KIND>
 static FoldConfig cfg_fold() {
   constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
-  constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : 0;
+  constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : KIND == 6 ? 4 : 0;
   constexpr bool MAP = KIND >= 8;
   constexpr int KC = CGP ? 2 : 3;
   constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
@@ -419,8 +435,38 @@ static FoldConfig cfg_fold() {
                     2 * (size_t)KC * JF * 64 * sizeof(double)};
 }
 
+// plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only)
+template <int KC, int MINW, int OPT>
+static FoldConfig cfg_fold_var() {
+  constexpr int JT = 7, TT = 1;
+  constexpr int JF = 2 * (JT - 1 + TT);
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, 0, MINW, 0, false, OPT>, KC, JF,
+                    2 * (size_t)KC * JF * 64 * sizeof(double)};
+}
+
+static int fold_variant() {
+  const char* e = getenv("GG_FOLD_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
+static FoldConfig fold_variant_cfg(int v) {
+  switch (v) {
+    case 1: return cfg_fold_var<2, 3, 0>();
+    case 2: return cfg_fold_var<4, 3, 0>();
+    case 3: return cfg_fold_var<3, 2, 0>();
+    case 4: return cfg_fold_var<6, 2, 0>();
+    case 5: return cfg_fold_var<3, 3, 1>();
+    case 6: return cfg_fold_var<3, 3, 2>();
+    case 7: return cfg_fold_var<1, 3, 0>();
+    default: return cfg_fold_var<3, 3, 0>();
+  }
+}
+
 template <int JT, int TT>
 static FoldConfig fold_by_kind(int kind) {
+  if constexpr (JT == 7 && TT == 1) {
+    if (kind == 0 && fold_variant() != 0) return fold_variant_cfg(fold_variant());
+  }
   switch (kind) {
     case 8: return cfg_fold<JT, TT, 8>();
     case 9: return cfg_fold<JT, TT, 9>();
@@ -428,6 +474,7 @@ static FoldConfig fold_by_kind(int kind) {
     case 2: return cfg_fold<JT, TT, 2>();
     case 3: return cfg_fold<JT, TT, 3>();
     case 4: return cfg_fold<JT, TT, 4>();
+    case 6: return cfg_fold<JT, TT, 6>();
     case 7: return cfg_fold<JT, TT, 7>();
     default: return cfg_fold<JT, TT, 0>();
   }
@@ -460,6 +507,11 @@ FoldConfig select_fold(int JT, int TT, int kind) {
 }
 
 void set_fold_lds_limits() {
+  for (int v = 1; v <= 7; ++v) {
+    const FoldConfig fc = fold_variant_cfg(v);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+  }
   for (int jt = 1; jt <= 8; ++jt)
     for (int tt = 0; tt <= 2; ++tt) {
       if (tt > 0 && jt < 4) continue;

@@ -516,9 +516,10 @@ struct gg_cg {
   double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
   double* p2 = nullptr;        // second direction buffer (fused recurrence)
   double* p3 = nullptr;        // third (x_defer: p_{j-1} outlives the next prologue)
+  double* first_dst = nullptr; // odd d: the first mode product's output (not q)
   bool fused = true;           // recurrence: fused (default) or textbook
   int fusion = 0;              // fused layout (gg_cg_set_fusion): 0, 1 or 2
-  bool xdefer = true;          // layout 0: x updated every other iteration
+  bool xdefer = true;          // layouts 0 / 1: x updated every other iteration
   double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
   double* rr_part = nullptr;   // device, prologue r.r partials (fused)
   int64_t rr_count = 0;
@@ -640,8 +641,9 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
-    // r, p, q, p2, p3 (x_defer) + the matvec scratch
-    *elems = 5 * n + gg::kron_work_elems(K, false);
+    // r, p, q, p2, p3 (x_defer) + the matvec scratch (+ the first mode
+    // product's own output for an odd number of factors, MpFuse::first_dst)
+    *elems = 5 * n + gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
   });
 }
 
@@ -662,6 +664,7 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->p2 = work_dev + 3 * nr;
       cg->p3 = work_dev + 4 * nr;
       cg->mv_work = work_dev + 5 * nr;
+      if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
       const char* xd = getenv("GG_CG_XDEFER");   // A/B knob
       cg->xdefer = !(xd && atoi(xd) == 0);
       cg->mv_partials = gg::kron_partials_needed(K, false);
@@ -779,6 +782,21 @@ int gg_cg_get_fusion(const gg_cg* cg, int* layout) {
   });
 }
 
+int gg_cg_set_xdefer(gg_cg* cg, int on) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set x deferral before gg_cg_start");
+    cg->xdefer = on != 0;
+  });
+}
+
+int gg_cg_get_xdefer(const gg_cg* cg, int* on) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && on, GG_ERR_VALUE, "NULL argument");
+    *on = (cg->fused && cg->xdefer && cg->fusion != 2) ? 1 : 0;
+  });
+}
+
 int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
   return gg::guard([&] {
     GG_REQUIRE(cg && fused, GG_ERR_VALUE, "NULL argument");
@@ -818,7 +836,7 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         ev = cg->events.data() + cg->events_used;
         cg->events_used = need;
       }
-      const bool xdefer = cg->fused && cg->xdefer && cg->fusion == 0;
+      const bool xdefer = cg->fused && cg->xdefer && cg->fusion != 2;
       if (cg->fused) {
         // repair (no-op unless the last beta cancelled): x += alpha p,
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
@@ -842,6 +860,7 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.sp = cg->p;
         fz.sn = n;
         fz.xdefer = xdefer ? 1 : 0;
+        fz.first_dst = cg->first_dst;
         fz.er = cg->r;
         fz.pstride = cg->mv_partials;
         gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
@@ -884,7 +903,7 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
       }
     }
     if (cg->fused) {
-      const bool xdefer = cg->xdefer && cg->fusion == 0;
+      const bool xdefer = cg->xdefer && cg->fusion != 2;
       // closing update (no-op unless pending): x += alpha p, r -= alpha q,
       // rho = r.r, beta, iteration count -- the textbook state.  x_defer: the
       // deferred steps first (also after convergence), then r only

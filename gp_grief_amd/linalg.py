@@ -104,18 +104,20 @@ class CGResult(object):
 class KronCG(object):
     """Resident CG state for (K + shift I) x = b on one MI355X.
 
-    The operator and all CG vectors (x, r, two p buffers, q + one matvec
+    The operator and all CG vectors (x, r, three p buffers, q + one matvec
     scratch) live in HBM; no host synchronisation inside an iteration.
 
     recurrence="fused" (default for d >= 2): an iteration is the d mode
     products plus one scalar kernel -- r -= alpha q, p = r + beta p (and r.r)
-    ride on the first mode product, x += alpha p on the second, p.q / r.q /
-    q.q on the last; beta comes from |r - alpha q|^2 expanded (gg_vec.hip).
-    recurrence="textbook": scipy's operation order, with a separate
-    x / r update pass.  Both leave iterate() in the textbook state.
+    ride on the first mode product, the x update on the second / third, p.q /
+    r.q / q.q on the last; beta comes from |r - alpha q|^2 expanded
+    (gg_vec.hip).  xdefer (default True, fusion layouts 0 / 1): x is updated
+    every other iteration, two steps in one pass.  recurrence="textbook":
+    scipy's operation order, with a separate x / r update pass.  Both leave
+    iterate() in the textbook state.
     """
 
-    def __init__(self, K, shift, recurrence="fused", fusion=None):
+    def __init__(self, K, shift, recurrence="fused", fusion=None, xdefer=None):
         from . import device as dev
         from . import native
         self.K = K
@@ -140,6 +142,10 @@ class KronCG(object):
             native.check(L.gg_cg_set_fusion(h, int(fusion)), "gg_cg_set_fusion")
         native.check(L.gg_cg_get_fusion(h, ctypes.byref(f)))
         self.fusion = f.value
+        if xdefer is not None:
+            native.check(L.gg_cg_set_xdefer(h, int(bool(xdefer))), "gg_cg_set_xdefer")
+        native.check(L.gg_cg_get_xdefer(h, ctypes.byref(f)))
+        self.xdefer = bool(f.value)
         self.n = int(K.shape[0])
         self.x = None
 

@@ -126,6 +126,13 @@ int gg_cg_get_recurrence(const gg_cg* cg, int* fused);
  * Layouts 1 / 2 need the first factor's rows within one launch (<= 256).   */
 int gg_cg_set_fusion(gg_cg* cg, int layout);
 int gg_cg_get_fusion(const gg_cg* cg, int* layout);
+/* Fused recurrence, layouts 0 / 1: x updated every other iteration (default
+ * on; GG_CG_XDEFER=0 at gg_cg_create turns it off): the side job applies two
+ * deferred steps x += a_{j-1} p_{j-1} + a_j p_j in one pass (three direction
+ * buffers in work_dev); gg_cg_iterate still returns the textbook state.
+ * set: before gg_cg_start; get: 1 when the deferral is in effect.         */
+int gg_cg_set_xdefer(gg_cg* cg, int on);
+int gg_cg_get_xdefer(const gg_cg* cg, int* on);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */

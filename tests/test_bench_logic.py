@@ -44,6 +44,9 @@ def test_roofline_folded_launches_are_hbm_bound():
     assert roof["positions"] == [1, 2] and roof["bound"] == "hbm"
     assert abs(roof["flop_per_launch"] - 200 ** 4 * 200) < 1
     assert abs(roof["achieved"] - 3.5 * 8 * 200 ** 4 / 9.25e-3 / 1e9) < 1e-6
+    # x deferred to every other iteration: 1 pass per side launch on average
+    assert bench.launch_passes(4, "fused", 0, True) == [6, 3, 3, 4]
+    assert bench.launch_passes(4, "fused", 1, True) == [5, 3, 3, 5]
     assert extra["fold_mask"] == 0b1111
     assert abs(extra["matvec_dense_equivalent_tflops"] - 2 * extra["matvec_tflops"]) < 1e-9
 
@@ -66,7 +69,7 @@ def test_rhs_identical_in_every_shard_layout():
 
 def test_pmc_traffic_requires_matching_sources(tmp_path, monkeypatch):
     import json
-    rec = {"recurrence": "fused", "fusion_layout": 0, "fold_mask": 15,
+    rec = {"recurrence": "fused", "fusion_layout": 0, "fold_mask": 15, "x_deferred": True,
            "source_sha256": bench.kernel_source_hash(), "calibrated_on_own_pattern": True,
            "per_position": [{"position": k, "traffic_bytes": 1e10 * (k + 1)} for k in range(4)]}
     os.makedirs(tmp_path / "profiles" / "r03")

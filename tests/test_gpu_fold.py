@@ -178,3 +178,37 @@ def test_fold_partial_strips(gg, fold_small):
     assert rel(K * x, oracle.kron_matvec(F, x[:, 0])) < 1e-13
     y = K._device().matvec(gg.device.to_device(x[:, 0]), shift=0.7)
     assert rel(y.cpu().numpy(), oracle.kron_matvec(F, x[:, 0]) + 0.7 * x[:, 0]) < 1e-13
+
+
+@pytest.mark.parametrize("fusion", [0, 1, 2])
+@pytest.mark.parametrize("xdefer", ["1", "0"])
+def test_fold_cg_fusion_layouts_and_deferred_x(gg, fold_small, monkeypatch, fusion, xdefer):
+    """Fused CG on folded factors with each fusion layout (1: p_new recomputed
+    in the folded epilogue; 2: the dense epilogue kernel with the x update) and
+    the x update deferred to every other iteration or not: same solution as
+    the exact solve, and iterate() chunks of odd length (deferred steps
+    pending across calls) reach the same iterate as one call."""
+    import torch
+    monkeypatch.setenv("GG_CG_XDEFER", xdefer)
+    F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate((24, 20, 16, 18))]
+    K = kron(gg, F)
+    n = 24 * 20 * 16 * 18
+    s = 0.05
+    b = np.random.default_rng(12).standard_normal((n, 1))
+    x, info = gg.linalg.cg(K, b, shift=s, rtol=1e-10, fusion=fusion)
+    assert info == 0
+    Q, lam = oracle.factor_eigh(F)
+    ex = oracle.solve_schur(Q, oracle.kron_expand(lam), b[:, 0], s)
+    assert rel(x, ex) < 1e-8
+    one = gg.linalg.KronCG(K, s, fusion=fusion)
+    assert one.xdefer == (xdefer == "1" and fusion != 2)
+    bt = torch.tensor(b[:, 0], device="cuda")
+    one.start(bt, rtol=0.0)
+    one.iterate(23)
+    chunks = gg.linalg.KronCG(K, s, fusion=fusion)
+    chunks.start(bt, rtol=0.0)
+    for k in (3, 1, 7, 5, 7):
+        chunks.iterate(k)
+    torch.cuda.synchronize()
+    assert one.status()[0] == chunks.status()[0] == 23
+    assert rel(chunks.x.cpu().numpy(), one.x.cpu().numpy()) < 1e-12

@@ -454,3 +454,25 @@ def test_cg_fusion_layout_needs_single_launch(gg):
     K = gg.tensors.KronMatrix(F, sym=True)
     with pytest.raises(ValueError):
         gg.linalg.KronCG(K, 0.1, fusion=1)
+
+
+@pytest.mark.parametrize("ms", [(40, 36, 10), (24, 20, 16), (16, 12, 10, 8, 6)])
+def test_cg_fused_odd_d_deterministic(gg, ms):
+    """Odd d: the first mode product's output has its own scratch (the fused
+    prologue reads q_old across workgroups in the same launch, so writing the
+    output over q raced).  Repeated solves are bitwise identical and match
+    scipy's iteration count."""
+    F = _rbf_factors(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(3).standard_normal((n, 1))
+    s = 0.05
+    runs = []
+    for _ in range(3):
+        x, info = gg.linalg.cg(K, b, shift=s, rtol=1e-10, recurrence="fused")
+        assert info == 0
+        runs.append((gg.linalg.cg.last.iters, x.copy()))
+    assert len({r[0] for r in runs}) == 1
+    assert all(np.array_equal(runs[0][1], r[1]) for r in runs[1:])
+    xo, _, ito = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + s * v, b[:, 0], rtol=1e-10)
+    assert abs(runs[0][0] - ito) <= max(3, 0.05 * ito), (runs[0][0], ito)

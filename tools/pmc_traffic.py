@@ -1,6 +1,6 @@
 """HBM traffic per launch of the fused-CG mode products from rocprofv3 PMC passes.
 
-usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON
+usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON [--fusion F] [--no-xdefer]
 
 Counters (two separate --pmc runs of `bench.py --steps 2 --warmup 1`, kernel
 trace only, as MI355X_MICROARCH.md prescribes):
@@ -40,22 +40,31 @@ def dispatches(d):
 
 def main():
     rd_dir, wr_dir, out = sys.argv[1:4]
+    fusion = int(sys.argv[sys.argv.index("--fusion") + 1]) if "--fusion" in sys.argv else 0
+    xdefer = "--no-xdefer" not in sys.argv
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
     rd, names = dispatches(rd_dir)
     wr, _ = dispatches(wr_dir)
     ids = sorted(rd)
     d = 4
     iters = [ids[i:i + d] for i in range(0, len(ids) - d + 1, d)]
-    last = iters[-1]                     # a pending (fully fused) iteration
+    # the last two iterations: fully fused (pending updates), and with the
+    # deferred x update one with and one without the x pass -- averaged, as
+    # bench.launch_passes counts them
+    last2 = iters[-2:]
     per_pos = []
-    for k, did in enumerate(last):
-        rbytes = sum(rd[did].get(c, 0.0) * s for c, s in SIZES.items())
-        wbytes = wr.get(did, {}).get("TCC_EA0_WRREQ_64B_sum", 0.0) * 64
-        per_pos.append({"position": k, "kernel": names[did], "read_bytes": rbytes,
-                        "write_bytes": wbytes, "traffic_bytes": rbytes + wbytes})
+    for k in range(d):
+        dids = [it[k] for it in last2]
+        rbytes = sum(sum(rd[did].get(c, 0.0) * s for c, s in SIZES.items())
+                     for did in dids) / len(dids)
+        wbytes = sum(wr.get(did, {}).get("TCC_EA0_WRREQ_64B_sum", 0.0) * 64
+                     for did in dids) / len(dids)
+        per_pos.append({"position": k, "kernel": names[dids[-1]], "read_bytes": rbytes,
+                        "write_bytes": wbytes, "traffic_bytes": rbytes + wbytes,
+                        "dispatches": dids})
     n = 200 ** 4
-    # algorithmic passes per position (fusion layout 0, d = 4: prologue, x
-    # side job on halves of x at positions 1 and 2, fused epilogue)
-    passes = [6.0, 3.5, 3.5, 4.0]
+    passes = [float(v) for v in bench.launch_passes(d, "fused", fusion, xdefer)]
     for k, pp in enumerate(per_pos):
         pp["algorithmic_bytes"] = passes[k] * 8.0 * n
         pp["ratio"] = pp["traffic_bytes"] / pp["algorithmic_bytes"]
@@ -63,24 +72,23 @@ def main():
     calib = {"iteration_ratio": tot / (sum(passes) * 8.0 * n),
              "per_position_ratio": [pp["ratio"] for pp in per_pos]}
     dom = per_pos[0]
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    import bench
     fold_mask = sum(1 << k for k, pp in enumerate(per_pos) if "fold" in pp["kernel"])
     res = {
-        "position": 0, "recurrence": "fused", "fusion_layout": 0,
+        "position": 0, "recurrence": "fused", "fusion_layout": fusion, "x_deferred": xdefer,
         "fold_mask": fold_mask,
         # bench.py reuses these counters only for kernels built from the same sources
         "source_sha256": bench.kernel_source_hash(),
         "sources": bench.KERNEL_SOURCES,
         "kernel": dom["kernel"], "traffic_bytes": dom["traffic_bytes"],
         "read_bytes": dom["read_bytes"], "write_bytes": dom["write_bytes"],
-        "algorithmic_bytes": 6 * 8.0 * n,
+        "algorithmic_bytes": passes[0] * 8.0 * n,
         "calibrated_on_own_pattern": all(abs(pp["ratio"] - 1) < 0.05 for pp in per_pos),
         "calibration": calib, "per_position": per_pos,
         "method": "separate rocprofv3 --pmc passes (reads by request size / writes), kernel "
-                  "trace only, bench.py --steps 2 --warmup 1 at 200^4; bytes = request "
-                  "counts x request sizes; checked per launch against its algorithmic "
-                  "passes (6 / 3.5 / 3.5 / 4 x 12.8 GB) on the kernels' own patterns",
+                  "trace only, bench.py --steps 4 --warmup 2 at 200^4; bytes = request "
+                  "counts x request sizes, averaged over the last two iterations; checked "
+                  "per launch against its algorithmic passes (%s x 12.8 GB) on the "
+                  "kernels' own patterns" % " / ".join("%g" % v for v in passes),
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_position"}))
