@@ -1107,7 +1107,20 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         const bool fold = f.ffrag != nullptr && jt0 == 0 && variant == 0 && fold_kind(kind) &&
                           !(pro && last) && !(kind == 2 && pro_variant() != 0);
         if (fold) {
-          const FoldConfig fc = select_fold(f.fJT, f.fTT, kind);
+          const double* xs_ = last && (shift != 0.0 || dot_partials != nullptr)
+                                  ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
+                                                                                      : x)
+                                  : nullptr;
+          const bool aligned =
+              f.p % 2 == 0 &&
+              ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(xs_) |
+                reinterpret_cast<uintptr_t>(cg != nullptr ? cg->er : nullptr) |
+                reinterpret_cast<uintptr_t>(cg != nullptr ? cg->ep_out : nullptr)) & 15) == 0;
+          // the LDS-staged epilogue only where it reads the fused operands
+          const FoldConfig fc =
+              (aligned && xs_ != nullptr && fold_staged_available(f.fJT, f.fTT, kind))
+                  ? select_fold_staged(f.fJT, f.fTT, kind)
+                  : select_fold(f.fJT, f.fTT, kind);
           mc = ModeConfig{fc.fn, 4, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
         }
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);

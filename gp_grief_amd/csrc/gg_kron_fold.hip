@@ -45,14 +45,20 @@ namespace gg {
 // kOpt (A/B variants, GG_FOLD_VARIANT): bit 0 s_setprio(1) around each
 // k-step's MFMAs; bit 1 issue the next chunk's loads before the first k-step
 // instead of after it.
+// kStg: the identity epilogue staged through LDS -- each accumulator
+// register's 4 rows go to a wave-private LDS image in the global layout (row
+// stride m), then the wave streams them with 16-byte lanes (1 KiB contiguous
+// per instruction) together with the fused operands (p, r) it loads the same
+// way.  Needs m even and 16-byte aligned vectors (kron_apply checks).
 template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi, bool kMap = false,
-          int kOpt = 0>
+          int kOpt = 0, bool kStg = false>
 __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int, int KS, int, int,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
     const int* __restrict__ skip, OutMap om, MpFuse fz) {
   static_assert(!kMap || kEpi == 0, "the mapped epilogue stores only");
+  static_assert(!(kMap && kStg), "staged epilogue: identity layout only");
   constexpr int kWaves = 4;
   constexpr int kThreads = 256;
   constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;   // S fragments per k-step
@@ -320,7 +326,72 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     return (e & 1) ? sv - tv : sv + tv;
   };
   double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
-  if (kMap) {
+  if (kStg) {
+    double* wl = lds + (int64_t)wave * 4 * m;   // this wave's 4 x m image
+    const double* __restrict__ er = fz.er;
+    double* __restrict__ epo = kRecomp ? fz.ep_out : nullptr;
+    const bool first = kRecomp && fz.sc->first != 0;
+    const double beta = kRecomp ? fz.sc->beta : 0.0;
+    const int rl = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int t = 0; t < JS; ++t) {
+        const int j = 16 * t + col;
+        const double sv = accs[t][r];
+        const double tv = t < JA ? acca[t < JA ? t : 0][r] : 0.0;
+        if (j < hS) wl[rl * m + j] = sv + tv;
+        if (j < h) wl[rl * m + (m - 1 - j)] = sv - tv;
+      }
+      // a wave's LDS instructions complete in order: the reads below see the
+      // writes above (wave-private image, no barrier)
+      const int nr = min(4, max(0, rows_left - 4 * r));
+      const int tot2 = (nr * m) >> 1;              // double2 of this round (m even)
+      const int64_t g0 = (b0u + 4 * r) * m;        // first element (16-B aligned)
+      constexpr int kU = 4;
+      for (int base = 0; base < tot2; base += 64 * kU) {
+        double2 av[kU], pv[kU], ev[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int i2 = base + lane + 64 * u;
+          const bool ok = i2 < tot2;
+          const int64_t g = g0 + 2 * (int64_t)i2;
+          av[u] = ok ? *reinterpret_cast<const double2*>(wl + 2 * i2) : double2{0.0, 0.0};
+          pv[u] = (ok && xs != nullptr) ? *reinterpret_cast<const double2*>(xs + g)
+                                        : double2{0.0, 0.0};
+          ev[u] = (ok && edots) ? *reinterpret_cast<const double2*>(er + g) : double2{0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int i2 = base + lane + 64 * u;
+          if (i2 >= tot2) continue;
+          const int64_t g = g0 + 2 * (int64_t)i2;
+          if (xs == nullptr) {
+            *reinterpret_cast<double2*>(Y + g) = av[u];
+            continue;
+          }
+          double2 p2 = pv[u];
+          if (kRecomp) {
+            p2.x = first ? ev[u].x : fma(beta, p2.x, ev[u].x);
+            p2.y = first ? ev[u].y : fma(beta, p2.y, ev[u].y);
+          }
+          double2 v;
+          v.x = fma(shift, p2.x, av[u].x);
+          v.y = fma(shift, p2.y, av[u].y);
+          dsum = fma(p2.x, v.x, dsum);
+          dsum = fma(p2.y, v.y, dsum);
+          if (edots) {
+            rqsum = fma(ev[u].x, v.x, rqsum);
+            rqsum = fma(ev[u].y, v.y, rqsum);
+            qqsum = fma(v.x, v.x, qqsum);
+            qqsum = fma(v.y, v.y, qqsum);
+          }
+          *reinterpret_cast<double2*>(Y + g) = v;
+          if (kRecomp) *reinterpret_cast<double2*>(epo + g) = p2;
+        }
+      }
+    }
+  } else if (kMap) {
     // rows: a = row / mi, h = (row % mi) / cr, br = (row % mi) % cr; columns
     // grouped by cg (include gg_internal.h OutMap)
     int64_t rowoff[4];
@@ -410,8 +481,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
       }
     }
   }
-  mp_block_sums<kWaves, CGP, edots, false>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz, lds,
-                                           blockIdx.x);
+  // the staged epilogue's images occupy the first 16 m doubles of LDS
+  mp_block_sums<kWaves, CGP, edots, false>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz,
+                                           kStg ? lds + 16 * m : lds, blockIdx.x);
   if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
 }
 
@@ -424,15 +496,18 @@ bool fold_kind(int kind) {
 
 // KIND: kron_apply's launch kind; 8 / 9: the sharded operator's mapped
 // epilogue without / with the textbook CG prologue (gg_kron_dist_*)
-template <int JT, int TT, int KIND>
+template <int JT, int TT, int KIND, bool STG = false>
 static FoldConfig cfg_fold() {
   constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
   constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : KIND == 6 ? 4 : 0;
   constexpr bool MAP = KIND >= 8;
   constexpr int KC = CGP ? 2 : 3;
   constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI, MAP>, KC, JF,
-                    2 * (size_t)KC * JF * 64 * sizeof(double)};
+  constexpr size_t kB = 2 * (size_t)KC * JF * 64 * sizeof(double);
+  // staged epilogue: 4 waves x 4 rows x m (<= 32 JT) doubles + the reduction
+  constexpr size_t kS = STG ? ((size_t)16 * 32 * JT + 16) * sizeof(double) : 0;
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI, MAP, 0, STG>, KC,
+                    JF, kB > kS ? kB : kS};
 }
 
 // plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only)
@@ -460,6 +535,52 @@ static FoldConfig fold_variant_cfg(int v) {
     case 7: return cfg_fold_var<1, 3, 0>();
     default: return cfg_fold_var<3, 3, 0>();
   }
+}
+
+// the staged epilogue (kStg) for the launches whose epilogue reads the fused
+// operands (kinds 0 with a shift / dot operand, 3 and 6): measured at 200^4
+// the fused-CG epilogue launch 11.7 -> 10.2 ms, while plain-store launches
+// lose 0.4 ms to the LDS round trip (profiles/r03/h_bench_stage*.json)
+template <int JT, int TT>
+static FoldConfig fold_staged_by_kind(int kind) {
+  switch (kind) {
+    case 3: return cfg_fold<JT, TT, 3, true>();
+    case 6: return cfg_fold<JT, TT, 6, true>();
+    default: return cfg_fold<JT, TT, 0, true>();
+  }
+}
+
+bool fold_staged_available(int JT, int TT, int kind) {
+  const char* e = getenv("GG_FOLD_STAGE");   // A/B knob: 0 = direct stores
+  if (e && atoi(e) == 0) return false;
+  return (kind == 0 || kind == 3 || kind == 6) && JT >= 1 && JT <= 8 &&
+         (TT == 0 || JT >= 4);
+}
+
+FoldConfig select_fold_staged(int JT, int TT, int kind) {
+  if (TT == 0) {
+    switch (JT) {
+      case 1: return fold_staged_by_kind<1, 0>(kind);
+      case 2: return fold_staged_by_kind<2, 0>(kind);
+      case 3: return fold_staged_by_kind<3, 0>(kind);
+      case 4: return fold_staged_by_kind<4, 0>(kind);
+      case 5: return fold_staged_by_kind<5, 0>(kind);
+      case 6: return fold_staged_by_kind<6, 0>(kind);
+      case 7: return fold_staged_by_kind<7, 0>(kind);
+      case 8: return fold_staged_by_kind<8, 0>(kind);
+      default: break;
+    }
+  } else {
+    switch (JT) {
+      case 4: return TT == 1 ? fold_staged_by_kind<4, 1>(kind) : fold_staged_by_kind<4, 2>(kind);
+      case 5: return TT == 1 ? fold_staged_by_kind<5, 1>(kind) : fold_staged_by_kind<5, 2>(kind);
+      case 6: return TT == 1 ? fold_staged_by_kind<6, 1>(kind) : fold_staged_by_kind<6, 2>(kind);
+      case 7: return TT == 1 ? fold_staged_by_kind<7, 1>(kind) : fold_staged_by_kind<7, 2>(kind);
+      case 8: return TT == 1 ? fold_staged_by_kind<8, 1>(kind) : fold_staged_by_kind<8, 2>(kind);
+      default: break;
+    }
+  }
+  throw Error(GG_ERR_VALUE, "no staged folded kernel for this factor shape");
 }
 
 template <int JT, int TT>
@@ -507,6 +628,15 @@ FoldConfig select_fold(int JT, int TT, int kind) {
 }
 
 void set_fold_lds_limits() {
+  for (int jt = 1; jt <= 8; ++jt)
+    for (int tt = 0; tt <= 2; ++tt) {
+      if (tt > 0 && jt < 4) continue;
+      for (int kind : {0, 3, 6}) {
+        const FoldConfig fc = select_fold_staged(jt, tt, kind);
+        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+      }
+    }
   for (int v = 1; v <= 7; ++v) {
     const FoldConfig fc = fold_variant_cfg(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),

@@ -123,6 +123,10 @@ struct FoldConfig {
 };
 bool fold_kind(int kind);
 FoldConfig select_fold(int JT, int TT, int kind);
+// the LDS-staged identity epilogue for launches with a shift / dot operand
+// (kinds 0, 3, 6; m even, 16-byte aligned vectors; GG_FOLD_STAGE=0 disables)
+bool fold_staged_available(int JT, int TT, int kind);
+FoldConfig select_fold_staged(int JT, int TT, int kind);
 void set_fold_lds_limits();
 
 }  // namespace gg
