@@ -135,6 +135,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   };
   // raw loads of chunk c: [0] = row i', [1] = row m-1-i' (only the last
   // chunk can step past the rows: clamp there, masked when consumed)
+  // raw loads of chunk c: [0] = row i', [1] = row m-1-i' (only the last
+  // chunk can step past the rows: clamp there, masked when consumed)
   auto aload = [&](int c, double (&a)[2][kKC], double (&r)[2][kKC], double (&q)[2][kKC]) {
     int64_t ol = lo0 + (int64_t)c * achunk;
     int64_t oh = hi0 - (int64_t)c * achunk;
@@ -269,8 +271,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     __syncthreads();
   }
 
-  // 4x4x4_4b tails -> the 16x16 layout (see mode_product_kernel kT4)
-  {
+  // 4x4x4_4b tails -> the 16x16 layout (see mode_product_kernel kT4); the
+  // staged epilogue writes them from their own layout instead
+  if (!kStg) {
     const int cc = lane & 15;
     const int src0 = 16 * (lane >> 4) + (lane & 3);
     if (TS > 0) {
@@ -333,15 +336,30 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const bool first = kRecomp && fz.sc->first != 0;
     const double beta = kRecomp ? fz.sc->beta : 0.0;
     const int rl = lane >> 4;
+    static_assert(TS == TA, "staged epilogue: equal S / T tails");
+    constexpr int JFULL = JS - (TS > 0 ? 1 : 0);   // 16x16 tiles per half
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
-      for (int t = 0; t < JS; ++t) {
+      for (int t = 0; t < JFULL; ++t) {
         const int j = 16 * t + col;
         const double sv = accs[t][r];
         const double tv = t < JA ? acca[t < JA ? t : 0][r] : 0.0;
         if (j < hS) wl[rl * m + j] = sv + tv;
         if (j < h) wl[rl * m + (m - 1 - j)] = sv - tv;
+      }
+      if (TS > 0) {
+        // 4x4x4_4b D: lane 16 rr + 4 g + c holds row 4 g + rr, column
+        // 16 JFULL + 4 i + c of tail i; round r takes the lanes with g == r
+        if (((lane >> 2) & 3) == r) {
+          const int rr = lane >> 4;
+#pragma unroll
+          for (int i = 0; i < (TS > 0 ? TS : 1); ++i) {
+            const int j = 16 * JFULL + 4 * i + (lane & 3);
+            if (j < hS) wl[rr * m + j] = t4s[i] + t4a[i];
+            if (j < h) wl[rr * m + (m - 1 - j)] = t4s[i] - t4a[i];
+          }
+        }
       }
       // a wave's LDS instructions complete in order: the reads below see the
       // writes above (wave-private image, no barrier)
@@ -501,13 +519,19 @@ static FoldConfig cfg_fold() {
   constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
   constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : KIND == 6 ? 4 : 0;
   constexpr bool MAP = KIND >= 8;
-  constexpr int KC = CGP ? 2 : 3;
+  // the fused / Lanczos prologues hold three operands per row pair: one
+  // k-step per chunk keeps them within the 3-wave register budget (A/B at
+  // 200^4: 15.7 vs 18.7 ms with two, profiles/r03/j_*)
+  constexpr int KC = CGP >= 2 ? 1 : CGP ? 2 : 3;
   constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
+  // 2 x (JT - 1) full 16x16 accumulators beside the tails: beyond 12 of them
+  // (m > 200) three waves per SIMD would spill -- two instead
+  constexpr int MINW = ((JT - (TT > 0 ? 1 : 0)) <= 6 && TT <= 1) ? 3 : 2;
   constexpr size_t kB = 2 * (size_t)KC * JF * 64 * sizeof(double);
   // staged epilogue: 4 waves x 4 rows x m (<= 32 JT) doubles + the reduction
   constexpr size_t kS = STG ? ((size_t)16 * 32 * JT + 16) * sizeof(double) : 0;
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, 3, EPI, MAP, 0, STG>, KC,
-                    JF, kB > kS ? kB : kS};
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, MINW, EPI, MAP, 0, STG>,
+                    KC, JF, kB > kS ? kB : kS};
 }
 
 // plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only)
@@ -583,10 +607,22 @@ FoldConfig select_fold_staged(int JT, int TT, int kind) {
   throw Error(GG_ERR_VALUE, "no staged folded kernel for this factor shape");
 }
 
+// fused-CG prologue with one k-step per chunk (A/B: GG_FOLD_PRO_KC=1)
+static FoldConfig fold_pro_kc1() {
+  constexpr int JT = 7, TT = 1;
+  constexpr int JF = 2 * (JT - 1 + TT);
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, 1, 2, 3, 0, false, 0, false>, 1, JF,
+                    2 * (size_t)1 * JF * 64 * sizeof(double)};
+}
+
 template <int JT, int TT>
 static FoldConfig fold_by_kind(int kind) {
   if constexpr (JT == 7 && TT == 1) {
     if (kind == 0 && fold_variant() != 0) return fold_variant_cfg(fold_variant());
+    if (kind == 2) {
+      const char* e = getenv("GG_FOLD_PRO_KC");
+      if (e && atoi(e) == 1) return fold_pro_kc1();
+    }
   }
   switch (kind) {
     case 8: return cfg_fold<JT, TT, 8>();
@@ -628,6 +664,11 @@ FoldConfig select_fold(int JT, int TT, int kind) {
 }
 
 void set_fold_lds_limits() {
+  {
+    const FoldConfig fc = fold_pro_kc1();
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+  }
   for (int jt = 1; jt <= 8; ++jt)
     for (int tt = 0; tt <= 2; ++tt) {
       if (tt > 0 && jt < 4) continue;

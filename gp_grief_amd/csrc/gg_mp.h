@@ -62,7 +62,9 @@ __device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
   constexpr int kB = 4;
   if (fz.xdefer) {
     // two deferred steps at once: x += c0 p0 + c1 p1 (4 passes per two CG
-    // iterations instead of 6)
+    // iterations instead of 6); 2 double2 per operand in flight keeps the
+    // fused kernels within their register budget
+    constexpr int kB = 2;
     if (fz.sc->xpend != 2) return;
     const double c0 = fz.sc->xc[0], c1 = fz.sc->xc[1];
     const double* __restrict__ p0 = fz.sc->xp[0] + fz.soff;
