@@ -1018,11 +1018,17 @@ __global__ __launch_bounds__(256) void trsv_chain_kernel(int n, const double* __
                                                          int64_t lda,
                                                          const double* __restrict__ Winv,
                                                          double* B, int* flags,
-                                                         int* __restrict__ status) {
+                                                         int* __restrict__ status,
+                                                         int* __restrict__ ticket) {
   __shared__ double rhs[kNB];
-  __shared__ int ok;
+  __shared__ int ok, tk;
   const int nblk = (n + kNB - 1) / kNB;
-  const int b = kTrans ? nblk - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  // block rows are taken in arrival order from a ticket counter, not from
+  // blockIdx: every row this workgroup waits on belongs to a workgroup that
+  // is already running, whatever order the hardware dispatches them in
+  if (threadIdx.x == 0) tk = atomicAdd(ticket, 1);
+  __syncthreads();
+  const int b = kTrans ? nblk - 1 - tk : tk;
   const int k0 = b * kNB, nb = min(kNB, n - k0);
   const int tid = threadIdx.x, i = tid >> 2, q = tid & 3;
   const int row = k0 + i;
@@ -1115,12 +1121,17 @@ __global__ __launch_bounds__(256) void trsm_chain_kernel(int n, int r, const dou
                                                          const double* __restrict__ Winv,
                                                          double* Bm, int64_t ldb, int trans,
                                                          int tri, int* flags,
-                                                         int* __restrict__ status) {
+                                                         int* __restrict__ status,
+                                                         int* __restrict__ ticket) {
   __shared__ double Ls[kNB][kNB + 1];
   __shared__ double Xs[kNB][kNB + 1];
-  __shared__ int ok;
+  __shared__ int ok, tk;
   const int nblk = (n + kNB - 1) / kNB, nch = (r + kNB - 1) / kNB;
-  const int order = (int)(blockIdx.x / nch), j = (int)(blockIdx.x % nch);
+  // (block row, column chunk) in arrival order from a ticket counter
+  // (trsv_chain_kernel): dispatch order cannot deadlock the chain
+  if (threadIdx.x == 0) tk = atomicAdd(ticket, 1);
+  __syncthreads();
+  const int order = tk / nch, j = tk % nch;
   const int b = trans ? nblk - 1 - order : order;
   const int k0 = b * kNB, nb = min(kNB, n - k0);
   const int j0 = j * kNB, cw = min(kNB, r - j0);
@@ -1547,16 +1558,17 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
     // (trsv_chain_kernel) instead of a GEMM pair per block row
     const char* ch = getenv("GG_TRSV_CHAIN");
     if (r == 1 && !tri && ldb == 1 && !(ch != nullptr && atoi(ch) == 0)) {
+      // [forward flags | backward flags | status | two tickets]
       int* flags = nullptr;
-      GG_HIP(hipMallocAsync(&flags, (2 * (size_t)nblk + 1) * sizeof(int), s));
-      GG_HIP(hipMemsetAsync(flags, 0, (2 * (size_t)nblk + 1) * sizeof(int), s));
+      GG_HIP(hipMallocAsync(&flags, (2 * (size_t)nblk + 3) * sizeof(int), s));
+      GG_HIP(hipMemsetAsync(flags, 0, (2 * (size_t)nblk + 3) * sizeof(int), s));
       int* st = flags + 2 * nblk;
       if (which & 1)
         hipLaunchKernelGGL(gg::trsv_chain_kernel<false>, dim3(nblk), dim3(256), 0, s, n, L_dev,
-                           lda, winv_dev, B_dev, flags, st);
+                           lda, winv_dev, B_dev, flags, st, st + 1);
       if (which & 2)
         hipLaunchKernelGGL(gg::trsv_chain_kernel<true>, dim3(nblk), dim3(256), 0, s, n, L_dev,
-                           lda, winv_dev, B_dev, flags + nblk, st);
+                           lda, winv_dev, B_dev, flags + nblk, st, st + 2);
       GG_LAUNCH_CHECK();
       int hst = 0;
       GG_HIP(hipMemcpyAsync(&hst, st, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1573,16 +1585,16 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
       const int nch = (int)gg::ceil_div(r, gg::kNB);
       const size_t nflags = (size_t)nblk * nch;
       int* flags = nullptr;
-      GG_HIP(hipMallocAsync(&flags, (2 * nflags + 1) * sizeof(int), s));
-      GG_HIP(hipMemsetAsync(flags, 0, (2 * nflags + 1) * sizeof(int), s));
+      GG_HIP(hipMallocAsync(&flags, (2 * nflags + 3) * sizeof(int), s));
+      GG_HIP(hipMemsetAsync(flags, 0, (2 * nflags + 3) * sizeof(int), s));
       int* st = flags + 2 * nflags;
       const unsigned grid = (unsigned)((int64_t)nblk * nch);
       if (which & 1)
         hipLaunchKernelGGL(gg::trsm_chain_kernel, dim3(grid), dim3(256), 0, s, n, r, L_dev, lda,
-                           winv_dev, B_dev, ldb, 0, tri ? 1 : 0, flags, st);
+                           winv_dev, B_dev, ldb, 0, tri ? 1 : 0, flags, st, st + 1);
       if (which & 2)
         hipLaunchKernelGGL(gg::trsm_chain_kernel, dim3(grid), dim3(256), 0, s, n, r, L_dev, lda,
-                           winv_dev, B_dev, ldb, 1, 0, flags + nflags, st);
+                           winv_dev, B_dev, ldb, 1, 0, flags + nflags, st, st + 2);
       GG_LAUNCH_CHECK();
       int hst = 0;
       GG_HIP(hipMemcpyAsync(&hst, st, sizeof(int), hipMemcpyDeviceToHost, s));

@@ -527,9 +527,18 @@ class GPGriefModel(BaseModel):
 
     def _compute_log_likelihood(self, parameters):
         self.parameters = parameters
-        self.fit()
+        # the log det needs chol(P) whatever the p-solver: a p_solver='cg'
+        # model factors first and solves alpha with the same factor (fit()
+        # then takes it) instead of running PCG beside it
+        if self.p_solver == 'cg':
+            self._phi_setup()
+            ld = self._cov_log_det()
+            self.fit()
+        else:
+            self.fit()
+            ld = self._cov_log_det()
         yd = self._y_dev()
-        ll = -0.5 * (self._sum_scalar(dense.dot(yd, self._alpha)) + self._cov_log_det()
+        ll = -0.5 * (self._sum_scalar(dense.dot(yd, self._alpha)) + ld
                      + self.num_data * np.log(np.pi * 2))
         return np.array([[ll]])
 
@@ -594,12 +603,21 @@ class GPGriefModel(BaseModel):
             dense.axpby(1.0, z, rz_new / rz, d)
             rz = rz_new
         self.cg_iters.append(it)
+        if it >= maxiter:
+            res = np.sqrt(dense.dot(r, r)) / bnorm
+            if not res <= rtol:
+                logger.warning("p-system PCG stopped at maxiter=%d with relative residual "
+                               "%.3g > rtol=%.3g" % (maxiter, res, rtol))
+                self.cg_converged = False
+                return x
+        self.cg_converged = True
         return x
 
     def _mv_cov_inv_dev(self, xd):
         """(x - Phi P^-1 Phi^T x) / s for a 1-D device vector."""
         t = self._sum(dense.matvec(self._Phi, xd, trans=True))
-        if self.p_solver == 'cg':
+        if self.p_solver == 'cg' and self._Pchol is None:
+            # no factor for these parameters: PCG (fit / predictive mean only)
             t = self.solve_p_cg(t)
         else:
             t = self._Pchol.solve(t, which=3)
@@ -902,18 +920,71 @@ class GPwebModel(BaseModel):
         return dense.host(yhat).reshape((-1, 1)), dense.host(var)
 
 
+def _gram_svd(Pd):
+    """Right singular vectors / values of Phi from the device eigensolver on
+    A = Phi^T Phi (descending); returns (sv, V, eigenvalues of A)."""
+    A = dense.host(dense.matmul(Pd, Pd, ta=True))
+    A = 0.5 * (A + A.T)
+    from .tensors import device_sym_eig
+    Qs, lams = device_sym_eig([A])
+    lam, V = lams[0], Qs[0]
+    order = np.argsort(-lam, kind='stable')
+    lam, V = lam[order], V[:, order]
+    return np.sqrt(np.maximum(lam, 0.0)), V, lam
+
+
+def _cholqr3_svd(Pd):
+    """Singular values (descending) and right singular vectors of the n x p
+    device matrix Phi (n >= p) by shifted CholeskyQR3: A1 = Phi^T Phi + s I
+    (s = 11 (n p + p (p + 1)) eps ||A||_F), Q1 = Phi L1^-T, then CholeskyQR2 on
+    Q1 -- R = L3^T L2^T L1^T with Phi = Q3 R -- and the SVD of the p x p R on
+    the host.  None when a Gram is not numerically positive definite beyond
+    the shift's reach (rank deficiency): (None, None), the caller falls back."""
+    t = dev.torch()
+    n, p = int(Pd.shape[0]), int(Pd.shape[1])
+    eps = np.finfo(np.float64).eps
+    A = dense.matmul(Pd, Pd, ta=True)
+    fro = float(np.sqrt(max(dense.dot(A.reshape(-1), A.reshape(-1)), 0.0)))
+    if not fro > 0.0:
+        return None, None
+    shift = 11.0 * (n * p + p * (p + 1)) * eps * fro
+    R = np.eye(p)
+    Q = Pd
+    try:
+        for stage in range(3):
+            if stage > 0:
+                A = dense.matmul(Q, Q, ta=True)
+            C = dense.Cholesky(dense.add_diag(A, shift) if stage == 0 else A)
+            L = np.tril(dense.host(C.L))
+            d = np.diag(L)
+            # a near-singular Gram after the shifted first stage means a null
+            # direction of Phi (its singular value is far below 1e-7)
+            if stage > 0 and not np.min(d) ** 2 > 1e3 * eps * np.max(d) ** 2:
+                return None, None
+            R = L.T.dot(R)
+            if stage < 2:
+                Q = dense.matmul(Q, C.inverse(), tb=True)   # Q L^-T
+    except np.linalg.LinAlgError:
+        return None, None
+    del t
+    _, sv, VT = np.linalg.svd(R)
+    return sv, np.ascontiguousarray(VT.T)
+
+
 class GPwebTransformedModel(BaseModel):
     """WEB GP with the basis rotated to Phi's left singular vectors so that the
     likelihood and gradient are O(p) (gp_web_transformed_model.py:13-127).
 
-    The thin SVD is formed on the MI355X from the Gram matrix: A = Phi^T Phi
-    (FP64 MFMA), A = V S^2 V^T by the device Jacobi eigensolver, and
-    Phit^T y = S^-1 V^T (Phi^T y).  Bases with singular value <= 1e-7 are
-    dropped as in the reference (:27-35).  The Gram route squares the condition
-    number: singular values below ~sqrt(eps) * s_max lose relative accuracy, so
-    a nearly rank-deficient Phi can keep a different number of bases than
-    LAPACK's SVD would.  The O(p) likelihood / gradient stay on the host, as
-    in the reference; predictions are device GEMV / GEMM.
+    The thin SVD: Phi = Q R by shifted CholeskyQR3 on the MI355X (three Grams
+    and two Q L^-T products on FP64 MFMA, three device Cholesky factors; Q is
+    orthonormal to working precision for cond(Phi) up to ~1/eps), then the
+    small p x p SVD R = U_R S V^T on the host (factor-sized, LAPACK), so S and
+    V carry the accuracy of LAPACK's SVD of Phi; Phit^T y = S^-1 V^T (Phi^T y).
+    Bases with singular value <= 1e-7 are dropped as in the reference
+    (:27-35).  A numerically rank-deficient Phi (or n < p) falls back to the
+    Gram spectrum A = V S^2 V^T with a floor at its rounding level, logged.
+    The O(p) likelihood / gradient stay on the host, as in the reference;
+    predictions are device GEMV / GEMM.
     """
 
     def __init__(self, Phi, y, noise_var=1.):
@@ -924,22 +995,27 @@ class GPwebTransformedModel(BaseModel):
         assert Phi.shape[0] == self.n
         self.p_orig = int(Phi.shape[1])
         Pd = _dev_matrix(Phi)
-        A = dense.host(dense.matmul(Pd, Pd, ta=True))
-        A = 0.5 * (A + A.T)
-        from .tensors import device_sym_eig
-        Qs, lams = device_sym_eig([A])
-        lam, V = lams[0], Qs[0]
-        order = np.argsort(-lam, kind='stable')
-        lam, V = lam[order], V[:, order]
-        sv = np.sqrt(np.maximum(lam, 0.0))
-        # The reference keeps LAPACK singular values above 1e-7 (at most
-        # min(n, p) of them).  Gram eigenvalues carry an absolute error of
-        # ~eps * s_max^2, so null directions surface as ~sqrt(eps) * s_max
-        # "singular values": drop eigenvalues under the Gram's own rounding
-        # floor, and never keep more than min(n, p_orig) bases.
-        floor = max(self.n, self.p_orig) * np.finfo(np.float64).eps * max(float(lam[0]), 0.0)
-        ikeep = (sv > 1e-7) & (lam > floor)
-        ikeep &= np.arange(lam.size) < min(self.n, self.p_orig)
+        sv, V = _cholqr3_svd(Pd) if self.n >= self.p_orig else (None, None)
+
+        if sv is not None:
+            ikeep = sv > 1e-7
+        else:
+            if self.n >= self.p_orig:
+                logger.warning("Phi is numerically rank deficient: its singular values come "
+                               "from the Gram spectrum (accurate to ~sqrt(eps) s_max)")
+            sv, V, lam = _gram_svd(Pd)
+            # The reference keeps LAPACK singular values above 1e-7 (at most
+            # min(n, p) of them).  Gram eigenvalues carry an absolute error of
+            # ~eps * s_max^2, so null directions surface as ~sqrt(eps) * s_max
+            # "singular values": drop eigenvalues under the Gram's own rounding
+            # floor, and never keep more than min(n, p_orig) bases.
+            floor = max(self.n, self.p_orig) * np.finfo(np.float64).eps * max(float(lam[0]), 0.0)
+            ikeep = (sv > 1e-7) & (lam > floor)
+            dropped = int(np.sum((sv > 1e-7) & ~(lam > floor)))
+            if dropped:
+                logger.warning("%d Gram directions with apparent singular value > 1e-7 lie "
+                               "under the Gram rounding floor and were dropped" % dropped)
+        ikeep &= np.arange(sv.size) < min(self.n, self.p_orig)
         self.singular_vals = sv[ikeep]
         self.V = np.ascontiguousarray(V[:, ikeep])
         self.p = int(self.singular_vals.size)

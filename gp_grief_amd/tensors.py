@@ -119,6 +119,10 @@ def _vector_out(yd, was_device):
     return dev.to_host(yd).reshape((-1, 1))
 
 
+def _is_symmetric(M):
+    return np.allclose(M, M.T, rtol=1e-12, atol=1e-14 * max(1.0, float(np.abs(M).max())))
+
+
 def device_sym_eig(factors, max_sweeps=40):
     """Eigendecomposition of symmetric factors on the device (ascending)."""
     L = native.lib()
@@ -299,23 +303,64 @@ class KronMatrix(object):
                 C[i] = np.linalg.cholesky(Ki).T
         return KronMatrix(C)
 
+    def _split_symmetric(self):
+        """Indices of the factors that are numerically symmetric (the device
+        eigensolver's domain) and the factor matrices."""
+        mats = [_as_matrix(Ki) for Ki in self.K]
+        sym = [i for i, M in enumerate(mats)
+               if M.ndim == 2 and M.shape[0] == M.shape[1] and _is_symmetric(M)]
+        return sym, mats
+
     def schur(self):
-        """(Q, T) per factor (kron_matrix.py:161-171); device Jacobi for symmetric factors."""
+        """(Q, T) per factor (kron_matrix.py:161-171): symmetric factors by the
+        device eigensolver (T diagonal), other factors by the real Schur form
+        (scipy.linalg.schur, factor-sized host LAPACK, as the reference)."""
         assert self.square
-        Q, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
-        T = [np.diag(l) for l in lam]
+        import scipy.linalg as sla
+        Q = [None] * self.n
+        T = [None] * self.n
+        todo = []
+        for i, Ki in enumerate(self.K):
+            if hasattr(Ki, "schur"):
+                T[i], Q[i] = Ki.schur()
+            else:
+                todo.append(i)
+        sym, mats = self._split_symmetric()
+        dev_idx = [i for i in todo if i in sym]
+        if dev_idx:
+            Qd, lam = device_sym_eig([mats[i] for i in dev_idx])
+            for i, q, l in zip(dev_idx, Qd, lam):
+                Q[i], T[i] = q, np.diag(l)
+        for i in todo:
+            if i not in dev_idx:
+                T[i], Q[i] = sla.schur(mats[i])
         return KronMatrix(Q), KronMatrix(T)
 
     def svd(self):
-        """(Q, eig_vals) of a PSD KronMatrix (kron_matrix.py:174-200), descending."""
+        """(Q, eig_vals) of a PSD KronMatrix (kron_matrix.py:174-200), descending:
+        symmetric factors by the device eigensolver, others by the factor-sized
+        host SVD (np.linalg.svd, as the reference)."""
         assert self.square, "matrix must be square for current implementation"
+        sym, mats = self._split_symmetric()
+        Q = [None] * self.n
+        lam = [None] * self.n
+        dev_idx = [i for i in range(self.n) if i in sym and not hasattr(self.K[i], "svd")]
         try:
-            Q, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
+            if dev_idx:
+                Qd, ld = device_sym_eig([mats[i] for i in dev_idx])
+                for i, q, l in zip(dev_idx, Qd, ld):
+                    Q[i] = np.asfortranarray(q[:, ::-1])
+                    lam[i] = l[::-1].copy()
+            for i, Ki in enumerate(self.K):
+                if i in dev_idx:
+                    continue
+                if hasattr(Ki, "svd"):
+                    Q[i], lam[i] = Ki.svd()
+                else:
+                    Q[i], lam[i] = np.linalg.svd(mats[i], full_matrices=0, compute_uv=1)[:2]
         except np.linalg.LinAlgError:
             logger.error('SVD failed on a dimension.')
             raise
-        Q = [np.asfortranarray(q[:, ::-1]) for q in Q]
-        lam = [l[::-1].copy() for l in lam]
         return KronMatrix(Q), KronMatrix(lam)
 
     def transpose(self):
@@ -415,15 +460,24 @@ class KronMatrix(object):
         return _vector_out(out, was_dev)
 
     def eig_vals(self):
-        """Eigenvalues per factor as a 1-D KronMatrix (kron_matrix.py:355-366)."""
+        """Eigenvalues per factor as a 1-D KronMatrix (kron_matrix.py:355-366):
+        symmetric factors (sym=True or numerically symmetric) by the device
+        eigensolver, others by np.linalg.eigvals on the host (factor-sized;
+        complex for a non-normal factor, as in the reference)."""
         assert self.ndim == 2
-        if not self.sym:
-            for Ki in self.K:
-                M = _as_matrix(Ki)
-                if not np.allclose(M, M.T):
-                    raise NotImplementedError("eig_vals of non-symmetric factors")
-        _, lam = device_sym_eig([_as_matrix(Ki) for Ki in self.K])
-        return KronMatrix(lam)
+        sym, mats = self._split_symmetric()
+        if self.sym:
+            sym = list(range(self.n))
+        eigs = [None] * self.n
+        dev_idx = [i for i in range(self.n) if i in sym and not hasattr(self.K[i], "eig_vals")]
+        if dev_idx:
+            _, lam = device_sym_eig([mats[i] for i in dev_idx])
+            for i, l in zip(dev_idx, lam):
+                eigs[i] = l
+        for i, Ki in enumerate(self.K):
+            if eigs[i] is None:
+                eigs[i] = Ki.eig_vals() if hasattr(Ki, "eig_vals") else np.linalg.eigvals(mats[i])
+        return KronMatrix(eigs)
 
     def find_extremum_eigs(eigs, n_eigs, mode='largest', log_expand=False, sort=True,
                            compute_global_loc=False):

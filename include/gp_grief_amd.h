@@ -254,11 +254,17 @@ int gg_potrf_work_elems(int n, int64_t* elems);
 int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet_host,
              gg_stream stream);
 /* B <- L^-1 B (which=1), L^-T B (2) or P^-1 B (3), B: n x r (cho_solve).
- * tmp_dev: 64 * r doubles.                                                   */
+ * tmp_dev: 64 * r doubles.  The chained kernels take their block rows from a
+ * ticket counter in arrival order, so progress does not depend on the order
+ * the hardware dispatches workgroups; a bounded spin turns a lost flag into
+ * GG_ERR_RUNTIME (B is then undefined).  GG_TRSV_CHAIN=0 selects the blocked
+ * GEMM substitution instead.                                                 */
 int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_dev,
              double* B_dev, int64_t ldb, int which, double* tmp_dev, gg_stream stream);
-/* X = L^-1 (lower; entries above the diagonal untouched) from gg_potrf's
- * factor and winv_dev, by recursive halving on the MFMA GEMM.  Replaces the
+/* X = L^-1 (lower) from gg_potrf's factor and winv_dev, by recursive halving
+ * on the MFMA GEMM.  The 64 x 64 diagonal blocks of X are written in full
+ * (zeros above their diagonal); X's entries above the diagonal outside those
+ * blocks are neither read nor written.  Replaces the
  * reference's cho_solve(P, I) for the adjoint gradient's diag(P^-1)
  * (gp_grief_model.py:228-235).                                               */
 int gg_trtri(int n, const double* L_dev, int64_t lda, const double* winv_dev, double* X_dev,

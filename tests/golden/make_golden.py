@@ -31,6 +31,10 @@ Fixtures:
                      setting, plus a 300 x 800 case)
   web.npz            GPwebModel / GPwebTransformedModel: the reference tests'
                      setting (test_gp_web_model.py:12-31) and a 1200 x 48 case
+  kron_nonsym.npz    KronMatrix.eig_vals / schur / svd of non-symmetric factors
+                     (kron_matrix.py:161-200, 355-366: scipy schur, numpy
+                     eigvals / svd per factor) and the SPD sym=True/False log det
+                     of test_kron_eigenvalues.py:95-102
 
 Usage:  python tests/golden/make_golden.py [--ref /root/reference]
 """
@@ -484,6 +488,36 @@ def f9_rowcol_kr(gg):
     save("rowcol_kr.npz", **out)
 
 
+def f10_kron_nonsym(gg):
+    from gp_grief.tensors import KronMatrix
+    out = {}
+    np.random.seed(3)
+    F = [np.random.rand(5, 5) + np.eye(5), np.random.rand(3, 3), np.random.rand(4, 4) - 0.5]
+    K = KronMatrix(F, sym=False)
+    eig = K.eig_vals()
+    for i, e in enumerate(eig.K):
+        out["eig%d" % i] = np.asarray(e)
+    Q, T = K.schur()
+    U, S = K.svd()
+    for i in range(3):
+        out["F%d" % i] = F[i]
+        out["schurQ%d" % i] = np.asarray(Q.K[i])
+        out["schurT%d" % i] = np.asarray(T.K[i])
+        out["svdU%d" % i] = np.asarray(U.K[i])
+        out["svdS%d" % i] = np.asarray(S.K[i])
+    # test_kron_eigenvalues.py:95-102: SPD factors, sym True / False, log det
+    for sym in (True, False):
+        np.random.seed(0)
+        A = [np.random.rand(5, 5) + np.eye(5) for _ in range(2)]
+        A = [Ai.dot(Ai.T) + 1e-6 * np.eye(5) for Ai in A]
+        KA = KronMatrix(A, sym=sym)
+        tag = "spd_sym%d" % int(sym)
+        out[tag + "_A0"], out[tag + "_A1"] = A
+        out[tag + "_logdet"] = np.float64(KA.eig_vals().log_det())
+        out[tag + "_slogdet"] = np.float64(np.linalg.slogdet(KA.expand())[1])
+    save("kron_nonsym.npz", **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -503,6 +537,7 @@ def main():
     f7_web(gg)
     f8_grid_offgrid(gg)
     f9_rowcol_kr(gg)
+    f10_kron_nonsym(gg)
 
 
 if __name__ == "__main__":

@@ -211,4 +211,6 @@ def test_fold_cg_fusion_layouts_and_deferred_x(gg, fold_small, monkeypatch, fusi
         chunks.iterate(k)
     torch.cuda.synchronize()
     assert one.status()[0] == chunks.status()[0] == 23
-    assert rel(chunks.x.cpu().numpy(), one.x.cpu().numpy()) < 1e-12
+    # a chunk boundary closes with the textbook update (true r.r for beta
+    # instead of the expansion, deferred x steps flushed): rounding-level
+    assert rel(chunks.x.cpu().numpy(), one.x.cpu().numpy()) < 1e-9

@@ -325,6 +325,11 @@ def test_grief_p_system_cg_matches_cholesky(gg, case):
     assert rel(mean_g[:, 0], z["pred_mean"]) < 1e-6
     ll = float(np.squeeze(mg.log_likelihood()))
     assert abs(ll - z["lml"]) < 1e-6 * abs(z["lml"])
+    # an LML needs chol(P) for its log det: a fresh 'cg' model solves alpha
+    # with that factor rather than running PCG beside it
+    m2 = build('cg')
+    ll2 = float(np.squeeze(m2.log_likelihood()))
+    assert m2.cg_iters == [] and abs(ll2 - z["lml"]) < 1e-6 * abs(z["lml"])
 
 
 # ------------------------------------------------ eigensolver subset path

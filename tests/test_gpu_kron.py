@@ -476,3 +476,16 @@ def test_cg_fused_odd_d_deterministic(gg, ms):
     assert all(np.array_equal(runs[0][1], r[1]) for r in runs[1:])
     xo, _, ito = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + s * v, b[:, 0], rtol=1e-10)
     assert abs(runs[0][0] - ito) <= max(3, 0.05 * ito), (runs[0][0], ito)
+
+
+@pytest.mark.parametrize("sym", [True, False])
+def test_eig_vals_log_det_reference_setting(gg, sym):
+    """test_kron_eigenvalues.py:95-102: SPD factors with sym True / False --
+    symmetric either way, so the device eigensolver -- log det of the
+    eigenvalue KronMatrix vs the reference's value and slogdet (fixture)."""
+    z = golden("kron_nonsym.npz")
+    tag = "spd_sym%d" % int(sym)
+    K = gg.tensors.KronMatrix([z[tag + "_A0"], z[tag + "_A1"]], sym=sym)
+    ld = K.eig_vals().log_det()
+    assert abs(ld - float(z[tag + "_logdet"])) < 1e-10 * abs(float(z[tag + "_logdet"]))
+    assert abs(ld - float(z[tag + "_slogdet"])) < 1e-9 * abs(float(z[tag + "_slogdet"]))

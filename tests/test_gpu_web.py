@@ -140,3 +140,37 @@ def test_web_transformed_basis_count_matches_lapack(models, case):
     ll_ref = -0.5 * (np.sum(np.log(Pd)) + np.sum(np.log(w)) + (n - m.p) * np.log(0.3)
                      + (y.dot(y) - np.sum(c2 / Pd)) / 0.3 + n * np.log(2 * np.pi))
     assert abs(float(np.squeeze(m.log_likelihood())) - ll_ref) < 1e-9 * abs(ll_ref)
+
+
+@pytest.mark.parametrize("smin", [1e-3, 1e-5, 2e-7])
+def test_web_transformed_ill_conditioned_full_rank(models, smin):
+    """A full-rank Phi with singular values from 300 down to smin (> 1e-7):
+    the reference's LAPACK SVD keeps every basis, and so does the device
+    CholeskyQR3 route -- singular values to LAPACK's accuracy, LML and
+    predictions to 1e-8 (the Gram spectrum alone dropped every
+    direction below ~1e-3 here)."""
+    import oracle
+    rng = np.random.default_rng(21)
+    n, p = 1500, 40
+    U, _ = np.linalg.qr(rng.standard_normal((n, p)))
+    Vq, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    S = np.logspace(np.log10(300.0), np.log10(smin), p)
+    Phi = (U * S).dot(Vq.T)
+    y = Phi.dot(rng.standard_normal(p)) * 1e-3 + 0.1 * rng.standard_normal(n)
+    st = oracle.web.web_transformed_setup(Phi, y)
+    m = models.GPwebTransformedModel(Phi, y, noise_var=0.3)
+    assert m.p == st["p"] == p
+    # both SVDs carry an absolute error ~ p eps s_max
+    np.testing.assert_allclose(m.singular_vals, st["sv"], rtol=1e-10, atol=1e-10)
+    params = np.concatenate([[0.3], np.linspace(0.5, 2.0, p)])
+    m.kern.parameters = params[1:]
+    ll_ref, g_ref = oracle.web.web_transformed_lml_grad(st, params)
+    assert abs(float(np.squeeze(m.log_likelihood())) - ll_ref) < 1e-8 * abs(ll_ref)
+    Pn = rng.standard_normal((7, p))
+    mean, var = m.predict(Pn)
+    mo, vo = oracle.web.web_transformed_predict(st, params, Pn)
+    # the mean divides by the singular values: singular-vector angle errors
+    # (~ p eps s_max / gap in either SVD) grow by s_max / smin
+    tol = 2e-13 * (300.0 / smin) + 1e-9
+    assert np.linalg.norm(mean - mo) < tol * np.linalg.norm(mo) + 1e-12
+    assert np.linalg.norm(var - vo) < 1e-8 * np.linalg.norm(vo)
