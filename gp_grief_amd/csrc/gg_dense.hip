@@ -425,6 +425,47 @@ __global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
                                 partial, m0, n0, blockIdx.z, gl);
 }
 
+// Split-K, XCD-grouped by K-slab: a 1-D grid of gn gm S8 workgroups (S8 = S
+// rounded up to 8); workgroup b runs on XCD b % 8 (round-robin dispatch) and
+// takes slab z = 8 (i / T) + b % 8, tile i % T (i = b / 8, T = gm gn), so all
+// tiles of one K-slab run on the same XCD, start together and read the same
+// k-rows of A and B at about the same time: each slab crosses the fabric once
+// into that XCD's L2 instead of once per XCD.
+template <int kBKg, int kNSg, int kMinWg>
+__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_xcd_kernel(
+    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
+    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
+    int kchunk, double* __restrict__ partial, int gn, int gm, int S) {
+  extern __shared__ __attribute__((aligned(16))) double gl[];
+  const int b = blockIdx.x, i = b >> 3, T = gm * gn;
+  const int z = 8 * (i / T) + (b & 7), t = i % T;
+  if (z >= S) return;
+  const int m0 = (t / gn) * kBM, n0 = (t % gn) * kBN;
+  if (uplo == 1 && n0 > m0 + kBM - 1) return;
+  if (uplo == 2 && m0 > n0 + kBN - 1) return;
+  gemm_tn_glds_tile<kBKg, kNSg>(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk,
+                                partial, m0, n0, z, gl);
+}
+
+template <int BK, int NS, int MW>
+static void launch_tn_xcd(dim3 grid, hipStream_t s, int M, int N, int K, double alpha,
+                          const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                          double* C, int64_t ldc, int uplo, int kchunk, double* part) {
+  static bool attr = false;
+  const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_xcd_kernel<BK, NS, MW>);
+  if (!attr) {
+    GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)((size_t)NS * 2 * BK * kLdT * sizeof(double))));
+    attr = true;
+  }
+  const int gn = (int)grid.x, gm = (int)grid.y, S = (int)grid.z;
+  const int64_t S8 = ceil_div(S, 8) * 8;
+  const size_t lds = (size_t)NS * 2 * BK * kLdT * sizeof(double);
+  hipLaunchKernelGGL((gemm_tn_glds_xcd_kernel<BK, NS, MW>), dim3((unsigned)(gn * gm * S8)),
+                     dim3(kGemmThreads), lds, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                     uplo, kchunk, part, gn, gm, S);
+}
+
 // Persistent, XCD-grouped variant: the grid is the resident slot count (a
 // multiple of 8); workgroup g works on XCD g % 8 (round-robin dispatch), and
 // in round r the XCD's slots take the contiguous range [r G + x S, r G +
@@ -569,12 +610,15 @@ static void launch_tn_wide(dim3 grid, hipStream_t s, int M, int N, int K, double
 }
 
 // TN-GEMM variant (A/B knob, read per call): GG_GEMM_TN=0 register-staged
-// gemm_kernel, 1..5 the LDS-DMA kernel's stage shapes.  Default 3 (BK 8,
-// 2 stages, 3 waves/SIMD): 53.0 TF on the C5 Gram (n 1e5, p 1e4) against
+// gemm_kernel, 1..5 the LDS-DMA kernel's stage shapes, 14 the same tile with
+// the XCD-slab split-K grid.  Default 14 (BK 8, 2 stages, 3 waves/SIMD, each
+// K-slab's tiles on one XCD): n = 1e5, p = 1000 3.37 -> 2.60 ms (29.7 -> 38.5
+// TF), p = 5000 47.0 -> 43.8 ms against 3 (the same tile, launch-order grid;
+// profiles/r03/n/gram_xcd_ab.jsonl); 3 was 53.0 TF on the C5 Gram against
 // 46.9 TF for the register-staged kernel (profiles/r02_g_gram_tn_variants.jsonl)
 static int gemm_tn_variant() {
   const char* e = getenv("GG_GEMM_TN");
-  return e ? atoi(e) : 3;
+  return e ? atoi(e) : 14;
 }
 
 // split-K factor gemm() chooses when the workspace is not the limit
@@ -610,7 +654,10 @@ static int tn_splitk(int M, int N, int K, int uplo) {
   const char* e = getenv("GG_GEMM_SPLITK");
   if (e != nullptr) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), cap_k));
   const int64_t cap_mem = std::max<int64_t>(1, (int64_t)1e9 / ((int64_t)M * N));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(8, std::min(cap_k, cap_mem)));
+  // the XCD-slab grid wants whole groups of 8 slabs; small Grams (few tiles)
+  // take two groups (p = 1000: 38.5 TF at 16 and 32 slabs, 29.5 at 8)
+  const int64_t want = (int64_t)M * N <= (int64_t)2000 * 2000 ? 16 : 8;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, std::min(cap_k, cap_mem)));
 }
 
 // the split gemm() will use for this call (given an unlimited workspace)
@@ -652,6 +699,11 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
       case 12: launch_tn_wide<8, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
       case 13: launch_tn_wide<8, 4>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
       case 7: launch_tn_pers<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
+      case 14:
+        // unsplit products keep the launch-order grid (one slab: nothing to group)
+        if (grid.z > 1) launch_tn_xcd<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
+        else launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
+        break;
       default: launch_tn<8, 4, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
     }
     GG_LAUNCH_CHECK();

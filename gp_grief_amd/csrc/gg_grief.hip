@@ -7,7 +7,7 @@
 //   log     = sum_f log|X_f|[inv_f]
 //   Phi     = sign^T * exp(log^T - 0.5 log_lam)                    (n x p)
 // Two kernels:
-//   grief_tables_kernel: one thread per data point computes the m_f kernel
+//   grief_tables_kernel: a lane quad per data point computes the m_f kernel
 //     values on the fly (never storing Kux) and contracts them with the u_f
 //     selected eigenvector rows; writes log|X| and sign(X) as an n x U table
 //     (U = sum_f u_f), i.e. exactly the reference's x_unique, per point.
@@ -70,30 +70,55 @@ __global__ __launch_bounds__(256) void cov_kernel(int kind, double var, double l
 }
 
 constexpr int kUG = 16;  // selected eigenvector rows per thread
+constexpr int kTQ = 4;   // lanes per data point: each takes every kTQ-th grid point
 
 // For dim f: X[u][a] = sum_k Qsel[u][k] * k_f(xg[k], x[a]) for u in a group of
 // kUG rows; writes table L[a][col0+u] = log|X| (X == 0 -> 0), S = sign(X).
+// A lane quad owns a data point: lane q evaluates the kernel at grid points
+// k = q, q + 4, ... (m / 4 exps, independent chains), the quad's partial sums
+// are combined by two xor-shuffles, and lane q stores the rows t = q mod 4.
+// The group's Qsel rows (kUG x m) are staged in LDS once per block.
+// kLds = false (m > 512): the rows are read from global memory instead.
+template <bool kLds>
 __global__ __launch_bounds__(256) void grief_tables_kernel(
     int kind, double var, double ls, const double* __restrict__ x, int64_t x_stride,
     int64_t n, const double* __restrict__ xg, int m, const double* __restrict__ Qsel, int u,
     double* __restrict__ Ltab, double* __restrict__ Stab, int U, int col0) {
-  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  extern __shared__ double qlds[];   // kUG x m
   const int ug = blockIdx.y * kUG;
-  if (a >= n) return;
-  const double xa = x[a * x_stride];
+  const int nu = min(kUG, u - ug);
+  if (kLds) {
+    for (int e = threadIdx.x; e < kUG * m; e += blockDim.x) {
+      const int t = e / m;
+      qlds[e] = t < nu ? Qsel[(int64_t)(ug + t) * m + (e - t * m)] : 0.0;
+    }
+    __syncthreads();
+  }
+  // rows past u read row ug (any finite value: never stored)
+  const double* qs = kLds ? qlds : Qsel + (int64_t)ug * m;
+  const int tmax = kLds ? kUG : nu;
+  const int64_t a = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kTQ;
+  const int q = threadIdx.x % kTQ;
+  const bool live = a < n;
+  const double xa = live ? x[a * x_stride] : 0.0;
   double acc[kUG];
 #pragma unroll
   for (int t = 0; t < kUG; ++t) acc[t] = 0.0;
-  for (int k = 0; k < m; ++k) {
+  for (int k = q; k < m; k += kTQ) {
     const double d = xg[k] - xa;
     const double kv = stationary(kind, d * d, var, ls);
 #pragma unroll
-    for (int t = 0; t < kUG; ++t)
-      if (ug + t < u) acc[t] = fma(Qsel[(int64_t)(ug + t) * m + k], kv, acc[t]);
+    for (int t = 0; t < kUG; ++t) acc[t] = fma(qs[(t < tmax ? t : 0) * m + k], kv, acc[t]);
   }
 #pragma unroll
   for (int t = 0; t < kUG; ++t) {
-    if (ug + t < u) {
+    acc[t] += __shfl_xor(acc[t], 1, 64);
+    acc[t] += __shfl_xor(acc[t], 2, 64);
+  }
+  if (!live) return;
+#pragma unroll
+  for (int t = 0; t < kUG; ++t) {
+    if (t % kTQ == q && t < nu) {
       const double v = acc[t];
       const int64_t o = a * U + col0 + ug + t;
       Stab[o] = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
@@ -260,8 +285,11 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
     GG_REQUIRE(m >= 1 && u >= 1 && col0 >= 0 && col0 + u <= U && n >= 0, GG_ERR_VALUE,
                "bad table geometry");
     if (n == 0) return;
-    dim3 grid((unsigned)gg::ceil_div(n, 256), (unsigned)gg::ceil_div(u, gg::kUG));
-    hipLaunchKernelGGL(gg::grief_tables_kernel, grid, dim3(256), 0, gg::as_stream(stream),
+    const bool in_lds = m <= 512;   // the kUG x m rows in at most 64 KiB of LDS
+    const size_t lds = in_lds ? (size_t)gg::kUG * m * sizeof(double) : 0;
+    dim3 grid((unsigned)gg::ceil_div(n * gg::kTQ, 256), (unsigned)gg::ceil_div(u, gg::kUG));
+    hipLaunchKernelGGL(in_lds ? gg::grief_tables_kernel<true> : gg::grief_tables_kernel<false>,
+                       grid, dim3(256), lds, gg::as_stream(stream),
                        kind, variance, lengthscale, x_dev, x_stride, n, xg_dev, m, qsel_dev, u,
                        ltab_dev, stab_dev, U, col0);
     GG_LAUNCH_CHECK();

@@ -116,7 +116,8 @@ def test_gemm_tn_splitk(gg, monkeypatch, S, uplo):
 
 
 def test_gemm_tn_splitk_model(gg):
-    """The Gram (K = n >> p) is split 8-way over K (gg_dense.hip tn_splitk);
+    """The Gram (K = n >> p) is split 8-way over K, 16-way up to p = 2000
+    (gg_dense.hip tn_splitk, whole groups of 8 slabs for the XCD-slab grid);
     a small-K product is not split."""
     import ctypes
     from gp_grief_amd import native
@@ -124,6 +125,9 @@ def test_gemm_tn_splitk_model(gg):
     native.check(native.lib().gg_gemm_workspace_elems(1, 0, 5000, 5000, 100000, 1,
                                                       ctypes.byref(need)))
     assert need.value == 8 * 5000 * 5000
+    native.check(native.lib().gg_gemm_workspace_elems(1, 0, 1000, 1000, 100000, 1,
+                                                      ctypes.byref(need)))
+    assert need.value == 16 * 1000 * 1000
     native.check(native.lib().gg_gemm_workspace_elems(1, 0, 5000, 5000, 256, 1,
                                                       ctypes.byref(need)))
     assert need.value == 0
