@@ -514,6 +514,11 @@ __global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restri
   }
 }
 
+// Dynamic LDS the next TN launches of this host thread reserve at least
+// (0: the kernel's own need; gg_potrf's GG_POTRF_WIDE_LDS A/B knob).
+static thread_local size_t g_tn_min_lds = 0;
+constexpr size_t kTnMaxLds = 64 * 1024;
+
 template <int BK, int NS, int MW>
 static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alpha, const double* A,
                       int64_t lda, const double* B, int64_t ldb, double beta, double* C,
@@ -522,10 +527,10 @@ static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alph
   const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_kernel<BK, NS, MW>);
   if (!attr) {
     GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)tn_glds_lds<BK, NS>()));
+                               (int)std::max(tn_glds_lds<BK, NS>(), kTnMaxLds)));
     attr = true;
   }
-  const size_t lds = tn_glds_lds<BK, NS>();
+  const size_t lds = std::max(tn_glds_lds<BK, NS>(), std::min(g_tn_min_lds, kTnMaxLds));
   hipLaunchKernelGGL((gemm_tn_glds_kernel<BK, NS, MW>), grid, dim3(kGemmThreads), lds, s, M, N,
                      K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
 }
@@ -807,7 +812,8 @@ constexpr int kNB = 64;
 // Streams of the calling device for gg_potrf's look-ahead (created once per
 // device, never destroyed: they live as long as the process).  which 0: the
 // factorisation chain (the critical path) at the highest priority; 1: the
-// wide trailing updates at the lowest.
+// wide trailing updates at the lowest; 2: the in-panel updates beside the
+// chain (highest).
 hipStream_t aux_stream(int which) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, hipStream_t> streams;
@@ -819,7 +825,7 @@ hipStream_t aux_stream(int which) {
   int least = 0, greatest = 0;
   GG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t st;
-  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 0 ? greatest : least));
+  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 1 ? least : greatest));
   streams[{dev, which}] = st;
   return st;
 }
@@ -864,7 +870,17 @@ __device__ __forceinline__ double quad_sum(double v) {
 __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
                                                            int n, int k0, int nb, int P0,
                                                            int* __restrict__ status,
-                                                           int* __restrict__ arrived) {
+                                                           int* __restrict__ arrived,
+                                                           long long* __restrict__ stamps) {
+  // optional phase timing (GG_POTRF_PROF): wave 0 of every workgroup writes
+  // the 100 MHz clock at the phase boundaries (lane-varying slots keep these
+  // vector stores)
+  auto stamp = [&](int k) {
+    if (stamps != nullptr && threadIdx.x < 64)
+      stamps[(((int64_t)(k0 / kNB) * 160 + blockIdx.x) * 4 + k) * 64 + threadIdx.x] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   __shared__ double Lf[kNB][kNB + 1];
   __shared__ double Lb[kNB][kNB + 1];   // panel rows of the block / its update
   __shared__ double Lr[kNB][kNB + 1];   // panel rows of this workgroup's rows / their update
@@ -920,6 +936,7 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
       }
     __syncthreads();
   }
+  stamp(1);
   double d[16];
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
@@ -957,6 +974,7 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
   }
   __syncthreads();
   if (tid < kNB) invd[tid] = 1.0 / Lf[tid][tid];
+  stamp(2);
   // The block is factored in place: the LAST workgroup to have read it (every
   // workgroup holds the same L_bb) stores L_bb and W, so no workgroup can
   // read a half-written block.  No waiting: the counter only picks the writer.
@@ -1005,6 +1023,439 @@ __global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A
     const int j = q + 4 * u;
     if (j < nb) Ar[j] = x[u];
   }
+  stamp(3);
+}
+
+// ---- Cholesky block step, round 3 (potrf_fac_kernel + potrf_upd_kernel).
+// The round-2 block kernel spent ~27 us of its ~40-75 us factoring the 64 x 64
+// diagonal block (two barriers and a correctly rounded sqrt + divide per
+// column), ~9 us in a column-at-a-time TRSM and ~12 us per in-panel update
+// chunk (GG_POTRF_PROF stamps, profiles/r03/p_potrf_prof.jsonl).  Here the
+// factor and the TRSM proceed four columns at a time and the in-panel
+// updates are a separate right-looking MFMA launch (potrf_upd_kernel).
+
+// LDS row stride of 64-wide blocks read four doubles at a time: 68 doubles
+// keeps rows 16-byte aligned and puts rows 4u + q (q < 4) on disjoint banks.
+constexpr int kLdf = 68;
+// row stride of the MFMA operand tiles (64 x 64, column reads by 16 lanes)
+constexpr int kLdu = kNB + 1;
+
+// 1/sqrt(t): v_rsq_f64 plus one second-order Newton-Raphson correction,
+// r = r0 (1 + h/2 + 3h^2/8), h = 1 - t r0^2 (error ~ h^3: full precision).
+__device__ __forceinline__ double rsq_refined(double t) {
+  const double r0 = __builtin_amdgcn_rsq(t);
+  const double h = fma(-(t * r0), r0, 1.0);
+  return fma(r0 * h, fma(0.375, h, 0.5), r0);
+}
+
+// v[q] for q < 4 as three independent selects (a nested ?: chain on q
+// becomes a divergent switch)
+__device__ __forceinline__ double pick4(int q, double v0, double v1, double v2, double v3) {
+  double r = v0;
+  r = q == 1 ? v1 : r;
+  r = q == 2 ? v2 : r;
+  r = q == 3 ? v3 : r;
+  return r;
+}
+
+__device__ __forceinline__ double2 lds_ld2(const double* p) {
+  return *reinterpret_cast<const double2*>(p);
+}
+
+// Fused diagonal-block factor + panel TRSM of one 64-column block (k0, nb):
+//   L_bb = chol(A[k0:k0+nb, k0:k0+nb])           (every workgroup, registers)
+//   L[rows, k0:k0+nb] = A[rows, k0:k0+nb] L_bb^-T  (workgroup b: 64 rows
+//                                                   k0 + nb + 64 b ...)
+// Column block k0 is fully updated on entry (potrf_upd_kernel / the narrow
+// update did it).  Thread t owns row i = t / 4 and columns 4u + q (q = t & 3,
+// u < 16) of the block.  Factor: super-step s handles columns 4s..4s+3 with
+// ONE barrier: every thread factors the 4 x 4 pivot block itself (rsq
+// pivots), forms the L values of its own row and of row 4(s+1) + q, updates
+// its entry of the next column block (written to the pan buffer for step
+// s + 1), and applies the previous super-step's rank-4 term to the rest of
+// its row (Lp buffer, double-buffered).  TRSM: the four unknowns of a
+// super-step are gathered within the lane quad by DPP and solved by every
+// quad lane, then the rank-4 term updates the later columns -- no barriers.
+// Rows >= pend (below the panel) are also stored transposed into LT
+// (LT[c - P0][row - pend]) for the narrow / wide TN updates.  The last
+// workgroup to arrive stores L_bb (the block is factored in place).
+__global__ __launch_bounds__(256) void potrf_fac_kernel(double* __restrict__ A, int64_t lda,
+                                                        int n, int k0, int nb, int P0, int pend,
+                                                        int kp,
+                                                        double* __restrict__ LT, int64_t ldt,
+                                                        int* __restrict__ status,
+                                                        int* __restrict__ arrived,
+                                                        long long* __restrict__ stamps) {
+  auto stamp = [&](int k) {
+    if (stamps != nullptr && threadIdx.x < 64)
+      stamps[(((int64_t)(k0 / kNB) * 160 + blockIdx.x) * 4 + k) * 64 + threadIdx.x] =
+          __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  __shared__ __attribute__((aligned(16))) double Lf[kNB][kLdf];
+  __shared__ __attribute__((aligned(16))) double pan[2][kNB][4];
+  __shared__ __attribute__((aligned(16))) double Lp[2][kNB][4];
+  __shared__ __attribute__((aligned(16))) double invd[kNB];
+  __shared__ double term_lds[2 * kNB][kLdu];   // the fused term's operands / products
+  __shared__ int last;
+  const int tid = threadIdx.x;
+  const int i = tid >> 2, q = tid & 3;
+  double* Abb = A + (int64_t)k0 * lda + k0;
+  const int64_t row = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB + i;   // TRSM row
+  const bool has_row = row < n;
+  // the TRSM rows first (their latency hides under the factor), then D; the
+  // rows wait in this thread's own slots of Lf (the slots its L entries take
+  // after the factor), not in registers
+  // (unconditional loads from clamped addresses, then selects: guarded loads
+  // become exec-mask branches whose saved masks spill)
+  double x[16], d[16];
+  {
+    const double* xr = A + (has_row ? row : (int64_t)k0) * lda + k0;
+    const double* dr = Abb + (int64_t)min(i, nb - 1) * lda;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = 4 * u + q, jc = min(j, nb - 1);
+      x[u] = xr[jc];
+      d[u] = dr[jc];
+    }
+  }
+  if (kp >= 0) {
+    // the newest in-panel term (column block kp = k0 - 64, finished by the
+    // previous block step) on MFMA: D -= L_k L_k^T, R -= L_r L_k^T with
+    // L_k = L[k0:k0+64, kp:kp+64], L_r = L[rows, kp:kp+64] (potrf_upd_kernel
+    // gave the panel's later column blocks the older terms)
+    double(*Tk)[kLdu] = reinterpret_cast<double(*)[kLdu]>(&term_lds[0][0]);
+    double(*Tr)[kLdu] = reinterpret_cast<double(*)[kLdu]>(&term_lds[kNB][0]);
+    const int lane = tid & 63, wave = tid >> 6;
+    const int64_t rb0 = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB;
+    for (int e = tid; e < kNB * kNB; e += 256) {
+      const int r = e >> 6, c = e & 63;
+      Tk[r][c] = A[(int64_t)(k0 + min(r, nb - 1)) * lda + kp + c];
+      Tr[r][c] = A[min(rb0 + r, (int64_t)n - 1) * lda + kp + c];
+    }
+    __syncthreads();
+    d4 dacc[4], racc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      dacc[t] = d4{0.0, 0.0, 0.0, 0.0};
+      racc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+#pragma unroll
+    for (int ks = 0; ks < kNB / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double ad = Tk[16 * wave + (lane & 15)][kk];
+      const double ar = Tr[16 * wave + (lane & 15)][kk];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double bv = Tk[16 * t + (lane & 15)][kk];
+        if (t <= wave) dacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ad, bv, dacc[t], 0, 0, 0);
+        racc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv, racc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    // MFMA result layout: row 4 r + (lane >> 4), column lane & 15 of tile t
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Tk[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = dacc[t][r];
+        Tr[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = racc[t][r];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      d[u] -= Tk[i][4 * u + q];
+      x[u] -= Tr[i][4 * u + q];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = 4 * u + q;
+    x[u] = (has_row && j < nb) ? x[u] : 0.0;
+    d[u] = (i < nb && j <= i) ? d[u] : (i == j ? 1.0 : 0.0);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) Lf[i][4 * u + q] = x[u];
+  stamp(1);
+  pan[0][i][q] = d[0];
+  // pivot check kept in two registers (a per-pivot boolean would be a lane
+  // mask per column, spilled): the smallest pivot, and NaN if any was not finite
+  double pivmin = 1.0, pivnan = 0.0;
+  double lo[4] = {0.0, 0.0, 0.0, 0.0};   // own row's L of the previous super-step
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int cb = s & 1, nx = cb ^ 1;
+    // ---- the 4 x 4 pivot block (rows 4s..4s+3 of column block s), factored
+    // by every thread
+    double p[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const double2 v0 = lds_ld2(&pan[cb][4 * s + a][0]), v1 = lds_ld2(&pan[cb][4 * s + a][2]);
+      p[a][0] = v0.x;
+      p[a][1] = v0.y;
+      p[a][2] = v1.x;
+      p[a][3] = v1.y;
+    }
+    double l[4][4], iv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      double t = p[c][c];
+#pragma unroll
+      for (int e = 0; e < c; ++e) t = fma(-l[c][e], l[c][e], t);
+      pivmin = t < pivmin ? t : pivmin;
+      pivnan += t * 0.0;
+      // materialise the running check here: sunk to its use after the loop,
+      // it would keep all 64 pivots live across the factor
+      asm volatile("" : "+v"(pivmin), "+v"(pivnan));
+      const double r = rsq_refined(t);
+      iv[c] = r;
+      l[c][c] = t * r;
+#pragma unroll
+      for (int a = c + 1; a < 4; ++a) {
+        double v = p[a][c];
+#pragma unroll
+        for (int e = 0; e < c; ++e) v = fma(-l[a][e], l[c][e], v);
+        l[a][c] = v * r;
+      }
+    }
+    if (tid == 0) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) invd[4 * s + c] = iv[c];
+    }
+    // ---- L of a row from its four column-block-s entries (rows >= 4s + 4)
+    auto row_l = [&](const double (&rv)[4], double (&lv)[4]) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double v = rv[c];
+#pragma unroll
+        for (int e = 0; e < c; ++e) v = fma(-lv[e], l[c][e], v);
+        lv[c] = v * iv[c];
+      }
+    };
+    // own row i: rows inside the pivot block take its factor, rows above it
+    // are zero in this column block
+    double ro[4], lc[4];
+    {
+      const double2 v0 = lds_ld2(&pan[cb][i][0]), v1 = lds_ld2(&pan[cb][i][2]);
+      ro[0] = v0.x;
+      ro[1] = v0.y;
+      ro[2] = v1.x;
+      ro[3] = v1.y;
+    }
+    row_l(ro, lc);
+    const int rel = i - 4 * s;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lc[c] = rel >= c ? lc[c] : 0.0;
+    // this thread's entry of column 4s + q is final
+    d[s] = pick4(q, lc[0], lc[1], lc[2], lc[3]);
+    Lp[cb][i][0] = lc[0];
+    Lp[cb][i][1] = lc[1];
+    Lp[cb][i][2] = lc[2];
+    Lp[cb][i][3] = lc[3];
+    if (s < 15) {
+      // row j = 4(s+1) + q: the column this thread owns in block s + 1
+      const int j = 4 * (s + 1) + q;
+      double rj[4], lj[4];
+      {
+        const double2 v0 = lds_ld2(&pan[cb][j][0]), v1 = lds_ld2(&pan[cb][j][2]);
+        rj[0] = v0.x;
+        rj[1] = v0.y;
+        rj[2] = v1.x;
+        rj[3] = v1.y;
+      }
+      row_l(rj, lj);
+      double t = d[s + 1];
+      if (s > 0) {   // term s - 1 on column block s + 1 (its bulk was deferred)
+        const double2 w0 = lds_ld2(&Lp[nx][j][0]), w1 = lds_ld2(&Lp[nx][j][2]);
+        t = fma(-lo[0], w0.x, t);
+        t = fma(-lo[1], w0.y, t);
+        t = fma(-lo[2], w1.x, t);
+        t = fma(-lo[3], w1.y, t);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t = fma(-lc[c], lj[c], t);
+      d[s + 1] = t;
+      pan[nx][i][q] = t;
+      // term s - 1 on column blocks s + 2.. (rows 4u + q of the Lp buffer)
+      if (s > 0) {
+#pragma unroll
+        for (int u = s + 2; u < 16; ++u) {
+          const double2 w0 = lds_ld2(&Lp[nx][4 * u + q][0]), w1 = lds_ld2(&Lp[nx][4 * u + q][2]);
+          double v = d[u];
+          v = fma(-lo[0], w0.x, v);
+          v = fma(-lo[1], w0.y, v);
+          v = fma(-lo[2], w1.x, v);
+          v = fma(-lo[3], w1.y, v);
+          d[u] = v;
+          if ((u & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) lo[c] = lc[c];
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int j = 4 * u + q;
+    x[u] = Lf[i][j];
+    Lf[i][j] = (j <= i) ? d[u] : 0.0;
+  }
+  stamp(2);
+  // The block is factored in place: the LAST workgroup to have read it (every
+  // workgroup holds the same L_bb) stores it, so no workgroup can read a
+  // half-written block.  No waiting: the counter only picks the writer.
+  if (tid == 0) last = atomicAdd(arrived, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (last) {
+    if (tid == 0 && !(pivmin > 0.0 && pivnan == 0.0)) *status = 1;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = 4 * u + q;
+      if (i < nb && j <= i) Abb[(int64_t)i * lda + j] = d[u];
+    }
+  }
+  if (!has_row) return;
+  // ---- TRSM of this workgroup's row: x L_bb^T = r, four columns at a time
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    double lb[4][4];
+#pragma unroll
+    for (int a = 1; a < 4; ++a) {
+      const double2 v0 = lds_ld2(&Lf[4 * s + a][4 * s]), v1 = lds_ld2(&Lf[4 * s + a][4 * s + 2]);
+      lb[a][0] = v0.x;
+      lb[a][1] = v0.y;
+      lb[a][2] = v1.x;
+      lb[a][3] = v1.y;
+    }
+    const double2 i01 = lds_ld2(&invd[4 * s]), i23 = lds_ld2(&invd[4 * s + 2]);
+    const double v0 = quad_bcast<0>(x[s]), v1 = quad_bcast<1>(x[s]);
+    const double v2 = quad_bcast<2>(x[s]), v3 = quad_bcast<3>(x[s]);
+    const double y0 = v0 * i01.x;
+    const double y1 = fma(-y0, lb[1][0], v1) * i01.y;
+    const double y2 = fma(-y1, lb[2][1], fma(-y0, lb[2][0], v2)) * i23.x;
+    const double y3 = fma(-y2, lb[3][2], fma(-y1, lb[3][1], fma(-y0, lb[3][0], v3))) * i23.y;
+    x[s] = pick4(q, y0, y1, y2, y3);
+#pragma unroll
+    for (int u = s + 1; u < 16; ++u) {
+      const double2 w0 = lds_ld2(&Lf[4 * u + q][4 * s]), w1 = lds_ld2(&Lf[4 * u + q][4 * s + 2]);
+      double v = x[u];
+      v = fma(-y0, w0.x, v);
+      v = fma(-y1, w0.y, v);
+      v = fma(-y2, w1.x, v);
+      v = fma(-y3, w1.y, v);
+      x[u] = v;
+      if ((u & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+    // keep the scheduler from hoisting every super-step's Lf loads (they do
+    // not depend on x) to the top: that spills
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  double* Ar = A + row * lda + k0;
+  double* Lt = (LT != nullptr && row >= pend) ? LT + (int64_t)(k0 - P0 + q) * ldt + (row - pend)
+                                              : nullptr;
+  if (nb == kNB) {   // (uniform) full block: unguarded stores
+#pragma unroll
+    for (int u = 0; u < 16; ++u) Ar[4 * u + q] = x[u];
+    if (Lt != nullptr) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) Lt[(int64_t)(4 * u) * ldt] = x[u];
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = 4 * u + q;
+      if (j < nb) Ar[j] = x[u];
+      if (Lt != nullptr && j < nb) Lt[(int64_t)(4 * u) * ldt] = x[u];
+    }
+  }
+  stamp(3);
+}
+
+// Right-looking update of 64 x 64 blocks by one or more finished 64-column
+// blocks: A[r, c] -= L[r, ka:kb] L[c, ka:kb]^T for the column blocks c of
+// [c0, c1) and the row blocks r >= c (lower), L read from A itself.  One
+// workgroup per (row block, column block): the in-panel update after each
+// block step (kb - ka = 64, the panel's later column blocks) and the narrow
+// look-ahead update of the next panel (kb - ka = the panel width).  Wave w
+// owns rows 16w..16w+15 of the tile (4 MFMA column tiles).
+// Diagonal tiles store only their lower triangle.  kPf: the next chunk's
+// operands are prefetched into registers while the current one is
+// multiplied; without it (the default) they are loaded per chunk and the
+// kernel fits three workgroups per CU.
+template <bool kPf>
+__global__ __launch_bounds__(256, 3) void potrf_upd_kernel(double* __restrict__ A, int64_t lda,
+                                                        int n, int ka, int kb, int c0, int c1) {
+  // K in chunks of 32: two 64 x 33 operand tiles (33 KB) fit three
+  // workgroups per CU
+  constexpr int kKc = 32;
+  __shared__ double Lr[kNB][kKc + 1];
+  __shared__ double Lc[kNB][kKc + 1];
+  const int r0 = c0 + (int)blockIdx.x * kNB, cc0 = c0 + (int)blockIdx.y * kNB;
+  if (r0 < cc0) return;   // above the diagonal
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  d4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  // staging: thread t loads rows (t >> 3) + 32 m, columns 4 (t & 7) .. +3
+  const int sr = tid >> 3, sc = 4 * (tid & 7);
+  double2 vr[2][2], vc[2][2];
+  auto fetch = [&](int kc) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int rr = sr + 32 * m;
+      const int64_t gr = min((int64_t)r0 + rr, (int64_t)n - 1), gc = min(cc0 + rr, n - 1);
+      const double* pr = A + gr * lda + kc + sc;
+      const double* pc = A + gc * lda + kc + sc;
+      vr[m][0] = *reinterpret_cast<const double2*>(pr);
+      vr[m][1] = *reinterpret_cast<const double2*>(pr + 2);
+      vc[m][0] = *reinterpret_cast<const double2*>(pc);
+      vc[m][1] = *reinterpret_cast<const double2*>(pc + 2);
+    }
+  };
+  if (kPf) fetch(ka);
+  for (int kc = ka; kc < kb; kc += kKc) {
+    if (!kPf) fetch(kc);
+    __syncthreads();   // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int rr = sr + 32 * m;
+      Lr[rr][sc] = vr[m][0].x;
+      Lr[rr][sc + 1] = vr[m][0].y;
+      Lr[rr][sc + 2] = vr[m][1].x;
+      Lr[rr][sc + 3] = vr[m][1].y;
+      Lc[rr][sc] = vc[m][0].x;
+      Lc[rr][sc + 1] = vc[m][0].y;
+      Lc[rr][sc + 2] = vc[m][1].x;
+      Lc[rr][sc + 3] = vc[m][1].y;
+    }
+    __syncthreads();
+    if (kPf && kc + kKc < kb) fetch(kc + kKc);
+#pragma unroll
+    for (int ks = 0; ks < kKc / 4; ++ks) {
+      const int kk = 4 * ks + (lane >> 4);
+      const double a = Lr[16 * wave + (lane & 15)][kk];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, Lc[16 * t + (lane & 15)][kk], acc[t], 0,
+                                                      0, 0);
+    }
+  }
+  // MFMA result layout: row 4 r + (lane >> 4), column lane & 15 of tile t
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = 16 * wave + 4 * r + (lane >> 4), cc = 16 * t + (lane & 15);
+      const int64_t gr = (int64_t)r0 + rr;
+      const int gc = cc0 + cc;
+      if (gr < n && gc < c1 && (r0 != cc0 || rr >= cc)) {
+        double* pa = A + gr * lda + gc;
+        *pa -= acc[t][r];
+      }
+    }
 }
 
 // W_b = L_bb^-1 for every 64-column diagonal block (gg_potrs's diagonal
@@ -1482,12 +1933,20 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     // flops, one K = kPanel MFMA GEMM) runs beside it and yields CUs to the
     // chain.  Ordering: wide(P) waits for panel P's factor; narrow(P -> P + 1)
     // waits for wide(P - 1), which wrote the same columns; s joins both.
-    constexpr int kPanel = 4 * gg::kNB;
+    // Panel width: 512 columns from n = 4096 (the wide update's K = 512 halves
+    // its read-modify-write passes over the trailing matrix: p = 10^4 13.4 ->
+    // 12.9 ms, p = 5000 4.09 -> 3.95), else 256 (p = 1000: 0.74 vs 0.89 ms;
+    // profiles/r03/w_potrf_ab.jsonl).  GG_POTRF_PANEL=<columns> (multiple of
+    // 64) for A/B.
+    const char* pe = getenv("GG_POTRF_PANEL");
+    const int kPanel = pe ? std::max(gg::kNB, (atoi(pe) / gg::kNB) * gg::kNB)
+                          : (n >= 4096 ? 8 : 4) * gg::kNB;
     // GG_POTRF_LOOKAHEAD=0: everything on s (A/B and debugging)
     const char* la = getenv("GG_POTRF_LOOKAHEAD");
     const bool lookahead = !(la != nullptr && atoi(la) == 0);
     hipStream_t cs = lookahead ? gg::aux_stream(0) : s;   // factor chain, high priority
     hipStream_t ws = lookahead ? gg::aux_stream(1) : s;   // wide updates, low priority
+    hipStream_t us = lookahead ? gg::aux_stream(2) : s;   // in-panel updates, high priority
     std::vector<hipEvent_t> evs;
     auto new_event = [&]() {
       hipEvent_t e;
@@ -1501,6 +1960,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipEventRecord(e0, s));
       GG_HIP(hipStreamWaitEvent(cs, e0, 0));
       GG_HIP(hipStreamWaitEvent(ws, e0, 0));
+      GG_HIP(hipStreamWaitEvent(us, e0, 0));
     }
     // two transposed-panel buffers (kPanel x ldt each), stream-ordered
     const int64_t ldt = (n + 1) & ~1;   // even: 16-byte aligned rows for the DMA
@@ -1512,7 +1972,108 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipStreamWaitEvent(cs, ea, 0));
       GG_HIP(hipStreamWaitEvent(ws, ea, 0));
     }
-    for (int P0 = 0; P0 < n; P0 += kPanel) {
+    // GG_POTRF_PROF=<file>: per-block-launch phase stamps of every workgroup
+    // (raw int64: nblk, 160, 4, then [nblk][160][4] 100 MHz ticks; 0 = absent)
+    const char* prof = getenv("GG_POTRF_PROF");
+    long long* pstamps = nullptr;
+    const size_t nstamp = (size_t)nblk * 160 * 4 * 64;
+    if (prof != nullptr && nblk <= 160) {
+      GG_HIP(hipMallocAsync(&pstamps, nstamp * sizeof(long long), s));
+      GG_HIP(hipMemsetAsync(pstamps, 0, nstamp * sizeof(long long), s));
+      if (lookahead) {
+        hipEvent_t ep = new_event();
+        GG_HIP(hipEventRecord(ep, s));
+        GG_HIP(hipStreamWaitEvent(cs, ep, 0));
+      }
+    }
+    // GG_POTRF_V1=1: the round-2 block step (left-looking in-panel update and
+    // column-at-a-time factor inside the block launch, transpose + MFMA GEMM
+    // narrow update) for A/B
+    const char* v1e = getenv("GG_POTRF_V1");
+    const bool v1 = v1e != nullptr && atoi(v1e) != 0;
+    const char* fue = getenv("GG_POTRF_FUSE");
+    const bool fuse = fue != nullptr && atoi(fue) != 0;
+    // GG_POTRF_WIDE_LDS=<bytes>: pad the wide update's workgroups (A/B: at 56 KB
+    // two share a CU and a block step fits beside them; measured no faster,
+    // the block steps slow down beside FP64 MFMA waves -- unpadded by default)
+    const char* wl = getenv("GG_POTRF_WIDE_LDS");
+    const size_t wide_lds = (lookahead && wl) ? (size_t)atol(wl) : 0;
+    for (int P0 = 0; P0 < n && !v1; P0 += kPanel) {
+      const int pend = std::min(n, P0 + kPanel);
+      double* LT = (lt_buf && pend < n) ? lt_buf + (int64_t)((P0 / kPanel) & 1) * kPanel * ldt
+                                        : nullptr;
+      // Block step k: F(k) factors column block k and solves the rows below
+      // it; U(k) gives the panel's later column blocks the term of block k.
+      // GG_POTRF_FUSE=1 (A/B): F(k) applies the newest term (block k - 1) to its
+      // own column block itself and U(k) covers blocks k + 2.. on the side
+      // stream us, beside F(k + 1) (F(k + 2) waits for it) -- measured slower:
+      // the fused MFMA term costs the block step ~8 us, about the U launch it
+      // replaces (profiles/r03/v_potrf_fused.txt).
+      std::vector<hipEvent_t> ev_u((size_t)gg::ceil_div(pend - P0, gg::kNB), nullptr);
+      for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
+        const int b = k0 / gg::kNB, bi = (k0 - P0) / gg::kNB;
+        const int nb = std::min(gg::kNB, n - k0);
+        const int grid = std::max(1, (int)gg::ceil_div(n - k0 - nb, gg::kNB));
+        if (fuse && bi >= 2 && ev_u[bi - 2] != nullptr)
+          GG_HIP(hipStreamWaitEvent(cs, ev_u[bi - 2], 0));
+        hipLaunchKernelGGL(gg::potrf_fac_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n, k0,
+                           nb, P0, pend, (fuse && bi >= 1) ? k0 - gg::kNB : -1, LT, ldt, status,
+                           arrived + b, pstamps);
+        GG_LAUNCH_CHECK();
+        const int c0 = k0 + (fuse ? 2 : 1) * gg::kNB;
+        if (c0 < pend) {
+          hipStream_t u = fuse ? us : cs;
+          if (u != cs) {
+            hipEvent_t ef = new_event();
+            GG_HIP(hipEventRecord(ef, cs));
+            GG_HIP(hipStreamWaitEvent(u, ef, 0));
+          }
+          dim3 ug((unsigned)gg::ceil_div(n - c0, gg::kNB), (unsigned)gg::ceil_div(pend - c0, gg::kNB));
+          hipLaunchKernelGGL(gg::potrf_upd_kernel<false>, ug, dim3(256), 0, u, A_dev, lda, n, k0,
+                             k0 + gg::kNB, c0, pend);
+          GG_LAUNCH_CHECK();
+          if (u != cs) {
+            ev_u[bi] = new_event();
+            GG_HIP(hipEventRecord(ev_u[bi], u));
+          }
+        }
+      }
+      if (pend >= n) break;
+      const int nend = std::min(n, pend + kPanel);
+      // the wide update may start as soon as LT (written by the block steps) is
+      // complete
+      hipEvent_t ef = nullptr;
+      if (lookahead && nend < n) {
+        ef = new_event();
+        GG_HIP(hipEventRecord(ef, cs));
+      }
+      // narrow: A[pend:, pend:nend] -= L[pend:, P] L[pend:nend, P]^T (lower),
+      // after the previous wide update (it wrote the same columns)
+      if (ev_wide) GG_HIP(hipStreamWaitEvent(cs, ev_wide, 0));
+      {
+        dim3 ug((unsigned)gg::ceil_div(n - pend, gg::kNB), (unsigned)gg::ceil_div(nend - pend, gg::kNB));
+        hipLaunchKernelGGL(gg::potrf_upd_kernel<false>, ug, dim3(256), 0, cs, A_dev, lda, n, P0,
+                           pend, pend, nend);
+        GG_LAUNCH_CHECK();
+      }
+      if (nend < n) {
+        // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on ws
+        if (lookahead) GG_HIP(hipStreamWaitEvent(ws, ef, 0));
+        const int pw = pend - P0;
+        const double* Lw = LT + (nend - pend);
+        gg::g_tn_min_lds = wide_lds;
+        gg::gemm(true, false, n - nend, n - nend, pw, -1.0, Lw, ldt, Lw, ldt, 1.0,
+                 A_dev + (int64_t)nend * lda + nend, lda, 1, ws);
+        gg::g_tn_min_lds = 0;
+        if (lookahead) {
+          ev_wide = new_event();
+          GG_HIP(hipEventRecord(ev_wide, ws));
+        }
+      } else {
+        ev_wide = nullptr;
+      }
+    }
+    for (int P0 = 0; P0 < n && v1; P0 += kPanel) {
       const int pend = std::min(n, P0 + kPanel);
       for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
         const int b = k0 / gg::kNB;
@@ -1522,7 +2083,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         // the block's update by the panel's earlier blocks is left-looking,
         // inside the same launch (no in-panel GEMM)
         hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n,
-                           k0, nb, P0, status, arrived + b);
+                           k0, nb, P0, status, arrived + b, pstamps);
         GG_LAUNCH_CHECK();
         (void)rest;
       }
@@ -1563,12 +2124,14 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       }
     }
     if (lookahead) {
-      // join: s waits for everything issued on cs and ws
-      hipEvent_t ec = new_event(), ew = new_event();
+      // join: s waits for everything issued on cs, ws and us
+      hipEvent_t ec = new_event(), ew = new_event(), eu = new_event();
       GG_HIP(hipEventRecord(ec, cs));
       GG_HIP(hipEventRecord(ew, ws));
+      GG_HIP(hipEventRecord(eu, us));
       GG_HIP(hipStreamWaitEvent(s, ec, 0));
       GG_HIP(hipStreamWaitEvent(s, ew, 0));
+      GG_HIP(hipStreamWaitEvent(s, eu, 0));
     }
     if (lt_buf) GG_HIP(hipFreeAsync(lt_buf, s));
     hipLaunchKernelGGL(gg::potrf_winv_kernel, dim3(nblk), dim3(256), 0, s, A_dev, lda, n,
@@ -1582,6 +2145,19 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     GG_HIP(hipMemcpyAsync(&lds, ld, sizeof(double), hipMemcpyDeviceToHost, s));
     GG_HIP(hipStreamSynchronize(s));
     for (hipEvent_t e : evs) GG_HIP(hipEventDestroy(e));
+    if (pstamps) {
+      std::vector<long long> h64(nstamp), h((size_t)nblk * 160 * 4 + 3);
+      GG_HIP(hipMemcpy(h64.data(), pstamps, nstamp * sizeof(long long), hipMemcpyDeviceToHost));
+      GG_HIP(hipFree(pstamps));
+      h[0] = nblk;
+      h[1] = 160;
+      h[2] = 4;
+      for (size_t q = 0; q + 3 < h.size(); ++q) h[q + 3] = h64[q * 64];
+      if (FILE* f = fopen(prof, "wb")) {
+        fwrite(h.data(), sizeof(long long), h.size(), f);
+        fclose(f);
+      }
+    }
     GG_REQUIRE(st == 0, GG_ERR_LINALG, "Matrix is not positive definite (device Cholesky)");
     if (logdet_host) *logdet_host = 2.0 * lds;
   });
