@@ -450,7 +450,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True)
         return None, "PMC passes taken with another recurrence / fusion layout"
     if rec.get("fold_mask", 0) != fold_mask:
         return None, "PMC passes taken with another fold state"
-    if bool(rec.get("x_deferred", False)) != bool(xdefer):
+    if int(rec.get("x_deferred", 0)) != int(xdefer):
         return None, "PMC passes taken with another x-update schedule"
     if rec.get("source_sha256") != kernel_source_hash():
         return None, "stale: the kernel sources changed since the PMC passes (%s)" % PMC_JSON

@@ -86,6 +86,14 @@ struct CgScalars {
   int xpend;
   double xc[2];
   const double* xp[2];
+  // x_defer mode 2 (balanced): the pair (xc, xp) completed two iterations ago
+  // is applied half of x per iteration -- xh = the half the next side job
+  // takes (2: none active); a completed step waiting for its partner is
+  // (xsc, xsp) when xs
+  int xh;
+  int xs;
+  double xsc;
+  const double* xsp;
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
@@ -108,9 +116,12 @@ struct MpFuse {
   const double* sp = nullptr;
   int64_t sn = 0, schunk = 0;
   // x_defer: the side job applies sc->xc / sc->xp (at element offset soff of
-  // the slice) when sc->xpend == 2, instead of alpha p_side when pending
+  // the slice) when sc->xpend == 2, instead of alpha p_side when pending.
+  // xdefer 2: the slice is [soff, soff + sn) of x for half sc->xh == 0 and
+  // [soff_h1, soff_h1 + sn_h1) for half 1 (sx / sp are then x / p at offset 0)
   int xdefer = 0;
   int64_t soff = 0;
+  int64_t soff_h1 = 0, sn_h1 = 0;
   // output of the first mode product when the ping-pong would put it in y
   // (odd d): the fused prologue still reads q_old == y in other workgroups
   double* first_dst = nullptr;

@@ -1135,7 +1135,38 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           }
           if (pro == 7) fz.coef = cg->coef;
         }
-        if (side) {
+        if (side && cg->xdefer == 2) {
+          // balanced x_defer: this launch's share of half 0 and of half 1 (the
+          // device picks by sc->xh); x / p at offset 0
+          const int64_t sn = cg->sn;
+          int64_t off0, len0, off1, len1;
+          if (split_side) {
+            const int64_t Q = 2 * ceil_div(sn, (int64_t)8);
+            const int L = (k == 2) ? 1 : 0;
+            auto quarter = [&](int qd, int64_t& off, int64_t& len) {
+              off = std::min<int64_t>((int64_t)qd * Q, sn);
+              const int64_t end = qd == 3 ? sn : std::min<int64_t>((int64_t)(qd + 1) * Q, sn);
+              len = std::max<int64_t>(end - off, 0);
+            };
+            quarter(L, off0, len0);
+            quarter(2 + L, off1, len1);
+          } else {
+            const int64_t H = 2 * ceil_div(sn, (int64_t)4);
+            off0 = 0;
+            len0 = std::min(H, sn);
+            off1 = std::min(H, sn);
+            len1 = sn - off1;
+          }
+          fz.sc = cg->sc;
+          fz.sx = cg->sx;
+          fz.sp = cg->sp;
+          fz.xdefer = 2;
+          fz.soff = off0;
+          fz.sn = len0;
+          fz.soff_h1 = off1;
+          fz.sn_h1 = len1;
+          fz.schunk = 2 * ceil_div(std::max<int64_t>(std::max(len0, len1), 1), 2 * nblk);
+        } else if (side) {
           // [off, off + len): all of x, or its half (even split: 16-byte
           // aligned double2 accesses stay aligned)
           const int64_t h = split_side ? 2 * ceil_div(cg->sn, 4) : cg->sn;
@@ -1214,6 +1245,12 @@ bool kron_first_single_launch(const gg_kron* K) { return K->fwd[0].JT <= kMaxJT;
 
 int64_t kron_n(const gg_kron* K) { return K->n_rows; }
 int kron_d(const gg_kron* K) { return K->d; }
+// x_defer mode 2: the side jobs' half boundary of an n-vector (d >= 4: two
+// launches per half, quarters of 2 ceil(n / 8) elements; else one launch per
+// half of 2 ceil(n / 4)); the closing flush uses the same boundary
+int64_t kron_side_half(const gg_kron* K, int64_t n) {
+  return K->d >= 4 ? 4 * ceil_div(n, (int64_t)8) : 2 * ceil_div(n, (int64_t)4);
+}
 
 static void set_lds_limits() {
   static bool done = false;

@@ -56,10 +56,45 @@ __device__ __forceinline__ void mp_block_sums(double dsum, double rqsum, double 
 template <int kThreads>
 __device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
   if (fz.sx == nullptr) return;
-  const int64_t lo = blk * fz.schunk;
-  const int64_t hi = min(fz.sn, lo + fz.schunk);
+  int64_t lo = blk * fz.schunk;
+  int64_t hi = min(fz.sn, lo + fz.schunk);
   double* __restrict__ sx = fz.sx;
   constexpr int kB = 4;
+  if (fz.xdefer == 2) {
+    // balanced: half sc->xh of the pair completed two iterations ago (this
+    // launch's quarter of it), so every side launch carries about one pass
+    const int h = fz.sc->xh;
+    if (h >= 2) return;
+    const int64_t off = h ? fz.soff_h1 : fz.soff;
+    const int64_t len = h ? fz.sn_h1 : fz.sn;
+    hi = min(len, lo + fz.schunk);
+    const double c0 = fz.sc->xc[0], c1 = fz.sc->xc[1];
+    const double* __restrict__ p0 = fz.sc->xp[0] + off;
+    const double* __restrict__ p1 = fz.sc->xp[1] + off;
+    double* __restrict__ xo = sx + off;
+    constexpr int kB2 = 2;
+    int64_t i = lo + 2 * threadIdx.x;
+    for (; i + 2 * kThreads * (kB2 - 1) + 1 < hi; i += 2 * kThreads * kB2) {
+      double2 xv2[kB2], a2[kB2], b2[kB2];
+#pragma unroll
+      for (int u = 0; u < kB2; ++u) {
+        xv2[u] = *reinterpret_cast<const double2*>(xo + i + 2 * kThreads * u);
+        a2[u] = *reinterpret_cast<const double2*>(p0 + i + 2 * kThreads * u);
+        b2[u] = *reinterpret_cast<const double2*>(p1 + i + 2 * kThreads * u);
+      }
+#pragma unroll
+      for (int u = 0; u < kB2; ++u) {
+        xv2[u].x += c0 * a2[u].x + c1 * b2[u].x;
+        xv2[u].y += c0 * a2[u].y + c1 * b2[u].y;
+        *reinterpret_cast<double2*>(xo + i + 2 * kThreads * u) = xv2[u];
+      }
+    }
+    for (; i < hi; i += 2 * kThreads) {
+      xo[i] += c0 * p0[i] + c1 * p1[i];
+      if (i + 1 < hi) xo[i + 1] += c0 * p0[i + 1] + c1 * p1[i + 1];
+    }
+    return;
+  }
   if (fz.xdefer) {
     // two deferred steps at once: x += c0 p0 + c1 p1 (4 passes per two CG
     // iterations instead of 6); 2 double2 per operand in flight keeps the

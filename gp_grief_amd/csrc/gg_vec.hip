@@ -23,6 +23,7 @@ int64_t kron_work_elems(const gg_kron* K, bool transpose);
 int64_t kron_n(const gg_kron* K);
 int kron_d(const gg_kron* K);
 bool kron_first_single_launch(const gg_kron* K);
+int64_t kron_side_half(const gg_kron* K, int64_t n);
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -204,7 +205,33 @@ __global__ __launch_bounds__(kVecThreads) void cg_x_flush_kernel(double* __restr
     x[i] += c0 * p0[i] + c1 * p1[i];
 }
 
-__global__ void cg_x_flushed_kernel(CgScalars* sc) { sc->xpend = 0; }
+// x_defer mode 2: x += xsc xsp (the waiting single step) + the active pair
+// on the halves not yet applied (half 0 = [0, H), half 1 = [H, n))
+__global__ __launch_bounds__(kVecThreads) void cg_x_flush2_kernel(double* __restrict__ x,
+                                                                  int64_t n, int64_t H,
+                                                                  const CgScalars* __restrict__ sc) {
+  const int h = sc->xh, xs = sc->xs;
+  if (h >= 2 && !xs) return;
+  const double cs = xs ? sc->xsc : 0.0;
+  const double* __restrict__ ps = xs ? sc->xsp : x;
+  const double c0 = h < 2 ? sc->xc[0] : 0.0, c1 = h < 2 ? sc->xc[1] : 0.0;
+  const double* __restrict__ p0 = h < 2 ? sc->xp[0] : x;
+  const double* __restrict__ p1 = h < 2 ? sc->xp[1] : x;
+  const int64_t from = h == 0 ? 0 : H;   // first element the pair still owes
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double v = x[i];
+    if (xs) v += cs * ps[i];
+    if (h < 2 && i >= from) v += c0 * p0[i] + c1 * p1[i];
+    x[i] = v;
+  }
+}
+
+__global__ void cg_x_flushed_kernel(CgScalars* sc) {
+  sc->xpend = 0;
+  sc->xh = 2;
+  sc->xs = 0;
+}
 
 // Fused recurrence, end of iteration j (after the last mode product):
 //   rho_j = r_j.r_j (partials of the first mode product's prologue, which
@@ -222,9 +249,15 @@ __global__ void cg_x_flushed_kernel(CgScalars* sc) { sc->xpend = 0; }
 // 2 pending, (p_j, alpha_j) and (p_{j-1}, alpha_{j-1}).  p_new = p_j (this
 // iteration's direction buffer); the host keeps three direction buffers so
 // p_{j-1} survives the next prologue.
+//
+// x_defer mode 2 (xmode 2, balanced): the pair of steps (2i, 2i + 1) becomes
+// active at the end of iteration 2i + 1 and the side jobs of the next two
+// iterations apply it half of x each (sc->xh: 0, 1, then 2 = done), so every
+// side launch carries one pass instead of two in every other iteration; four
+// direction buffers keep the pair alive.
 __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     const double* __restrict__ rr_part, int64_t nrr, const double* __restrict__ mv_part,
-    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new) {
+    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new, int xmode) {
   if (sc->done) return;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
@@ -251,8 +284,10 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
         sc->done = 1;
         sc->pending = 0;
         // x_defer: xpend 2 was folded into x by this iteration's side job;
-        // xpend 1 (alpha_{j-1} p_{j-1}) stays for the closing flush
-        if (p_new != nullptr && sc->xpend == 2) sc->xpend = 0;
+        // xpend 1 (alpha_{j-1} p_{j-1}) stays for the closing flush.  Mode 2:
+        // this iteration's side job took half xh; the flush does the rest
+        if (p_new != nullptr && xmode != 2 && sc->xpend == 2) sc->xpend = 0;
+        if (p_new != nullptr && xmode == 2 && sc->xh < 2) sc->xh += 1;
         return;
       }
     }
@@ -270,7 +305,21 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     sc->beta = sc->repair ? 0.0 : rt / rho;
     sc->first = 0;
     sc->pending = 1;
-    if (p_new != nullptr) {
+    if (p_new != nullptr && xmode == 2) {
+      if (sc->xh < 2) sc->xh += 1;   // this iteration's side job took a half
+      if (!sc->xs) {
+        sc->xs = 1;
+        sc->xsc = alpha;
+        sc->xsp = p_new;
+      } else {   // the pair is complete (the previous one finished just now)
+        sc->xc[0] = sc->xsc;
+        sc->xp[0] = sc->xsp;
+        sc->xc[1] = alpha;
+        sc->xp[1] = p_new;
+        sc->xh = 0;
+        sc->xs = 0;
+      }
+    } else if (p_new != nullptr) {
       if (sc->xpend == 1) {
         sc->xc[1] = sc->xc[0];
         sc->xp[1] = sc->xp[0];
@@ -300,6 +349,8 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->alpha = sc->beta = sc->pq = sc->rq = sc->qq = 0.0;
     sc->repair = 0;
     sc->xpend = 0;
+    sc->xh = 2;
+    sc->xs = 0;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -516,10 +567,12 @@ struct gg_cg {
   double *r = nullptr, *p = nullptr, *q = nullptr, *mv_work = nullptr;
   double* p2 = nullptr;        // second direction buffer (fused recurrence)
   double* p3 = nullptr;        // third (x_defer: p_{j-1} outlives the next prologue)
+  double* p4 = nullptr;        // fourth (x_defer mode 2: p_{j-2} too)
   double* first_dst = nullptr; // odd d: the first mode product's output (not q)
   bool fused = true;           // recurrence: fused (default) or textbook
   int fusion = 0;              // fused layout (gg_cg_set_fusion): 0, 1 or 2
-  bool xdefer = true;          // layouts 0 / 1: x updated every other iteration
+  int xdefer = 2;              // layouts 0 / 1: x updated in deferred pairs (1: every
+                               // other iteration; 2: balanced, half a pair per iteration)
   double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
   double* rr_part = nullptr;   // device, prologue r.r partials (fused)
   int64_t rr_count = 0;
@@ -641,9 +694,9 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
-    // r, p, q, p2, p3 (x_defer) + the matvec scratch (+ the first mode
+    // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
     // product's own output for an odd number of factors, MpFuse::first_dst)
-    *elems = 5 * n + gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
+    *elems = 6 * n + gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
   });
 }
 
@@ -663,10 +716,11 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->q = work_dev + 2 * nr;
       cg->p2 = work_dev + 3 * nr;
       cg->p3 = work_dev + 4 * nr;
-      cg->mv_work = work_dev + 5 * nr;
+      cg->p4 = work_dev + 5 * nr;
+      cg->mv_work = work_dev + 6 * nr;
       if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
-      const char* xd = getenv("GG_CG_XDEFER");   // A/B knob
-      cg->xdefer = !(xd && atoi(xd) == 0);
+      const char* xd = getenv("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
+      if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
       cg->mv_partials = gg::kron_partials_needed(K, false);
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
       GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
@@ -786,14 +840,15 @@ int gg_cg_set_xdefer(gg_cg* cg, int on) {
   return gg::guard([&] {
     GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
     GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set x deferral before gg_cg_start");
-    cg->xdefer = on != 0;
+    GG_REQUIRE(on >= 0 && on <= 2, GG_ERR_VALUE, "x deferral mode must be 0, 1 or 2");
+    cg->xdefer = on;
   });
 }
 
 int gg_cg_get_xdefer(const gg_cg* cg, int* on) {
   return gg::guard([&] {
     GG_REQUIRE(cg && on, GG_ERR_VALUE, "NULL argument");
-    *on = (cg->fused && cg->xdefer && cg->fusion != 2) ? 1 : 0;
+    *on = (cg->fused && cg->fusion != 2) ? cg->xdefer : 0;
   });
 }
 
@@ -836,7 +891,8 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         ev = cg->events.data() + cg->events_used;
         cg->events_used = need;
       }
-      const bool xdefer = cg->fused && cg->xdefer && cg->fusion != 2;
+      const bool xdefer = cg->fused && cg->xdefer != 0 && cg->fusion != 2;
+      const int xmode = xdefer ? cg->xdefer : 0;
       if (cg->fused) {
         // repair (no-op unless the last beta cancelled): x += alpha p,
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
@@ -859,7 +915,7 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.sx = cg->fusion == 2 ? nullptr : cg->x;
         fz.sp = cg->p;
         fz.sn = n;
-        fz.xdefer = xdefer ? 1 : 0;
+        fz.xdefer = xmode;
         fz.first_dst = cg->first_dst;
         fz.er = cg->r;
         fz.pstride = cg->mv_partials;
@@ -867,9 +923,18 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
                        &cg->sc->done, s, &nparts, &fz, 2, ev);
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
                            cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc,
-                           xdefer ? (const double*)cg->p2 : nullptr);
+                           xdefer ? (const double*)cg->p2 : nullptr, xmode);
         GG_LAUNCH_CHECK();
-        if (xdefer) {
+        if (xmode == 2) {
+          // (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2}): the
+          // active pair (at most p_{j-1}, p_{j-2} next iteration) stays alive
+          double* cur = cg->p;
+          double* o2 = cg->p3;
+          cg->p = cg->p2;
+          cg->p2 = cg->p4;
+          cg->p3 = cur;
+          cg->p4 = o2;
+        } else if (xdefer) {
           // (cur, free, old) <- (free, old, cur): p_j becomes current, p_{j-1}
           // is kept one more iteration for the deferred x update
           double* old_ = cg->p3;
@@ -903,11 +968,17 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
       }
     }
     if (cg->fused) {
-      const bool xdefer = cg->xdefer && cg->fusion != 2;
+      const bool xdefer = cg->xdefer != 0 && cg->fusion != 2;
       // closing update (no-op unless pending): x += alpha p, r -= alpha q,
       // rho = r.r, beta, iteration count -- the textbook state.  x_defer: the
       // deferred steps first (also after convergence), then r only
-      if (xdefer) {
+      if (xdefer && cg->xdefer == 2) {
+        hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
+                           n, gg::kron_side_half(cg->K, n), cg->sc);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+        GG_LAUNCH_CHECK();
+      } else if (xdefer) {
         hipLaunchKernelGGL(gg::cg_x_flush_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
                            n, cg->sc);
         GG_LAUNCH_CHECK();

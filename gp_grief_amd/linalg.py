@@ -111,8 +111,11 @@ class KronCG(object):
     products plus one scalar kernel -- r -= alpha q, p = r + beta p (and r.r)
     ride on the first mode product, the x update on the second / third, p.q /
     r.q / q.q on the last; beta comes from |r - alpha q|^2 expanded
-    (gg_vec.hip).  xdefer (default True, fusion layouts 0 / 1): x is updated
-    every other iteration, two steps in one pass.  recurrence="textbook":
+    (gg_vec.hip).  xdefer (fusion layouts 0 / 1; default 2): x is updated in
+    deferred pairs of steps, two steps in one pass -- 2: each pair applied to
+    half of x in each of the next two iterations (every side launch carries one
+    pass), 1: the whole pair every other iteration, 0: every iteration (True =
+    2, False = 0).  recurrence="textbook":
     scipy's operation order, with a separate x / r update pass.  Both leave
     iterate() in the textbook state.
     """
@@ -143,9 +146,11 @@ class KronCG(object):
         native.check(L.gg_cg_get_fusion(h, ctypes.byref(f)))
         self.fusion = f.value
         if xdefer is not None:
-            native.check(L.gg_cg_set_xdefer(h, int(bool(xdefer))), "gg_cg_set_xdefer")
+            # True: the library default (2, balanced); an int selects 0 / 1 / 2
+            mode = (2 if xdefer else 0) if isinstance(xdefer, bool) else int(xdefer)
+            native.check(L.gg_cg_set_xdefer(h, mode), "gg_cg_set_xdefer")
         native.check(L.gg_cg_get_xdefer(h, ctypes.byref(f)))
-        self.xdefer = bool(f.value)
+        self.xdefer = f.value
         self.n = int(K.shape[0])
         self.x = None
 

@@ -181,13 +181,14 @@ def test_fold_partial_strips(gg, fold_small):
 
 
 @pytest.mark.parametrize("fusion", [0, 1, 2])
-@pytest.mark.parametrize("xdefer", ["1", "0"])
+@pytest.mark.parametrize("xdefer", ["2", "1", "0"])
 def test_fold_cg_fusion_layouts_and_deferred_x(gg, fold_small, monkeypatch, fusion, xdefer):
     """Fused CG on folded factors with each fusion layout (1: p_new recomputed
     in the folded epilogue; 2: the dense epilogue kernel with the x update) and
-    the x update deferred to every other iteration or not: same solution as
-    the exact solve, and iterate() chunks of odd length (deferred steps
-    pending across calls) reach the same iterate as one call."""
+    the x update deferred in pairs (2: half a pair per iteration, 1: a whole
+    pair every other iteration) or not: same solution as the exact solve, and
+    iterate() chunks of odd length (deferred steps pending across calls) reach
+    the same iterate as one call."""
     import torch
     monkeypatch.setenv("GG_CG_XDEFER", xdefer)
     F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate((24, 20, 16, 18))]
@@ -201,7 +202,7 @@ def test_fold_cg_fusion_layouts_and_deferred_x(gg, fold_small, monkeypatch, fusi
     ex = oracle.solve_schur(Q, oracle.kron_expand(lam), b[:, 0], s)
     assert rel(x, ex) < 1e-8
     one = gg.linalg.KronCG(K, s, fusion=fusion)
-    assert one.xdefer == (xdefer == "1" and fusion != 2)
+    assert one.xdefer == (int(xdefer) if fusion != 2 else 0)
     bt = torch.tensor(b[:, 0], device="cuda")
     one.start(bt, rtol=0.0)
     one.iterate(23)
@@ -214,3 +215,27 @@ def test_fold_cg_fusion_layouts_and_deferred_x(gg, fold_small, monkeypatch, fusi
     # a chunk boundary closes with the textbook update (true r.r for beta
     # instead of the expansion, deferred x steps flushed): rounding-level
     assert rel(chunks.x.cpu().numpy(), one.x.cpu().numpy()) < 1e-9
+
+
+@pytest.mark.parametrize("dims", [(24, 20, 16, 18), (30, 22, 14)])
+def test_fold_cg_xdefer_modes_agree(gg, fold_small, dims):
+    """The three x-update schedules (immediate, a pair every other iteration,
+    half a pair per iteration) give the same iterate after the same number of
+    iterations, for every count (pairs open, half applied, complete at the
+    exit), d = 4 (two side launches per half) and d = 3 (one)."""
+    import torch
+    F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate(dims)]
+    K = kron(gg, F)
+    n = int(np.prod(dims))
+    b = torch.tensor(np.random.default_rng(5).standard_normal(n), device="cuda")
+    for its in (1, 2, 3, 4, 5, 9):
+        xs = []
+        for mode in (0, 1, 2):
+            cg = gg.linalg.KronCG(K, 0.05, xdefer=mode)
+            assert cg.xdefer == mode
+            cg.start(b, rtol=0.0)
+            cg.iterate(its)
+            assert cg.status()[0] == its
+            xs.append(cg.x.cpu().numpy())
+        assert rel(xs[1], xs[0]) < 1e-12
+        assert rel(xs[2], xs[0]) < 1e-12

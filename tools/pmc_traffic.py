@@ -1,6 +1,6 @@
 """HBM traffic per launch of the fused-CG mode products from rocprofv3 PMC passes.
 
-usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON [--fusion F] [--no-xdefer]
+usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON [--fusion F] [--xdefer MODE]
 
 Counters (two separate --pmc runs of `bench.py --steps 2 --warmup 1`, kernel
 trace only, as MI355X_MICROARCH.md prescribes):
@@ -41,7 +41,10 @@ def dispatches(d):
 def main():
     rd_dir, wr_dir, out = sys.argv[1:4]
     fusion = int(sys.argv[sys.argv.index("--fusion") + 1]) if "--fusion" in sys.argv else 0
-    xdefer = "--no-xdefer" not in sys.argv
+    # the x-update schedule the passes were taken with (gg_cg_set_xdefer mode;
+    # the library default 2 unless GG_CG_XDEFER overrides it)
+    xdefer = (int(sys.argv[sys.argv.index("--xdefer") + 1]) if "--xdefer" in sys.argv
+              else int(os.environ.get("GG_CG_XDEFER", "2")))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     rd, names = dispatches(rd_dir)
