@@ -958,6 +958,34 @@ __global__ __launch_bounds__(kOrthoThreads) void rows_orthonormalize_kernel(
 // (kTqWaves m; the two are never live together), or Jacobi's 2 m^2
 inline int64_t eig_work_per(int64_t m) { return std::max(2 * m * m, m * m + (2 + kTqWaves) * m); }
 
+// Full-length eigenvectors of centrosymmetric factors from their half-order
+// problems (tensors.centro_halves): factor f's rows r < ke are [y; J y] / sqrt 2
+// of the even half's row r, rows ke + r are [y; -J y] / sqrt 2 of the odd
+// half's row r.  In: per factor the even block (ke x h) then the odd block
+// (ko x h); out: (ke + ko) x 2h per factor.  One launch for up to kCentroMax
+// factors (parameters by value), blockIdx.y = factor.
+constexpr int kCentroMax = 32;
+struct CentroBatch {
+  int nf;
+  int64_t h[kCentroMax], ke[kCentroMax], ko[kCentroMax], in[kCentroMax], out[kCentroMax];
+};
+
+__global__ __launch_bounds__(256) void centro_expand_kernel(CentroBatch B,
+                                                            const double* __restrict__ V,
+                                                            double* __restrict__ out) {
+  const int f = blockIdx.y;
+  const int64_t h = B.h[f], m = 2 * h, k = B.ke[f] + B.ko[f];
+  const double c = 0.70710678118654752440;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < k * m;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / m, col = e - r * m;
+    const bool odd = r >= B.ke[f];
+    const int64_t src = B.in[f] + r * h;   // the odd block follows the even one
+    const double y = col < h ? V[src + col] : V[src + (m - 1 - col)];
+    out[B.out[f] + e] = (col >= h && odd) ? -c * y : c * y;
+  }
+}
+
 }  // namespace gg
 
 extern "C" {
@@ -1209,6 +1237,36 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* R_dev,
   });
 }
 
+
+int gg_centro_expand(int nf, const int64_t* h, const int64_t* ke, const int64_t* ko,
+                     const double* V_dev, double* out_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(nf >= 1 && h && ke && ko && V_dev && out_dev, GG_ERR_VALUE, "bad argument");
+    hipStream_t s = gg::as_stream(stream);
+    int64_t in = 0, out = 0;
+    for (int f0 = 0; f0 < nf; f0 += gg::kCentroMax) {
+      gg::CentroBatch B;
+      B.nf = std::min(gg::kCentroMax, nf - f0);
+      int64_t maxel = 1;
+      for (int j = 0; j < B.nf; ++j) {
+        const int f = f0 + j;
+        GG_REQUIRE(h[f] >= 1 && ke[f] >= 0 && ko[f] >= 0 && ke[f] + ko[f] <= 2 * h[f],
+                   GG_ERR_VALUE, "bad half block");
+        B.h[j] = h[f];
+        B.ke[j] = ke[f];
+        B.ko[j] = ko[f];
+        B.in[j] = in;
+        B.out[j] = out;
+        in += (ke[f] + ko[f]) * h[f];
+        out += (ke[f] + ko[f]) * 2 * h[f];
+        maxel = std::max(maxel, (ke[f] + ko[f]) * 2 * h[f]);
+      }
+      dim3 grid((unsigned)gg::ceil_div(maxel, 256), (unsigned)B.nf);
+      hipLaunchKernelGGL(gg::centro_expand_kernel, grid, dim3(256), 0, s, B, V_dev, out_dev);
+      GG_LAUNCH_CHECK();
+    }
+  });
+}
 
 int gg_rows_orthonormalize(int count, const int64_t* k, const int64_t* m, double* V_dev,
                            gg_stream stream) {

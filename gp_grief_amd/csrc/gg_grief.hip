@@ -17,12 +17,16 @@
 //     j (their table columns c_{j,f} in LDS); every Phi element is d LDS
 //     loads and d multiplies, and the transposed tile is stored through LDS.
 // Also the dense stationary covariance used for the grid factors K_f.
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "gg_internal.h"
 
 namespace gg {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
 
 enum KernKind { kRBF = 0, kExponential = 1, kMatern32 = 2, kMatern52 = 3 };
 
@@ -125,6 +129,162 @@ __global__ __launch_bounds__(256) void grief_tables_kernel(
       Ltab[o] = log(fabs(v == 0.0 ? 1.0 : v));
     }
   }
+}
+
+// MFMA form of the tables (round 3): X[u][a] = sum_k Qsel[u][k] k_f(xg[k], x[a])
+// is a (u x m) . (m x n) product on v_mfma_f64_16x16x4_f64.  A wave owns 16
+// data points at a time; per k-step its A operand is 16 Qsel rows (LDS, row
+// stride m + 1: no bank conflicts) and its B operand the kernel values, each
+// lane evaluating the one k(xg[4s + l / 16], x[a_l % 16]) it supplies -- K_ux
+// never exists and the contraction costs one MFMA per 4 grid points instead of
+// 16 LDS reads + FMAs per grid point per lane (grief_tables_kernel: 72 us per
+// C2 factor, profiles/r03/y_c2_phi_trace.txt).  blockIdx.y: a group of 16
+// selected rows.
+// k(d) for the tables with the per-kernel constants hoisted (one multiply for
+// the RBF exponent instead of a divide; r = |d| / l as |d| * (1 / l)): the same
+// values as stationary() up to a few ulp of the exponent
+template <int kKind>
+__device__ __forceinline__ double stationary_fast(double d, double var, double c) {
+  if (kKind == kRBF) return var * exp(c * (d * d));                 // c = -1 / (2 l^2)
+  const double r = fabs(d) * c;                                      // c = 1 / l
+  if (kKind == kExponential) return var * exp(-r);
+  if (kKind == kMatern32) {
+    const double s3 = 1.7320508075688772;
+    return var * fma(s3, r, 1.0) * exp(-s3 * r);
+  }
+  const double s5 = 2.23606797749979;
+  return var * fma(5.0 / 3.0 * r, r, fma(s5, r, 1.0)) * exp(-s5 * r);
+}
+
+// One factor's share of the batched tables launch (gg_grief_tables_all).
+constexpr int kTabMaxF = 16;
+struct TabFactor {
+  int kind, m, u, col0, g0;   // g0: first blockIdx.y of this factor's row groups
+  double var, c;
+  const double* xg;
+  const double* qsel;
+  int64_t xoff;               // element offset of this dimension in x
+};
+struct TabBatch {
+  int nf;
+  TabFactor f[kTabMaxF];
+};
+
+template <int kKind>
+__device__ __forceinline__ void tables_mfma_body(const TabFactor& F, int grp,
+                                                 const double* __restrict__ x, int64_t x_stride,
+                                                 int64_t n, double* __restrict__ Ltab,
+                                                 double* __restrict__ Stab, int U, double* tl) {
+  const int m = F.m, mp = (m + 15) & ~15, ld = mp + 1;
+  double* qs = tl;              // 16 x ld
+  double* xgs = tl + 16 * ld;   // mp
+  const int ug = grp * 16, nu = min(16, F.u - ug);
+  for (int e = threadIdx.x; e < 16 * mp; e += blockDim.x) {
+    const int t = e / mp, k = e - t * mp;
+    qs[t * ld + k] = (t < nu && k < m) ? F.qsel[(int64_t)(ug + t) * m + k] : 0.0;
+  }
+  // grid points past m: a finite kernel value times a zero Qsel column
+  for (int k = threadIdx.x; k < mp; k += blockDim.x) xgs[k] = F.xg[min(k, m - 1)];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t tiles = (n + 15) / 16;
+  const double var = F.var, c = F.c;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < tiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t a = t * 16 + (lane & 15);
+    const double xa = x[min(a, n - 1) * x_stride + F.xoff];
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    const double* qrow = qs + (lane & 15) * ld + (lane >> 4);
+    const double* xk = xgs + (lane >> 4);
+    // four k-steps per iteration: their kernel values are independent
+    for (int s = 0; s < mp / 4; s += 4) {
+      double kv[4], av[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        kv[e] = stationary_fast<kKind>(xk[4 * (s + e)] - xa, var, c);
+        av[e] = qrow[4 * (s + e)];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[e], kv[e], acc, 0, 0, 0);
+    }
+    // D[4 r + l / 16][l % 16]: selected row ug + 4 r + l / 16 of point a
+    if (a < n) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int uu = 4 * r + (lane >> 4);
+        if (uu < nu) {
+          const double v = acc[r];
+          const int64_t o = a * U + F.col0 + ug + uu;
+          Stab[o] = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
+          Ltab[o] = log(fabs(v == 0.0 ? 1.0 : v));
+        }
+      }
+    }
+  }
+}
+
+// blockIdx.y runs over every factor's 16-row groups (the factor found by its
+// g0); the kernel kind is uniform per block
+__global__ __launch_bounds__(256) void grief_tables_mfma_kernel(TabBatch B,
+                                                                const double* __restrict__ x,
+                                                                int64_t x_stride, int64_t n,
+                                                                double* __restrict__ Ltab,
+                                                                double* __restrict__ Stab, int U) {
+  extern __shared__ double tl[];
+  int f = 0;
+  while (f + 1 < B.nf && (int)blockIdx.y >= B.f[f + 1].g0) ++f;
+  const TabFactor& F = B.f[f];
+  const int grp = (int)blockIdx.y - F.g0;
+  switch (F.kind) {
+    case kRBF: tables_mfma_body<kRBF>(F, grp, x, x_stride, n, Ltab, Stab, U, tl); break;
+    case kExponential:
+      tables_mfma_body<kExponential>(F, grp, x, x_stride, n, Ltab, Stab, U, tl);
+      break;
+    case kMatern32: tables_mfma_body<kMatern32>(F, grp, x, x_stride, n, Ltab, Stab, U, tl); break;
+    default: tables_mfma_body<kMatern52>(F, grp, x, x_stride, n, Ltab, Stab, U, tl); break;
+  }
+}
+
+// host: one launch of the batched MFMA tables for factors [0, nf) (nf <=
+// kTabMaxF); false when a factor needs the generic kernel (delta RBF, m too
+// large for the LDS staging)
+static bool launch_tables_mfma(int nf, const int* kinds, const double* variances,
+                               const double* lengthscales, const double* x_dev, int64_t x_stride,
+                               const int64_t* xoffs, int64_t n, const double* const* xgs,
+                               const int* ms, const double* const* qsels, const int* us,
+                               double* ltab, double* stab, int U, const int* col0s,
+                               hipStream_t s) {
+  const char* tv = getenv("GG_GRIEF_TABLES");   // 0: the lane-quad kernel (A/B)
+  if (tv && atoi(tv) == 0) return false;
+  if (nf < 1 || nf > kTabMaxF) return false;
+  TabBatch B;
+  B.nf = nf;
+  int g = 0, mmax = 1;
+  for (int f = 0; f < nf; ++f) {
+    if (kinds[f] == kRBF && lengthscales[f] < 1e-6) return false;
+    const int mp = (ms[f] + 15) & ~15;
+    if ((size_t)(16 * (mp + 1) + mp) * sizeof(double) > 64 * 1024) return false;
+    mmax = std::max(mmax, mp);
+    TabFactor& F = B.f[f];
+    F.kind = kinds[f];
+    F.m = ms[f];
+    F.u = us[f];
+    F.col0 = col0s[f];
+    F.g0 = g;
+    F.var = variances[f];
+    F.c = kinds[f] == kRBF ? -0.5 / (lengthscales[f] * lengthscales[f]) : 1.0 / lengthscales[f];
+    F.xg = xgs[f];
+    F.qsel = qsels[f];
+    F.xoff = xoffs[f];
+    g += (int)ceil_div(us[f], 16);
+  }
+  const size_t lds = (size_t)(16 * (mmax + 1) + mmax) * sizeof(double);
+  const int64_t tiles = ceil_div(n, (int64_t)16);
+  dim3 grid((unsigned)std::min<int64_t>(ceil_div(tiles, (int64_t)4), 1024), (unsigned)g);
+  hipLaunchKernelGGL(grief_tables_mfma_kernel, grid, dim3(256), lds, s, B, x_dev, x_stride, n,
+                     ltab, stab, U);
+  GG_LAUNCH_CHECK();
+  return true;
 }
 
 constexpr int kPhiRows = 64;    // data points per block (row-major Phi)
@@ -285,6 +445,13 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
     GG_REQUIRE(m >= 1 && u >= 1 && col0 >= 0 && col0 + u <= U && n >= 0, GG_ERR_VALUE,
                "bad table geometry");
     if (n == 0) return;
+    // MFMA contraction (default; GG_GRIEF_TABLES=0 selects the lane-quad kernel)
+    // the MFMA contraction (default; GG_GRIEF_TABLES=0 selects the lane-quad kernel)
+    const int64_t zero = 0;
+    if (gg::launch_tables_mfma(1, &kind, &variance, &lengthscale, x_dev, x_stride, &zero, n,
+                               &xg_dev, &m, &qsel_dev, &u, ltab_dev, stab_dev, U, &col0,
+                               gg::as_stream(stream)))
+      return;
     const bool in_lds = m <= 512;   // the kUG x m rows in at most 64 KiB of LDS
     const size_t lds = in_lds ? (size_t)gg::kUG * m * sizeof(double) : 0;
     dim3 grid((unsigned)gg::ceil_div(n * gg::kTQ, 256), (unsigned)gg::ceil_div(u, gg::kUG));
@@ -293,6 +460,43 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
                        kind, variance, lengthscale, x_dev, x_stride, n, xg_dev, m, qsel_dev, u,
                        ltab_dev, stab_dev, U, col0);
     GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_grief_tables_all(int nf, const int* kinds, const double* variances,
+                        const double* lengthscales, const double* x_dev, int64_t x_stride,
+                        const int64_t* x_offsets, int64_t n, const double* const* xg_devs,
+                        const int* ms, const double* const* qsel_devs, const int* us,
+                        double* ltab_dev, double* stab_dev, int U, const int* col0s,
+                        gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(nf >= 1 && kinds && variances && lengthscales && x_dev && x_offsets && xg_devs &&
+                   ms && qsel_devs && us && ltab_dev && stab_dev && col0s && n >= 0,
+               GG_ERR_VALUE, "bad argument");
+    for (int f = 0; f < nf; ++f) {
+      GG_REQUIRE(kinds[f] >= 0 && kinds[f] <= 3, GG_ERR_VALUE, "unknown kernel kind");
+      GG_REQUIRE(xg_devs[f] && qsel_devs[f], GG_ERR_VALUE, "NULL");
+      GG_REQUIRE(ms[f] >= 1 && us[f] >= 1 && col0s[f] >= 0 && col0s[f] + us[f] <= U &&
+                     x_offsets[f] >= 0 && x_offsets[f] < x_stride,
+                 GG_ERR_VALUE, "bad table geometry");
+    }
+    if (n == 0) return;
+    hipStream_t s = gg::as_stream(stream);
+    // batches of kTabMaxF factors in one launch each
+    for (int f0 = 0; f0 < nf; f0 += gg::kTabMaxF) {
+      const int c = std::min(gg::kTabMaxF, nf - f0);
+      if (gg::launch_tables_mfma(c, kinds + f0, variances + f0, lengthscales + f0, x_dev,
+                                 x_stride, x_offsets + f0, n, xg_devs + f0, ms + f0,
+                                 qsel_devs + f0, us + f0, ltab_dev, stab_dev, U, col0s + f0, s))
+        continue;
+      for (int f = f0; f < f0 + c; ++f) {
+        const int st = gg_grief_tables(kinds[f], variances[f], lengthscales[f],
+                                       x_dev + x_offsets[f], x_stride, n, xg_devs[f], ms[f],
+                                       qsel_devs[f], us[f], ltab_dev, stab_dev, U, col0s[f],
+                                       stream);
+        GG_REQUIRE(st == GG_OK, st, "gg_grief_tables_all: a factor's table failed");
+      }
+    }
   });
 }
 

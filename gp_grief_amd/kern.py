@@ -28,8 +28,9 @@ import numpy as np
 from . import device as dev
 from . import native
 from .grid import InducingGrid
-from .tensors import (KronMatrix, KhatriRaoMatrix, SelectionMatrixSparse, device_sym_eig,
-                      device_sym_eig_tridiag, device_sym_eig_tridiag_vectors)
+from .tensors import (KronMatrix, KhatriRaoMatrix, SelectionMatrixSparse, centro_expand,
+                      centro_halves_host, centro_merge, device_sym_eig, device_sym_eig_tridiag,
+                      device_sym_eig_tridiag_vectors)
 
 logger = logging.getLogger(__name__)
 
@@ -121,6 +122,25 @@ class BaseKernel(object):
         c = deepcopy(self)
         c._children = [(deepcopy(op), ch.copy()) for op, ch in c._children]
         return c
+
+
+def _stationary_host(kind, var, ls, d2):
+    """k(r^2) on the host, the same formulas as the device kernels
+    (gg_grief.hip stationary(); the reference's stationary.py:108-258)."""
+    if kind == "RBF":
+        if ls < 1e-6:
+            return np.where(d2 == 0.0, var, 0.0)
+        return var * np.exp(-0.5 * d2 / (ls * ls))
+    r = np.sqrt(d2) / ls
+    if kind == "Exponential":
+        return var * np.exp(-r)
+    if kind == "Matern32":
+        s3 = 1.7320508075688772
+        return var * (1.0 + s3 * r) * np.exp(-s3 * r)
+    if kind == "Matern52":
+        s5 = 2.23606797749979
+        return var * (1.0 + s5 * r + (5.0 / 3) * r * r) * np.exp(-s5 * r)
+    raise NotImplementedError(kind)
 
 
 class Stationary(BaseKernel):
@@ -379,17 +399,30 @@ class GriefKernel(GridKernel):
         L = native.lib()
         ltab = dev.empty(max(n * B["U"], 1))
         stab = dev.empty(max(n * B["U"], 1))
+        # every dimension's table in one launch (factor f reads input dim d-1-f)
+        kinds = (ctypes.c_int * d)()
+        var = (ctypes.c_double * d)()
+        ls = (ctypes.c_double * d)()
+        xoff = (ctypes.c_int64 * d)()
+        xgp = (ctypes.c_void_p * d)()
+        qsp = (ctypes.c_void_p * d)()
+        ms = (ctypes.c_int * d)(*[int(v) for v in B["m"]])
+        us = (ctypes.c_int * d)(*[int(v) for v in B["u"]])
+        c0 = (ctypes.c_int * d)(*[int(v) for v in B["col0"]])
         for f in range(d):
             i = d - 1 - f
             kern = self.kern_list[i]
             if not isinstance(kern, Stationary) or kern._children:
                 raise NotImplementedError("GRIEF device basis needs plain stationary kernels")
-            native.check(L.gg_grief_tables(
-                native.GG_KERN[kern._kind], float(np.asarray(kern.variance).reshape(-1)[0]),
-                float(np.asarray(kern.lengthscale).reshape(-1)[0]),
-                ctypes.c_void_p(xd.data_ptr() + 8 * i), d, n, native.dptr(B["xg"][f]),
-                B["m"][f], native.dptr(B["qsel"][f]), B["u"][f], native.dptr(ltab),
-                native.dptr(stab), B["U"], B["col0"][f], native.stream_ptr()), "gg_grief_tables")
+            kinds[f] = native.GG_KERN[kern._kind]
+            var[f] = float(np.asarray(kern.variance).reshape(-1)[0])
+            ls[f] = float(np.asarray(kern.lengthscale).reshape(-1)[0])
+            xoff[f] = i
+            xgp[f] = native.dptr(B["xg"][f])
+            qsp[f] = native.dptr(B["qsel"][f])
+        native.check(L.gg_grief_tables_all(d, kinds, var, ls, native.dptr(xd), d, xoff, n, xgp,
+                                           ms, qsp, us, native.dptr(ltab), native.dptr(stab),
+                                           B["U"], c0, native.stream_ptr()), "gg_grief_tables_all")
         p = self.n_eigs
         phi = dev.empty(n * p)
         native.check(L.gg_grief_phi(native.dptr(ltab), native.dptr(stab), B["U"], n,
@@ -444,15 +477,39 @@ class GriefKernel(GridKernel):
         key = np.asarray(base, dtype=np.float64).tobytes()
         hit = self._eig_cache.get(key)
         qsel_dev = None
+        qperm = None
         if hit is None and not self.opt_kernel_params and \
                 os.environ.get("GG_EIG_SUBSET", "1") != "0":
-            Kuu = self.cov_grid(self.grid.xg, dim_noise_var=self.dim_noise_var)
-            factors = [np.asarray(k) for k in Kuu.K]
-            lam, handle = device_sym_eig_tridiag(factors)
+            factors = self._grid_factors_host()
+            if factors is None:
+                factors = self._grid_factors_device()
+            # centrosymmetric factors (evenly spaced grids): two half-order
+            # problems each (tensors.centro_halves); GG_EIG_CENTRO=0 disables
+            # (from m = 96: below it the halves' saving is under the extra
+            # bookkeeping, profiles/r03/aa_centro_setup.jsonl)
+            halves = None
+            cmin = int(os.environ.get("GG_EIG_CENTRO_MIN", "96"))
+            if os.environ.get("GG_EIG_CENTRO", "1") != "0" and \
+                    not dev.is_device_array(factors[0]) and \
+                    min(int(F.shape[0]) for F in factors) >= cmin:
+                halves = [centro_halves_host(F) for F in factors]
+                if any(hv is None for hv in halves):
+                    halves = None
+            split = halves is not None
+            if split:
+                lamh, handle = device_sym_eig_tridiag([M for hv in halves for M in hv])
+                merged = [centro_merge(lamh[2 * f], lamh[2 * f + 1]) for f in range(len(factors))]
+                lam = [mg[0] for mg in merged]
+            else:
+                lam, handle = device_sym_eig_tridiag(factors)
             eig_pos, log_lam = self._select(lam)
             Sp = [SelectionMatrixSparse((col, lam[i].shape[0])) for i, col in enumerate(eig_pos.T)]
             if self._separated(lam, [S.unique for S in Sp]):
-                qsel_dev = device_sym_eig_tridiag_vectors(handle, [S.unique for S in Sp])
+                if split:
+                    qsel_dev, qperm = self._centro_vectors(handle, merged,
+                                                           [S.unique for S in Sp])
+                else:
+                    qsel_dev = device_sym_eig_tridiag_vectors(handle, [S.unique for S in Sp])
                 self._Quu_factors = factors
                 self._Quu_full = None
         if qsel_dev is None:
@@ -463,7 +520,61 @@ class GriefKernel(GridKernel):
         self._log_lam = log_lam
         self._Sp = Sp
         self._old_base_kern_params = base
-        self._build_device_basis(qsel_dev)
+        self._build_device_basis(qsel_dev, qperm)
+
+    def _grid_factors_host(self):
+        """The inducing-grid factors K_f + dim_noise_var I on the host, in
+        KronMatrix order (input dims reversed, grid_kernel.py:56-115), for
+        plain stationary kernels (the reference's own formulas,
+        stationary.py:108-258; m x m, cheaper here than per-factor device
+        launches and copies); None for composed kernels."""
+        if not all(isinstance(k, Stationary) and not k._children for k in self.kern_list):
+            return None
+        host = []
+        for i, kern in enumerate(self.kern_list):
+            g = np.asarray(self.grid.xg[i], dtype=np.float64).reshape(-1)
+            d2 = (g[:, None] - g[None, :]) ** 2
+            Fi = _stationary_host(kern._kind, float(np.asarray(kern.variance).reshape(-1)[0]),
+                                  float(np.asarray(kern.lengthscale).reshape(-1)[0]), d2)
+            if self.dim_noise_var != 0.:
+                Fi[np.diag_indices_from(Fi)] += float(self.dim_noise_var)
+            host.append(Fi)
+        return host[::-1]
+
+    def _grid_factors_device(self):
+        """The grid factors on the device (composed kernels: the device cov)."""
+        t = dev.torch()
+        F = []
+        for i, kern in enumerate(self.kern_list):
+            xg = np.asarray(self.grid.xg[i], dtype=np.float64)
+            xd = t.from_numpy(np.ascontiguousarray(xg.reshape(xg.shape[0], -1))).to(dev.device())
+            Fi = kern.cov(xd)
+            if self.dim_noise_var != 0.:
+                Fi = Fi + float(self.dim_noise_var) * t.eye(Fi.shape[0], dtype=t.float64,
+                                                             device=dev.device())
+            F.append(Fi)
+        return F[::-1]
+
+    @staticmethod
+    def _centro_vectors(handle, merged, uniques):
+        """Selected eigenvector rows of each factor from its halves' problems
+        (tensors.centro_halves): inverse iteration on the half tridiagonals
+        for the selected indices of each half, then [y; +-J y] / sqrt 2 in one
+        launch (gg_centro_expand).  The rows come even-half first; returns them
+        and, per factor, the row of each selected index (unique order)."""
+        sel_h, hs, kes, kos, perms = [], [], [], [], []
+        for f, (lamf, half, idx) in enumerate(merged):
+            u = np.asarray(uniques[f], dtype=np.int64).reshape(-1)
+            hr, ir = half[u], idx[u]
+            se, so = np.sort(ir[hr == 0]), np.sort(ir[hr == 1])
+            sel_h += [se, so]
+            hs.append(lamf.size // 2)
+            kes.append(se.size)
+            kos.append(so.size)
+            perms.append(np.where(hr == 0, np.searchsorted(se, ir),
+                                  se.size + np.searchsorted(so, ir)).astype(np.int64))
+        Vh = device_sym_eig_tridiag_vectors(handle, sel_h)
+        return centro_expand(Vh, hs, kes, kos), perms
 
     # inverse iteration converges by eps ||T|| / gap per step and the Cholesky
     # QR restores orthogonality: a gap of 1e-10 ||T|| leaves each vector within
@@ -496,7 +607,8 @@ class GriefKernel(GridKernel):
         """Per-factor eigenvectors (KronMatrix); after a subset setup the full
         decomposition is computed on first access."""
         if getattr(self, "_Quu_full", None) is None and getattr(self, "_Quu_factors", None):
-            Q, _ = device_sym_eig(self._Quu_factors)
+            Q, _ = device_sym_eig([dev.to_host(F) if dev.is_device_array(F) else F
+                                   for F in self._Quu_factors])
             self._Quu_full = KronMatrix(Q)
         return self._Quu_full
 
@@ -548,9 +660,10 @@ class GriefKernel(GridKernel):
             self._cache_put(key, (Q[i * d:(i + 1) * d], lam[i * d:(i + 1) * d]))
         return len(keys)
 
-    def _build_device_basis(self, qsel_dev=None):
+    def _build_device_basis(self, qsel_dev=None, qperm=None):
         """Device basis tables; qsel_dev (subset setup): the selected
-        eigenvector rows Q_f^T[unique_f, :] already on the device."""
+        eigenvector rows Q_f^T[unique_f, :] already on the device, row
+        qperm[f][r] holding unique index r when qperm is given."""
         d = self.grid_dim
         qsel, xg, us, ms, col0 = [], [], [], [], []
         cidx = np.zeros((self.n_eigs, d), dtype=np.int32)
@@ -568,7 +681,8 @@ class GriefKernel(GridKernel):
             xg.append(dev.to_device(np.asarray(self.grid.xg[i], dtype=np.float64).reshape(-1)))
             us.append(int(S.unique.size))
             col0.append(c)
-            cidx[:, f] = c + np.asarray(S.unique_inverse).reshape(-1)
+            inv = np.asarray(S.unique_inverse).reshape(-1)
+            cidx[:, f] = c + (inv if qperm is None else qperm[f][inv])
             c += int(S.unique.size)
         t = dev.torch()
         self._dev_basis = dict(

@@ -385,6 +385,8 @@ class GPGriefModel(BaseModel):
         else:
             self.grad_method = ['adjoint', 'finite_difference'][0]
         self._Yd = None
+        self._Xd = None
+        self._Xd_src = None
         self._gram_uplo = 1   # A = Phi^T Phi is formed in its lower triangle only
         if p_solver not in ('chol', 'cg'):
             raise ValueError("p_solver must be 'chol' or 'cg'")
@@ -414,6 +416,14 @@ class GPGriefModel(BaseModel):
         if self._Yd is None:
             self._Yd = dev.to_device(self.Y[:, 0])
         return self._Yd
+
+    def _x_dev(self):
+        """The training inputs on the device, uploaded once: Phi is rebuilt at
+        every new kernel parameter (optimize), X never changes."""
+        if self._Xd is None or self._Xd_src is not self.X:
+            self._Xd = dev.to_device(self.X)
+            self._Xd_src = self.X
+        return self._Xd
 
     def fit(self, **kwargs):
         self.parameters
@@ -455,7 +465,7 @@ class GPGriefModel(BaseModel):
     def _phi_setup(self):
         self._w = self.kern.w
         if self._Phi is None:
-            self._Phi = self.kern.phi_device(self.X)          # n x p
+            self._Phi = self.kern.phi_device(self._x_dev())   # n x p
 
     def _cov_setup(self):
         if self._P is not None:
@@ -463,7 +473,7 @@ class GPGriefModel(BaseModel):
         self._w = self.kern.w
         if self._A is None:
             if self._Phi is None:
-                self._Phi = self.kern.phi_device(self.X)      # n x p
+                self._Phi = self.kern.phi_device(self._x_dev())  # n x p
             self._A = self._gram()
         wd = dev.to_device(np.asarray(self._w, dtype=np.float64))
         self._P = dense.add_diag(self._A, float(self.noise_var), wd)

@@ -79,11 +79,18 @@ SIGNATURES = {
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                    _c_dp, _vp],
     "gg_rows_orthonormalize": [ctypes.c_int, _c_i64p, _c_i64p, _c_dp, _vp],
+    "gg_centro_expand": [ctypes.c_int, _c_i64p, _c_i64p, _c_i64p, _c_dp, _c_dp, _vp],
     "gg_cov": [ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _c_dp,
                ctypes.c_int64, _c_dp, ctypes.c_int64, ctypes.c_int, _c_dp, _vp],
     "gg_grief_tables": [ctypes.c_int, ctypes.c_double, ctypes.c_double, _c_dp, ctypes.c_int64,
                         ctypes.c_int64, _c_dp, ctypes.c_int, _c_dp, ctypes.c_int, _c_dp, _c_dp,
                         ctypes.c_int, ctypes.c_int, _vp],
+    "gg_grief_tables_all": [ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                            _c_dp, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int),
+                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int),
+                            _c_dp, _c_dp, ctypes.c_int, ctypes.POINTER(ctypes.c_int), _vp],
     "gg_grief_phi": [_c_dp, _c_dp, ctypes.c_int, ctypes.c_int64, _c_dp, ctypes.c_int, _c_dp,
                      ctypes.c_int, ctypes.c_int, _c_dp, _vp],
     "gg_kr_work_elems": [ctypes.c_int, _c_i64p, ctypes.c_int64, _c_i64p],

@@ -159,18 +159,102 @@ def device_sym_eig(factors, max_sweeps=40):
     return outQ, outL
 
 
+def centro_halves(F):
+    """(Ke, Ko) with eig(F) = eig(Ke) u eig(Ko) for a symmetric centrosymmetric
+    F of even order m = 2h (J F J = F, J the exchange matrix -- every
+    stationary kernel on an evenly spaced grid: the GRIEF inducing factors).
+    With F = [[A, B], [B^T, J A J]] the orthogonal Q = [[I, I], [J, -J]] / sqrt 2
+    gives Q^T F Q = diag(A + B J, A - B J): the even eigenvectors of F are
+    [y; J y] / sqrt 2 (y of Ke), the odd ones [y; -J y] / sqrt 2 (y of Ko).
+    Half the order: a quarter of the tridiagonalisation work per half, two
+    independent problems.  F a device tensor; None when F is not
+    centrosymmetric to 16 eps max|F| (or m is odd or below 16).  The split
+    uses the centrosymmetric part (F + J F J) / 2 (a perturbation below the
+    eigensolver's own rounding)."""
+    t = dev.torch()
+    m = int(F.shape[0])
+    if m % 2 or m < 16:
+        return None
+    Fr = t.flip(F, (0, 1))
+    scale = float(F.abs().max())
+    if float((F - Fr).abs().max()) > 16 * np.finfo(np.float64).eps * max(scale, 1e-300):
+        return None
+    Fs = 0.5 * (F + Fr)
+    h = m // 2
+    A = Fs[:h, :h]
+    BJ = t.flip(Fs[:h, h:], (1,))
+    Ke = A + BJ
+    Ko = A - BJ
+    return 0.5 * (Ke + Ke.t()), 0.5 * (Ko + Ko.t())
+
+
+def centro_halves_host(F):
+    """centro_halves for a host factor (numpy): the split the GRIEF setup uses
+    on its host-built grid factors, whose halves then go to the device in one
+    copy."""
+    m = F.shape[0]
+    if m % 2 or m < 16:
+        return None
+    Fr = F[::-1, ::-1]
+    if np.abs(F - Fr).max() > 16 * np.finfo(np.float64).eps * max(np.abs(F).max(), 1e-300):
+        return None
+    Fs = 0.5 * (F + Fr)
+    h = m // 2
+    A = Fs[:h, :h]
+    BJ = Fs[:h, h:][:, ::-1]
+    Ke, Ko = A + BJ, A - BJ
+    return 0.5 * (Ke + Ke.T), 0.5 * (Ko + Ko.T)
+
+
+def centro_merge(lam_e, lam_o):
+    """The ascending spectrum of F from its halves, and for every position the
+    half (0 even, 1 odd) and the index within it."""
+    lam = np.concatenate([lam_e, lam_o])
+    half = np.concatenate([np.zeros(lam_e.size, np.int64), np.ones(lam_o.size, np.int64)])
+    idx = np.concatenate([np.arange(lam_e.size), np.arange(lam_o.size)])
+    order = np.argsort(lam, kind="stable")
+    return lam[order], half[order], idx[order]
+
+
+def centro_expand(Vh, hs, kes, kos):
+    """Eigenvector rows of centrosymmetric factors from their halves' rows
+    (gg_centro_expand, one launch): Vh = [V_e0, V_o0, V_e1, V_o1, ...] as
+    returned by device_sym_eig_tridiag_vectors (one buffer, in that order);
+    factor f gets (ke + ko) x 2h rows, the even ones first: [y; J y] / sqrt 2,
+    then [y; -J y] / sqrt 2."""
+    L = native.lib()
+    nf = len(hs)
+    tot = sum((int(ke) + int(ko)) * 2 * int(h) for h, ke, ko in zip(hs, kes, kos))
+    out = dev.empty(max(tot, 1))
+    native.check(L.gg_centro_expand(nf, native.i64_array(hs), native.i64_array(kes),
+                                    native.i64_array(kos), native.dptr(Vh[0]), native.dptr(out),
+                                    native.stream_ptr()), "gg_centro_expand")
+    res, o = [], 0
+    for h, ke, ko in zip(hs, kes, kos):
+        k, m = int(ke) + int(ko), 2 * int(h)
+        res.append(out[o:o + k * m].view(k, m))
+        o += k * m
+    return res
+
+
 def device_sym_eig_tridiag(factors):
     """Eigenvalues of symmetric factors (ascending, host arrays) by Householder
     tridiagonalisation + bisection on the device, plus a handle for
     device_sym_eig_tridiag_vectors (the GRIEF setup needs every eigenvalue but
-    only the selected eigenvectors: grief_kernel.py:168-190)."""
+    only the selected eigenvectors: grief_kernel.py:168-190).  Factors may be
+    host arrays or device tensors (no host round trip)."""
     L = native.lib()
-    mats = [np.asarray(f, dtype=np.float64) for f in factors]
+    t = dev.torch()
+    on_dev = all(dev.is_device_array(f) for f in factors)
+    mats = list(factors) if on_dev else [np.asarray(f, dtype=np.float64) for f in factors]
     for f in mats:
         if f.ndim != 2 or f.shape[0] != f.shape[1]:
             raise AssertionError("factor must be square")
-    m = [f.shape[0] for f in mats]
-    A = dev.to_device(np.concatenate([f.reshape(-1) for f in mats]))
+    m = [int(f.shape[0]) for f in mats]
+    if on_dev:
+        A = t.cat([f.to(t.float64).contiguous().reshape(-1) for f in mats])
+    else:
+        A = dev.to_device(np.concatenate([f.reshape(-1) for f in mats]))
     R = dev.empty(A.numel())
     lam = dev.empty(sum(m))
     marr = native.i64_array(m)

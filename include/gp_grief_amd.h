@@ -184,6 +184,13 @@ int gg_sym_eig_tridiag_vectors(int count, const int64_t* m, const double* R_dev,
                                double* Y_dev, gg_stream stream);
 /* Rows of each k[i] x m[i] block of V_dev (concatenated, row-major)
  * orthonormalised in place (classical Gram-Schmidt twice, last row first). */
+/* Eigenvector rows of centrosymmetric factors (order 2 h[f]) from their
+ * half-order problems: V_dev holds, per factor, the even half's ke[f] rows
+ * then the odd half's ko[f] rows (h[f] each); out_dev receives per factor
+ * ke[f] + ko[f] rows of 2 h[f]: [y; J y] / sqrt 2 (even), [y; -J y] / sqrt 2
+ * (odd).  The GRIEF subset setup's split of grief_kernel.py:168-190.       */
+int gg_centro_expand(int nf, const int64_t* h, const int64_t* ke, const int64_t* ko,
+                     const double* V_dev, double* out_dev, gg_stream stream);
 int gg_rows_orthonormalize(int count, const int64_t* k, const int64_t* m, double* V_dev,
                            gg_stream stream);
 
@@ -207,6 +214,16 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
                     int64_t x_stride, int64_t n, const double* xg_dev, int m,
                     const double* qsel_dev, int u, double* ltab_dev, double* stab_dev, int U,
                     int col0, gg_stream stream);
+/* The tables of all nf dimensions in one launch (the same values as nf
+ * gg_grief_tables calls; GriefKernel.cov's expand_SKC loop over dims,
+ * gp_grief/kern/grief_kernel.py:96-104).  Host arrays of nf entries; factor f
+ * reads x_dev[a * x_stride + x_offsets[f]].                                  */
+int gg_grief_tables_all(int nf, const int* kinds, const double* variances,
+                        const double* lengthscales, const double* x_dev, int64_t x_stride,
+                        const int64_t* x_offsets, int64_t n, const double* const* xg_devs,
+                        const int* ms, const double* const* qsel_devs, const int* us,
+                        double* ltab_dev, double* stab_dev, int U, const int* col0s,
+                        gg_stream stream);
 /* Phi[a][j] = prod_f stab[a][c_jf] * exp(sum_f ltab[a][c_jf] - log_lam[j] / 2)
  * (GriefKernel.cov, gp_grief/kern/grief_kernel.py:96-104); cidx: p x d int32.
  * transposed != 0 writes Phi^T (p x n).                                      */

@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 3: X uploaded once per model (own "h2d" stage); C2 Phi stage breakdown by kernel trace
+set -o pipefail
+cd "$(dirname "$0")/../.."
+export TMPDIR=/tmp
+O=gpurun_out/r03y
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_grief.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -1 $O/pytest.log
+[ $rc -eq 0 ] || { grep -E "^E |FAILED|Error" $O/pytest.log | head -20; exit $rc; }
+timeout -k 10 300 python -u bench_grief.py --configs C2 --cpu off > $O/grief.jsonl 2> $O/grief.err || { tail -5 $O/grief.err; exit 1; }
+python -c "
+import json
+for l in open('$O/grief.jsonl'):
+    d=json.loads(l); print(d['config']['workload'], round(d['fit_ms'],3), {k: round(v,3) for k,v in d['stage_ms'].items()})"
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $O/kt -o run -- python3 -u bench_grief.py --configs C2 --cpu off > $O/kt.log 2>&1 || { tail -5 $O/kt.log; exit 1; }
+echo done

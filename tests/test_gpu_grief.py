@@ -399,6 +399,78 @@ def test_grief_subset_setup_matches_full(gg, monkeypatch):
     assert rel(m1, m0) < 1e-9
 
 
+@pytest.mark.parametrize("m,ls", [(128, 0.1), (64, 0.2), (200, 0.05), (32, 0.3)])
+def test_centro_halves_eigenpairs(gg, m, ls):
+    """A centrosymmetric grid factor's spectrum from its two half-order
+    problems (tensors.centro_halves / centro_merge / centro_expand) against
+    numpy's LAPACK eigh: eigenvalues to 1e-13 m ||K||, selected eigenvectors
+    to 1e-9 up to sign, orthonormal to 1e-12; odd m and a perturbed
+    (non-centrosymmetric) factor are refused."""
+    import torch
+    from gp_grief_amd.tensors import (centro_expand, centro_halves, centro_merge,
+                                      device_sym_eig_tridiag, device_sym_eig_tridiag_vectors)
+    F = _grid_factor(m, ls, noise=1e-8)
+    Fd = torch.tensor(F, device="cuda")
+    Ke, Ko = centro_halves(Fd)
+    (le, lo), h = device_sym_eig_tridiag([Ke, Ko])
+    lam, half, idx = centro_merge(le, lo)
+    ln, Qn = np.linalg.eigh(F)
+    scale = np.abs(ln).max()
+    assert np.abs(lam - ln).max() <= 1e-13 * scale * m
+    k = min(12, m // 4)   # well-separated top eigenpairs (vectors to 1e-9)
+    sel = np.arange(m - k, m)
+    se, so = np.sort(idx[sel][half[sel] == 0]), np.sort(idx[sel][half[sel] == 1])
+    Vh = device_sym_eig_tridiag_vectors(h, [se, so])
+    V = centro_expand(Vh, [m // 2], [se.size], [so.size])[0].cpu().numpy()
+    # rows: the even half's selected indices, then the odd half's
+    where = {(int(hh), int(i)): kk for kk, (hh, i) in enumerate(zip(half, idx))}
+    full = [where[(0, int(v))] for v in se] + [where[(1, int(v))] for v in so]
+    assert np.abs(V @ V.T - np.eye(k)).max() < 1e-12
+    Qs = Qn[:, full].T
+    signs = np.sign(np.sum(V * Qs, axis=1)).reshape(-1, 1)
+    assert np.abs(V - signs * Qs).max() < 1e-9
+    assert np.abs(V @ F - lam[full][:, None] * V).max() < 1e-12 * scale
+    assert centro_halves(torch.tensor(_grid_factor(m + 1, ls), device="cuda")) is None
+    Fp = F.copy()
+    Fp[0, 1] += 1e-6
+    Fp[1, 0] += 1e-6
+    assert centro_halves(torch.tensor(Fp, device="cuda")) is None
+
+
+def test_grief_centro_setup_matches_unsplit(gg, monkeypatch):
+    monkeypatch.setenv("GG_EIG_CENTRO_MIN", "16")
+    _centro_setup_cases(gg, monkeypatch)
+
+
+def _centro_setup_cases(gg, monkeypatch):
+    """The GRIEF setup with the factors split into half-order problems
+    (default) and without (GG_EIG_CENTRO=0): same eigenvalue selection, LML to
+    1e-10, predictions to 1e-9, Matern-5/2 and RBF factors of even and odd
+    order (odd ones stay unsplit)."""
+    rng = np.random.default_rng(9)
+    d, n, p = 3, 3000, 300
+    x = rng.random((n, d))
+    y = (np.sin(5 * x).sum(axis=1) + 0.1 * rng.standard_normal(n)).reshape(-1, 1)
+    xt = rng.random((200, d))
+    for ms, kind in (((48, 40, 56), "RBF"), ((48, 40, 56), "Matern52"), ((47, 40, 56), "RBF")):
+        out = []
+        for flag in ("1", "0"):
+            monkeypatch.setenv("GG_EIG_CENTRO", flag)
+            kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=0.15 + 0.03 * i)
+                  for i in range(d)]
+            grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1) for m in ms])
+            kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+            model = gg.models.GPGriefModel(x, y, kern, noise_var=0.05)
+            ll = float(np.squeeze(model.log_likelihood()))
+            mean = np.asarray(model.predict(xt)[0]).reshape(-1)
+            out.append((ll, mean, kern._log_lam.copy(), kern._Quu_full is None))
+        (l1, m1, g1, s1), (l0, m0, g0, s0) = out
+        assert s1 and s0
+        assert np.allclose(g1, g0, rtol=1e-11, atol=1e-11)
+        assert abs(l1 - l0) <= 1e-10 * abs(l0)
+        assert rel(m1, m0) < 1e-9
+
+
 def test_grief_subset_falls_back_on_clusters(gg, monkeypatch):
     """A factor with a clustered spectrum (a kernel so short that K ~ I) fails
     the separation test: the setup takes the full QL path and stays correct."""

@@ -33,13 +33,18 @@ def main():
             torch.cuda.synchronize()
             times.setdefault(key, []).append(1e3 * (time.perf_counter() - t0))
             return r
+        import inspect
+        if isinstance(inspect.getattr_static(mod, fname), staticmethod):
+            g = staticmethod(g)
         setattr(mod, fname, g)
 
     wrap(kern_mod, "device_sym_eig_tridiag", "tridiag_values")
     wrap(kern_mod, "device_sym_eig_tridiag_vectors", "vectors")
     wrap(kern_mod, "device_sym_eig", "full_eig")
-    for meth, key in (("cov_grid", "cov_grid"), ("_select", "select"),
-                      ("_separated", "separated"), ("_build_device_basis", "basis")):
+    for meth, key in (("cov_grid", "cov_grid"), ("_grid_factors_host", "factors"),
+                      ("_select", "select"), ("_separated", "separated"),
+                      ("_centro_vectors", "vectors_centro"),
+                      ("_build_device_basis", "basis")):
         wrap(kern_mod.GriefKernel, meth, key)
     for r in range(reps):
         kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=0.2 * (1 + 0.05 * i))
