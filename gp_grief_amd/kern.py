@@ -399,30 +399,16 @@ class GriefKernel(GridKernel):
         L = native.lib()
         ltab = dev.empty(max(n * B["U"], 1))
         stab = dev.empty(max(n * B["U"], 1))
-        # every dimension's table in one launch (factor f reads input dim d-1-f)
-        kinds = (ctypes.c_int * d)()
-        var = (ctypes.c_double * d)()
-        ls = (ctypes.c_double * d)()
-        xoff = (ctypes.c_int64 * d)()
-        xgp = (ctypes.c_void_p * d)()
-        qsp = (ctypes.c_void_p * d)()
-        ms = (ctypes.c_int * d)(*[int(v) for v in B["m"]])
-        us = (ctypes.c_int * d)(*[int(v) for v in B["u"]])
-        c0 = (ctypes.c_int * d)(*[int(v) for v in B["col0"]])
-        for f in range(d):
-            i = d - 1 - f
-            kern = self.kern_list[i]
-            if not isinstance(kern, Stationary) or kern._children:
-                raise NotImplementedError("GRIEF device basis needs plain stationary kernels")
-            kinds[f] = native.GG_KERN[kern._kind]
-            var[f] = float(np.asarray(kern.variance).reshape(-1)[0])
-            ls[f] = float(np.asarray(kern.lengthscale).reshape(-1)[0])
-            xoff[f] = i
-            xgp[f] = native.dptr(B["xg"][f])
-            qsp[f] = native.dptr(B["qsel"][f])
-        native.check(L.gg_grief_tables_all(d, kinds, var, ls, native.dptr(xd), d, xoff, n, xgp,
-                                           ms, qsp, us, native.dptr(ltab), native.dptr(stab),
-                                           B["U"], c0, native.stream_ptr()), "gg_grief_tables_all")
+        # every dimension's table in one launch (factor f reads input dim d-1-f);
+        # the host argument arrays are built once per basis
+        a = B.get("tab_args")
+        if a is None:
+            a = self._table_args()
+            B["tab_args"] = a
+        native.check(L.gg_grief_tables_all(d, a["kinds"], a["var"], a["ls"], native.dptr(xd), d,
+                                           a["xoff"], n, a["xgp"], a["ms"], a["qsp"], a["us"],
+                                           native.dptr(ltab), native.dptr(stab), B["U"], a["c0"],
+                                           native.stream_ptr()), "gg_grief_tables_all")
         p = self.n_eigs
         phi = dev.empty(n * p)
         native.check(L.gg_grief_phi(native.dptr(ltab), native.dptr(stab), B["U"], n,
@@ -430,6 +416,29 @@ class GriefKernel(GridKernel):
                                     int(bool(transposed)), native.dptr(phi),
                                     native.stream_ptr()), "gg_grief_phi")
         return phi.reshape(p, n) if transposed else phi.reshape(n, p)
+
+    def _table_args(self):
+        """ctypes arrays of gg_grief_tables_all for the current basis."""
+        B = self._dev_basis
+        d = self.grid_dim
+        a = dict(kinds=(ctypes.c_int * d)(), var=(ctypes.c_double * d)(),
+                 ls=(ctypes.c_double * d)(), xoff=(ctypes.c_int64 * d)(),
+                 xgp=(ctypes.c_void_p * d)(), qsp=(ctypes.c_void_p * d)(),
+                 ms=(ctypes.c_int * d)(*[int(v) for v in B["m"]]),
+                 us=(ctypes.c_int * d)(*[int(v) for v in B["u"]]),
+                 c0=(ctypes.c_int * d)(*[int(v) for v in B["col0"]]))
+        for f in range(d):
+            i = d - 1 - f
+            kern = self.kern_list[i]
+            if not isinstance(kern, Stationary) or kern._children:
+                raise NotImplementedError("GRIEF device basis needs plain stationary kernels")
+            a["kinds"][f] = native.GG_KERN[kern._kind]
+            a["var"][f] = float(np.asarray(kern.variance).reshape(-1)[0])
+            a["ls"][f] = float(np.asarray(kern.lengthscale).reshape(-1)[0])
+            a["xoff"][f] = i
+            a["xgp"][f] = native.dptr(B["xg"][f])
+            a["qsp"][f] = native.dptr(B["qsel"][f])
+        return a
 
     def cov_grad(self, x, grad_dim):
         raise NotImplementedError  # needs GPyKernel gradients (grid_kernel.py:196-199)
