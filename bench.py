@@ -294,20 +294,22 @@ def sharded_roofline(phases, n, m, d, world, fold_mask):
 
 
 # ---------------------------------------------------------------- roofline
-def launch_passes(d, recurrence, fusion=0, xdefer=False):
+def launch_passes(d, recurrence, fusion=0, xdefer=False, rq=False):
     """Algorithmic 8-byte passes over N of each mode-product launch position of
     one CG iteration (reads + writes, gg_kron.hip kron_apply / MpFuse),
     averaged over iterations.  xdefer: the x update runs every other
     iteration as x += c0 p0 + c1 p1 (4 passes per two iterations, 2 per
-    iteration on average instead of 3)."""
+    iteration on average instead of 3).  rq: r.q from the conjugacy identity
+    (gg_cg_set_rq 1), so the epilogue reads p only."""
     if d == 1:
         return [4] if recurrence == "fused" else [5]
     passes = [2] * d
     if recurrence == "fused":
         # prologue: r, q_old read, r written (p_old is X); layout 0 also writes p_new
         passes[0] += 3 if fusion else 4
-        # epilogue: p and r read (shift, p.q, r.q); layouts 1/2 also write p_new
-        passes[d - 1] += 3 if fusion else 2
+        # epilogue: p and r read (shift, p.q, r.q; p only with the conjugacy
+        # r.q); layouts 1/2 also write p_new
+        passes[d - 1] += 3 if fusion else (1 if rq else 2)
         xp = 2.0 if (xdefer and fusion != 2) else 3.0
         if fusion == 2:
             passes[d - 1] += 2  # x += alpha p_old in the epilogue (x read + written)
@@ -348,12 +350,12 @@ def dominant_group(per_pos, kinds):
 
 
 def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0,
-                    xdefer=False):
+                    xdefer=False, rq=False):
     """fold_mask bit k: mode product k runs on the centrosymmetric split
     (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
     the roofline prices the work the kernel actually does."""
     flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
-    passes = launch_passes(d, recurrence, fusion, xdefer)
+    passes = launch_passes(d, recurrence, fusion, xdefer, rq)
     kinds = launch_kernels(d, recurrence, fusion)
     group, kind = dominant_group(per_pos, kinds)
     dom = group[0]
@@ -433,7 +435,7 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
-def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True):
+def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True, rq=False):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
     positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
     when they were taken on this workload, recurrence, fusion layout and fold
@@ -452,6 +454,8 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True)
         return None, "PMC passes taken with another fold state"
     if int(rec.get("x_deferred", 0)) != int(xdefer):
         return None, "PMC passes taken with another x-update schedule"
+    if int(rec.get("rq_identity", 0)) != int(rq):
+        return None, "PMC passes taken with another r.q source"
     if rec.get("source_sha256") != kernel_source_hash():
         return None, "stale: the kernel sources changed since the PMC passes (%s)" % PMC_JSON
     if not rec.get("calibrated_on_own_pattern"):
@@ -651,9 +655,9 @@ def main():
     per_pos = [t / n_mv for t in mode_ms]
     fold_mask = K._device().fold_mask()
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
-                                  solver.fusion, fold_mask, solver.xdefer)
+                                  solver.fusion, fold_mask, solver.xdefer, solver.rq)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
-                               fold_mask, solver.xdefer)
+                               fold_mask, solver.xdefer, solver.rq)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -674,6 +678,7 @@ def main():
                    "cg_recurrence": solver.recurrence,
                    "cg_fusion_layout": solver.fusion,
                    "cg_x_deferred": solver.xdefer,
+                   "cg_rq_identity": solver.rq,
                    "fold_mask": fold_mask,
                    "parallelism": "single-gpu"},
         "roofline": roof,

@@ -110,6 +110,11 @@ struct MpFuse {
   double* p_out = nullptr;
   const CgScalars* sc = nullptr;
   double* rr_part = nullptr;
+  // conjugacy r.q (gg_cg_set_rq 1): the CG prologue also writes block partials
+  // of p_new.q_old to rr_part[pqo_stride + blk] (0 = off), and the last epilogue
+  // gets er == nullptr -- r_j.q_j = p_j.q_j - beta_j p_j.q_{j-1} (A symmetric)
+  // replaces the epilogue's pass over r
+  int64_t pqo_stride = 0;
   // side job of the second mode product (fused CG): x += alpha p_side over
   // this workgroup's slice [blk * schunk, (blk + 1) * schunk) of sn elements
   double* sx = nullptr;

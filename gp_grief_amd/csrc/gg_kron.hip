@@ -64,7 +64,8 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
                                           int p, int jt0, const double* __restrict__ xs,
                                           double shift, double* __restrict__ dot_partials,
                                           const OutMap& om, const MpFuse& fz, double rr_acc,
-                                          int64_t b0, int hp, double* red, int64_t blk) {
+                                          int64_t b0, int hp, double* red, int64_t blk,
+                                          double pqo_acc = 0.0) {
   constexpr int kThreads = kWaves * 64;
   const int lane = threadIdx.x & 63;
   // ---- epilogue: D[b][j] at lane (j & 15), register r = row 4r + (lane >> 4).
@@ -123,6 +124,9 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
   }
   double dsum = 0.0, rqsum = 0.0, qqsum = 0.0;
   const double* __restrict__ er = fz.er;
+  // er == nullptr with the fused epilogue: r.q from the conjugacy identity
+  // (MpFuse::pqo_stride), no pass over r; the recomputing layouts need r
+  const bool rq_on = (kEpi >= 2) && (kEpi == 3 || kEpi == 4 || er != nullptr);
   // kEpi 2: fused-CG epilogue (p.q, r.q, q.q) of fusion layout 0; 4: layout 1
   // (p_new recomputed from p_old and r, and stored); 3: layout 2 (also the x
   // update: one more operand per element, so one tile per load batch)
@@ -195,10 +199,10 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
         if (kIdent) {
           const uint32_t o = boff(r, t);
           xo[r] = ok ? *reinterpret_cast<const double*>(xbase + o) : 0.0;
-          eo[r] = (ok && edots) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
+          eo[r] = (ok && rq_on) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
         } else {
           xo[r] = ok ? xs[rowoff[r] + co] : 0.0;
-          eo[r] = (ok && edots) ? er[rowoff[r] + co] : 0.0;
+          eo[r] = (ok && rq_on) ? er[rowoff[r] + co] : 0.0;
         }
       }
     };
@@ -286,7 +290,8 @@ __device__ __forceinline__ void mp_finish(const d4 (&acc)[JT], double* __restric
       }
     }
   }
-  mp_block_sums<kWaves, CGP, edots, kRaw>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz, red, blk);
+  mp_block_sums<kWaves, CGP, edots, kRaw>(dsum, edots ? rqsum : pqo_acc, qqsum, rr_acc,
+                                          dot_partials, fz, red, blk);
   if (kEpi >= 1) mp_side_job<kThreads>(fz, blk);
 }
 
@@ -464,6 +469,7 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
         }                                                                             \
         v_ = cg_first ? r_ : fma(cg_beta, v_, r_);                                    \
         if (Pout != nullptr && ok_ && hp == 0) Pout[e_] = v_;                         \
+        if (CGP == 2 && pqo_on && ok_ && hp == 0) pqo_acc = fma(v_, qq[s_], pqo_acc); \
       }                                                                               \
       a[s_] = ok_ ? v_ : 0.0;                                                         \
     }                                                                                 \
@@ -476,8 +482,8 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
 
   double a_cur[kKC], a_nxt[kKC], r_cur[kKC], r_nxt[kKC], q_cur[kKC], q_nxt[kKC];
   double stx[kPerT], sty[kPerT];
-  bool cg_first = false, cg_pending = false;
-  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0;
+  bool cg_first = false, cg_pending = false, pqo_on = false;
+  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
   double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
   if (CGP == 3) {
     lz_cy = fz.coef[2];
@@ -489,6 +495,8 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     if (CGP == 2) {
       cg_pending = fz.sc->pending != 0;
       cg_alpha = fz.sc->alpha;
+      // p_new.q_old (conjugacy r.q); q_old is not A p_old on the first step
+      pqo_on = fz.pqo_stride > 0 && !cg_first;
     }
   }
   GG_STAGE_LOAD(0, st);
@@ -561,7 +569,8 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
     }
   }
   mp_finish<JT, kWaves, kSplit, kIdent, kEpi, CGP, false, kEpiBatch, (kOpt & 4) != 0>(
-      acc, Y, M, p, jt0, xs, shift, dot_partials, om, fz, rr_acc, b0, hp, lds, blockIdx.x);
+      acc, Y, M, p, jt0, xs, shift, dot_partials, om, fz, rr_acc, b0, hp, lds, blockIdx.x,
+      pqo_acc);
 }
 
 // All-LDS-DMA pipeline (plain / side-job / fused-epilogue roles, CGP = 0):
@@ -1133,6 +1142,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             fz.q_old = cg->q_old;
             fz.rr_part = cg->rr_part;
           }
+          if (pro == 2) fz.pqo_stride = cg->pqo_stride;
           if (pro == 7) fz.coef = cg->coef;
         }
         if (side && cg->xdefer == 2) {

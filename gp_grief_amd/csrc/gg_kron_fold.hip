@@ -107,8 +107,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   const double* Qa = fz.q_old;   // CGP 3 writes over q_old (same lane): no restrict
   double* Pout = fz.p_out;
 
-  bool cg_first = false, cg_pending = false;
-  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0;
+  bool cg_first = false, cg_pending = false, pqo_on = false;
+  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
   double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
   if (CGP == 3) {
     lz_cy = fz.coef[2];
@@ -120,6 +120,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     if (CGP == 2) {
       cg_pending = fz.sc->pending != 0;
       cg_alpha = fz.sc->alpha;
+      // p_new.q_old (conjugacy r.q); q_old is not A p_old on the first step
+      pqo_on = fz.pqo_stride > 0 && !cg_first;
     }
   }
 
@@ -177,6 +179,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
       }
       v = cg_first ? r : fma(cg_beta, v, r);
       if (Pout != nullptr && ok) Pout[e] = v;
+      if (CGP == 2 && pqo_on && ok) pqo_acc = fma(v, q, pqo_acc);
     }
     return v;
   };
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   if (kStg) {
     double* wl = lds + (int64_t)wave * 4 * m;   // this wave's 4 x m image
     const double* __restrict__ er = fz.er;
+    const bool rq_on = edots && (kRecomp || er != nullptr);   // null: conjugacy r.q
     double* __restrict__ epo = kRecomp ? fz.ep_out : nullptr;
     const bool first = kRecomp && fz.sc->first != 0;
     const double beta = kRecomp ? fz.sc->beta : 0.0;
@@ -377,7 +381,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
           av[u] = ok ? *reinterpret_cast<const double2*>(wl + 2 * i2) : double2{0.0, 0.0};
           pv[u] = (ok && xs != nullptr) ? *reinterpret_cast<const double2*>(xs + g)
                                         : double2{0.0, 0.0};
-          ev[u] = (ok && edots) ? *reinterpret_cast<const double2*>(er + g) : double2{0.0, 0.0};
+          ev[u] = (ok && rq_on) ? *reinterpret_cast<const double2*>(er + g) : double2{0.0, 0.0};
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -459,8 +463,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     // shift / dots: the loads of half-tile e + 1 are issued before e's stores
     // (CDNA4 retires vmcnt in order and stores count)
     const double* __restrict__ er = fz.er;
+    const bool rq_on = edots && (kRecomp || er != nullptr);
     const char* xbase = reinterpret_cast<const char*>(xs + b0u * m);
-    const char* ebase = edots ? reinterpret_cast<const char*>(er + b0u * m) : nullptr;
+    const char* ebase = rq_on ? reinterpret_cast<const char*>(er + b0u * m) : nullptr;
     char* pbase = kRecomp ? reinterpret_cast<char*>(fz.ep_out + b0u * m) : nullptr;
     const bool first = kRecomp && fz.sc->first != 0;
     const double beta = kRecomp ? fz.sc->beta : 0.0;
@@ -472,7 +477,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
         const bool ok = cok && (lane >> 4) + 4 * r < rows_left;
         const uint32_t o = boff_of(r, e);
         xo[r] = ok ? *reinterpret_cast<const double*>(xbase + o) : 0.0;
-        eo[r] = (ok && edots) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
+        eo[r] = (ok && rq_on) ? *reinterpret_cast<const double*>(ebase + o) : 0.0;
       }
     };
     load_e(0, xv[0], ev[0]);
@@ -500,8 +505,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     }
   }
   // the staged epilogue's images occupy the first 16 m doubles of LDS
-  mp_block_sums<kWaves, CGP, edots, false>(dsum, rqsum, qqsum, rr_acc, dot_partials, fz,
-                                           kStg ? lds + 16 * m : lds, blockIdx.x);
+  mp_block_sums<kWaves, CGP, edots, false>(dsum, edots ? rqsum : pqo_acc, qqsum, rr_acc,
+                                           dot_partials, fz, kStg ? lds + 16 * m : lds,
+                                           blockIdx.x);
   if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
 }
 

@@ -13,7 +13,8 @@ typedef void (*mode_kernel_t)(const double*, double*, const double*, int64_t, in
                               MpFuse);
 
 // Per-workgroup partial sums of a mode product: p.q (+ r.q, q.q when edots)
-// of the epilogue, r.r (or |w|^2) of the fused prologue.  Called after the
+// of the epilogue, r.r (or |w|^2) of the fused prologue; a CG prologue passes
+// p_new.q_old in the r.q slot (MpFuse::pqo_stride).  Called after the
 // k-loop's last barrier (LDS is free); red: 4 * kWaves doubles of LDS.
 template <int kWaves, int CGP, bool edots, bool kRaw>
 __device__ __forceinline__ void mp_block_sums(double dsum, double rqsum, double qqsum,
@@ -47,6 +48,8 @@ __device__ __forceinline__ void mp_block_sums(double dsum, double rqsum, double 
     if (i == 1 && edots && want_dot) dot_partials[fz.pstride + blk] = s;
     if (i == 2 && want_dot && edots) dot_partials[2 * fz.pstride + blk] = s;
     if (i == 3 && want_rr) fz.rr_part[blk] = s;
+    if (i == 1 && CGP == 2 && !edots && want_rr && fz.pqo_stride > 0)
+      fz.rr_part[fz.pqo_stride + blk] = s;
   }
 }
 

@@ -257,20 +257,25 @@ __global__ void cg_x_flushed_kernel(CgScalars* sc) {
 // direction buffers keep the pair alive.
 __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     const double* __restrict__ rr_part, int64_t nrr, const double* __restrict__ mv_part,
-    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new, int xmode) {
+    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new, int xmode, int rq_ident) {
   if (sc->done) return;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
     a0 += mv_part[i];
-    a1 += mv_part[pstride + i];
+    if (!rq_ident) a1 += mv_part[pstride + i];
     a2 += mv_part[2 * pstride + i];
   }
+  // conjugacy r.q: p_j = r_j + beta_j p_{j-1}, so r_j.q_j = p_j.q_j -
+  // beta_j p_{j-1}.A p_j = p_j.q_j - beta_j p_j.q_{j-1} (A symmetric); the
+  // prologue summed p_j.q_{j-1} (zero on the first step, where beta = 0)
+  if (rq_ident)
+    for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a1 += rr_part[nrr + i];
   const bool pend = sc->pending != 0;
   if (pend)
     for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a3 += rr_part[i];
   const double pq = block_sum(a0);
   __syncthreads();
-  const double rq = block_sum(a1);
+  const double rq_raw = block_sum(a1);   // r.q, or p_j.q_{j-1} (rq_ident)
   __syncthreads();
   const double qq = block_sum(a2);
   __syncthreads();
@@ -293,6 +298,7 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     }
     const double rho = sc->rho;
     const double alpha = rho / pq;
+    const double rq = rq_ident ? pq - sc->beta * rq_raw : rq_raw;   // beta_j: not yet replaced
     double rt = rho - 2.0 * alpha * rq + alpha * alpha * qq;
     sc->pq = pq;
     sc->rq = rq;
@@ -574,8 +580,9 @@ struct gg_cg {
   int xdefer = 2;              // layouts 0 / 1: x updated in deferred pairs (1: every
                                // other iteration; 2: balanced, half a pair per iteration)
   double* partials = nullptr;  // device, max(kVecBlocks, 3 x matvec partials)
-  double* rr_part = nullptr;   // device, prologue r.r partials (fused)
+  double* rr_part = nullptr;   // device, prologue r.r (+ p_new.q_old) partials (fused)
   int64_t rr_count = 0;
+  int rq = 1;                  // layout 0: r.q from the conjugacy identity (gg_cg_set_rq)
   gg::CgScalars* sc = nullptr; // device
   gg::CgScalars* sc_host = nullptr;  // pinned mirror
   const double* b = nullptr;
@@ -721,6 +728,8 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
       const char* xd = getenv("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
       if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
+      const char* rqe = getenv("GG_CG_RQ");       // A/B knob: 0 (epilogue reads r) or 1
+      if (rqe) cg->rq = std::min(2, std::max(0, atoi(rqe)));   // 2: diagnostic
       cg->mv_partials = gg::kron_partials_needed(K, false);
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
       GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
@@ -730,7 +739,7 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
                   (reinterpret_cast<uintptr_t>(work_dev) & 15) == 0;
       if (cg->fused) {
         cg->rr_count = gg::kron_prologue_blocks(K);
-        GG_HIP(hipMalloc(&cg->rr_part, cg->rr_count * sizeof(double)));
+        GG_HIP(hipMalloc(&cg->rr_part, 2 * cg->rr_count * sizeof(double)));
       }
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
@@ -852,6 +861,22 @@ int gg_cg_get_xdefer(const gg_cg* cg, int* on) {
   });
 }
 
+int gg_cg_set_rq(gg_cg* cg, int mode) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set the r.q source before gg_cg_start");
+    GG_REQUIRE(mode == 0 || mode == 1, GG_ERR_VALUE, "r.q mode must be 0 or 1");
+    cg->rq = mode;
+  });
+}
+
+int gg_cg_get_rq(const gg_cg* cg, int* mode) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && mode, GG_ERR_VALUE, "NULL argument");
+    *mode = (cg->fused && cg->fusion == 0 && cg->rq) ? 1 : 0;
+  });
+}
+
 int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
   return gg::guard([&] {
     GG_REQUIRE(cg && fused, GG_ERR_VALUE, "NULL argument");
@@ -917,13 +942,17 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.sn = n;
         fz.xdefer = xmode;
         fz.first_dst = cg->first_dst;
-        fz.er = cg->r;
+        // r.q: conjugacy identity (layout 0: the prologue adds p_new.q_old
+        // partials, the epilogue skips its pass over r) or read in the epilogue
+        const bool rq_ident = cg->rq != 0 && cg->fusion == 0;
+        fz.er = (rq_ident && cg->rq != 2) ? nullptr : cg->r;
+        fz.pqo_stride = rq_ident ? cg->rr_count : 0;
         fz.pstride = cg->mv_partials;
         gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
                        &cg->sc->done, s, &nparts, &fz, 2, ev);
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
                            cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc,
-                           xdefer ? (const double*)cg->p2 : nullptr, xmode);
+                           xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
         GG_LAUNCH_CHECK();
         if (xmode == 2) {
           // (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2}): the

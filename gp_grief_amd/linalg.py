@@ -115,12 +115,15 @@ class KronCG(object):
     deferred pairs of steps, two steps in one pass -- 2: each pair applied to
     half of x in each of the next two iterations (every side launch carries one
     pass), 1: the whole pair every other iteration, 0: every iteration (True =
-    2, False = 0).  recurrence="textbook":
+    2, False = 0).  rq (layout 0; default 1): beta's r.q from the conjugacy
+    identity p.q - beta p.q_prev (the prologue sums p.q_prev; the last
+    epilogue does not read r), 0: r.q read in the epilogue.
+    recurrence="textbook":
     scipy's operation order, with a separate x / r update pass.  Both leave
     iterate() in the textbook state.
     """
 
-    def __init__(self, K, shift, recurrence="fused", fusion=None, xdefer=None):
+    def __init__(self, K, shift, recurrence="fused", fusion=None, xdefer=None, rq=None):
         from . import device as dev
         from . import native
         self.K = K
@@ -151,6 +154,10 @@ class KronCG(object):
             native.check(L.gg_cg_set_xdefer(h, mode), "gg_cg_set_xdefer")
         native.check(L.gg_cg_get_xdefer(h, ctypes.byref(f)))
         self.xdefer = f.value
+        if rq is not None:
+            native.check(L.gg_cg_set_rq(h, int(bool(rq))), "gg_cg_set_rq")
+        native.check(L.gg_cg_get_rq(h, ctypes.byref(f)))
+        self.rq = f.value
         self.n = int(K.shape[0])
         self.x = None
 

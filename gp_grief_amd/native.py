@@ -61,6 +61,8 @@ SIGNATURES = {
     "gg_cg_get_fusion": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_xdefer": [_vp, ctypes.c_int],
     "gg_cg_get_xdefer": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_set_rq": [_vp, ctypes.c_int],
+    "gg_cg_get_rq": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
     "gg_cg_profile": [_vp, ctypes.c_int],

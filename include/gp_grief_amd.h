@@ -133,6 +133,14 @@ int gg_cg_get_fusion(const gg_cg* cg, int* layout);
  * set: before gg_cg_start; get: 1 when the deferral is in effect.         */
 int gg_cg_set_xdefer(gg_cg* cg, int on);
 int gg_cg_get_xdefer(const gg_cg* cg, int* on);
+/* Fused recurrence, layout 0: where r_j.q_j (for beta's |r - alpha q|^2
+ * expansion) comes from.  1 (default; GG_CG_RQ=0 at gg_cg_create turns it
+ * off): the conjugacy identity r_j.q_j = p_j.q_j - beta_j p_j.q_{j-1}, with
+ * p_j.q_{j-1} summed by the first mode product's prologue (which reads q_{j-1}
+ * anyway), so the last epilogue makes no pass over r; 0: the epilogue reads r.
+ * set: before gg_cg_start; get: 1 when the identity is in effect.         */
+int gg_cg_set_rq(gg_cg* cg, int mode);
+int gg_cg_get_rq(const gg_cg* cg, int* mode);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */

@@ -47,6 +47,8 @@ def test_roofline_folded_launches_are_hbm_bound():
     # x deferred to every other iteration: 1 pass per side launch on average
     assert bench.launch_passes(4, "fused", 0, True) == [6, 3, 3, 4]
     assert bench.launch_passes(4, "fused", 1, True) == [5, 3, 3, 5]
+    # conjugacy r.q: the epilogue reads p only
+    assert bench.launch_passes(4, "fused", 0, 2, True) == [6, 3, 3, 3]
     assert extra["fold_mask"] == 0b1111
     assert abs(extra["matvec_dense_equivalent_tflops"] - 2 * extra["matvec_tflops"]) < 1e-9
 

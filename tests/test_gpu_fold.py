@@ -239,3 +239,63 @@ def test_fold_cg_xdefer_modes_agree(gg, fold_small, dims):
             xs.append(cg.x.cpu().numpy())
         assert rel(xs[1], xs[0]) < 1e-12
         assert rel(xs[2], xs[0]) < 1e-12
+
+
+@pytest.mark.parametrize("dims,centro", [((24, 20, 16, 18), True), ((30, 22, 14), True),
+                                         ((26, 18, 20, 12), False)])
+def test_cg_rq_identity_matches_epilogue_rq(gg, fold_small, dims, centro):
+    """beta's r.q from the conjugacy identity (p.q - beta p.q_prev, the
+    prologue summing p.q_prev; gg_cg_set_rq 1) against r.q read in the
+    epilogue (0): the same iterate at every iteration count, single calls and
+    chunked calls (each re-entry starts with a non-pending prologue), on the
+    folded kernels and on mode_product_kernel (non-centrosymmetric factors);
+    and the same convergence to a tolerance."""
+    import torch
+    rng = np.random.default_rng(11)
+    F = []
+    for k, m in enumerate(dims):
+        if centro:
+            F.append(grid_factor(m, 0.15 * (1 + 0.05 * k)))
+        else:
+            g = np.sort(rng.uniform(0.0, 1.0, m))
+            F.append(oracle.cov_1d("RBF", g, g, 1.0, 0.2) + 1e-10 * np.eye(m))
+    K = kron(gg, F)
+    assert (fold_mask(K) != 0) == centro
+    n = int(np.prod(dims))
+    b = torch.tensor(rng.standard_normal(n), device="cuda")
+    s = 0.05
+    # at s = 0.05 the system is ill-conditioned enough that any rounding
+    # change grows by ~1e8 over 25 iterations (the textbook and the fused
+    # recurrence differ by 5e-8 there): the identity must stay as close to the
+    # textbook iterate as the epilogue r.q does
+    for its in (1, 2, 3, 7, 25):
+        xs = []
+        for kw in (dict(recurrence="textbook"), dict(rq=0), dict(rq=1)):
+            cg = gg.linalg.KronCG(K, s, **kw)
+            if "rq" in kw:
+                assert cg.rq == kw["rq"]
+            cg.start(b, rtol=0.0)
+            cg.iterate(its)
+            assert cg.status()[0] == its
+            xs.append(cg.x.cpu().numpy())
+        base = max(rel(xs[1], xs[0]), 1e-13)
+        assert rel(xs[2], xs[0]) < 4 * base, (its, rel(xs[2], xs[0]), base)
+    chunks = gg.linalg.KronCG(K, s, rq=1)
+    chunks.start(b, rtol=0.0)
+    for k in (3, 1, 7, 5, 9):
+        chunks.iterate(k)
+    assert rel(chunks.x.cpu().numpy(), xs[0]) < 4 * base
+    counts = []
+    s = 2.0   # a conditioning that converges in a few hundred iterations
+    for rq in (0, 1):
+        cg = gg.linalg.KronCG(K, s, rq=rq)
+        cg.start(b, rtol=1e-10)
+        cg.iterate(4000, check_every=10)
+        it, conv, res, tol = cg.status()
+        assert conv, (rq, it, res, tol)
+        counts.append(it)
+        x = cg.x.cpu().numpy()
+        bh = b.cpu().numpy()
+        r_true = bh - (oracle.kron_matvec(F, x) + s * x)
+        assert np.linalg.norm(r_true) <= 1e-8 * np.linalg.norm(bh)
+    assert abs(counts[0] - counts[1]) <= 1, counts

@@ -278,11 +278,17 @@ def test_cg_fused_state_is_textbook_after_iterate(gg):
     errs = [rel(c.x.cpu().numpy(), xo) for c in (one, chunks, text)]
     assert max(errs) < 1e-6, errs
     assert max(errs[:2]) < 3 * errs[2] + 1e-9, errs
-    # the recursively updated residual norms track the true ||b - A x_30||
-    # (||r_30|| ~ 2e-4 ||b||: the usual residual gap is ~1e-4 relative here)
+    # the recursively updated residual norms track the true ||b - A x_30|| of
+    # each run's own iterate (||r_30|| ~ 2e-4 ||b||: the usual residual gap is
+    # ~1e-4 relative here), and all stay within 1 % of the oracle's: 30
+    # unconverged steps move ||r_30|| by 0.05 % (textbook vs fused, r.q read)
+    # to 0.5 % (r.q from the conjugacy identity) -- summation order alone
     r30 = b.cpu().numpy() - (oracle.kron_matvec(F, xo) + s * xo)
     for c in (one, chunks, text):
-        assert abs(c.status()[2] - np.linalg.norm(r30)) < 1e-3 * np.linalg.norm(r30)
+        xc = c.x.cpu().numpy()
+        rc = np.linalg.norm(b.cpu().numpy() - (oracle.kron_matvec(F, xc) + s * xc))
+        assert abs(c.status()[2] - rc) < 1e-3 * rc
+        assert abs(rc - np.linalg.norm(r30)) < 1e-2 * np.linalg.norm(r30)
 
 
 @pytest.mark.parametrize("shift", [5.0, 200.0])
@@ -421,7 +427,8 @@ def test_cg_fusion_layouts_same_iterates(gg, fusion):
     """Fusion layouts 1 / 2 move where the fused recurrence's vector passes ride
     (p_new recomputed and stored by the last mode product; layout 2 also does
     the x update there) -- the same arithmetic, so the same iterates as
-    layout 0, step for step, and the same converged solve."""
+    layout 0 (r.q read in the epilogue, gg_cg_set_rq 0), step for step, and
+    the same converged solve."""
     import torch
     F = _rbf_factors((20, 16, 12))
     K = gg.tensors.KronMatrix(F, sym=True)
@@ -430,8 +437,9 @@ def test_cg_fusion_layouts_same_iterates(gg, fusion):
     s = 0.5
     runs = []
     for layout in (0, fusion):
-        c = gg.linalg.KronCG(K, s, fusion=layout)
-        assert c.fusion == layout
+        # layout 0 with r.q read in the epilogue, as layouts 1 / 2 do
+        c = gg.linalg.KronCG(K, s, fusion=layout, rq=0)
+        assert c.fusion == layout and c.rq == 0
         c.start(b, rtol=0.0)
         for k in (5, 1, 14):          # chunked: each call closes the pending update
             c.iterate(k)

@@ -1,6 +1,6 @@
 """HBM traffic per launch of the fused-CG mode products from rocprofv3 PMC passes.
 
-usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON [--fusion F] [--xdefer MODE]
+usage: python tools/pmc_traffic.py RD_DIR WR_DIR OUT_JSON [--fusion F] [--xdefer MODE] [--rq 0|1]
 
 Counters (two separate --pmc runs of `bench.py --steps 2 --warmup 1`, kernel
 trace only, as MI355X_MICROARCH.md prescribes):
@@ -45,6 +45,9 @@ def main():
     # the library default 2 unless GG_CG_XDEFER overrides it)
     xdefer = (int(sys.argv[sys.argv.index("--xdefer") + 1]) if "--xdefer" in sys.argv
               else int(os.environ.get("GG_CG_XDEFER", "2")))
+    # the r.q source (gg_cg_set_rq; the library default 1 unless GG_CG_RQ=0)
+    rq = (int(sys.argv[sys.argv.index("--rq") + 1]) if "--rq" in sys.argv
+          else int(os.environ.get("GG_CG_RQ", "1") != "0"))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     rd, names = dispatches(rd_dir)
@@ -67,7 +70,7 @@ def main():
                         "write_bytes": wbytes, "traffic_bytes": rbytes + wbytes,
                         "dispatches": dids})
     n = 200 ** 4
-    passes = [float(v) for v in bench.launch_passes(d, "fused", fusion, xdefer)]
+    passes = [float(v) for v in bench.launch_passes(d, "fused", fusion, xdefer, rq and not fusion)]
     for k, pp in enumerate(per_pos):
         pp["algorithmic_bytes"] = passes[k] * 8.0 * n
         pp["ratio"] = pp["traffic_bytes"] / pp["algorithmic_bytes"]
@@ -78,6 +81,7 @@ def main():
     fold_mask = sum(1 << k for k, pp in enumerate(per_pos) if "fold" in pp["kernel"])
     res = {
         "position": 0, "recurrence": "fused", "fusion_layout": fusion, "x_deferred": xdefer,
+        "rq_identity": int(bool(rq and not fusion)),
         "fold_mask": fold_mask,
         # bench.py reuses these counters only for kernels built from the same sources
         "source_sha256": bench.kernel_source_hash(),
