@@ -353,6 +353,87 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
   }
 }
 
+// Row-major Phi with column pairs (p even, 16-byte aligned Phi): one block
+// owns kR data points and every column, so the kR x U slice of T is read and
+// exponentiated once (not once per 256-column block), and a thread stores two
+// adjacent columns as one 16-byte non-temporal store -- 1 KiB contiguous per
+// wave instruction instead of 512 B of 8-byte lanes.  kD = d (1..8).
+typedef double gg_d2 __attribute__((ext_vector_type(2)));
+template <int kR, int kD>
+__global__ __launch_bounds__(kPhiCols) void grief_phi_pair_kernel(
+    const double* __restrict__ Ltab, const double* __restrict__ Stab, int U, int64_t n,
+    const int* __restrict__ cidx, const double* __restrict__ log_lam, int p,
+    double* __restrict__ Phi) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* sT = sm;   // kR x U
+  const int64_t a0 = (int64_t)blockIdx.x * kR;
+  const int rows = (int)min<int64_t>(kR, n - a0);
+  for (int e = threadIdx.x; e < rows * U; e += blockDim.x)
+    sT[e] = Stab[a0 * U + e] * exp(Ltab[a0 * U + e]);
+  __syncthreads();
+  const int pairs = p >> 1;
+  for (int jp = threadIdx.x; jp < pairs; jp += kPhiCols) {
+    const int j = 2 * jp;
+    int c0[kD], c1[kD];
+#pragma unroll
+    for (int f = 0; f < kD; ++f) {
+      c0[f] = cidx[(int64_t)j * kD + f];
+      c1[f] = cidx[(int64_t)(j + 1) * kD + f];
+    }
+    const double s0 = exp(-0.5 * log_lam[j]), s1 = exp(-0.5 * log_lam[j + 1]);
+    double* out = Phi + a0 * p + j;
+    for (int r = 0; r < rows; ++r) {
+      const double* tr = sT + r * U;
+      gg_d2 v = {s0, s1};
+#pragma unroll
+      for (int f = 0; f < kD; ++f) {
+        v.x *= tr[c0[f]];
+        v.y *= tr[c1[f]];
+      }
+      __builtin_nontemporal_store(v, reinterpret_cast<gg_d2*>(out + (int64_t)r * p));
+    }
+  }
+}
+
+template <int kR, int kD>
+static void launch_phi_pair(dim3 grid, size_t lds, hipStream_t s, const double* L,
+                            const double* S, int U, int64_t n, const int* cidx,
+                            const double* ll, int p, double* phi) {
+  static bool attr = false;
+  if (!attr) {
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&grief_phi_pair_kernel<kR, kD>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((grief_phi_pair_kernel<kR, kD>), grid, dim3(kPhiCols), lds, s, L, S, U, n,
+                     cidx, ll, p, phi);
+}
+
+// the pair kernel for d <= 8; false: not taken (the caller launches the other)
+static bool launch_phi_pair_d(hipStream_t s, const double* L, const double* S, int U, int64_t n,
+                              const int* cidx, int d, const double* ll, int p, double* phi) {
+  static const bool on = [] {
+    const char* e = getenv("GG_PHI_PAIR");   // A/B knob: 0 = the 256-column kernel
+    return !(e != nullptr && atoi(e) == 0);
+  }();
+  if (!on || d > 8 || (p & 1) || (reinterpret_cast<uintptr_t>(phi) & 15)) return false;
+  constexpr int kR = kPhiRows;
+  const size_t lds = (size_t)kR * U * sizeof(double);
+  if (lds > 160 * 1024) return false;
+  const dim3 grid((unsigned)ceil_div(n, (int64_t)kR));
+  switch (d) {
+    case 1: launch_phi_pair<kR, 1>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 2: launch_phi_pair<kR, 2>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 3: launch_phi_pair<kR, 3>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 4: launch_phi_pair<kR, 4>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 5: launch_phi_pair<kR, 5>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 6: launch_phi_pair<kR, 6>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    case 7: launch_phi_pair<kR, 7>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+    default: launch_phi_pair<kR, 8>(grid, lds, s, L, S, U, n, cidx, ll, p, phi); break;
+  }
+  return true;
+}
+
 template <int kR, bool kT, int kD>
 static void launch_phi(dim3 grid, size_t lds, hipStream_t s, const double* L, const double* S,
                        int U, int64_t n, const int* cidx, int d, const double* ll, int p,
@@ -517,7 +598,8 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
     if (transposed)
       gg::launch_phi_d<gg::kPhiRowsT, true>(grid, lds, gg::as_stream(stream), ltab_dev,
                                             stab_dev, U, n, cidx_dev, d, log_lam_dev, p, phi_dev);
-    else
+    else if (!gg::launch_phi_pair_d(gg::as_stream(stream), ltab_dev, stab_dev, U, n, cidx_dev,
+                                    d, log_lam_dev, p, phi_dev))
       gg::launch_phi_d<gg::kPhiRows, false>(grid, lds, gg::as_stream(stream), ltab_dev,
                                             stab_dev, U, n, cidx_dev, d, log_lam_dev, p, phi_dev);
     GG_LAUNCH_CHECK();
