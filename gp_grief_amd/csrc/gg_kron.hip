@@ -1130,6 +1130,11 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
               (aligned && xs_ != nullptr && fold_staged_available(f.fJT, f.fTT, kind))
                   ? select_fold_staged(f.fJT, f.fTT, kind)
                   : select_fold(f.fJT, f.fTT, kind);
+          if (fc.lean) {
+            const int64_t nch = ceil_div((int64_t)f.fKS, (int64_t)fc.kc);
+            GG_REQUIRE(4 * nch * fc.kc <= (int64_t)f.q && 32 * M < ((int64_t)1 << 32),
+                       GG_ERR_VALUE, "lean folded variant outside its row / offset range");
+          }
           mc = ModeConfig{fc.fn, 4, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
         }
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);

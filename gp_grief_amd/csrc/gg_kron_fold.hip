@@ -44,7 +44,12 @@ namespace gg {
 // mp_finish), no shift / dots.
 // kOpt (A/B variants, GG_FOLD_VARIANT): bit 0 s_setprio(1) around each
 // k-step's MFMAs; bit 1 issue the next chunk's loads before the first k-step
-// instead of after it.
+// instead of after it; bit 2 (kLean) address the A rows as a wave-uniform row
+// base (SGPRs) plus a 32-bit lane byte offset -- no 64-bit address registers
+// or clamps (the host takes it only when every chunk's rows lie inside the
+// factor, 4 kKC nchunks <= m, and 4 M * 8 < 2^32); bit 3 (kBdb) read the next
+// pair of B fragments from LDS before the current pair's MFMAs (register
+// double buffer) instead of waiting on each read.
 // kStg: the identity epilogue staged through LDS -- each accumulator
 // register's 4 rows go to a wave-private LDS image in the global layout (row
 // stride m), then the wave streams them with 16-byte lanes (1 KiB contiguous
@@ -58,6 +63,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
     const int* __restrict__ skip, OutMap om, MpFuse fz) {
   static_assert(!kMap || kEpi == 0, "the mapped epilogue stores only");
+  constexpr bool kLean = (kOpt & 4) != 0;
+  constexpr bool kBdb = (kOpt & 8) != 0;
   static_assert(!(kMap && kStg), "staged epilogue: identity layout only");
   constexpr int kWaves = 4;
   constexpr int kThreads = 256;
@@ -135,11 +142,41 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
             (const __attribute__((address_space(1))) void*)(cb + boff[u]),
             (__attribute__((address_space(3))) void*)(dstb + u * kThreads * 2), 16, 0, 0);
   };
-  // raw loads of chunk c: [0] = row i', [1] = row m-1-i' (only the last
-  // chunk can step past the rows: clamp there, masked when consumed)
+  // kLean: lane byte offsets of rows krow and 3 - krow from a 4-row base;
+  // the row bases go through readfirstlane, opaque to loop strength
+  // reduction, so every access keeps the SGPR-base + 32-bit VGPR-offset form
+  const uint32_t loff = (uint32_t)(((int64_t)krow * M + bclamp) * 8);
+  const uint32_t hoff = (uint32_t)(((int64_t)(3 - krow) * M + bclamp) * 8);
+  auto sbase = [](const void* p, int64_t off) -> char* {
+    const uint64_t a = reinterpret_cast<uint64_t>(p) + (uint64_t)off;
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t u = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return reinterpret_cast<char*>(((uint64_t)u << 32) | l);
+  };
+  // byte offsets of k-step t's low / high row bases
+  auto lrow_b = [&](int64_t t) -> int64_t { return 4 * t * M * 8; };
+  auto hrow_b = [&](int64_t t) -> int64_t { return ((int64_t)(m - 4) - 4 * t) * M * 8; };
   // raw loads of chunk c: [0] = row i', [1] = row m-1-i' (only the last
   // chunk can step past the rows: clamp there, masked when consumed)
   auto aload = [&](int c, double (&a)[2][kKC], double (&r)[2][kKC], double (&q)[2][kKC]) {
+    if constexpr (kLean) {
+#pragma unroll
+      for (int s = 0; s < kKC; ++s) {
+        const int64_t t = (int64_t)c * kKC + s;
+        const int64_t lb = lrow_b(t), hb = hrow_b(t);
+        a[0][s] = *reinterpret_cast<const double*>(sbase(X, lb) + loff);
+        a[1][s] = *reinterpret_cast<const double*>(sbase(X, hb) + hoff);
+        if (CGP) {
+          r[0][s] = *reinterpret_cast<const double*>(sbase(Rg, lb) + loff);
+          r[1][s] = *reinterpret_cast<const double*>(sbase(Rg, hb) + hoff);
+        }
+        if (CGP >= 2) {
+          q[0][s] = *reinterpret_cast<const double*>(sbase(Qa, lb) + loff);
+          q[1][s] = *reinterpret_cast<const double*>(sbase(Qa, hb) + hoff);
+        }
+      }
+      return;
+    }
     int64_t ol = lo0 + (int64_t)c * achunk;
     int64_t oh = hi0 - (int64_t)c * achunk;
     const bool last = c == nchunks - 1;
@@ -162,23 +199,29 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
     }
   };
   // one element of the CG / Lanczos prologue (mode_product_kernel GG_A_MASK)
-  auto upd = [&](double v, double r, double q, bool ok, int64_t e) -> double {
+  // e: element index; kLean: rb = the row base's byte offset, o = the lane's
+  auto upd = [&](double v, double r, double q, bool ok, int64_t e, int64_t rb,
+                 uint32_t o) -> double {
+    auto at = [&](double* base) -> double* {
+      if constexpr (kLean) return reinterpret_cast<double*>(sbase(base, rb) + o);
+      return base + e;
+    };
     if (CGP == 3) {
       v = fma(lz_cp, q, fma(lz_cu, r, lz_cy * v));
       if (ok) {
-        Pout[e] = v;
+        *at(Pout) = v;
         rr_acc = fma(v, v, rr_acc);
       }
     } else if (CGP) {
       if (CGP == 2 && cg_pending) {
         r = r - cg_alpha * q;
         if (ok) {
-          Rg[e] = r;
+          *at(Rg) = r;
           rr_acc = fma(r, r, rr_acc);
         }
       }
       v = cg_first ? r : fma(cg_beta, v, r);
-      if (Pout != nullptr && ok) Pout[e] = v;
+      if (Pout != nullptr && ok) *at(Pout) = v;
       if (CGP == 2 && pqo_on && ok) pqo_acc = fma(v, q, pqo_acc);
     }
     return v;
@@ -192,8 +235,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
       const bool okh = bvalid && k < h;   // a distinct mirrored row
       double xl = a[0][s], xh = a[1][s];
       if (CGP) {
-        xl = upd(xl, r[0][s], q[0][s], okl, (int64_t)k * M + brow);
-        xh = upd(xh, r[1][s], q[1][s], okh, (int64_t)(m - 1 - k) * M + brow);
+        const int64_t t = (int64_t)c * kKC + s;
+        xl = upd(xl, r[0][s], q[0][s], okl, (int64_t)k * M + brow, lrow_b(t), loff);
+        xh = upd(xh, r[1][s], q[1][s], okh, (int64_t)(m - 1 - k) * M + brow, hrow_b(t), hoff);
       }
       a[0][s] = okl ? (okh ? xl + xh : xl) : 0.0;
       a[1][s] = okh ? xl - xh : 0.0;
@@ -236,6 +280,38 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
         const double* bs = buf + s * JF * 64;
         const double au = a_cur[0][s], av = a_cur[1][s];
         if (kOpt & 1) __builtin_amdgcn_s_setprio(1);
+        // fragment f of the k-step: [S tiles][S tails][T tiles][T tails]
+        auto frag = [&](int f, double bv) {
+          if (f < FS) {
+            if (TS > 0 && f >= JS - 1) {
+              const int i = TS > 0 ? f - (JS - 1) : 0;
+              t4s[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(au, bv, t4s[i], 0, 0, 0);
+            } else {
+              accs[f] = __builtin_amdgcn_mfma_f64_16x16x4f64(au, bv, accs[f], 0, 0, 0);
+            }
+          } else {
+            const int g = f - FS;
+            if (TA > 0 && g >= JA - 1) {
+              const int i = TA > 0 ? g - (JA - 1) : 0;
+              t4a[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv, t4a[i], 0, 0, 0);
+            } else {
+              acca[g] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acca[g], 0, 0, 0);
+            }
+          }
+        };
+        if constexpr (kBdb) {
+          double bc0 = bs[0], bc1 = JF > 1 ? bs[64] : 0.0;
+#pragma unroll
+          for (int f = 0; f < JF; f += 2) {
+            double bn0 = 0.0, bn1 = 0.0;
+            if (f + 2 < JF) bn0 = bs[(f + 2) * 64];
+            if (f + 3 < JF) bn1 = bs[(f + 3) * 64];
+            frag(f, bc0);
+            if (f + 1 < JF) frag(f + 1, bc1);
+            bc0 = bn0;
+            bc1 = bn1;
+          }
+        } else {
 #pragma unroll
         for (int t = 0; t < JS; ++t) {
           if (TS > 0 && t == JS - 1) {
@@ -256,6 +332,7 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
           } else {
             acca[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bs[(FS + t) * 64], acca[t], 0, 0, 0);
           }
+        }
         }
         if (kOpt & 1) __builtin_amdgcn_s_setprio(0);
       }
@@ -520,7 +597,8 @@ bool fold_kind(int kind) {
 
 // KIND: kron_apply's launch kind; 8 / 9: the sharded operator's mapped
 // epilogue without / with the textbook CG prologue (gg_kron_dist_*)
-template <int JT, int TT, int KIND, bool STG = false>
+// OPT: kOpt (4 = kLean); KCO > 0 overrides the k-steps per chunk
+template <int JT, int TT, int KIND, bool STG = false, int OPT = 0, int KCO = 0>
 static FoldConfig cfg_fold() {
   constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
   constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : KIND == 6 ? 4 : 0;
@@ -528,7 +606,7 @@ static FoldConfig cfg_fold() {
   // the fused / Lanczos prologues hold three operands per row pair: one
   // k-step per chunk keeps them within the 3-wave register budget (A/B at
   // 200^4: 15.7 vs 18.7 ms with two, profiles/r03/j_*)
-  constexpr int KC = CGP >= 2 ? 1 : CGP ? 2 : 3;
+  constexpr int KC = KCO > 0 ? KCO : CGP >= 2 ? 1 : CGP ? 2 : 3;
   constexpr int JF = 2 * (JT - (TT > 0 ? 1 : 0) + TT);
   // 2 x (JT - 1) full 16x16 accumulators beside the tails: beyond 12 of them
   // (m > 200) three waves per SIMD would spill -- two instead
@@ -536,8 +614,42 @@ static FoldConfig cfg_fold() {
   constexpr size_t kB = 2 * (size_t)KC * JF * 64 * sizeof(double);
   // staged epilogue: 4 waves x 4 rows x m (<= 32 JT) doubles + the reduction
   constexpr size_t kS = STG ? ((size_t)16 * 32 * JT + 16) * sizeof(double) : 0;
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, MINW, EPI, MAP, 0, STG>,
-                    KC, JF, kB > kS ? kB : kS};
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, MINW, EPI, MAP, OPT, STG>,
+                    KC, JF, kB > kS ? kB : kS, (OPT & 4) != 0};
+}
+
+// A/B knobs for the m = 200 shape (JT 7, TT 1): GG_FOLD_LEAN=1 takes the
+// kLean kernels for the plain / side / epilogue launches (kinds 0, 3, 4, 6),
+// GG_FOLD_LEAN_PRO=1 / 2 for the fused-CG prologue (kind 2) with 1 / 2
+// k-steps per chunk
+static int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+
+static bool lean_kind(int kind, bool staged) {
+  return (kind == 0 || kind == 3 || kind == 4 || kind == 6) && !(staged && kind == 4);
+}
+
+static FoldConfig lean_cfg(int kind, bool staged) {
+  constexpr int JT = 7, TT = 1;
+  if (staged) {
+    switch (kind) {
+      case 3: return cfg_fold<JT, TT, 3, true, 4>();
+      case 6: return cfg_fold<JT, TT, 6, true, 4>();
+      default: return cfg_fold<JT, TT, 0, true, 4>();
+    }
+  }
+  switch (kind) {
+    case 3: return cfg_fold<JT, TT, 3, false, 4>();
+    case 4: return cfg_fold<JT, TT, 4, false, 4>();
+    case 6: return cfg_fold<JT, TT, 6, false, 4>();
+    default: return cfg_fold<JT, TT, 0, false, 4>();
+  }
+}
+
+static FoldConfig lean_pro_cfg(int mode) {
+  return mode == 2 ? cfg_fold<7, 1, 2, false, 4, 2>() : cfg_fold<7, 1, 2, false, 4, 1>();
 }
 
 // plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only)
@@ -546,7 +658,7 @@ static FoldConfig cfg_fold_var() {
   constexpr int JT = 7, TT = 1;
   constexpr int JF = 2 * (JT - 1 + TT);
   return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, 0, MINW, 0, false, OPT>, KC, JF,
-                    2 * (size_t)KC * JF * 64 * sizeof(double)};
+                    2 * (size_t)KC * JF * 64 * sizeof(double), (OPT & 4) != 0};
 }
 
 static int fold_variant() {
@@ -563,6 +675,11 @@ static FoldConfig fold_variant_cfg(int v) {
     case 5: return cfg_fold_var<3, 3, 1>();
     case 6: return cfg_fold_var<3, 3, 2>();
     case 7: return cfg_fold_var<1, 3, 0>();
+    case 8: return cfg_fold_var<3, 3, 4>();
+    case 9: return cfg_fold_var<3, 3, 8>();
+    case 10: return cfg_fold_var<3, 3, 12>();
+    case 11: return cfg_fold_var<3, 2, 12>();
+    case 12: return cfg_fold_var<6, 2, 12>();
     default: return cfg_fold_var<3, 3, 0>();
   }
 }
@@ -573,6 +690,8 @@ static FoldConfig fold_variant_cfg(int v) {
 // lose 0.4 ms to the LDS round trip (profiles/r03/h_bench_stage*.json)
 template <int JT, int TT>
 static FoldConfig fold_staged_by_kind(int kind) {
+  if constexpr (JT == 7 && TT == 1)
+    if (env_int("GG_FOLD_LEAN") == 1 && lean_kind(kind, true)) return lean_cfg(kind, true);
   switch (kind) {
     case 3: return cfg_fold<JT, TT, 3, true>();
     case 6: return cfg_fold<JT, TT, 6, true>();
@@ -626,9 +745,12 @@ static FoldConfig fold_by_kind(int kind) {
   if constexpr (JT == 7 && TT == 1) {
     if (kind == 0 && fold_variant() != 0) return fold_variant_cfg(fold_variant());
     if (kind == 2) {
+      const int lp = env_int("GG_FOLD_LEAN_PRO");
+      if (lp == 1 || lp == 2) return lean_pro_cfg(lp);
       const char* e = getenv("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }
+    if (env_int("GG_FOLD_LEAN") == 1 && lean_kind(kind, false)) return lean_cfg(kind, false);
   }
   switch (kind) {
     case 8: return cfg_fold<JT, TT, 8>();
@@ -684,7 +806,19 @@ void set_fold_lds_limits() {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
       }
     }
-  for (int v = 1; v <= 7; ++v) {
+  for (int kind : {0, 3, 4, 6})
+    for (bool staged : {false, true}) {
+      if (!lean_kind(kind, staged)) continue;
+      const FoldConfig fc = lean_cfg(kind, staged);
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+    }
+  for (int lp : {1, 2}) {
+    const FoldConfig fc = lean_pro_cfg(lp);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+  }
+  for (int v = 1; v <= 12; ++v) {
     const FoldConfig fc = fold_variant_cfg(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));

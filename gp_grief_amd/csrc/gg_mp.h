@@ -160,6 +160,7 @@ struct FoldConfig {
   mode_kernel_t fn;
   int kc, jf;     // k-steps per LDS chunk, fragments per k-step (both halves)
   size_t lds;     // dynamic LDS bytes
+  bool lean = false;   // kLean A addressing: the launch checks its row / offset range
 };
 bool fold_kind(int kind);
 FoldConfig select_fold(int JT, int TT, int kind);
