@@ -1125,15 +1125,21 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
               ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(xs_) |
                 reinterpret_cast<uintptr_t>(cg != nullptr ? cg->er : nullptr) |
                 reinterpret_cast<uintptr_t>(cg != nullptr ? cg->ep_out : nullptr)) & 15) == 0;
-          // the LDS-staged epilogue only where it reads the fused operands
+          // the LDS-staged epilogue only where it reads the fused operands;
+          // the kLean kernels where every chunk's rows (at most 3 k-steps
+          // per chunk) lie inside the factor and the lane offsets fit 32 bits
+          const bool lean_ok =
+              4 * 3 * ceil_div((int64_t)f.fKS, (int64_t)3) <= (int64_t)f.q &&
+              4 * 2 * ceil_div((int64_t)f.fKS, (int64_t)2) <= (int64_t)f.q &&
+              32 * M < ((int64_t)1 << 32);
           const FoldConfig fc =
               (aligned && xs_ != nullptr && fold_staged_available(f.fJT, f.fTT, kind))
-                  ? select_fold_staged(f.fJT, f.fTT, kind)
-                  : select_fold(f.fJT, f.fTT, kind);
+                  ? select_fold_staged(f.fJT, f.fTT, kind, lean_ok)
+                  : select_fold(f.fJT, f.fTT, kind, lean_ok);
           if (fc.lean) {
             const int64_t nch = ceil_div((int64_t)f.fKS, (int64_t)fc.kc);
             GG_REQUIRE(4 * nch * fc.kc <= (int64_t)f.q && 32 * M < ((int64_t)1 << 32),
-                       GG_ERR_VALUE, "lean folded variant outside its row / offset range");
+                       GG_ERR_VALUE, "lean folded kernel outside its row / offset range");
           }
           mc = ModeConfig{fc.fn, 4, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
         }

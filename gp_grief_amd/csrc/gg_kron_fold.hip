@@ -618,13 +618,16 @@ static FoldConfig cfg_fold() {
                     KC, JF, kB > kS ? kB : kS, (OPT & 4) != 0};
 }
 
-// A/B knobs for the m = 200 shape (JT 7, TT 1): GG_FOLD_LEAN=1 takes the
-// kLean kernels for the plain / side / epilogue launches (kinds 0, 3, 4, 6),
-// GG_FOLD_LEAN_PRO=1 / 2 for the fused-CG prologue (kind 2) with 1 / 2
-// k-steps per chunk
-static int env_int(const char* name) {
+// kLean kernels, instantiated for the m = 200 shape (JT 7, TT 1): default for
+// the plain / side / epilogue launches (kinds 0, 3, 4, 6) when the launch is
+// in their range (lean_ok); fused CG at 200^4, interleaved processes:
+// 41.25 -> 40.98 ms per iteration (side launches 8.05 -> 7.95 ms, the side
+// kernel's 3 spilled VGPRs gone; profiles/r03/ak_lean_cg_ab.jsonl).
+// GG_FOLD_LEAN=0 disables them; GG_FOLD_LEAN_PRO=1 / 2 (A/B only) takes a
+// lean fused-CG prologue with 1 / 2 k-steps per chunk -- 0.2-0.3 ms slower.
+static int env_int(const char* name, int dflt = 0) {
   const char* e = getenv(name);
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : dflt;
 }
 
 static bool lean_kind(int kind, bool staged) {
@@ -689,9 +692,10 @@ static FoldConfig fold_variant_cfg(int v) {
 // the fused-CG epilogue launch 11.7 -> 10.2 ms, while plain-store launches
 // lose 0.4 ms to the LDS round trip (profiles/r03/h_bench_stage*.json)
 template <int JT, int TT>
-static FoldConfig fold_staged_by_kind(int kind) {
+static FoldConfig fold_staged_by_kind(int kind, bool lean_ok) {
   if constexpr (JT == 7 && TT == 1)
-    if (env_int("GG_FOLD_LEAN") == 1 && lean_kind(kind, true)) return lean_cfg(kind, true);
+    if (lean_ok && env_int("GG_FOLD_LEAN", 1) == 1 && lean_kind(kind, true))
+      return lean_cfg(kind, true);
   switch (kind) {
     case 3: return cfg_fold<JT, TT, 3, true>();
     case 6: return cfg_fold<JT, TT, 6, true>();
@@ -706,26 +710,26 @@ bool fold_staged_available(int JT, int TT, int kind) {
          (TT == 0 || JT >= 4);
 }
 
-FoldConfig select_fold_staged(int JT, int TT, int kind) {
+FoldConfig select_fold_staged(int JT, int TT, int kind, bool lean_ok) {
   if (TT == 0) {
     switch (JT) {
-      case 1: return fold_staged_by_kind<1, 0>(kind);
-      case 2: return fold_staged_by_kind<2, 0>(kind);
-      case 3: return fold_staged_by_kind<3, 0>(kind);
-      case 4: return fold_staged_by_kind<4, 0>(kind);
-      case 5: return fold_staged_by_kind<5, 0>(kind);
-      case 6: return fold_staged_by_kind<6, 0>(kind);
-      case 7: return fold_staged_by_kind<7, 0>(kind);
-      case 8: return fold_staged_by_kind<8, 0>(kind);
+      case 1: return fold_staged_by_kind<1, 0>(kind, lean_ok);
+      case 2: return fold_staged_by_kind<2, 0>(kind, lean_ok);
+      case 3: return fold_staged_by_kind<3, 0>(kind, lean_ok);
+      case 4: return fold_staged_by_kind<4, 0>(kind, lean_ok);
+      case 5: return fold_staged_by_kind<5, 0>(kind, lean_ok);
+      case 6: return fold_staged_by_kind<6, 0>(kind, lean_ok);
+      case 7: return fold_staged_by_kind<7, 0>(kind, lean_ok);
+      case 8: return fold_staged_by_kind<8, 0>(kind, lean_ok);
       default: break;
     }
   } else {
     switch (JT) {
-      case 4: return TT == 1 ? fold_staged_by_kind<4, 1>(kind) : fold_staged_by_kind<4, 2>(kind);
-      case 5: return TT == 1 ? fold_staged_by_kind<5, 1>(kind) : fold_staged_by_kind<5, 2>(kind);
-      case 6: return TT == 1 ? fold_staged_by_kind<6, 1>(kind) : fold_staged_by_kind<6, 2>(kind);
-      case 7: return TT == 1 ? fold_staged_by_kind<7, 1>(kind) : fold_staged_by_kind<7, 2>(kind);
-      case 8: return TT == 1 ? fold_staged_by_kind<8, 1>(kind) : fold_staged_by_kind<8, 2>(kind);
+      case 4: return TT == 1 ? fold_staged_by_kind<4, 1>(kind, lean_ok) : fold_staged_by_kind<4, 2>(kind, lean_ok);
+      case 5: return TT == 1 ? fold_staged_by_kind<5, 1>(kind, lean_ok) : fold_staged_by_kind<5, 2>(kind, lean_ok);
+      case 6: return TT == 1 ? fold_staged_by_kind<6, 1>(kind, lean_ok) : fold_staged_by_kind<6, 2>(kind, lean_ok);
+      case 7: return TT == 1 ? fold_staged_by_kind<7, 1>(kind, lean_ok) : fold_staged_by_kind<7, 2>(kind, lean_ok);
+      case 8: return TT == 1 ? fold_staged_by_kind<8, 1>(kind, lean_ok) : fold_staged_by_kind<8, 2>(kind, lean_ok);
       default: break;
     }
   }
@@ -741,16 +745,17 @@ static FoldConfig fold_pro_kc1() {
 }
 
 template <int JT, int TT>
-static FoldConfig fold_by_kind(int kind) {
+static FoldConfig fold_by_kind(int kind, bool lean_ok) {
   if constexpr (JT == 7 && TT == 1) {
-    if (kind == 0 && fold_variant() != 0) return fold_variant_cfg(fold_variant());
+    if (kind == 0 && fold_variant() != 0 && lean_ok) return fold_variant_cfg(fold_variant());
     if (kind == 2) {
       const int lp = env_int("GG_FOLD_LEAN_PRO");
-      if (lp == 1 || lp == 2) return lean_pro_cfg(lp);
+      if (lean_ok && (lp == 1 || lp == 2)) return lean_pro_cfg(lp);
       const char* e = getenv("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }
-    if (env_int("GG_FOLD_LEAN") == 1 && lean_kind(kind, false)) return lean_cfg(kind, false);
+    if (lean_ok && env_int("GG_FOLD_LEAN", 1) == 1 && lean_kind(kind, false))
+      return lean_cfg(kind, false);
   }
   switch (kind) {
     case 8: return cfg_fold<JT, TT, 8>();
@@ -765,26 +770,26 @@ static FoldConfig fold_by_kind(int kind) {
   }
 }
 
-FoldConfig select_fold(int JT, int TT, int kind) {
+FoldConfig select_fold(int JT, int TT, int kind, bool lean_ok) {
   if (TT == 0) {
     switch (JT) {
-      case 1: return fold_by_kind<1, 0>(kind);
-      case 2: return fold_by_kind<2, 0>(kind);
-      case 3: return fold_by_kind<3, 0>(kind);
-      case 4: return fold_by_kind<4, 0>(kind);
-      case 5: return fold_by_kind<5, 0>(kind);
-      case 6: return fold_by_kind<6, 0>(kind);
-      case 7: return fold_by_kind<7, 0>(kind);
-      case 8: return fold_by_kind<8, 0>(kind);
+      case 1: return fold_by_kind<1, 0>(kind, lean_ok);
+      case 2: return fold_by_kind<2, 0>(kind, lean_ok);
+      case 3: return fold_by_kind<3, 0>(kind, lean_ok);
+      case 4: return fold_by_kind<4, 0>(kind, lean_ok);
+      case 5: return fold_by_kind<5, 0>(kind, lean_ok);
+      case 6: return fold_by_kind<6, 0>(kind, lean_ok);
+      case 7: return fold_by_kind<7, 0>(kind, lean_ok);
+      case 8: return fold_by_kind<8, 0>(kind, lean_ok);
       default: break;
     }
   } else if (TT == 1 || TT == 2) {
     switch (JT) {
-      case 4: return TT == 1 ? fold_by_kind<4, 1>(kind) : fold_by_kind<4, 2>(kind);
-      case 5: return TT == 1 ? fold_by_kind<5, 1>(kind) : fold_by_kind<5, 2>(kind);
-      case 6: return TT == 1 ? fold_by_kind<6, 1>(kind) : fold_by_kind<6, 2>(kind);
-      case 7: return TT == 1 ? fold_by_kind<7, 1>(kind) : fold_by_kind<7, 2>(kind);
-      case 8: return TT == 1 ? fold_by_kind<8, 1>(kind) : fold_by_kind<8, 2>(kind);
+      case 4: return TT == 1 ? fold_by_kind<4, 1>(kind, lean_ok) : fold_by_kind<4, 2>(kind, lean_ok);
+      case 5: return TT == 1 ? fold_by_kind<5, 1>(kind, lean_ok) : fold_by_kind<5, 2>(kind, lean_ok);
+      case 6: return TT == 1 ? fold_by_kind<6, 1>(kind, lean_ok) : fold_by_kind<6, 2>(kind, lean_ok);
+      case 7: return TT == 1 ? fold_by_kind<7, 1>(kind, lean_ok) : fold_by_kind<7, 2>(kind, lean_ok);
+      case 8: return TT == 1 ? fold_by_kind<8, 1>(kind, lean_ok) : fold_by_kind<8, 2>(kind, lean_ok);
       default: break;
     }
   }

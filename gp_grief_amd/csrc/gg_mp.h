@@ -163,11 +163,13 @@ struct FoldConfig {
   bool lean = false;   // kLean A addressing: the launch checks its row / offset range
 };
 bool fold_kind(int kind);
-FoldConfig select_fold(int JT, int TT, int kind);
+// lean_ok: the launch is in the kLean kernels' range (every chunk's rows
+// inside the factor, 4 kc ceil(KS / kc) <= m, and 32 M < 2^32)
+FoldConfig select_fold(int JT, int TT, int kind, bool lean_ok = false);
 // the LDS-staged identity epilogue for launches with a shift / dot operand
 // (kinds 0, 3, 6; m even, 16-byte aligned vectors; GG_FOLD_STAGE=0 disables)
 bool fold_staged_available(int JT, int TT, int kind);
-FoldConfig select_fold_staged(int JT, int TT, int kind);
+FoldConfig select_fold_staged(int JT, int TT, int kind, bool lean_ok = false);
 void set_fold_lds_limits();
 
 }  // namespace gg
