@@ -86,7 +86,15 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   const int wave = threadIdx.x >> 6;
   const int h = m >> 1;
   const int hS = m - h;
-  const int64_t b0 = ((int64_t)blockIdx.x * kWaves + wave) * 16;
+  // kOpt bit 4: XCD-contiguous block order -- dispatch deals consecutive
+  // block ids round-robin over the 8 XCDs; remapped, XCD x walks the x-th
+  // eighth of the rows b, so each XCD streams contiguous row segments
+  int64_t blk = blockIdx.x;
+  if constexpr ((kOpt & 16) != 0) {
+    const int64_t nb = gridDim.x, n8 = nb >> 3;
+    if (blk < 8 * n8) blk = (blk & 7) * n8 + (blk >> 3);
+  }
+  const int64_t b0 = (blk * kWaves + wave) * 16;
   const int64_t brow = b0 + (lane & 15);
   const bool bvalid = brow < M;
   const int64_t bclamp = bvalid ? brow : M - 1;
@@ -683,6 +691,7 @@ static FoldConfig fold_variant_cfg(int v) {
     case 10: return cfg_fold_var<3, 3, 12>();
     case 11: return cfg_fold_var<3, 2, 12>();
     case 12: return cfg_fold_var<6, 2, 12>();
+    case 13: return cfg_fold_var<3, 3, 20>();
     default: return cfg_fold_var<3, 3, 0>();
   }
 }
@@ -823,7 +832,7 @@ void set_fold_lds_limits() {
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
   }
-  for (int v = 1; v <= 12; ++v) {
+  for (int v = 1; v <= 13; ++v) {
     const FoldConfig fc = fold_variant_cfg(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));

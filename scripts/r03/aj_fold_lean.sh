@@ -7,5 +7,5 @@ cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
 O=gpurun_out/r03aj
 mkdir -p $O
-timeout -k 10 300 python -u tools/fold_variant_ab.py --variants 0,8,9,10,11,12,1 --rounds 3 > $O/ab.jsonl 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
+timeout -k 10 300 python -u tools/fold_variant_ab.py --variants ${VARS:-0,8,9,10,11,12,1} --rounds 3 > $O/ab.jsonl 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
 cat $O/ab.jsonl

@@ -87,6 +87,29 @@ def test_fold_matches_unfolded_kernel(gg, monkeypatch):
     assert rel(y1, oracle.kron_matvec(F, x[:, 0])) < 1e-13
 
 
+@pytest.mark.parametrize("m0", [199, 200])
+def test_fold_lean_matches_clamped(gg, monkeypatch, m0):
+    """The kLean kernels (SGPR row base + 32-bit lane offsets; default for the
+    m = 199 / 200 shape) and the clamped ones (GG_FOLD_LEAN=0) run the same
+    arithmetic: the plain matvec and a fused CG (prologue, side and epilogue
+    launches) agree bitwise."""
+    F = [grid_factor(m0, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
+    n = m0 * 200 * 200
+    x = np.random.default_rng(m0).standard_normal((n, 1))
+    out = {}
+    for lean in ("1", "0"):
+        monkeypatch.setenv("GG_FOLD_LEAN", lean)
+        K = kron(gg, F)
+        assert fold_mask(K) == 0b111
+        y = K * x
+        xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=6, recurrence="fused")
+        out[lean] = (np.asarray(y), np.asarray(xs))
+    monkeypatch.delenv("GG_FOLD_LEAN")
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert np.array_equal(out["1"][1], out["0"][1])
+    assert rel(out["1"][0], oracle.kron_matvec(F, x[:, 0])) < 1e-13
+
+
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
     """A centrosymmetric but non-symmetric factor: the transposed operator's
     split is packed from F^T."""
