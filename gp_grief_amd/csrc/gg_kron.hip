@@ -1141,7 +1141,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             GG_REQUIRE(4 * nch * fc.kc <= (int64_t)f.q && 32 * M < ((int64_t)1 << 32),
                        GG_ERR_VALUE, "lean folded kernel outside its row / offset range");
           }
-          mc = ModeConfig{fc.fn, 4, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
+          mc = ModeConfig{fc.fn, fc.waves, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
         }
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");

@@ -56,8 +56,8 @@ namespace gg {
 // per instruction) together with the fused operands (p, r) it loads the same
 // way.  Needs m even and 16-byte aligned vectors (kron_apply checks).
 template <int JS, int JA, int TS, int TA, int kKC, int CGP, int kMinW, int kEpi, bool kMap = false,
-          int kOpt = 0, bool kStg = false>
-__global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
+          int kOpt = 0, bool kStg = false, int kWv = 4>
+__global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int, int KS, int, int,
     const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
@@ -66,8 +66,8 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
   constexpr bool kLean = (kOpt & 4) != 0;
   constexpr bool kBdb = (kOpt & 8) != 0;
   static_assert(!(kMap && kStg), "staged epilogue: identity layout only");
-  constexpr int kWaves = 4;
-  constexpr int kThreads = 256;
+  constexpr int kWaves = kWv;   // waves per workgroup (A/B variants: 6, 12)
+  constexpr int kThreads = 64 * kWv;
   constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;   // S fragments per k-step
   constexpr int FA = JA - (TA > 0 ? 1 : 0) + TA;   // T fragments per k-step
   constexpr int JF = FS + FA;
@@ -589,9 +589,9 @@ __global__ __launch_bounds__(256, kMinW) void mode_product_fold_kernel(
       }
     }
   }
-  // the staged epilogue's images occupy the first 16 m doubles of LDS
+  // the staged epilogue's images occupy the first 4 kWaves m doubles of LDS
   mp_block_sums<kWaves, CGP, edots, false>(dsum, edots ? rqsum : pqo_acc, qqsum, rr_acc,
-                                           dot_partials, fz, kStg ? lds + 16 * m : lds,
+                                           dot_partials, fz, kStg ? lds + 4 * kWaves * m : lds,
                                            blockIdx.x);
   if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
 }
@@ -605,8 +605,9 @@ bool fold_kind(int kind) {
 
 // KIND: kron_apply's launch kind; 8 / 9: the sharded operator's mapped
 // epilogue without / with the textbook CG prologue (gg_kron_dist_*)
-// OPT: kOpt (4 = kLean); KCO > 0 overrides the k-steps per chunk
-template <int JT, int TT, int KIND, bool STG = false, int OPT = 0, int KCO = 0>
+// OPT: kOpt (4 = kLean); KCO > 0 overrides the k-steps per chunk; WV waves
+// per workgroup
+template <int JT, int TT, int KIND, bool STG = false, int OPT = 0, int KCO = 0, int WV = 4>
 static FoldConfig cfg_fold() {
   constexpr int CGP = (KIND == 1 || KIND == 9) ? 1 : KIND == 2 ? 2 : KIND == 7 ? 3 : 0;
   constexpr int EPI = KIND == 3 ? 2 : KIND == 4 ? 1 : KIND == 6 ? 4 : 0;
@@ -621,9 +622,10 @@ static FoldConfig cfg_fold() {
   constexpr int MINW = ((JT - (TT > 0 ? 1 : 0)) <= 6 && TT <= 1) ? 3 : 2;
   constexpr size_t kB = 2 * (size_t)KC * JF * 64 * sizeof(double);
   // staged epilogue: 4 waves x 4 rows x m (<= 32 JT) doubles + the reduction
-  constexpr size_t kS = STG ? ((size_t)16 * 32 * JT + 16) * sizeof(double) : 0;
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, MINW, EPI, MAP, OPT, STG>,
-                    KC, JF, kB > kS ? kB : kS, (OPT & 4) != 0};
+  constexpr size_t kS = STG ? ((size_t)4 * WV * 32 * JT + 4 * WV) * sizeof(double) : 0;
+  return FoldConfig{
+      mode_product_fold_kernel<JT, JT, TT, TT, KC, CGP, MINW, EPI, MAP, OPT, STG, WV>, KC, JF,
+      kB > kS ? kB : kS, (OPT & 4) != 0, WV};
 }
 
 // kLean kernels, instantiated for the m = 200 shape (JT 7, TT 1): default for
@@ -663,13 +665,25 @@ static FoldConfig lean_pro_cfg(int mode) {
   return mode == 2 ? cfg_fold<7, 1, 2, false, 4, 2>() : cfg_fold<7, 1, 2, false, 4, 1>();
 }
 
-// plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only)
-template <int KC, int MINW, int OPT>
+// 12-wave workgroups (one per CU, the B chunks staged once for 192 rows b,
+// 1.5 KB row segments): default for the fused-CG prologue of the m = 200
+// shape (GG_FOLD_PRO_W=4 restores 4 waves) -- 200^4, interleaved processes:
+// prologue 13.58-13.66 -> 13.18-13.21 ms, iteration 40.19-40.42 -> 39.93-39.95
+// ms (profiles/r03/an_wide_cg_ab.jsonl); the side-job launches lose 0.7 ms
+// each with them (GG_FOLD_SIDE_W=12, A/B only).  The prologue's r.r partials
+// array is sized for 4-wave blocks and zeroed at allocation (gg_cg_create).
+static FoldConfig wide_cfg(int kind) {
+  return kind == 2 ? cfg_fold<7, 1, 2, false, 0, 0, 12>() : cfg_fold<7, 1, 4, false, 4, 0, 12>();
+}
+
+// plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only); WV waves
+// per workgroup
+template <int KC, int MINW, int OPT, int WV = 4>
 static FoldConfig cfg_fold_var() {
   constexpr int JT = 7, TT = 1;
   constexpr int JF = 2 * (JT - 1 + TT);
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, 0, MINW, 0, false, OPT>, KC, JF,
-                    2 * (size_t)KC * JF * 64 * sizeof(double), (OPT & 4) != 0};
+  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, 0, MINW, 0, false, OPT, false, WV>,
+                    KC, JF, 2 * (size_t)KC * JF * 64 * sizeof(double), (OPT & 4) != 0, WV};
 }
 
 static int fold_variant() {
@@ -692,6 +706,10 @@ static FoldConfig fold_variant_cfg(int v) {
     case 11: return cfg_fold_var<3, 2, 12>();
     case 12: return cfg_fold_var<6, 2, 12>();
     case 13: return cfg_fold_var<3, 3, 20>();
+    case 14: return cfg_fold_var<3, 3, 4, 6>();
+    case 15: return cfg_fold_var<3, 3, 4, 12>();
+    case 16: return cfg_fold_var<6, 3, 4, 12>();
+    case 17: return cfg_fold_var<6, 3, 4, 6>();
     default: return cfg_fold_var<3, 3, 0>();
   }
 }
@@ -760,9 +778,11 @@ static FoldConfig fold_by_kind(int kind, bool lean_ok) {
     if (kind == 2) {
       const int lp = env_int("GG_FOLD_LEAN_PRO");
       if (lean_ok && (lp == 1 || lp == 2)) return lean_pro_cfg(lp);
+      if (env_int("GG_FOLD_PRO_W", 12) == 12) return wide_cfg(2);
       const char* e = getenv("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }
+    if (lean_ok && kind == 4 && env_int("GG_FOLD_SIDE_W") == 12) return wide_cfg(4);
     if (lean_ok && env_int("GG_FOLD_LEAN", 1) == 1 && lean_kind(kind, false))
       return lean_cfg(kind, false);
   }
@@ -827,12 +847,17 @@ void set_fold_lds_limits() {
       GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
     }
+  for (int kind : {2, 4}) {
+    const FoldConfig fc = wide_cfg(kind);
+    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
+  }
   for (int lp : {1, 2}) {
     const FoldConfig fc = lean_pro_cfg(lp);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
   }
-  for (int v = 1; v <= 13; ++v) {
+  for (int v = 1; v <= 17; ++v) {
     const FoldConfig fc = fold_variant_cfg(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));

@@ -161,6 +161,7 @@ struct FoldConfig {
   int kc, jf;     // k-steps per LDS chunk, fragments per k-step (both halves)
   size_t lds;     // dynamic LDS bytes
   bool lean = false;   // kLean A addressing: the launch checks its row / offset range
+  int waves = 4;       // waves per workgroup (16 rows b each)
 };
 bool fold_kind(int kind);
 // lean_ok: the launch is in the kLean kernels' range (every chunk's rows

@@ -740,6 +740,9 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       if (cg->fused) {
         cg->rr_count = gg::kron_prologue_blocks(K);
         GG_HIP(hipMalloc(&cg->rr_part, 2 * cg->rr_count * sizeof(double)));
+        // zeroed: a prologue launch with fewer (wider) workgroups than
+        // rr_count leaves the tail of both partial arrays at 0
+        GG_HIP(hipMemset(cg->rr_part, 0, 2 * cg->rr_count * sizeof(double)));
       }
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
