@@ -20,9 +20,13 @@ Prints ONE JSON line (rank 0):
                       sequence; fidelity vs the reference in
                       profiles/r02_cpu_fidelity.json) in a textbook CG on the
                       full grid, 1 warm-up + 3 timed iterations, host threads
+  matvec              (--matvec R, default 5) the isolated K*x on the same
+                      operator: HIP events per mode product, HBM / MFMA
+                      fractions of the 8-pass matvec; not part of `value`
   lanczos             (--lanczos K, default 30) K steps of device Lanczos on
-                      the same operator after the CG leg, timed with HIP
-                      events (SLQ log-det leg of C3); not part of `value`
+                      the same operator after the CG leg, per-step HIP events
+                      recorded by the library (SLQ log-det leg of C3); not
+                      part of `value`
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 200] [--dims 4]
 --gpus N > 1 without a launcher: this process starts
@@ -63,6 +67,9 @@ def parse():
     ap.add_argument("--lanczos", type=int, default=30,
                     help="also time this many device Lanczos steps (one probe; 0 = off; "
                          "single GPU only)")
+    ap.add_argument("--matvec", type=int, default=5,
+                    help="also time this many isolated K*x matvecs (HIP events per mode "
+                         "product; 0 = off; single GPU only)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "push", "a2a"])
     ap.add_argument("--fusion", type=int, default=None, choices=[0, 1, 2],
                     help="fused-CG layout (gg_cg_set_fusion); default: the library's")
@@ -579,20 +586,97 @@ def grief_leg(names, torch, cpu):
     return out
 
 
-def time_lanczos(K, s, steps, torch):
+def lanczos_passes(d):
+    """8-byte passes over N per fused Lanczos step by mode-product position
+    (gg_vec.hip gg_lanczos_probe, even d): the first mode product's prologue
+    reads the previous output Y (its MFMA operand), u and u_prev and writes
+    w = cy Y + cu u + cp u_prev over u_prev (+3 beyond the plain 2); the last
+    epilogue reads w for shift * w and w.(K w + shift w) (+1)."""
+    passes = [2.0] * d
+    passes[0] += 3.0
+    passes[d - 1] += 1.0
+    return passes
+
+
+def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
     """`steps` Lanczos steps of one probe on the same operator (the SLQ leg of
-    C3), timed with HIP events on the library's stream."""
+    C3).  The 4N workspace is allocated (and the allocator warmed) before
+    anything is timed; the library records HIP events at every step boundary on
+    the stream it launches on (gg_lanczos_probe_timed: after the probe is drawn,
+    before the tridiagonal is copied back) and around every mode product, so
+    ms_per_step is the mean of the per-step event times.  bracket_ms (events
+    around the whole call, workspace already resident) is reported beside it."""
+    from gp_grief_amd import device as gdev
     from gp_grief_amd import linalg
+    t0 = time.perf_counter()
+    work = gdev.empty(4 * n)
+    work.zero_()
     torch.cuda.synchronize()
+    alloc_s = time.perf_counter() - t0
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    a, b = linalg.lanczos_tridiag(K, s, steps, seed=0, probe=0)
+    a, b, step_ms, launch_ms = linalg.lanczos_tridiag(K, s, steps, seed=0, probe=0, work=work,
+                                                      timed=True)
     e1.record()
     torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1)
-    return {"steps": int(a.size), "ms": ms, "ms_per_step": ms / max(int(a.size), 1),
-            "steps_per_s": 1e3 * a.size / ms}
+    bracket = e0.elapsed_time(e1)
+    del work
+    k = int(a.size)
+    st = step_ms[:k]
+    ms = float(np.mean(st))
+    steady = float(np.mean(st[1:])) if k > 1 else ms
+    passes = lanczos_passes(d) if d % 2 == 0 else None
+    out = {"steps": k, "ms_per_step": ms, "steps_per_s": 1e3 / ms,
+           "steady_ms_per_step": steady, "first_step_ms": st[0],
+           "step_ms_min": float(np.min(st)), "step_ms_max": float(np.max(st)),
+           "ms_source": "mean of per-step HIP events the library records on its stream "
+                        "(gg_lanczos_probe_timed); workspace allocated before timing",
+           "mode_product_ms_by_position": [t / steps for t in launch_ms],
+           "bracket_ms": bracket, "bracket_ms_per_step": bracket / max(k, 1),
+           "workspace_alloc_s": alloc_s}
+    if passes is not None and k > 1:
+        byts = 8.0 * n * sum(passes)
+        flop = sum((1.0 if (fold_mask >> i) & 1 else 2.0) * n * m for i in range(d))
+        out["roofline"] = {
+            "passes_per_step": sum(passes), "passes_by_position": passes,
+            "algorithmic_bytes_per_step": byts, "flop_per_step": flop,
+            "achieved_gbs": byts / (steady * 1e-3) / 1e9,
+            "frac_hbm": byts / (steady * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "achieved_tflops": flop / (steady * 1e-3) / 1e12,
+            "frac_mfma": flop / (steady * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "basis": "steady steps (2..k): the fused step with the update pass as the "
+                     "first mode product's prologue"}
+    return out
+
+
+def time_matvec(K, n, m, d, fold_mask, torch, dev, reps=5):
+    """The north star's literal Kron-matvec: y = K x (no shift, no CG fusion)
+    on the 200^4 operator, inputs resident, reps back-to-back matvecs after one
+    warm-up, HIP events around every mode product on the library's stream
+    (gg_kron_matvec_timed).  Roofline: 2 passes (X read, Y written) per mode
+    product = 16 N bytes; n m MFMA FLOP per folded factor (2 n m dense)."""
+    dk = K._device()
+    x = grid_rhs_device(m, d, torch, dev)
+    y = torch.empty_like(x)
+    dk.matvec(x, out=y)          # warm-up (and the scratch allocation)
+    torch.cuda.synchronize()
+    per, tot = dk.matvec_timed(x, y, reps)
+    del x, y
+    ms = tot / reps
+    byts = 16.0 * n * d
+    flop = sum((1.0 if (fold_mask >> i) & 1 else 2.0) * n * m for i in range(d))
+    pos = [t / reps for t in per]
+    return {"reps": reps, "ms": ms, "mode_product_ms_by_position": pos,
+            "ms_source": "HIP events around every mode product on the library's stream "
+                         "(gg_kron_matvec_timed)",
+            "algorithmic_bytes": byts, "passes": 2 * d, "flop": flop,
+            "achieved_gbs": byts / (ms * 1e-3) / 1e9,
+            "frac_hbm": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "achieved_tflops": flop / (ms * 1e-3) / 1e12,
+            "frac_mfma": flop / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "dense_equivalent_tflops": d * 2.0 * n * m / (ms * 1e-3) / 1e12,
+            "launch_frac_hbm": [16.0 * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS for t in pos]}
 
 
 # ---------------------------------------------------------------- main
@@ -686,8 +770,11 @@ def main():
     result.update(extra)
     del solver, y
     torch.cuda.empty_cache()
+    if a.matvec > 0:
+        result["matvec"] = time_matvec(K, n, m, d, fold_mask, torch, dev, a.matvec)
+        torch.cuda.empty_cache()
     if a.lanczos > 0:
-        result["lanczos"] = time_lanczos(K, s, a.lanczos, torch)
+        result["lanczos"] = time_lanczos(K, s, a.lanczos, torch, n, m, d, fold_mask)
         torch.cuda.empty_cache()
     if a.grief != "off":
         result["grief"] = grief_leg([c.strip() for c in a.grief.split(",") if c.strip()], torch,

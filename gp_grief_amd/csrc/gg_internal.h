@@ -110,6 +110,12 @@ struct MpFuse {
   double* p_out = nullptr;
   const CgScalars* sc = nullptr;
   double* rr_part = nullptr;
+  // rr_part holds rr_cap partials per half (the prologue launch's workgroup
+  // count must not exceed it: kron_apply checks), and kron_apply reports the
+  // launch's actual workgroup count through pro_blocks (host memory), so the
+  // consumers sum exactly the partials this launch wrote
+  int64_t rr_cap = 0;
+  int64_t* pro_blocks = nullptr;
   // conjugacy r.q (gg_cg_set_rq 1): the CG prologue also writes block partials
   // of p_new.q_old to rr_part[pqo_stride + blk] (0 = off), and the last epilogue
   // gets er == nullptr -- r_j.q_j = p_j.q_j - beta_j p_j.q_{j-1} (A symmetric)

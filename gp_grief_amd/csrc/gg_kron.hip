@@ -907,6 +907,9 @@ struct Factor {
   // fJT 16-wide tiles per half, the last as fTT 4x4x4_4b fragments if fTT > 0
   double* ffrag = nullptr;
   int fKS = 0, fJT = 0, fTT = 0;
+  // the same fragments at 16 per k-step ([fKS][16][64], zero pads) for the
+  // ring kernel (gg_kron_ring.hip), when its shape is instantiated
+  double* rfrag = nullptr;
 };
 
 static bool t4_supported(int JT) { return JT == 13; }
@@ -1009,6 +1012,14 @@ static void pack_fold(const double* K, int64_t m, bool transpose, Factor& f) {
   f.fKS = KS;
   f.fJT = JT;
   f.fTT = TT;
+  if (ring_available(JT, TT, m) && JF <= 16) {
+    std::vector<double> rb((size_t)KS * 16 * 64, 0.0);
+    for (int ks = 0; ks < KS; ++ks)
+      std::copy(hb.begin() + (size_t)ks * JF * 64, hb.begin() + (size_t)(ks + 1) * JF * 64,
+                rb.begin() + (size_t)ks * 16 * 64);
+    GG_HIP(hipMalloc(&f.rfrag, rb.size() * sizeof(double)));
+    GG_HIP(hipMemcpy(f.rfrag, rb.data(), rb.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
 }
 
 }  // namespace gg
@@ -1120,6 +1131,21 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
                                   ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
                                                                                       : x)
                                   : nullptr;
+          // the persistent LDS-DMA ring kernel (gg_kron_ring.hip) for the plain
+          // launch (GG_FOLD_RING=<variant>)
+          const int rv = ring_variant_env();
+          if (rv > 0 && kind == 0 && xs_ == nullptr && skip == nullptr && f.rfrag != nullptr &&
+              M % 2 == 0 && M >= 2 &&
+              ((reinterpret_cast<uintptr_t>(step_src) | reinterpret_cast<uintptr_t>(dst)) & 15) ==
+                  0) {
+            const RingConfig rc = select_ring(f.fJT, f.fTT, rv);
+            const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
+            const int grid = ring_grid(rc, cu_count(), nb);
+            hipLaunchKernelGGL(rc.fn, dim3((unsigned)grid), dim3(64 * rc.waves), rc.lds, stream,
+                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb);
+            GG_LAUNCH_CHECK();
+            continue;
+          }
           const bool aligned =
               f.p % 2 == 0 &&
               ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(xs_) |
@@ -1152,6 +1178,11 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           if (pro == 2 || pro == 7) {
             fz.q_old = cg->q_old;
             fz.rr_part = cg->rr_part;
+            // the partial arrays are sized at handle creation; the launch
+            // shape is chosen here (env knobs may change between calls)
+            GG_REQUIRE(cg->rr_part == nullptr || nblk <= cg->rr_cap, GG_ERR_VALUE,
+                       "prologue launch has more workgroups than its partial array");
+            if (cg->pro_blocks != nullptr) *cg->pro_blocks = nblk;
           }
           if (pro == 2) fz.pqo_stride = cg->pqo_stride;
           if (pro == 7) fz.coef = cg->coef;
@@ -1247,12 +1278,13 @@ int64_t kron_partials_needed(const gg_kron* K, bool transpose) {
   return ceil_div(M, 2 * 16) * ceil_div(f.JT, kMaxJT);
 }
 
-// workgroups of the (forward) first mode product's first launch with the
-// fused CG prologue: the length of its r.r partial array
+// an upper bound on the workgroups of the (forward) first mode product's first
+// launch with a fused CG / Lanczos prologue, whatever kernel it selects (every
+// workgroup owns at least one 16-row strip): the capacity of its r.r partial
+// array.  The launch reports its actual count (MpFuse::pro_blocks).
 int64_t kron_prologue_blocks(const gg_kron* K) {
   const Factor& f = K->fwd[0];
-  const ModeConfig mc = select_kernel(std::min(kMaxJT, f.JT), 0, 2);
-  return ceil_div(K->n_cols / f.q, (int64_t)(mc.waves / mc.split) * 16);
+  return ceil_div(K->n_cols / f.q, (int64_t)16);
 }
 
 int64_t kron_work_elems(const gg_kron* K, bool transpose) {
@@ -1290,6 +1322,7 @@ static void set_lds_limits() {
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)mode_lds_bytes(mc)));
   }
   set_fold_lds_limits();
+  set_ring_lds_limits();
   done = true;
 }
 
@@ -1341,6 +1374,7 @@ int gg_kron_destroy(gg_kron* K) {
         if (f.frag) (void)hipFree(f.frag);
         if (f.frag4) (void)hipFree(f.frag4);
         if (f.ffrag) (void)hipFree(f.ffrag);
+        if (f.rfrag) (void)hipFree(f.rfrag);
       }
     delete K;
   });
@@ -1374,6 +1408,46 @@ int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double*
     GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
     gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
                    gg::as_stream(stream), nullptr, nullptr, 0, nullptr);
+  });
+}
+
+int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, double* y_dev,
+                         double shift, double* work_dev, int reps, double* launch_ms_host,
+                         double* total_ms_host, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev && launch_ms_host && total_ms_host && reps >= 1,
+               GG_ERR_VALUE, "bad argument");
+    GG_REQUIRE(work_dev != nullptr || K->d == 1, GG_ERR_VALUE, "work buffer required");
+    hipStream_t s = gg::as_stream(stream);
+    const int d = K->d;
+    std::vector<hipEvent_t> ev((size_t)reps * (d + 1));
+    for (auto& e : ev) e = nullptr;
+    auto release = [&] {
+      for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    };
+    try {
+      for (auto& e : ev) GG_HIP(hipEventCreate(&e));
+      for (int r = 0; r < reps; ++r)
+        gg::kron_apply(K, transpose != 0, x_dev, y_dev, shift, work_dev, nullptr, nullptr, s,
+                       nullptr, nullptr, 0, ev.data() + (size_t)r * (d + 1));
+      GG_HIP(hipStreamSynchronize(s));
+      for (int k = 0; k < d; ++k) launch_ms_host[k] = 0.0;
+      for (int r = 0; r < reps; ++r)
+        for (int k = 0; k < d; ++k) {
+          float ms = 0.f;
+          GG_HIP(hipEventElapsedTime(&ms, ev[(size_t)r * (d + 1) + k],
+                                     ev[(size_t)r * (d + 1) + k + 1]));
+          launch_ms_host[k] += ms;
+        }
+      float tot = 0.f;
+      GG_HIP(hipEventElapsedTime(&tot, ev.front(), ev.back()));
+      *total_ms_host = tot;
+    } catch (...) {
+      release();
+      throw;
+    }
+    release();
   });
 }
 
@@ -1517,6 +1591,7 @@ int gg_kron_dist_destroy(gg_kron_dist* D) {
       if (f.frag) (void)hipFree(f.frag);
       if (f.frag4) (void)hipFree(f.frag4);
       if (f.ffrag) (void)hipFree(f.ffrag);
+      if (f.rfrag) (void)hipFree(f.rfrag);
     }
     for (void* b : D->opened) (void)hipIpcCloseMemHandle(b);
     if (D->peers_recv) (void)hipFree(D->peers_recv);

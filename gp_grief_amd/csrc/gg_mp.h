@@ -173,4 +173,19 @@ bool fold_staged_available(int JT, int TT, int kind);
 FoldConfig select_fold_staged(int JT, int TT, int kind, bool lean_ok = false);
 void set_fold_lds_limits();
 
+// The persistent LDS-DMA ring version of the plain folded launch
+// (gg_kron_ring.hip): B fragments from Factor::rfrag ([fKS][16][64]).
+typedef void (*ring_kernel_t)(const double*, double*, const double*, int64_t, int, int, int64_t);
+struct RingConfig {
+  ring_kernel_t fn;
+  int waves, ns, kc;   // waves per workgroup, ring stages, k-steps per stage
+  size_t lds;          // dynamic LDS bytes
+};
+int ring_variant_env();   // GG_FOLD_RING: 0 = off, else the variant
+bool ring_available(int JT, int TT, int64_t m);
+RingConfig select_ring(int JT, int TT, int variant);
+// persistent grid: resident workgroups per CU x CUs, at most nblk
+int ring_grid(const RingConfig& rc, int cus, int64_t nblk);
+void set_ring_lds_limits();
+
 }  // namespace gg

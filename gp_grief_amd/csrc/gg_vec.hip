@@ -256,8 +256,9 @@ __global__ void cg_x_flushed_kernel(CgScalars* sc) {
 // side launch carries one pass instead of two in every other iteration; four
 // direction buffers keep the pair alive.
 __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
-    const double* __restrict__ rr_part, int64_t nrr, const double* __restrict__ mv_part,
-    int64_t nmv, int64_t pstride, CgScalars* sc, const double* p_new, int xmode, int rq_ident) {
+    const double* __restrict__ rr_part, int64_t nrr, int64_t rr_stride,
+    const double* __restrict__ mv_part, int64_t nmv, int64_t pstride, CgScalars* sc,
+    const double* p_new, int xmode, int rq_ident) {
   if (sc->done) return;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
@@ -269,7 +270,7 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
   // beta_j p_{j-1}.A p_j = p_j.q_j - beta_j p_j.q_{j-1} (A symmetric); the
   // prologue summed p_j.q_{j-1} (zero on the first step, where beta = 0)
   if (rq_ident)
-    for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a1 += rr_part[nrr + i];
+    for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a1 += rr_part[rr_stride + i];
   const bool pend = sc->pending != 0;
   if (pend)
     for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a3 += rr_part[i];
@@ -738,10 +739,10 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->fused = gg::kron_d(K) >= 2 && (nr % 2) == 0 &&
                   (reinterpret_cast<uintptr_t>(work_dev) & 15) == 0;
       if (cg->fused) {
+        // capacity for any prologue launch shape; each iteration sums exactly
+        // the partials its prologue launch wrote (MpFuse::pro_blocks)
         cg->rr_count = gg::kron_prologue_blocks(K);
         GG_HIP(hipMalloc(&cg->rr_part, 2 * cg->rr_count * sizeof(double)));
-        // zeroed: a prologue launch with fewer (wider) workgroups than
-        // rr_count leaves the tail of both partial arrays at 0
         GG_HIP(hipMemset(cg->rr_part, 0, 2 * cg->rr_count * sizeof(double)));
       }
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
@@ -940,6 +941,9 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.ex = cg->fusion == 2 ? cg->x : nullptr;
         fz.sc = cg->sc;
         fz.rr_part = cg->rr_part;
+        fz.rr_cap = cg->rr_count;
+        int64_t pro_blocks = 0;   // the prologue launch's workgroups (kron_apply)
+        fz.pro_blocks = &pro_blocks;
         fz.sx = cg->fusion == 2 ? nullptr : cg->x;
         fz.sp = cg->p;
         fz.sn = n;
@@ -953,8 +957,11 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.pstride = cg->mv_partials;
         gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
                        &cg->sc->done, s, &nparts, &fz, 2, ev);
+        GG_REQUIRE(pro_blocks > 0 && pro_blocks <= cg->rr_count, GG_ERR_RUNTIME,
+                   "fused CG: no prologue launch recorded");
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
-                           cg->rr_count, cg->partials, nparts, cg->mv_partials, cg->sc,
+                           pro_blocks, cg->rr_count, cg->partials, nparts, cg->mv_partials,
+                           cg->sc,
                            xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
         GG_LAUNCH_CHECK();
         if (xmode == 2) {
@@ -1044,10 +1051,72 @@ int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, doub
   });
 }
 
+}  // extern "C"
+
+namespace gg {
+
+// RAII set of HIP events (timed Lanczos)
+struct EventSet {
+  std::vector<hipEvent_t> ev;
+  explicit EventSet(size_t n) {
+    ev.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      hipEvent_t e;
+      GG_HIP(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+  }
+  ~EventSet() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  EventSet(const EventSet&) = delete;
+  EventSet& operator=(const EventSet&) = delete;
+};
+
+// gg_lanczos_probe / gg_lanczos_probe_timed.  step_ms (steps entries, may be
+// null): HIP events on the stream at every step boundary -- the first after
+// the probe is drawn, so allocation, the u_prev memset and the probe kernel
+// are outside -- and the last after the final |w|^2 reduction, before the
+// alphas / betas are copied back; launch_ms (d entries, may be null): the
+// summed time of each mode-product position over the steps.
+static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                          double* work_dev, double* alphas_host, double* betas_host,
+                          int* steps_done, double* step_ms, double* launch_ms,
+                          gg_stream stream);
+
+}  // namespace gg
+
+extern "C" {
+
 int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
                      double* work_dev, double* alphas_host, double* betas_host,
                      int* steps_done, gg_stream stream) {
   return gg::guard([&] {
+    gg::lanczos_probe(K, shift, seed, probe, steps, work_dev, alphas_host, betas_host,
+                      steps_done, nullptr, nullptr, stream);
+  });
+}
+
+int gg_lanczos_probe_timed(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                           double* work_dev, double* alphas_host, double* betas_host,
+                           int* steps_done, double* step_ms_host, double* launch_ms_host,
+                           gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(step_ms_host != nullptr, GG_ERR_VALUE, "step_ms_host is NULL");
+    gg::lanczos_probe(K, shift, seed, probe, steps, work_dev, alphas_host, betas_host,
+                      steps_done, step_ms_host, launch_ms_host, stream);
+  });
+}
+
+}  // extern "C"
+
+namespace gg {
+
+static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                          double* work_dev, double* alphas_host, double* betas_host,
+                          int* steps_done, double* step_ms, double* launch_ms,
+                          gg_stream stream) {
+  {
     GG_REQUIRE(K && work_dev && alphas_host && betas_host && steps >= 1, GG_ERR_VALUE,
                "bad argument");
     int64_t nr = 0, nc = 0, we = 0;
@@ -1080,6 +1149,14 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
     hipLaunchKernelGGL(gg::probe_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                        gg::probe_base(seed, probe), 1.0 / std::sqrt((double)n), V, n);
     GG_LAUNCH_CHECK();
+    const int d = gg::kron_d(K);
+    const bool timed = step_ms != nullptr;
+    gg::EventSet sev(timed ? (size_t)steps + 1 : 0);
+    gg::EventSet mev(timed && launch_ms ? (size_t)steps * (d + 1) : 0);
+    auto mp_ev = [&](int j) -> hipEvent_t* {
+      return mev.ev.empty() ? nullptr : mev.ev.data() + (size_t)j * (d + 1);
+    };
+    if (timed) GG_HIP(hipEventRecord(sev.ev[0], s));
     // w = cy W + cu u + cp u_prev in place of W, |w|^2 -> betas[j], scales
     auto update_beta = [&](int j) {
       const int wide = ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(V) |
@@ -1100,17 +1177,22 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
       int64_t np = 0;
       if (j == 0 || !fuse) {
         // W = K u + shift u, and u.W per block of the last mode product
-        gg::kron_apply(K, false, V, W, shift, mvw, parts, nullptr, s, &np, nullptr, 0, nullptr);
+        gg::kron_apply(K, false, V, W, shift, mvw, parts, nullptr, s, &np, nullptr, 0, mp_ev(j));
       } else {
         gg::MpFuse lf;
         lf.r = V;
         lf.q_old = P;
         lf.p_out = P;
         lf.rr_part = rrparts;
+        lf.rr_cap = nrr;
+        int64_t pro_blocks = 0;
+        lf.pro_blocks = &pro_blocks;
         lf.coef = lzs;
-        gg::kron_apply(K, false, W, W, shift, mvw, parts, nullptr, s, &np, &lf, 3, nullptr);
+        gg::kron_apply(K, false, W, W, shift, mvw, parts, nullptr, s, &np, &lf, 3, mp_ev(j));
+        GG_REQUIRE(pro_blocks > 0 && pro_blocks <= nrr, GG_ERR_RUNTIME,
+                   "Lanczos: no prologue launch recorded");
         // |w|^2 of the prologue -> beta_{j-1}; w (now in P) is the new u
-        gg::launch_reduce_to(rrparts, gg::kron_prologue_blocks(K), betas + (j - 1), s);
+        gg::launch_reduce_to(rrparts, pro_blocks, betas + (j - 1), s);
         hipLaunchKernelGGL(gg::lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + (j - 1));
         GG_LAUNCH_CHECK();
         std::swap(P, V);   // u_prev <- u, u <- w
@@ -1130,12 +1212,29 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
           W = oldP;
         }
       }
+      if (timed) GG_HIP(hipEventRecord(sev.ev[j + 1], s));
     }
     GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost,
                           s));
     GG_HIP(hipMemcpyAsync(betas_host, betas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
     GG_HIP(hipFreeAsync(scal, s));
     GG_HIP(hipStreamSynchronize(s));
+    if (timed) {
+      for (int j = 0; j < steps; ++j) {
+        float ms = 0.f;
+        GG_HIP(hipEventElapsedTime(&ms, sev.ev[j], sev.ev[j + 1]));
+        step_ms[j] = ms;
+      }
+      if (launch_ms) {
+        for (int k = 0; k < d; ++k) launch_ms[k] = 0.0;
+        for (int j = 0; j < steps; ++j)
+          for (int k = 0; k < d; ++k) {
+            float ms = 0.f;
+            GG_HIP(hipEventElapsedTime(&ms, mp_ev(j)[k], mp_ev(j)[k + 1]));
+            launch_ms[k] += ms;
+          }
+      }
+    }
     int done = steps;
     for (int j = 0; j < steps; ++j)
       if (!(betas_host[j] > 1e-300)) {
@@ -1143,10 +1242,10 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
         break;
       }
     if (steps_done) *steps_done = done;
-  });
+  }
 }
 
-}  // extern "C"
+}  // namespace gg
 
 // ============================================ CG scalars for a host-driven (sharded) CG
 // The sharded solve (gp_grief_amd/distributed.py) runs the same recurrence as

@@ -252,22 +252,41 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
     return out, info
 
 
-def lanczos_tridiag(K, shift, steps, seed=0, probe=0):
-    """Device Lanczos on (K + shift I) from a Rademacher probe: (alphas, betas)."""
+def lanczos_tridiag(K, shift, steps, seed=0, probe=0, work=None, timed=False):
+    """Device Lanczos on (K + shift I) from a Rademacher probe: (alphas, betas).
+
+    work: optional device workspace of >= 4 N elements (allocated here
+    otherwise).  timed=True also returns the per-step HIP-event times (ms, one
+    per step run) and the summed time of each mode-product position
+    (gg_lanczos_probe_timed): (alphas, betas, step_ms, launch_ms)."""
     from . import device as dev
     from . import native
     dk = K._device()
     n = int(K.shape[0])
-    work = dev.empty(4 * n)
+    if work is None:
+        work = dev.empty(4 * n)
+    elif int(work.numel()) < 4 * n:
+        raise ValueError("Lanczos workspace needs %d elements" % (4 * n))
     a = (ctypes.c_double * steps)()
     b = (ctypes.c_double * steps)()
     done = ctypes.c_int()
-    native.check(native.lib().gg_lanczos_probe(dk.h, float(shift), int(seed), int(probe),
-                                               int(steps), native.dptr(work), a, b,
-                                               ctypes.byref(done), native.stream_ptr()),
-                 "gg_lanczos_probe")
+    if timed:
+        d = len(dk._keep)
+        sm = (ctypes.c_double * steps)()
+        lm = (ctypes.c_double * d)()
+        native.check(native.lib().gg_lanczos_probe_timed(
+            dk.h, float(shift), int(seed), int(probe), int(steps), native.dptr(work), a, b,
+            ctypes.byref(done), sm, lm, native.stream_ptr()), "gg_lanczos_probe_timed")
+    else:
+        native.check(native.lib().gg_lanczos_probe(dk.h, float(shift), int(seed), int(probe),
+                                                   int(steps), native.dptr(work), a, b,
+                                                   ctypes.byref(done), native.stream_ptr()),
+                     "gg_lanczos_probe")
     k = done.value
-    return np.array(a[:k]), np.array(b[:max(k - 1, 0)])
+    out = np.array(a[:k]), np.array(b[:max(k - 1, 0)])
+    if timed:
+        return out + ([sm[j] for j in range(steps)], [lm[i] for i in range(d)])
+    return out
 
 
 def slq_logdet(K, shift, probes=8, steps=30, seed=0):

@@ -42,6 +42,9 @@ SIGNATURES = {
     "gg_kron_shape": [_vp, ctypes.c_int, _c_i64p, _c_i64p, _c_i64p],
     "gg_kron_fold_mask": [_vp, ctypes.c_int, _c_i64p],
     "gg_kron_matvec": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_double, _c_dp, _vp],
+    "gg_kron_matvec_timed": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_double, _c_dp,
+                             ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_double), _vp],
     "gg_kron_diag_scale": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double, ctypes.c_int, _c_dp,
                            _c_dp, _vp],
     "gg_kron_logdet_shifted": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double,
@@ -71,6 +74,11 @@ SIGNATURES = {
     "gg_lanczos_probe": [_vp, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                          _c_dp, ctypes.POINTER(ctypes.c_double),
                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), _vp],
+    "gg_lanczos_probe_timed": [_vp, ctypes.c_double, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                               _c_dp, ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                               _vp],
     "gg_probe_fill": [ctypes.c_uint64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
     "gg_sym_eig_batched": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
                            ctypes.c_int, _vp],

@@ -87,6 +87,22 @@ class _DeviceKron(object):
                                                  native.stream_ptr()), "gg_kron_matvec")
         return y
 
+    def matvec_timed(self, xd, out, reps, transpose=False, shift=0.0):
+        """reps matvecs x -> out with HIP events around every mode product
+        (gg_kron_matvec_timed, synchronising): (per-position summed ms, total ms)."""
+        n_out, n_in, _ = self.shape(transpose)
+        if xd.numel() != n_in or out.numel() != n_out:
+            raise ValueError("x / out have the wrong length")
+        w = self.work(transpose)
+        d = len(self._keep)
+        lm = (ctypes.c_double * d)()
+        tot = ctypes.c_double()
+        native.check(native.lib().gg_kron_matvec_timed(
+            self.h, int(transpose), native.dptr(xd), native.dptr(out), float(shift),
+            native.dptr(w), int(reps), lm, ctypes.byref(tot), native.stream_ptr()),
+            "gg_kron_matvec_timed")
+        return [lm[k] for k in range(d)], tot.value
+
     def release_work(self):
         self._work = {}
 

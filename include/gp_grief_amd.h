@@ -70,6 +70,13 @@ int gg_kron_fold_mask(const gg_kron* K, int transpose, int64_t* mask);
  * (shift != 0 needs a square operator; x and y must not alias).            */
 int gg_kron_matvec(const gg_kron* K, int transpose, const double* x_dev, double* y_dev,
                    double shift, double* work_dev, gg_stream stream);
+/* reps back-to-back gg_kron_matvec calls with HIP events around every mode
+ * product on the stream (synchronising): launch_ms_host[k] (d entries) is the
+ * summed time of position k over the reps, *total_ms_host the event time of
+ * all reps.  Measurement entry (bench.py's isolated K*x leg).              */
+int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, double* y_dev,
+                         double shift, double* work_dev, int reps, double* launch_ms_host,
+                         double* total_ms_host, gg_stream stream);
 
 /* y = x / (prod_k lam_k[i_k] + shift), the eigenvalue product decoded from
  * the flat index on the fly (never expanded).  solve_schur's divide,
@@ -159,6 +166,15 @@ int gg_cg_profile_read(gg_cg* cg, int* n_matvecs, double* mode_ms, int mode_ms_l
 int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
                      double* work_dev, double* alphas_host, double* betas_host,
                      int* steps_done, gg_stream stream);
+/* The same with live per-step timing: step_ms_host[j] (steps entries) is the
+ * HIP-event time of step j on the stream (the first event after the probe is
+ * drawn, the last before alphas / betas are copied back); launch_ms_host
+ * (d entries, may be NULL) the summed time of each mode-product position over
+ * the steps.  No reference counterpart (SLQ is absent from the reference).  */
+int gg_lanczos_probe_timed(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                           double* work_dev, double* alphas_host, double* betas_host,
+                           int* steps_done, double* step_ms_host, double* launch_ms_host,
+                           gg_stream stream);
 int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream stream);
 
 /* --------------------------------------- per-factor symmetric eigensolver

@@ -322,3 +322,62 @@ def test_cg_rq_identity_matches_epilogue_rq(gg, fold_small, dims, centro):
         r_true = bh - (oracle.kron_matvec(F, x) + s * x)
         assert np.linalg.norm(r_true) <= 1e-8 * np.linalg.norm(bh)
     assert abs(counts[0] - counts[1]) <= 1, counts
+
+
+@pytest.mark.parametrize("ms", [(20, 18, 16, 12), (9, 8, 7)])
+def test_lanczos_timed_matches_untimed(gg, fold_small, ms):
+    """gg_lanczos_probe_timed (bench.py's Lanczos leg) runs the same steps as
+    gg_lanczos_probe: identical tridiagonal, one positive time per step, and a
+    per-position mode-product time for every factor."""
+    F = [grid_factor(m, 0.15 * (1 + 0.05 * k)) for k, m in enumerate(ms)]
+    K = kron(gg, F)
+    a0, b0 = gg.linalg.lanczos_tridiag(K, 0.03, 12, seed=3, probe=1)
+    a1, b1, step_ms, launch_ms = gg.linalg.lanczos_tridiag(K, 0.03, 12, seed=3, probe=1,
+                                                           timed=True)
+    assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
+    assert len(step_ms) == 12 and all(t > 0 for t in step_ms)
+    assert len(launch_ms) == len(ms) and all(t > 0 for t in launch_ms)
+
+
+def test_matvec_timed_matches_matvec(gg, fold_small):
+    """gg_kron_matvec_timed (bench.py's isolated K*x leg) computes the plain
+    matvec, reps times, with a time for every mode-product position."""
+    import torch
+    F = [grid_factor(200, 0.1), grid_factor(40, 0.13), grid_factor(36, 0.2, "Matern52")]
+    K = kron(gg, F)
+    n = 200 * 40 * 36
+    x = torch.from_numpy(np.random.default_rng(5).standard_normal(n)).cuda()
+    dk = K._device()
+    y0 = dk.matvec(x).clone()
+    y1 = torch.empty_like(x)
+    per, tot = dk.matvec_timed(x, y1, 3)
+    assert torch.equal(y0, y1)
+    assert len(per) == 3 and all(t > 0 for t in per) and tot >= 0.99 * sum(per)
+    assert rel(y1.cpu().numpy(), oracle.kron_matvec(F, x.cpu().numpy())) < 1e-13
+
+
+def test_cg_prologue_shape_change_on_live_handle(gg, monkeypatch):
+    """the prologue's workgroup shape is chosen per launch from env
+    knobs (GG_FOLD_PRO_W), while its r.r / p.q_old partial arrays are sized at
+    gg_cg_create.  Switching 12 -> 4 -> 12 waves between iterate calls on one
+    handle must sum exactly the partials each launch wrote (no stale tail, no
+    overrun): the iterate agrees with an unswitched run to rounding."""
+    F = [grid_factor(200, 0.1), grid_factor(48, 0.13), grid_factor(40, 0.2, "Matern52")]
+    K = kron(gg, F)
+    n = 200 * 48 * 40
+    import torch
+    b = torch.from_numpy(np.random.default_rng(11).standard_normal(n)).cuda()
+    monkeypatch.setenv("GG_FOLD_PRO_W", "12")
+    ref = gg.linalg.KronCG(K, 0.05)
+    ref.start(b, rtol=0.0)
+    ref.iterate(9)
+    sw = gg.linalg.KronCG(K, 0.05)
+    sw.start(b, rtol=0.0)
+    for w in ("12", "4", "12"):
+        monkeypatch.setenv("GG_FOLD_PRO_W", w)
+        sw.iterate(3)
+    it0, _, r0, _ = ref.status()
+    it1, _, r1, _ = sw.status()
+    assert it0 == it1 == 9
+    assert abs(r1 - r0) <= 1e-8 * abs(r0)
+    assert rel(sw.x.cpu().numpy(), ref.x.cpu().numpy()) < 1e-10
