@@ -73,24 +73,26 @@ __device__ __forceinline__ double swap_adjacent(double v) {
 // that slot; read stage c + 1's operands into the second register set; the
 // step's MFMAs on the first.  So the MFMAs never wait on LDS latency, and
 // NS - 1 stages are in flight across every barrier.
-template <int JS, int TS, int W, int NS, int MINW>
+template <int JS, int TS, int W, int NS, int MINW, int ABL = 0, int KC = 1>
 __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     const double* __restrict__ X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int KS, int64_t nblk) {
   constexpr int RB = 16 * W;           // rows b per block
   constexpr int kA = 8 * RB;           // A image doubles per k-step
   constexpr int kB = 16 * 64;          // B image doubles per k-step (16 fragments)
-  constexpr int kStage = kA + kB;
-  constexpr int kBw = 8 / W;           // B DMAs per wave per stage
-  constexpr int LW = 1 + kBw;          // DMAs per wave per stage
+  constexpr int kStep = kA + kB;
+  constexpr int kStage = KC * kStep;   // a stage: KC k-steps
+  constexpr int kBw = 8 / W;           // B DMAs per wave per k-step
+  constexpr int LW = KC * (1 + kBw);   // DMAs per wave per stage
   constexpr int kE = 4 * JS;           // epilogue stores per wave per block
-  constexpr int Y0 = (NS - 2) * LW;    // younger ops at a stage's wait
+  constexpr int Y0 = (NS - 3) * LW;    // younger ops at a stage's wait
   constexpr int YE = Y0 + kE;          // ... with an epilogue since its DMAs
   constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;
   constexpr int NF = 2 * FS;
   static_assert(W == 4 || W == 8, "one A DMA per wave: W KiB of A per k-step");
   static_assert(NF <= 16, "16 fragment slots per k-step");
-  static_assert(NS >= 3 && YE <= 63 && (NS - 1) * LW <= 63,
+  static_assert(KC == 1 || KC == 2, "one or two k-steps per stage");
+  static_assert(NS >= 4 && YE <= 63 && (NS - 2) * LW <= 63,
                 "ring depth outside the counted-vmcnt range");
   extern __shared__ __attribute__((aligned(16))) double lds[];
 
@@ -102,37 +104,76 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
   const int64_t nmine = (nblk - (int64_t)blockIdx.x + G - 1) / G;   // grid <= nblk
   const int nst = (int)(nmine * KS);
 
-  // this wave's 1 KiB piece of the A image: 128 doubles from row arow, column acol
+  // this wave's 1 KiB piece of the A image: 128 doubles from image row arow,
+  // column acol.  W = 8: one row per wave; W = 4: lanes 32..63 take the next
+  // row (the same half, so its X row is one row further in that half's order)
   const int ao = wave * 128 + 2 * lane;
   const int arow = ao / RB, acol = ao % RB;
+  const int arow0 = (wave * 128) / RB;   // the wave's first image row (uniform)
+  const int64_t drow = (int64_t)(arow - arow0) * (arow0 < 4 ? M : -M) * 8;
+  // the wave-uniform part of every DMA address goes through readfirstlane
+  // (SGPRs, scalar 64-bit arithmetic); lanes add a byte offset
+  auto sbase = [](const void* p, int64_t off) -> const char* {
+    const uint64_t v = reinterpret_cast<uint64_t>(p) + (uint64_t)off;
+    const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t u = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const char*>(((uint64_t)u << 32) | l);
+  };
+  const int64_t row_step = (int64_t)4 * M * 8;   // bytes between k-steps' rows
+  const uint32_t b_loff = (uint32_t)(2 * lane * 8);
 
-  // issue cursor: the next k-step (block it, step s) to stage
+  // issue cursor: the next k-step (block it, step s) to stage; a_off = byte
+  // offset of this wave's first A row segment at that step (uniform), a_loff
+  // = the lane's byte offset from it (column clamped in a partial last block)
   int64_t i_it = 0;
   int i_s = 0;
-  auto issue_stage = [&](int slot) {
-    double* st = lds + slot * kStage;
-    // past this workgroup's last block the DMAs re-read a valid block
-    // (never consumed): every wave issues LW DMAs per stage, always
+  int64_t a_off = 0;
+  int64_t a_loff = 0;
+  auto block_start = [&] {
+    // past this workgroup's last block the DMAs re-read a valid block (never
+    // consumed): every wave issues LW DMAs per stage, always
     const int64_t it = i_it < nmine ? i_it : nmine - 1;
-    const int64_t blk = (int64_t)blockIdx.x + it * G;
-    int64_t b = blk * RB + acol;
-    if (b > M - 2) b = M - 2;
-    const int s = i_s;
-    const int row = arow < 4 ? 4 * s + arow : m - 1 - 4 * s - (arow - 4);
-    __builtin_amdgcn_global_load_lds(
-        (const __attribute__((address_space(1))) void*)(X + (int64_t)row * M + b),
-        (__attribute__((address_space(3))) void*)(st + wave * 128), 16, 0, 0);
+    const int64_t b0 = ((int64_t)blockIdx.x + it * G) * RB;
+    const int row0 = arow0 < 4 ? arow0 : m - 1 - (arow0 - 4);
+    a_off = ((int64_t)row0 * M + b0) * 8;
+    const int64_t room = M - 2 - b0;   // the last valid pair start in this block
+    a_loff = drow + (acol <= room ? acol : room) * 8;
+  };
+  block_start();
+  // the next stage's DMA sources, prepared (with the cursor's branches)
+  // outside the MFMA region so that the DMAs issue branch-free inside it
+  int64_t na_off[KC], nb_off[KC], na_loff[KC];
+  auto prep_stage = [&] {
 #pragma unroll
-    for (int j = 0; j < kBw; ++j) {
-      const int p = wave * kBw + j;
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(Bf + (int64_t)s * kB + p * 128 +
-                                                          2 * lane),
-          (__attribute__((address_space(3))) void*)(st + kA + p * 128), 16, 0, 0);
+    for (int k = 0; k < KC; ++k) {
+      na_off[k] = a_off;
+      na_loff[k] = a_loff;
+      nb_off[k] = (int64_t)i_s * kB * 8;
+      if (++i_s == KS) {
+        i_s = 0;
+        ++i_it;
+        block_start();
+      } else {
+        a_off += arow0 < 4 ? row_step : -row_step;
+      }
     }
-    if (++i_s == KS) {
-      i_s = 0;
-      ++i_it;
+  };
+  auto issue_prepped = [&](int slot) {
+    if (ABL & 16) return;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      double* st = lds + slot * kStage + k * kStep;
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(sbase(X, na_off[k]) + na_loff[k]),
+          (__attribute__((address_space(3))) void*)(st + wave * 128), 16, 0, 0);
+#pragma unroll
+      for (int j = 0; j < kBw; ++j) {
+        const int p = wave * kBw + j;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(
+                sbase(Bf, nb_off[k] + (int64_t)p * 128 * 8) + b_loff),
+            (__attribute__((address_space(3))) void*)(st + kA + p * 128), 16, 0, 0);
+      }
     }
   };
 
@@ -149,8 +190,9 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
   };
 
   // a stage's operands: the two raw rows and the 2 FS B fragments
-  auto read_stage = [&](int slot, double (&op)[NF + 2]) {
-    const double* st = lds + slot * kStage;
+  // k-step g's operands (stage g / KC, step g % KC of it)
+  auto read_step = [&](int g, double (&op)[NF + 2]) {
+    const double* st = lds + ((g / KC) % NS) * kStage + (g % KC) * kStep;
     op[0] = st[krow * RB + wave * 16 + c16];
     op[1] = st[(4 + krow) * RB + wave * 16 + c16];
     const double* bs = st + kA + lane;
@@ -204,79 +246,157 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     const int64_t b0 = ((int64_t)blockIdx.x + it * G) * RB + wave * 16;
     const bool odd = (lane & 1) != 0;
     const int ce = c16 & ~1;
+    // even lanes store row rp with the odd neighbour's va, odd lanes row
+    // rp + 1 with the even neighbour's vb: (x, y) of the 16-byte pair
+    auto pair = [&](int t, int hf, int rp) -> double2 {
+      const double va = hf ? accs[t][rp] - acca[t][rp] : accs[t][rp] + acca[t][rp];
+      const double vb = hf ? accs[t][rp + 1] - acca[t][rp + 1] : accs[t][rp + 1] + acca[t][rp + 1];
+      const double w = swap_adjacent(odd ? va : vb);
+      double2 o;
+      if (hf == 0) {
+        o.x = odd ? w : va;
+        o.y = odd ? vb : w;
+      } else {   // S - T at m - 1 - j: the pair (m - 2 - j, m - 1 - j) swapped
+        o.x = odd ? vb : w;
+        o.y = odd ? w : va;
+      }
+      return o;
+    };
+    if (b0 + 16 <= M) {
+      // full strip: the wave's 16 x m output block is contiguous -- SGPR base
+      // + 32-bit lane offsets, the tile offset in the instruction; only the
+      // tail tile's pairs past column h are masked (lanes 0..3 of every row
+      // group stay active, so no store is ever skipped)
+      const char* y0 = sbase(Y, b0 * m * 8);
+      const char* y2 = sbase(Y, (b0 + 8) * m * 8);
+      const uint32_t rowoff = (uint32_t)(((odd ? 4 : 0) + krow) * m * 8);
+      uint32_t off0 = rowoff + (uint32_t)(ce * 8);
+      uint32_t off1 = rowoff + (uint32_t)((m - 2 - ce) * 8);
+      // opaque here: the per-tile offsets fold into each store's immediate
+      // instead of being hoisted out of the k-loop as live registers
+      asm volatile("" : "+v"(off0), "+v"(off1));
+#pragma unroll
+      for (int t = 0; t < JS; ++t)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+          for (int rp = 0; rp < 4; rp += 2) {
+            const double2 o = pair(t, hf, rp);
+            const char* yb = rp ? y2 : y0;
+            const uint32_t off = hf ? off1 - 128 * t : off0 + 128 * t;
+            if ((t < JS - 1 || 16 * t + ce < h) && !(ABL & 8)) {
+              if (ABL & 64)   // diagnostic: keep the arithmetic, drop the store
+                asm volatile("" ::"v"(o.x), "v"(o.y), "v"(yb + off));
+              else
+                *reinterpret_cast<double2*>(const_cast<char*>(yb) + off) = o;
+            }
+            // one pair at a time: the accumulators die as they are stored
+            __builtin_amdgcn_sched_barrier(0);
+          }
+      return;
+    }
+    // partial strip (the last block only): per-store bounds, out-of-range
+    // lanes to g_ring_trash so every store still issues
+    int ceo = ce;
+    asm volatile("" : "+v"(ceo));   // keep the per-tile addresses out of the k-loop
 #pragma unroll
     for (int t = 0; t < JS; ++t)
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
         for (int rp = 0; rp < 4; rp += 2) {
-          const double va = hf ? accs[t][rp] - acca[t][rp] : accs[t][rp] + acca[t][rp];
-          const double vb =
-              hf ? accs[t][rp + 1] - acca[t][rp + 1] : accs[t][rp + 1] + acca[t][rp + 1];
-          // even lanes store row rp with the odd neighbour's va, odd lanes
-          // row rp + 1 with the even neighbour's vb
-          const double w = swap_adjacent(odd ? va : vb);
-          const int j = 16 * t + ce;   // the pair's first column (S + T half)
+          const double2 o = pair(t, hf, rp);
+          const int j = 16 * t + ceo;   // the pair's first column (S + T half)
           const int64_t row = b0 + 4 * (rp + (odd ? 1 : 0)) + krow;
-          double2 o;
-          if (hf == 0) {
-            o.x = odd ? w : va;
-            o.y = odd ? vb : w;
-          } else {   // S - T at m - 1 - j: the pair (m - 2 - j, m - 1 - j) swapped
-            o.x = odd ? vb : w;
-            o.y = odd ? w : va;
-          }
           const int64_t col = hf ? (int64_t)(m - 2 - j) : (int64_t)j;
           double* dst = (j < h && row < M) ? Y + row * m + col : g_ring_trash + 2 * lane;
-          *reinterpret_cast<double2*>(dst) = o;
+          if (!(ABL & 8)) *reinterpret_cast<double2*>(dst) = o;
+          __builtin_amdgcn_sched_barrier(0);
         }
   };
 
+  if (ABL & 32) {
+    // desynchronise the workgroups' block epilogues (their store bursts):
+    // workgroup g starts (g * 7 mod 16) sixteenths of a block late
+    const int q = (int)((blockIdx.x * 7) & 15);
+    for (int i = 0; i < q; ++i) __builtin_amdgcn_s_sleep(60);
+  }
 #pragma unroll
-  for (int q = 0; q < NS; ++q) issue_stage(q);
-  wait_vm<(NS - 1) * LW>();
+  for (int q = 0; q < NS - 1; ++q) {
+    prep_stage();
+    issue_prepped(q);
+  }
+  prep_stage();
+  wait_vm<(NS - 3) * LW>();   // stages 0 and 1
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  double cur[NF + 2], nxt[NF + 2];
-  read_stage(0, cur);
+  double opa[NF + 2], opb[NF + 2];
+  read_step(0, opa);
   zero();
   int64_t c_it = 0;
   int c_s = 0;
-  int last_ep = -(1 << 30);   // step whose compute ran the latest epilogue
-  for (int c = 0; c < nst; ++c) {
+  int last_ep = -(1 << 30);   // stage whose compute ran the latest epilogue
+  // k-step c: MFMAs on `cur` (its operands, read during step c - 1), the
+  // reads of step c + 1 into `nxt`; the first step of stage j also retires
+  // stage j + 1 and refills stage j - 1's slot with stage j + NS - 1.  The
+  // DMAs and LDS reads are interleaved between the step's MFMAs, so they
+  // issue while the matrix core works.
+  auto step = [&](int c, double (&cur)[NF + 2], double (&nxt)[NF + 2], bool first) {
+    const int j = c / KC;
+    if (first) {
+      __builtin_amdgcn_sched_barrier(0);
+      // stage j + 1 landed (stages j + 2 .. j + NS - 2 stay in flight, plus an
+      // epilogue's stores if one ran after stage j + 1's DMAs were issued) and
+      // this wave's reads are back in registers
+      if (!(ABL & 1)) {
+        if (last_ep >= j - NS + 2)
+          wait_vm<YE>();
+        else
+          wait_vm<Y0>();
+      }
+      __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only (vmcnt 63, expcnt 7)
+      if (!(ABL & 2)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // nobody reads stage j - 1 any more: its slot takes stage j + NS - 1
+      issue_prepped((j + NS - 1) % NS);
+    }
+    // past the last step this reads a landed slot's stale operands (unused)
+    read_step(c + 1, nxt);
+    if (!(ABL & 4)) mma(cur);
+    if (ABL & 128) {
+      // interleave: after the u / v adds, one MFMA then up to two other
+      // instructions (LDS reads, DMAs, scalar / vector address work)
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+#pragma unroll
+      for (int i = 0; i < 2 * FS; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100 | 0x020 | 0x004 | 0x002, 2, 0);
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
-    // stage c + 1 landed (the DMAs of c + 2 .. c + NS - 1 stay in flight, plus
-    // an epilogue's stores if one ran after stage c + 1's DMAs were issued),
-    // and this wave's reads of stage c are back in registers
-    if (last_ep >= c + 1 - NS)
-      wait_vm<YE>();
-    else
-      wait_vm<Y0>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only (vmcnt 63, expcnt 7)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    issue_stage(c % NS);   // stage c + NS into the slot stage c came from
-    if (c + 1 < nst) read_stage((c + 1) % NS, nxt);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(cur);
+    if (first) prep_stage();
     if (++c_s == KS) {
       epilogue(c_it);
       zero();
       c_s = 0;
       ++c_it;
-      last_ep = c;
+      last_ep = j;
     }
-#pragma unroll
-    for (int f = 0; f < NF + 2; ++f) cur[f] = nxt[f];
+  };
+  int c = 0;
+  for (; c + 1 < nst; c += 2) {
+    step(c, opa, opb, true);
+    step(c + 1, opb, opa, KC == 1);
   }
+  if (c < nst) step(c, opa, opb, true);
   // no DMA may still be writing this workgroup's LDS when it exits
   wait_vm<0>();
 }
 
-template <int JS, int TS, int W, int NS, int MINW>
+template <int JS, int TS, int W, int NS, int MINW, int ABL = 0, int KC = 1>
 static RingConfig cfg_ring() {
-  return RingConfig{mode_product_ring_kernel<JS, TS, W, NS, MINW>, W, NS, 1,
-                    (size_t)NS * (8 * 16 * W + 16 * 64) * sizeof(double)};
+  return RingConfig{mode_product_ring_kernel<JS, TS, W, NS, MINW, ABL, KC>, W, NS, KC,
+                    (size_t)NS * KC * (8 * 16 * W + 16 * 64) * sizeof(double)};
 }
 
 // variants (GG_FOLD_RING=<v>): 1 = 8 waves, 9 stages (144 KiB, one workgroup
@@ -289,6 +409,27 @@ static RingConfig ring_variant(int v) {
     case 3: return cfg_ring<7, 1, 4, 6, 2>();
     case 4: return cfg_ring<7, 1, 8, 7, 2>();
     case 5: return cfg_ring<7, 1, 8, 5, 2>();
+    // diagnostic ablations of variant 1 (WRONG results; timing only): 11 no
+    // vmcnt wait, 12 no barrier, 13 neither, 14 no MFMA, 15 no epilogue
+    // stores, 16 no DMA (and no wait), 17 no wait / barrier / MFMA
+    case 11: return cfg_ring<7, 1, 8, 9, 2, 1>();
+    case 12: return cfg_ring<7, 1, 8, 9, 2, 2>();
+    case 13: return cfg_ring<7, 1, 8, 9, 2, 3>();
+    case 14: return cfg_ring<7, 1, 8, 9, 2, 4>();
+    case 15: return cfg_ring<7, 1, 8, 9, 2, 8>();
+    case 16: return cfg_ring<7, 1, 8, 9, 2, 17>();
+    case 17: return cfg_ring<7, 1, 8, 9, 2, 7>();
+    case 21: return cfg_ring<7, 1, 8, 9, 2, 32>();
+    case 27: return cfg_ring<7, 1, 8, 9, 2, 64>();
+    case 31: return cfg_ring<7, 1, 8, 5, 2, 0, 2>();
+    case 32: return cfg_ring<7, 1, 8, 4, 2, 0, 2>();
+    case 33: return cfg_ring<7, 1, 4, 6, 2, 0, 2>();
+    case 41: return cfg_ring<7, 1, 8, 9, 2, 128>();
+    case 42: return cfg_ring<7, 1, 8, 4, 2, 128, 2>();
+    case 43: return cfg_ring<7, 1, 8, 5, 2, 128, 2>();
+    case 28: return cfg_ring<7, 1, 8, 9, 2, 64 + 17>();
+    case 26: return cfg_ring<7, 1, 8, 9, 2, 49>();
+    case 25: return cfg_ring<7, 1, 8, 5, 2, 32>();
     default: return cfg_ring<7, 1, 8, 9, 2>();
   }
 }
@@ -317,7 +458,7 @@ int ring_grid(const RingConfig& rc, int cus, int64_t nblk) {
 }
 
 void set_ring_lds_limits() {
-  for (int v = 1; v <= 5; ++v) {
+  for (int v : {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 17, 21, 25, 26, 27, 28, 31, 32, 33, 41, 42, 43}) {
     const RingConfig rc = ring_variant(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rc.lds));
