@@ -220,7 +220,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     dist.barrier()
     sync()
     if on_gpu:
-        cg.profile(True)      # HIP events between the phases, on the compute stream
+        cg.profile(True, a.steps)   # HIP events between the phases, on the compute stream
     t0 = time.perf_counter()
     cg.iterate(a.steps)
     sync()

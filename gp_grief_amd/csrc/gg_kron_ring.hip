@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     // past the last step this reads a landed slot's stale operands (unused)
     read_step(c + 1, nxt);
     if (!(ABL & 4)) mma(cur);
-    if (ABL & 128) {
+    if (ABL & 128) {   // interleave (the default variant)
       // interleave: after the u / v adds, one MFMA then up to two other
       // instructions (LDS reads, DMAs, scalar / vector address work)
       __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
@@ -399,19 +399,25 @@ static RingConfig cfg_ring() {
                     (size_t)NS * KC * (8 * 16 * W + 16 * 64) * sizeof(double)};
 }
 
-// variants (GG_FOLD_RING=<v>): 1 = 8 waves, 9 stages (144 KiB, one workgroup
-// per CU, two waves per SIMD); 2 = 8 waves, 6 stages (96 KiB); 3 = 4 waves,
-// 6 stages (72 KiB, two per CU); 4 = 8 waves, 7 stages (112 KiB); 5 = 8
-// waves, 5 stages (80 KiB)
+// variants (GG_FOLD_RING=<v>; A/B in profiles/r04/, the default 42):
+//   1 = 8 waves, 9 one-k-step stages (144 KiB), 2 = 6 stages, 4 = 7, 5 = 5;
+//   3 = 4 waves, 6 stages (two workgroups per CU); 31 / 32 = 8 waves, 5 / 4
+//   two-k-step stages; 41 / 42 / 43 = 1 / 32 / 31 with the DMAs and LDS reads
+//   interleaved between the MFMAs (sched_group_barrier).  200^4 plain launch,
+//   interleaved in one process: chunked kernel 6.69-6.83 ms, 1: 6.60-6.68,
+//   32: 6.45-6.50, 42: 6.36-6.42 (profiles/r04/h_ring_ab.jsonl).
+//   Diagnostic ablations of 1 (WRONG results, timing only): 11 no vmcnt
+//   wait, 12 no barrier, 13 neither, 14 no MFMA, 15 no epilogue stores, 16 no
+//   DMA (and no wait), 17 no wait / barrier / MFMA, 21 / 25 workgroup start
+//   staggered, 26 = 16 + 21, 27 epilogue arithmetic without its stores, 28 =
+//   27 + 16 (profiles/r04/f_ring_ablate.jsonl).
 static RingConfig ring_variant(int v) {
   switch (v) {
+    case 1: return cfg_ring<7, 1, 8, 9, 2>();
     case 2: return cfg_ring<7, 1, 8, 6, 2>();
     case 3: return cfg_ring<7, 1, 4, 6, 2>();
     case 4: return cfg_ring<7, 1, 8, 7, 2>();
     case 5: return cfg_ring<7, 1, 8, 5, 2>();
-    // diagnostic ablations of variant 1 (WRONG results; timing only): 11 no
-    // vmcnt wait, 12 no barrier, 13 neither, 14 no MFMA, 15 no epilogue
-    // stores, 16 no DMA (and no wait), 17 no wait / barrier / MFMA
     case 11: return cfg_ring<7, 1, 8, 9, 2, 1>();
     case 12: return cfg_ring<7, 1, 8, 9, 2, 2>();
     case 13: return cfg_ring<7, 1, 8, 9, 2, 3>();
@@ -420,23 +426,23 @@ static RingConfig ring_variant(int v) {
     case 16: return cfg_ring<7, 1, 8, 9, 2, 17>();
     case 17: return cfg_ring<7, 1, 8, 9, 2, 7>();
     case 21: return cfg_ring<7, 1, 8, 9, 2, 32>();
+    case 25: return cfg_ring<7, 1, 8, 5, 2, 32>();
+    case 26: return cfg_ring<7, 1, 8, 9, 2, 49>();
     case 27: return cfg_ring<7, 1, 8, 9, 2, 64>();
+    case 28: return cfg_ring<7, 1, 8, 9, 2, 64 + 17>();
     case 31: return cfg_ring<7, 1, 8, 5, 2, 0, 2>();
     case 32: return cfg_ring<7, 1, 8, 4, 2, 0, 2>();
-    case 33: return cfg_ring<7, 1, 4, 6, 2, 0, 2>();
     case 41: return cfg_ring<7, 1, 8, 9, 2, 128>();
-    case 42: return cfg_ring<7, 1, 8, 4, 2, 128, 2>();
     case 43: return cfg_ring<7, 1, 8, 5, 2, 128, 2>();
-    case 28: return cfg_ring<7, 1, 8, 9, 2, 64 + 17>();
-    case 26: return cfg_ring<7, 1, 8, 9, 2, 49>();
-    case 25: return cfg_ring<7, 1, 8, 5, 2, 32>();
-    default: return cfg_ring<7, 1, 8, 9, 2>();
+    default: return cfg_ring<7, 1, 8, 4, 2, 128, 2>();   // 42
   }
 }
+static const int kRingVariants[] = {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 17,
+                                    21, 25, 26, 27, 28, 31, 32, 41, 42, 43};
 
 int ring_variant_env() {
-  const char* e = getenv("GG_FOLD_RING");
-  return e ? atoi(e) : 0;
+  const char* e = getenv("GG_FOLD_RING");   // unset: the default (42); 0: off
+  return e ? atoi(e) : 42;
 }
 
 bool ring_available(int JT, int TT, int64_t m) {
@@ -458,7 +464,7 @@ int ring_grid(const RingConfig& rc, int cus, int64_t nblk) {
 }
 
 void set_ring_lds_limits() {
-  for (int v : {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 17, 21, 25, 26, 27, 28, 31, 32, 33, 41, 42, 43}) {
+  for (int v : kRingVariants) {
     const RingConfig rc = ring_variant(v);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rc.lds));

@@ -277,13 +277,28 @@ class DistKronCG(object):
 
     # ---- per-phase timing (GPU engines): HIP events on the compute stream;
     # a collective's time is what the compute stream waits for it
-    def profile(self, enable):
+    def profile(self, enable, iterations=64):
+        """Start (or stop) per-phase timing.  The events for `iterations`
+        profiled iterations are created here, outside the timed loop, and
+        reused by later sessions; more are made only if a session runs
+        longer."""
         self._prof = [] if enable else None
+        if enable:
+            import torch
+            pool = getattr(self, "_ev_pool", [])
+            while len(pool) < 8 * max(1, int(iterations)) + 1:
+                pool.append(torch.cuda.Event(enable_timing=True))
+            self._ev_pool = pool
 
     def _mark(self, name):
         if self._prof is not None:
             import torch
-            e = torch.cuda.Event(enable_timing=True)
+            k = len(self._prof)
+            if k < len(self._ev_pool):
+                e = self._ev_pool[k]
+            else:
+                e = torch.cuda.Event(enable_timing=True)
+                self._ev_pool.append(e)
             e.record()
             self._prof.append((name, e))
 

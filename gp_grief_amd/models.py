@@ -418,11 +418,14 @@ class GPGriefModel(BaseModel):
         return self._Yd
 
     def _x_dev(self):
-        """The training inputs on the device, uploaded once: Phi is rebuilt at
-        every new kernel parameter (optimize), X never changes."""
-        if self._Xd is None or self._Xd_src is not self.X:
+        """The training inputs on the device, uploaded once per content of X:
+        Phi is rebuilt at every new kernel parameter (optimize), and the copy
+        is reused while X (same array, same bytes -- an in-place edit changes
+        the key) is unchanged."""
+        key = _content_key(self.X)
+        if self._Xd is None or self._Xd_src != key:
             self._Xd = dev.to_device(self.X)
-            self._Xd_src = self.X
+            self._Xd_src = key
         return self._Xd
 
     def fit(self, **kwargs):
@@ -821,6 +824,19 @@ class GPGridModel(BaseModel):
         return dense.host(mean).reshape(-1, 1), var.reshape(-1, 1)
 
 
+def _content_key(a):
+    """A cheap content key of a host array: identity, shape, dtype and a
+    64-bit hash of its bytes (xxh3 when importable, else blake2b)."""
+    a = np.ascontiguousarray(a)
+    try:
+        import xxhash
+        h = xxhash.xxh3_64_intdigest(memoryview(a).cast("B"))
+    except ImportError:  # pragma: no cover
+        import hashlib
+        h = hashlib.blake2b(memoryview(a).cast("B"), digest_size=8).hexdigest()
+    return (a.shape, a.dtype.str, h)
+
+
 def _dev_matrix(Phi):
     """Row-major float64 device copy of a 2-D basis matrix (or the tensor itself)."""
     t = dev.torch()
@@ -943,20 +959,21 @@ def _gram_svd(Pd):
     return np.sqrt(np.maximum(lam, 0.0)), V, lam
 
 
-def _cholqr3_svd(Pd):
+def _cholqr3_svd(Pd, left=False):
     """Singular values (descending) and right singular vectors of the n x p
     device matrix Phi (n >= p) by shifted CholeskyQR3: A1 = Phi^T Phi + s I
     (s = 11 (n p + p (p + 1)) eps ||A||_F), Q1 = Phi L1^-T, then CholeskyQR2 on
     Q1 -- R = L3^T L2^T L1^T with Phi = Q3 R -- and the SVD of the p x p R on
-    the host.  None when a Gram is not numerically positive definite beyond
-    the shift's reach (rank deficiency): (None, None), the caller falls back."""
-    t = dev.torch()
+    the host.  left=True also returns the left singular vectors Q3 U_R (n x p,
+    host).  None when a Gram is not numerically positive definite beyond the
+    shift's reach (rank deficiency): the caller falls back."""
     n, p = int(Pd.shape[0]), int(Pd.shape[1])
+    none = (None, None, None) if left else (None, None)
     eps = np.finfo(np.float64).eps
     A = dense.matmul(Pd, Pd, ta=True)
     fro = float(np.sqrt(max(dense.dot(A.reshape(-1), A.reshape(-1)), 0.0)))
     if not fro > 0.0:
-        return None, None
+        return none
     shift = 11.0 * (n * p + p * (p + 1)) * eps * fro
     R = np.eye(p)
     Q = Pd
@@ -970,15 +987,31 @@ def _cholqr3_svd(Pd):
             # a near-singular Gram after the shifted first stage means a null
             # direction of Phi (its singular value is far below 1e-7)
             if stage > 0 and not np.min(d) ** 2 > 1e3 * eps * np.max(d) ** 2:
-                return None, None
+                return none
             R = L.T.dot(R)
-            if stage < 2:
+            if stage < 2 or left:
                 Q = dense.matmul(Q, C.inverse(), tb=True)   # Q L^-T
     except np.linalg.LinAlgError:
-        return None, None
-    del t
-    _, sv, VT = np.linalg.svd(R)
+        return none
+    UR, sv, VT = np.linalg.svd(R)
+    if left:
+        U = dense.host(dense.matmul(Q, dev.to_device(np.ascontiguousarray(UR)).reshape(p, p)))
+        return sv, np.ascontiguousarray(VT.T), np.asarray(U).reshape(n, p)
     return sv, np.ascontiguousarray(VT.T)
+
+
+def _thin_svd(Pd):
+    """(singular values, right singular vectors) of the n x p device matrix
+    Phi by shifted CholeskyQR3 at LAPACK accuracy: on Phi itself when n >= p,
+    on Phi^T (p x n) when n < p -- Phi^T = Q3 R, R = U_R S W^T gives Phi =
+    W S (Q3 U_R)^T, so the right singular vectors are Q3 U_R (p x n).
+    (None, None) when the CholeskyQR3 test finds Phi numerically rank
+    deficient."""
+    n, p = int(Pd.shape[0]), int(Pd.shape[1])
+    if n >= p:
+        return _cholqr3_svd(Pd)
+    sv, _, U = _cholqr3_svd(Pd.t().contiguous(), left=True)
+    return sv, U
 
 
 class GPwebTransformedModel(BaseModel):
@@ -991,8 +1024,10 @@ class GPwebTransformedModel(BaseModel):
     small p x p SVD R = U_R S V^T on the host (factor-sized, LAPACK), so S and
     V carry the accuracy of LAPACK's SVD of Phi; Phit^T y = S^-1 V^T (Phi^T y).
     Bases with singular value <= 1e-7 are dropped as in the reference
-    (:27-35).  A numerically rank-deficient Phi (or n < p) falls back to the
-    Gram spectrum A = V S^2 V^T with a floor at its rounding level, logged.
+    (:27-35).  A wide Phi (n < p) takes the same route on Phi^T (its left
+    singular vectors are Phi's right ones).  A numerically rank-deficient Phi
+    falls back to the Gram spectrum A = V S^2 V^T with a floor at its rounding
+    level, logged.
     The O(p) likelihood / gradient stay on the host, as in the reference;
     predictions are device GEMV / GEMM.
     """
@@ -1005,14 +1040,13 @@ class GPwebTransformedModel(BaseModel):
         assert Phi.shape[0] == self.n
         self.p_orig = int(Phi.shape[1])
         Pd = _dev_matrix(Phi)
-        sv, V = _cholqr3_svd(Pd) if self.n >= self.p_orig else (None, None)
+        sv, V = _thin_svd(Pd)
 
         if sv is not None:
             ikeep = sv > 1e-7
         else:
-            if self.n >= self.p_orig:
-                logger.warning("Phi is numerically rank deficient: its singular values come "
-                               "from the Gram spectrum (accurate to ~sqrt(eps) s_max)")
+            logger.warning("Phi is numerically rank deficient: its singular values come "
+                           "from the Gram spectrum (accurate to ~sqrt(eps) s_max)")
             sv, V, lam = _gram_svd(Pd)
             # The reference keeps LAPACK singular values above 1e-7 (at most
             # min(n, p) of them).  Gram eigenvalues carry an absolute error of

@@ -65,9 +65,11 @@ def test_sharded_matvec_and_cg_virtual_ranks(gpu, monkeypatch, world, m, d, mode
     assert all(r[2] == 0 for r in res)
     assert len({r[3] for r in res}) == 1
     # finite-precision CG drifts with summation order: at 750 iterations
-    # (m = 200, d = 2) the split and the dense product differ by a few %,
-    # as the single-GPU fused / textbook comparison allows (test_gpu_kron)
-    assert abs(res[0][3] - it) <= max(2, 0.05 * it)
+    # (m = 200, d = 2) the folded product and the oracle's dense one differ
+    # by a few %, as the single-GPU fused / textbook comparison allows
+    # (test_gpu_kron); the dense cases keep the 2 % bound
+    slack = 0.05 if (fold == "fold" and m == 200) else 0.02
+    assert abs(res[0][3] - it) <= max(2, slack * it)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
 
 
