@@ -1046,6 +1046,13 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
   }
 }
 
+// GG_FOLD_RING_SIDE=1: the CG side-job launch on the ring kernel (opt-in:
+// 8.6 vs 8.2 ms per side launch at 200^4, profiles/r04/j_side_ab.txt)
+static bool ring_side_env() {
+  const char* e = getenv("GG_FOLD_RING_SIDE");
+  return e && atoi(e) == 1;
+}
+
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
                 int64_t* n_partials_out, const MpFuse* cg, int cgp, hipEvent_t* ev) {
@@ -1126,6 +1133,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // centrosymmetric factors: the even/odd split (half the MFMA work)
         const bool fold = f.ffrag != nullptr && jt0 == 0 && variant == 0 && fold_kind(kind) &&
                           !(pro && last) && !(kind == 2 && pro_variant() != 0);
+        bool ring_side = false;
         if (fold) {
           const double* xs_ = last && (shift != 0.0 || dot_partials != nullptr)
                                   ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
@@ -1134,18 +1142,25 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           // the persistent LDS-DMA ring kernel (gg_kron_ring.hip) for the plain
           // launch (GG_FOLD_RING=<variant>)
           const int rv = ring_variant_env();
-          if (rv > 0 && kind == 0 && xs_ == nullptr && skip == nullptr && f.rfrag != nullptr &&
-              M % 2 == 0 && M >= 2 &&
+          const bool ring_ok =
+              rv > 0 && xs_ == nullptr && f.rfrag != nullptr && M % 2 == 0 && M >= 2 &&
               ((reinterpret_cast<uintptr_t>(step_src) | reinterpret_cast<uintptr_t>(dst)) & 15) ==
-                  0) {
+                  0;
+          if (ring_ok && kind == 0 && skip == nullptr) {
             const RingConfig rc = select_ring(f.fJT, f.fTT, rv);
             const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
             const int grid = ring_grid(rc, cu_count(), nb);
             hipLaunchKernelGGL(rc.fn, dim3((unsigned)grid), dim3(64 * rc.waves), rc.lds, stream,
-                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb);
+                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb, nullptr,
+                               MpFuse());
             GG_LAUNCH_CHECK();
             continue;
           }
+          // the CG side-job launch (balanced x_defer) on the ring: the side
+          // chunks ride in its stages (GG_FOLD_RING_SIDE=0 keeps the chunked
+          // kernel)
+          // (decided here, launched below once the side-job fields of fz are set)
+          ring_side = ring_ok && kind == 4 && side && cg->xdefer == 2 && ring_side_env();
           const bool aligned =
               f.p % 2 == 0 &&
               ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(xs_) |
@@ -1246,6 +1261,19 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         }
         int64_t grid = nblk;
         if (mc.pers > 0) grid = std::min<int64_t>(nblk, (int64_t)cu_count() * mc.pers);
+        if (ring_side) {
+          const RingConfig rc = select_ring_side(f.fJT, f.fTT);
+          const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
+          if (fz.sc != nullptr && fz.sx != nullptr && fz.xdefer == 2 &&
+              ring_side_capacity(nb, f.fKS) >= std::max(fz.sn, fz.sn_h1) &&
+              ((reinterpret_cast<uintptr_t>(fz.sx) & 15) | ((fz.soff | fz.soff_h1) & 1)) == 0) {
+            const int rgrid = ring_grid(rc, cu_count(), nb);
+            hipLaunchKernelGGL(rc.fn, dim3((unsigned)rgrid), dim3(64 * rc.waves), rc.lds, stream,
+                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb, skip, fz);
+            GG_LAUNCH_CHECK();
+            continue;
+          }
+        }
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
                            mode_lds_bytes(mc), stream, step_src, dst,
                            fold ? f.ffrag : mc.t4 ? f.frag4 : f.frag, M, (int)f.q, (int)f.p,

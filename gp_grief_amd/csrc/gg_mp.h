@@ -175,7 +175,8 @@ void set_fold_lds_limits();
 
 // The persistent LDS-DMA ring version of the plain folded launch
 // (gg_kron_ring.hip): B fragments from Factor::rfrag ([fKS][16][64]).
-typedef void (*ring_kernel_t)(const double*, double*, const double*, int64_t, int, int, int64_t);
+typedef void (*ring_kernel_t)(const double*, double*, const double*, int64_t, int, int, int64_t,
+                              const int*, MpFuse);
 struct RingConfig {
   ring_kernel_t fn;
   int waves, ns, kc;   // waves per workgroup, ring stages, k-steps per stage
@@ -184,6 +185,10 @@ struct RingConfig {
 int ring_variant_env();   // GG_FOLD_RING: 0 = off, else the variant
 bool ring_available(int JT, int TT, int64_t m);
 RingConfig select_ring(int JT, int TT, int variant);
+// the CG side-job launch (kind 4, balanced x_defer): side slices up to
+// ring_side_capacity(nblk, KS) elements (256 per k-step of every block)
+RingConfig select_ring_side(int JT, int TT);
+int64_t ring_side_capacity(int64_t nblk, int KS);
 // persistent grid: resident workgroups per CU x CUs, at most nblk
 int ring_grid(const RingConfig& rc, int cus, int64_t nblk);
 void set_ring_lds_limits();
