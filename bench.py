@@ -183,6 +183,9 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     ex = TorchExchange()
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
     mode = os.environ.get("GG_DIST_MODE", a.exchange)
+    # the fused recurrence wherever the engine runs it (d >= 4, folded
+    # factors 1..d-1), else the textbook one
+    rec = "auto" if a.recurrence == "fused" else "textbook"
     if mode == "auto":
         # the library's default (DistKronCG): RCCL all-to-all; push (peer
         # stores over xGMI) is opt-in until it has run across devices
@@ -190,7 +193,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     # every rank must take the same exchange: a push setup that fails on any
     # rank (IPC mapping of a peer's buffer) sends all ranks to all-to-all
     try:
-        cg = DistKronCG(eng, ex, s, mode=mode)
+        cg = DistKronCG(eng, ex, s, mode=mode, recurrence=rec)
         ok = 1.0
     except Exception as exc:  # noqa: BLE001
         print("rank %d: %s exchange setup failed (%s); using a2a" % (rank, mode, exc),
@@ -199,7 +202,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     flag = torch.tensor([ok], dtype=torch.float64, device=dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if float(flag.item()) < 1.0:
-        cg = DistKronCG(eng, ex, s, mode="a2a")
+        cg = DistKronCG(eng, ex, s, mode="a2a", recurrence=rec)
     if cg.mode == "push":
         # one matvec through the peer-memory exchange against the all-to-all
         # path on the same input; any disagreement falls back to all-to-all
@@ -211,7 +214,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         dist.all_reduce(err, op=dist.ReduceOp.MAX)
         del ref, ya, yp
         if not float(err[0]) <= 1e-12 * float(err[1]):
-            cg = DistKronCG(eng, ex, s, mode="a2a")
+            cg = DistKronCG(eng, ex, s, mode="a2a", recurrence=rec)
         if on_gpu:
             torch.cuda.empty_cache()
     cg.start(y, rtol=0.0, atol=0.0)
@@ -258,11 +261,14 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
                                "sharded over %d GPUs" % (m, d, s, n, world),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
                    "exchange": cg.mode,
-                   "parallelism": ("shard factor-0 x%d: matvec exchange by %s, 2 scalar "
-                                   "all-reduce per iteration (RCCL)"
+                   "cg_recurrence": cg.recurrence,
+                   "parallelism": ("shard factor-0 x%d: matvec exchange by %s, %s per "
+                                   "iteration (RCCL)"
                                    % (world, "peer-memory stores in the mode-product "
                                              "epilogues + 2 RCCL barriers"
-                                      if cg.mode == "push" else "2 RCCL all-to-all"))},
+                                      if cg.mode == "push" else "2 RCCL all-to-all",
+                                      "one 5-double all-reduce" if cg.recurrence == "fused"
+                                      else "2 scalar all-reduces"))},
     }
     if phases is not None:
         res["phase_ms_per_iteration"] = phases

@@ -173,6 +173,12 @@ struct OutMap {
 constexpr int kVecBlocks = 2048;
 constexpr int kVecThreads = 256;
 
+// ---- the sharded CG's scalar state (gg_vec.hip gg_cgs), for the fused
+// sharded phase 1 in gg_kron.hip ----
+CgScalars* cgs_scalars_ptr(gg_cgs* c);
+double* cgs_rr_part(gg_cgs* c, int64_t cap, int64_t* cap_out);
+void cgs_set_pro_blocks(gg_cgs* c, int64_t nb);
+
 // ---- vector kernels (gg_vec.hip) used by other translation units ----
 void launch_dot_partials(const double* x, const double* y, int64_t n, double* partials,
                          int nblocks, hipStream_t s);

@@ -1742,6 +1742,108 @@ static int dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_
   });
 }
 
+// ---- fused sharded CG, phase 1 (gp_grief_amd/distributed.py, recurrence
+// "fused"): the single-GPU fused recurrence's launches on the local slab --
+// mode product 1 carries the prologue (r -= alpha q_old when pending, p_new
+// = r + beta p_old into its own buffer, r.r and p_new.q_old partials), mode
+// product 2 the balanced x side job (half sc->xh of the deferred pair), the
+// last one the all-to-all / push epilogue.  Folded (centrosymmetric)
+// factors 1..d-1 and d >= 4 only (the caller checks gg_kron_dist_fold_mask).
+static int dist_phase1_fused(const gg_kron_dist* D, const double* p_old, double* p_new,
+                             double* send_dev, double* work_dev, double* r_dev,
+                             const double* q_old, double* x_dev, gg_cgs* cgs, int push,
+                             gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(D && p_old && p_new && send_dev && work_dev && r_dev && q_old && x_dev && cgs,
+               GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(D->d >= 4, GG_ERR_VALUE, "the fused sharded CG needs d >= 4");
+    for (int k = 1; k < D->d; ++k)
+      GG_REQUIRE(D->f[k].ffrag != nullptr, GG_ERR_VALUE,
+                 "the fused sharded CG needs centrosymmetric (folded) factors 1..d-1");
+    GG_REQUIRE(!push || D->peers_recv, GG_ERR_VALUE, "push mode needs gg_kron_dist_set_peers");
+    GG_REQUIRE(D->n_local % 2 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(x_dev) | reinterpret_cast<uintptr_t>(p_new)) &
+                    15) == 0,
+               GG_ERR_VALUE, "the fused sharded CG needs 16-byte aligned, even-length vectors");
+    hipStream_t s = gg::as_stream(stream);
+    const int d = D->d;
+    const int G = D->world;
+    const int64_t nl = D->n_local;
+    gg::CgScalars* sc = gg::cgs_scalars_ptr(cgs);
+    const int* skip = &sc->done;
+    // balanced x deferral with one side launch per iteration: half h of x
+    const int64_t H = 2 * gg::ceil_div(nl, (int64_t)4);
+    const double* src = p_old;
+    for (int k = 1; k < d; ++k) {
+      const gg::Factor& f = D->f[k];
+      const int64_t M = nl / f.q;
+      const bool last = (k == d - 1);
+      gg::OutMap om = gg::OutMap::ident();
+      double* dst;
+      int kind = 0;
+      gg::MpFuse fz;
+      if (last) {
+        dst = send_dev;
+        const int64_t mi = M / D->s0;
+        const int64_t cr = mi / G;
+        om = gg::OutMap{0, f.p, 0, mi, cr, D->s0 * cr * f.p, cr * f.p};
+        if (push) {
+          om.push = 1;
+          om.self_off = (int64_t)D->rank * (D->n_local / G);
+          om.peers = D->peers_recv;
+        }
+        kind = 8;
+      } else {
+        dst = ((d - 1 - k) % 2 == 0) ? send_dev : work_dev;
+        kind = k == 1 ? 2 : k == 2 ? 4 : 0;
+      }
+      const bool lean_ok = 4 * 3 * gg::ceil_div((int64_t)f.fKS, (int64_t)3) <= (int64_t)f.q &&
+                           4 * 2 * gg::ceil_div((int64_t)f.fKS, (int64_t)2) <= (int64_t)f.q &&
+                           32 * M < ((int64_t)1 << 32);
+      const gg::FoldConfig fc = gg::select_fold(f.fJT, f.fTT, kind, lean_ok);
+      const int64_t nblk = gg::ceil_div(M, (int64_t)fc.waves * 16);
+      if (kind == 2) {
+        int64_t cap = 0;
+        fz.rr_part = gg::cgs_rr_part(cgs, nblk, &cap);
+        fz.rr_cap = cap;
+        fz.pqo_stride = cap;
+        fz.r = r_dev;
+        fz.q_old = q_old;
+        fz.p_out = p_new;
+        fz.sc = sc;
+        gg::cgs_set_pro_blocks(cgs, nblk);
+      } else if (kind == 4) {
+        fz.sc = sc;
+        fz.sx = x_dev;
+        fz.xdefer = 2;
+        fz.soff = 0;
+        fz.sn = std::min(H, nl);
+        fz.soff_h1 = std::min(H, nl);
+        fz.sn_h1 = nl - fz.soff_h1;
+        fz.schunk = 2 * gg::ceil_div(std::max<int64_t>(std::max(fz.sn, fz.sn_h1), 1), 2 * nblk);
+      }
+      if (fc.lean)
+        GG_REQUIRE(4 * gg::ceil_div((int64_t)f.fKS, (int64_t)fc.kc) * fc.kc <= (int64_t)f.q &&
+                       32 * M < ((int64_t)1 << 32),
+                   GG_ERR_VALUE, "lean folded kernel outside its row / offset range");
+      hipLaunchKernelGGL(fc.fn, dim3((unsigned)nblk), dim3(64 * fc.waves), fc.lds, s, src, dst,
+                         f.ffrag, M, (int)f.q, (int)f.p, f.fKS, fc.jf, 0, nullptr, 0.0, nullptr,
+                         skip, om, fz);
+      GG_LAUNCH_CHECK();
+      // the later steps read the updated direction
+      src = dst;
+    }
+  });
+}
+
+int gg_kron_dist_phase1_fused(const gg_kron_dist* D, const double* p_old_dev, double* p_new_dev,
+                              double* send_dev, double* work_dev, double* r_dev,
+                              const double* q_old_dev, double* x_dev, gg_cgs* cgs, int push,
+                              gg_stream stream) {
+  return dist_phase1_fused(D, p_old_dev, p_new_dev, send_dev, work_dev, r_dev, q_old_dev, x_dev,
+                           cgs, push, stream);
+}
+
 int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,
                         double* work_dev, const double* cg_r_dev, const void* cg_scalars_dev,
                         gg_stream stream) {

@@ -1304,7 +1304,91 @@ __global__ void cgs_init_kernel(CgScalars* sc, const double* rr, double rtol, do
   sc->first = 1;
   sc->pending = 0;
   sc->alpha = sc->beta = sc->pq = 0.0;
+  // the fused recurrence's state (unused by the textbook one)
+  sc->rq = sc->qq = 0.0;
+  sc->repair = 0;
+  sc->xpend = 0;
+  sc->xh = 2;
+  sc->xs = 0;
   sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
+}
+
+// ---- fused sharded CG (gg_cgs_fused_*): the single-GPU fused recurrence
+// with the dot products reduced across ranks by ONE all-reduce of five
+// doubles per iteration, red = [r.r, p.q_old, p.q, 0, q.q] (the caller
+// all-reduces it between gg_cgs_fused_post and gg_cgs_fused_scalars)
+
+// q = Y + shift p in place (Y = K p after the exchanges), block partials of
+// p.q and q.q -- 16-byte lanes (n even, 16-byte aligned vectors)
+__global__ __launch_bounds__(kVecThreads) void cgs_post_kernel(
+    double* __restrict__ q, const double* __restrict__ p, int64_t n, double shift,
+    const CgScalars* __restrict__ sc, double* __restrict__ part, int64_t pstride) {
+  if (sc->done) return;
+  double pq = 0.0, qq = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  double2* q2 = reinterpret_cast<double2*>(q);
+  const double2* p2 = reinterpret_cast<const double2*>(p);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 2; i += stride) {
+    const double2 pv = p2[i];
+    double2 v = q2[i];
+    v.x = fma(shift, pv.x, v.x);
+    v.y = fma(shift, pv.y, v.y);
+    q2[i] = v;
+    pq = fma(pv.x, v.x, pq);
+    pq = fma(pv.y, v.y, pq);
+    qq = fma(v.x, v.x, qq);
+    qq = fma(v.y, v.y, qq);
+  }
+  const double a = block_sum(pq);
+  __syncthreads();
+  const double b = block_sum(qq);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = a;
+    part[pstride + blockIdx.x] = b;
+  }
+}
+
+// red = [sum rr_part[0, nrr), sum rr_part[cap, cap + nrr), sum pq, 0, sum qq]
+__global__ __launch_bounds__(1024) void cgs_fused_red_kernel(
+    const double* __restrict__ rr_part, int64_t nrr, int64_t cap,
+    const double* __restrict__ part, int64_t np, int64_t pstride, double* __restrict__ red) {
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) {
+    a[0] += rr_part[i];
+    a[1] += rr_part[cap + i];
+  }
+  for (int64_t i = threadIdx.x; i < np; i += blockDim.x) {
+    a[2] += part[i];
+    a[3] += part[pstride + i];
+  }
+  double t[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    t[k] = block_sum(a[k]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    red[0] = t[0];
+    red[1] = t[1];
+    red[2] = t[2];
+    red[3] = 0.0;
+    red[4] = t[3];
+  }
+}
+
+// the closing textbook step (cg_rho_kernel's need_pending 1) from the global
+// r.r (all-reduced by the caller)
+__global__ void cgs_close_rho_kernel(CgScalars* sc, const double* rr) {
+  if (sc->done || !sc->pending) return;
+  const double s = *rr;
+  sc->rho_prev = sc->rho;
+  sc->rho = s;
+  sc->beta = s / sc->rho_prev;
+  sc->iters += 1;
+  sc->first = 0;
+  sc->pending = 0;
+  sc->repair = 0;
+  if (!(sqrt(s) >= sc->tol)) sc->done = 1;
 }
 
 __global__ void cgs_alpha_kernel(CgScalars* sc, const double* pq) {
@@ -1329,8 +1413,35 @@ __global__ void cgs_rho_kernel(CgScalars* sc, const double* rr) {
 struct gg_cgs {
   gg::CgScalars* sc = nullptr;
   gg::CgScalars* host = nullptr;
-  double* partials = nullptr;
+  double* partials = nullptr;   // kVecBlocks, or 2 x kVecBlocks (fused post)
+  // fused recurrence: the prologue launch's r.r / p.q_old partials
+  // (2 x rr_cap) and its actual workgroup count
+  double* rr_part = nullptr;
+  int64_t rr_cap = 0;
+  int64_t pro_blocks = 0;
 };
+
+namespace gg {
+
+CgScalars* cgs_scalars_ptr(gg_cgs* c) { return c->sc; }
+
+// the prologue partial arrays for launches of up to `cap` workgroups (grown
+// on demand, zero-filled)
+double* cgs_rr_part(gg_cgs* c, int64_t cap, int64_t* cap_out) {
+  if (c->rr_cap < cap) {
+    if (c->rr_part) GG_HIP(hipFree(c->rr_part));
+    c->rr_part = nullptr;
+    GG_HIP(hipMalloc(&c->rr_part, 2 * (size_t)cap * sizeof(double)));
+    GG_HIP(hipMemset(c->rr_part, 0, 2 * (size_t)cap * sizeof(double)));
+    c->rr_cap = cap;
+  }
+  *cap_out = c->rr_cap;
+  return c->rr_part;
+}
+
+void cgs_set_pro_blocks(gg_cgs* c, int64_t nb) { c->pro_blocks = nb; }
+
+}  // namespace gg
 
 extern "C" {
 
@@ -1342,7 +1453,7 @@ int gg_cgs_create(gg_cgs** out) {
       GG_HIP(hipMalloc(&c->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipMemset(c->sc, 0, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&c->host, sizeof(gg::CgScalars), hipHostMallocDefault));
-      GG_HIP(hipMalloc(&c->partials, gg::kVecBlocks * sizeof(double)));
+      GG_HIP(hipMalloc(&c->partials, 2 * gg::kVecBlocks * sizeof(double)));
     } catch (...) {
       gg_cgs_destroy(c);
       throw;
@@ -1357,6 +1468,7 @@ int gg_cgs_destroy(gg_cgs* c) {
     if (c->sc) (void)hipFree(c->sc);
     if (c->host) (void)hipHostFree(c->host);
     if (c->partials) (void)hipFree(c->partials);
+    if (c->rr_part) (void)hipFree(c->rr_part);
     delete c;
   });
 }
@@ -1429,6 +1541,71 @@ int gg_cgs_rho(gg_cgs* c, const double* rr_dev, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(c && rr_dev, GG_ERR_VALUE, "NULL argument");
     hipLaunchKernelGGL(gg::cgs_rho_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream), c->sc,
+                       rr_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_fused_post(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, double shift,
+                      double* red_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && q_dev && p_dev && red_dev && n >= 2 && n % 2 == 0, GG_ERR_VALUE,
+               "bad argument");
+    GG_REQUIRE(((reinterpret_cast<uintptr_t>(q_dev) | reinterpret_cast<uintptr_t>(p_dev)) & 15) ==
+                   0,
+               GG_ERR_VALUE, "fused post needs 16-byte aligned vectors");
+    GG_REQUIRE(c->rr_part && c->pro_blocks > 0, GG_ERR_VALUE,
+               "gg_cgs_fused_post needs a fused phase 1 first");
+    hipStream_t s = gg::as_stream(stream);
+    const int nb = gg::vec_blocks(n);
+    hipLaunchKernelGGL(gg::cgs_post_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, q_dev, p_dev,
+                       n, shift, c->sc, c->partials, (int64_t)gg::kVecBlocks);
+    GG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gg::cgs_fused_red_kernel, dim3(1), dim3(1024), 0, s, c->rr_part,
+                       c->pro_blocks, c->rr_cap, c->partials, (int64_t)nb,
+                       (int64_t)gg::kVecBlocks, red_dev);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_fused_scalars(gg_cgs* c, const double* red_dev, const double* p_new_dev,
+                         gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && red_dev && p_new_dev, GG_ERR_VALUE, "NULL argument");
+    // red = [rr, p.q_old | p.q, (r.q), q.q]: the single-GPU scalars kernel
+    // with one-element partial arrays (rr stride 1, matvec stride 1)
+    hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, gg::as_stream(stream),
+                       red_dev, (int64_t)1, (int64_t)1, red_dev + 2, (int64_t)1, (int64_t)1,
+                       c->sc, p_new_dev, 2, 1);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_dev, int64_t n,
+                       int64_t half, double* rr_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && x_dev && r_dev && q_dev && rr_dev && half >= 0 && half <= n, GG_ERR_VALUE,
+               "bad argument");
+    hipStream_t s = gg::as_stream(stream);
+    const int nb = gg::vec_blocks(n);
+    // the deferred x steps, then the pending r update with its r.r partials
+    hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, x_dev, n,
+                       half, c->sc);
+    GG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, c->sc);
+    GG_LAUNCH_CHECK();
+    GG_HIP(hipMemsetAsync(c->partials, 0, nb * sizeof(double), s));
+    hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, nullptr,
+                       r_dev, nullptr, q_dev, n, c->sc, c->partials, 1);
+    GG_LAUNCH_CHECK();
+    gg::launch_reduce_to(c->partials, nb, rr_dev, s);
+  });
+}
+
+int gg_cgs_fused_close_rho(gg_cgs* c, const double* rr_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(c && rr_dev, GG_ERR_VALUE, "NULL argument");
+    hipLaunchKernelGGL(gg::cgs_close_rho_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream), c->sc,
                        rr_dev);
     GG_LAUNCH_CHECK();
   });

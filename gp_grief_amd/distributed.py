@@ -5,9 +5,19 @@ Vectors are sharded along factor 0 (the slowest axis of the reference's
 flattening); every rank holds N/G elements in the local layout
 (m_1, ..., m_{d-1}, a), a = i_0 - rank * m_0/G fastest.  A matvec is two
 local MFMA phases with one exchange after each (include/gp_grief_amd.h,
-gg_kron_dist_*); each CG dot product is one scalar all-reduce.  The CG
-recurrence and its stopping rule are the single-GPU textbook ones (scipy's),
-so a sharded solve converges in the same number of iterations up to rounding.
+gg_kron_dist_*).  Two CG recurrences (DistKronCG(recurrence=...)):
+  "fused" (default where the engine supports it: d >= 4 with factors 1..d-1
+         on the centrosymmetric split): the single-GPU fused recurrence
+         (gg_cg_iterate) -- the CG prologue (r -= alpha q_old, p = r + beta p,
+         partial r.r and p.q_old) rides on phase 1's first mode product, the
+         deferred x update on its second, and the four dot products of an
+         iteration are ONE all-reduce of five doubles;
+  "textbook": scipy's order, two scalar all-reduces per iteration.
+Both stop on scipy's rule; a sharded solve takes the single-GPU iteration
+count up to rounding.  One difference from gg_cg_iterate: where the fused
+beta cancels (|r_{j+1}|^2 < 1e-6 rho_j from the three-term expansion), the
+single-GPU path repairs it with the true r.r; the sharded one restarts
+(beta = 0, p = r) instead of paying a second all-reduce every iteration.
 
 Two exchange modes (DistKronCG(mode=...)):
   "push" (opt-in; needs engine.supports_push): the last mode product of each
@@ -133,6 +143,7 @@ class HipEngine(object):
         native.check(L.gg_cgs_scalars(self.cgs, ctypes.byref(sc)))
         self.sc = sc
         self.red = dev.zeros(2)  # [0]: the scalar being all-reduced
+        self.red5 = dev.zeros(5)  # fused recurrence: [r.r, p.q_old, p.q, 0, q.q]
         self.xbuf = None         # push mode: [recv | out], 2 n_local
 
     def empty(self):
@@ -186,6 +197,42 @@ class HipEngine(object):
     def phase2_push(self):
         native.check(native.lib().gg_kron_dist_phase2_push(self.h, native.stream_ptr()),
                      "gg_kron_dist_phase2_push")
+
+    # ---- fused recurrence (gg_kron_dist_phase1_fused / gg_cgs_fused_*)
+    @property
+    def supports_fused(self):
+        d = len(self.m)
+        return d >= 4 and (self.fold_mask >> 1) == (1 << (d - 1)) - 1 and self.n_local % 2 == 0
+
+    def phase1_fused(self, p_old, p_new, send, r, q_old, x, push):
+        native.check(native.lib().gg_kron_dist_phase1_fused(
+            self.h, native.dptr(p_old), native.dptr(p_new), native.dptr(send),
+            native.dptr(self.work), native.dptr(r), native.dptr(q_old), native.dptr(x), self.cgs,
+            int(bool(push)), native.stream_ptr()), "gg_kron_dist_phase1_fused")
+
+    def fused_post(self, q, p, shift):
+        native.check(native.lib().gg_cgs_fused_post(
+            self.cgs, native.dptr(q), native.dptr(p), self.n_local, float(shift),
+            native.dptr(self.red5), native.stream_ptr()), "gg_cgs_fused_post")
+
+    def fused_scalars(self, p_new):
+        native.check(native.lib().gg_cgs_fused_scalars(
+            self.cgs, native.dptr(self.red5), native.dptr(p_new), native.stream_ptr()),
+            "gg_cgs_fused_scalars")
+
+    def fused_close(self, x, r, q):
+        half = 2 * ((self.n_local + 3) // 4)
+        native.check(native.lib().gg_cgs_fused_close(
+            self.cgs, native.dptr(x), native.dptr(r), native.dptr(q), self.n_local, half,
+            native.dptr(self.red), native.stream_ptr()), "gg_cgs_fused_close")
+
+    def fused_close_rho(self):
+        native.check(native.lib().gg_cgs_fused_close_rho(self.cgs, native.dptr(self.red),
+                                                         native.stream_ptr()),
+                     "gg_cgs_fused_close_rho")
+
+    def fused_reduce_buffer(self):
+        return self.red5
 
     # ---- CG scalar steps; each writes / reads self.red[0]
     def local_dot(self, x, y):
@@ -252,12 +299,23 @@ class DistKronCG(object):
     "auto" = "a2a".
     """
 
-    def __init__(self, engine, exchange, shift, mode="auto"):
+    def __init__(self, engine, exchange, shift, mode="auto", recurrence="auto"):
         self.e = engine
         self.x_ex = exchange
         self.shift = float(shift)
         n = engine.n_local
         self.n_local = n
+        # recurrence: "fused" (the single-GPU fused recurrence, one 5-double
+        # all-reduce per iteration; engines with supports_fused: d >= 4,
+        # folded factors 1..d-1), "textbook" (scipy's order, two scalar
+        # all-reduces), "auto" = fused where supported
+        if recurrence not in ("auto", "fused", "textbook"):
+            raise ValueError("recurrence must be 'auto', 'fused' or 'textbook'")
+        can_fuse = bool(getattr(engine, "supports_fused", False))
+        if recurrence == "fused" and not can_fuse:
+            raise ValueError("this engine / operator cannot run the fused recurrence")
+        self.recurrence = "fused" if (recurrence == "fused" or
+                                      (recurrence == "auto" and can_fuse)) else "textbook"
         if mode == "auto":
             # all-to-all unless asked: push mode's peer stores are validated
             # against it per run (bench.py) but not yet by a one-GPU-per-rank test
@@ -266,6 +324,10 @@ class DistKronCG(object):
             raise ValueError("mode must be 'push', 'a2a' or 'auto'")
         self.mode = mode
         self.r, self.p = engine.empty(), engine.zeros()
+        if self.recurrence == "fused":
+            # direction buffers (current, free, the deferred pair) as in
+            # gg_cg_iterate's balanced x deferral
+            self.pbuf = [self.p, engine.zeros(), engine.zeros(), engine.zeros()]
         self.send = engine.empty()
         if mode == "push":
             self.q = engine.setup_push(exchange)   # K p lands in the peer-visible buffer
@@ -352,8 +414,52 @@ class DistKronCG(object):
         self.e.local_dot(self.r, self.r)
         self._allreduce()
         self.e.cg_init(rtol, atol)
+        if self.recurrence == "fused":
+            self.e.zero(self.q)   # q_old of the first prologue (not pending)
+
+    def _iterate_fused(self, n_iter):
+        """The fused recurrence: per iteration phase 1 (prologue, x side job),
+        the exchanges and phase 2 (K p_new lands in q), q += shift p_new with
+        p.q / q.q, ONE all-reduce of five doubles, the scalars; leaving, the
+        deferred x and pending r update and one all-reduce of r.r -- the
+        textbook state (gg_cg_iterate's contract)."""
+        push = self.mode == "push"
+        pb = self.pbuf
+        for _ in range(int(n_iter)):
+            self._mark("start")
+            p_old, p_new = pb[0], pb[1]
+            self.e.phase1_fused(p_old, p_new, self.send, self.r, self.q, self.x, push)
+            self._mark("phase1")
+            if push:
+                self.x_ex.barrier()
+                self._mark("exchange1")
+                self.e.phase2_push()
+                self._mark("phase2")
+                self.x_ex.barrier()
+                self._mark("exchange2")
+            else:
+                self.x_ex.all_to_all(self.recv, self.send)
+                self._mark("exchange1")
+                self.e.phase2(self.recv, self.send)
+                self._mark("phase2")
+                self.x_ex.all_to_all(self.q, self.send)
+                self._mark("exchange2")
+            self.e.fused_post(self.q, p_new, self.shift)
+            self._mark("vector")
+            self.x_ex.all_reduce(self.e.fused_reduce_buffer())
+            self._mark("allreduce")
+            self.e.fused_scalars(p_new)
+            self._mark("scalars")
+            # (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2})
+            pb[0], pb[1], pb[2], pb[3] = p_new, pb[3], p_old, pb[2]
+        self.p = pb[0]
+        self.e.fused_close(self.x, self.r, self.q)
+        self._allreduce()
+        self.e.fused_close_rho()
 
     def iterate(self, n_iter):
+        if self.recurrence == "fused":
+            return self._iterate_fused(n_iter)
         for _ in range(int(n_iter)):
             self._mark("start")
             self._matvec_into_q(self.p, fuse_cg=True)        # p = r + beta p ; q = K p

@@ -52,12 +52,104 @@ class NumpyEngine(object):
         C = Z.shape[1]
         send.numpy()[:] = Z.T.reshape(C, self.G, self.s0).transpose(1, 0, 2).reshape(-1)
 
+    # ---- the fused recurrence (HipEngine.phase1_fused / fused_*), restated
+    # from cg_fused_scalars_kernel (xmode 2, conjugacy r.q) and the balanced
+    # x deferral; partial sums are plain local dot products here
+    supports_fused = True
+
+    def phase1_fused(self, p_old, p_new, send, r, q_old, x, push):
+        sc = self.sc
+        if sc["done"]:
+            return
+        rv, pn = r.numpy(), p_new.numpy()
+        if sc["pending"]:
+            rv -= sc["alpha"] * q_old.numpy()
+        self.rr_local = float(np.dot(rv, rv))
+        pn[:] = rv + sc["beta"] * p_old.numpy()
+        self.pqo_local = float(np.dot(pn, q_old.numpy()))
+        h = sc["xh"]
+        if h < 2:   # the side job: half h of the active pair
+            H = self.half()
+            lo, hi = (0, H) if h == 0 else (H, self.n_local)
+            xv = x.numpy()
+            xv[lo:hi] += sc["xc"][0] * sc["xp"][0].numpy()[lo:hi] + \
+                sc["xc"][1] * sc["xp"][1].numpy()[lo:hi]
+        self.phase1(p_new, send)
+
+    def half(self):
+        return min(2 * ((self.n_local + 3) // 4), self.n_local)
+
+    def fused_post(self, q, p, shift):
+        self.red5 = getattr(self, "red5", torch.zeros(5, dtype=torch.float64))
+        if self.sc["done"]:
+            return
+        qv = q.numpy()
+        qv += shift * p.numpy()
+        self.red5[:] = torch.tensor([self.rr_local, self.pqo_local, float(np.dot(p.numpy(), qv)),
+                                     0.0, float(np.dot(qv, qv))], dtype=torch.float64)
+
+    def fused_reduce_buffer(self):
+        self.red5 = getattr(self, "red5", torch.zeros(5, dtype=torch.float64))
+        return self.red5
+
+    def fused_scalars(self, p_new):
+        sc = self.sc
+        if sc["done"]:
+            return
+        rr, pqo, pq, _, qq = [float(v) for v in self.red5]
+        if sc["pending"]:
+            sc.update(rho_prev=sc["rho"], rho=rr, iters=sc["iters"] + 1)
+            if not np.sqrt(rr) >= sc["tol"]:
+                sc.update(done=True, pending=False)
+                if sc["xh"] < 2:
+                    sc["xh"] += 1
+                return
+        rho = sc["rho"]
+        alpha = rho / pq
+        rq = pq - sc["beta"] * pqo
+        rt = rho - 2.0 * alpha * rq + alpha * alpha * qq
+        repair = rt < 1e-6 * rho
+        sc.update(alpha=alpha, beta=0.0 if repair else rt / rho, first=False, pending=True)
+        if sc["xh"] < 2:
+            sc["xh"] += 1
+        if not sc["xs"]:
+            sc.update(xs=True, xsc=alpha, xsp=p_new)
+        else:
+            sc.update(xc=[sc["xsc"], alpha], xp=[sc["xsp"], p_new], xh=0, xs=False)
+
+    def fused_close(self, x, r, q):
+        sc = self.sc
+        xv = x.numpy()
+        if sc["xs"]:
+            xv += sc["xsc"] * sc["xsp"].numpy()
+        if sc["xh"] < 2:
+            lo = 0 if sc["xh"] == 0 else self.half()
+            xv[lo:] += sc["xc"][0] * sc["xp"][0].numpy()[lo:] + \
+                sc["xc"][1] * sc["xp"][1].numpy()[lo:]
+        sc.update(xh=2, xs=False)
+        self.red[0] = 0.0
+        if not sc["done"] and sc["pending"]:
+            rv = r.numpy()
+            rv -= sc["alpha"] * q.numpy()
+            self.red[0] = float(np.dot(rv, rv))
+
+    def fused_close_rho(self):
+        sc = self.sc
+        if sc["done"] or not sc["pending"]:
+            return
+        s = float(self.red[0])
+        sc.update(rho_prev=sc["rho"], rho=s, iters=sc["iters"] + 1, first=False, pending=False)
+        sc["beta"] = s / sc["rho_prev"]
+        if not np.sqrt(s) >= sc["tol"]:
+            sc["done"] = True
+
     def local_dot(self, x, y):
         self.red[0] = float(np.dot(x.numpy(), y.numpy()))
 
     def cg_init(self, rtol, atol):
         s = float(self.red[0])
-        self.sc.update(rho=s, tol=max(atol, rtol * np.sqrt(s)), iters=0, first=True)
+        self.sc.update(rho=s, tol=max(atol, rtol * np.sqrt(s)), iters=0, first=True,
+                       pending=False, alpha=0.0, beta=0.0, xh=2, xs=False)
         self.sc["done"] = s == 0.0 or not np.sqrt(s) >= self.sc["tol"]
 
     def shift_dot(self, q, p, shift):

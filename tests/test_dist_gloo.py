@@ -3,7 +3,9 @@
 The orchestration (gp_grief_amd.distributed.DistKronCG, its exchange order and
 local layouts) runs unchanged; the arithmetic is the NumPy test engine
 (tests/dist_helpers.py).  Checks: the sharded matvec equals the oracle's
-global matvec; the sharded CG reproduces the single-process CG.
+global matvec; the sharded CG reproduces the single-process CG, with the
+textbook recurrence and with the fused one (one 5-double all-reduce per
+iteration, deferred x updates over rotating direction buffers).
 """
 import os
 import socket
@@ -26,7 +28,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, m, d, shift, out_dir):
+def _worker(rank, world, port, m, d, shift, out_dir, recurrence):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -38,12 +40,15 @@ def _worker(rank, world, port, m, d, shift, out_dir):
     rng = np.random.default_rng(7)
     xg = rng.standard_normal(m ** d)
     eng = NumpyEngine(F, world, rank)
-    cg = DistKronCG(eng, TorchExchange(), shift)
+    cg = DistKronCG(eng, TorchExchange(), shift, recurrence=recurrence)
+    assert cg.recurrence == recurrence
     xl = torch.from_numpy(scatter_global(xg, [m] * d, world, rank).copy())
     yl = eng.empty()
     cg.apply(xl.clone(), yl)
     b = torch.from_numpy(scatter_global(xg, [m] * d, world, rank).copy())
-    x, info = cg.solve(b, rtol=1e-10, maxiter=5000)
+    # check_every 7: the fused recurrence is left (closing update) and
+    # re-entered mid-solve, with the x deferral's pair at every phase
+    x, info = cg.solve(b, rtol=1e-10, maxiter=5000, check_every=7)
     it = cg.status()[0]
     np.savez(os.path.join(out_dir, "rank%d.npz" % rank), y=yl.numpy(), x=x.numpy(),
              info=info, iters=it)
@@ -51,13 +56,14 @@ def _worker(rank, world, port, m, d, shift, out_dir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("recurrence", ["textbook", "fused"])
 @pytest.mark.parametrize("world,m,d", [(2, 8, 3), (2, 6, 2), (4, 8, 4)])
-def test_sharded_cg_gloo(tmp_path, world, m, d):
+def test_sharded_cg_gloo(tmp_path, world, m, d, recurrence):
     from gp_grief_amd.distributed import gather_global
     from dist_helpers import reference_factors
     shift = 0.05
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, m, d, shift, str(tmp_path)), nprocs=world,
+    mp.start_processes(_worker, args=(world, port, m, d, shift, str(tmp_path), recurrence), nprocs=world,
                        join=True, start_method="spawn")
     res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(world)]
     F = reference_factors(m, d)

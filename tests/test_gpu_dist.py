@@ -73,6 +73,65 @@ def test_sharded_matvec_and_cg_virtual_ranks(gpu, monkeypatch, world, m, d, mode
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
 
 
+@pytest.mark.parametrize("recurrence", ["fused", "textbook"])
+@pytest.mark.parametrize("mode", ["push", "a2a"])
+@pytest.mark.parametrize("world,m,d", [(2, 16, 4), (4, 16, 4), (8, 16, 4), (2, 12, 5),
+                                       (4, 40, 4)])
+def test_sharded_fused_cg_virtual_ranks(gpu, monkeypatch, world, m, d, mode, recurrence):
+    """The fused sharded recurrence (gg_kron_dist_phase1_fused + gg_cgs_fused_*:
+    CG prologue and deferred x side job inside phase 1, one 5-double
+    all-reduce per iteration) against the oracle's CG and the textbook
+    sharded recurrence; check_every 7 leaves and re-enters it mid-solve."""
+    import torch
+    from gp_grief_amd.distributed import DistKronCG, HipEngine, gather_global, scatter_global
+    monkeypatch.setenv("GG_KRON_FOLD_MIN", "8")
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(5).standard_normal(m ** d)
+    shift = 0.05
+    ex = ThreadExchange(world)
+    engines = [HipEngine(F, world, g) for g in range(world)]
+    assert all(e.supports_fused for e in engines)
+
+    def body(g):
+        ex.bind(g)
+        e = engines[g]
+        cg = DistKronCG(e, ex, shift, mode=mode, recurrence=recurrence)
+        assert cg.recurrence == recurrence
+        b = torch.from_numpy(scatter_global(xg, [m] * d, world, g).copy()).cuda()
+        x, info = cg.solve(b, rtol=1e-10, maxiter=3000, check_every=7)
+        torch.cuda.synchronize()
+        return x.cpu().numpy(), info, cg.status()[0]
+
+    res = run_threads(world, body)
+    x = gather_global([r[0] for r in res], [m] * d)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, xg,
+                                   rtol=1e-10)
+    assert all(r[1] == 0 for r in res)
+    assert len({r[2] for r in res}) == 1
+    assert abs(res[0][2] - it) <= max(2, 0.02 * it)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+
+
+def test_fused_recurrence_default_and_refusal(gpu, monkeypatch):
+    """recurrence "auto" picks the fused one exactly where the engine supports
+    it (d >= 4, factors 1..d-1 folded); asking for it elsewhere is an error."""
+    from gp_grief_amd.distributed import DistKronCG, HipEngine
+    ex = ThreadExchange(1)
+    ex.bind(0)
+    monkeypatch.setenv("GG_KRON_FOLD_MIN", "8")
+    e4 = HipEngine(reference_factors(16, 4), 2, 0)
+    assert DistKronCG(e4, ex, 0.1).recurrence == "fused"
+    assert DistKronCG(e4, ex, 0.1, recurrence="textbook").recurrence == "textbook"
+    e3 = HipEngine(reference_factors(16, 3), 2, 0)
+    assert DistKronCG(e3, ex, 0.1).recurrence == "textbook"
+    with pytest.raises(ValueError):
+        DistKronCG(e3, ex, 0.1, recurrence="fused")
+    monkeypatch.setenv("GG_KRON_FOLD", "0")
+    monkeypatch.delenv("GG_KRON_FOLD_MIN")
+    e4d = HipEngine(reference_factors(16, 4), 2, 0)
+    assert DistKronCG(e4d, ex, 0.1).recurrence == "textbook"
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -109,12 +168,14 @@ def _ipc_worker(rank, world, port, m, d, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,m,d,fold", [(2, 16, 3, False), (4, 24, 3, True)])
+@pytest.mark.parametrize("world,m,d,fold", [(2, 16, 3, False), (4, 24, 3, True),
+                                            (2, 16, 4, True)])
 def test_push_exchange_over_ipc_processes(gpu, tmp_path, monkeypatch, world, m, d, fold):
     """One process per rank (one GPU each on a multi-GPU node, else all on
     cuda:0): exchange buffers shared by IPC handle (gg_ipc_handle /
     gg_kron_dist_set_peers), barriers over gloo; fold: the ranks' factors on
-    the centrosymmetric split (the environment is inherited by the ranks)."""
+    the centrosymmetric split (the environment is inherited by the ranks);
+    d = 4 folded runs the fused recurrence over the peer exchange."""
     import torch.multiprocessing as mp
     from gp_grief_amd.distributed import gather_global
     monkeypatch.setenv("GG_KRON_FOLD_MIN", "8" if fold else "1000")
