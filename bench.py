@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--exchange", default="auto", choices=["auto", "push", "a2a"])
     ap.add_argument("--fusion", type=int, default=None, choices=[0, 1, 2],
                     help="fused-CG layout (gg_cg_set_fusion); default: the library's")
-    ap.add_argument("--grief", default="C2,C5",
+    ap.add_argument("--grief", default="C2,C4,C5",
                     help="P2 GRIEF fits timed after the CG leg (bench_grief configs, "
                          "comma-separated; 'off' = none); not part of `value`")
     return ap.parse_args()

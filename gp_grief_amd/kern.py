@@ -487,11 +487,14 @@ class GriefKernel(GridKernel):
         hit = self._eig_cache.get(key)
         qsel_dev = None
         qperm = None
+        # optional stage marks (bench_grief.py: HIP events between the parts)
+        mark = getattr(self, "_stage_mark", None) or (lambda name: None)
         if hit is None and not self.opt_kernel_params and \
                 os.environ.get("GG_EIG_SUBSET", "1") != "0":
             factors = self._grid_factors_host()
             if factors is None:
                 factors = self._grid_factors_device()
+            mark("setup_factors")
             # centrosymmetric factors (evenly spaced grids): two half-order
             # problems each (tensors.centro_halves); GG_EIG_CENTRO=0 disables
             # (from m = 96: below it the halves' saving is under the extra
@@ -511,8 +514,10 @@ class GriefKernel(GridKernel):
                 lam = [mg[0] for mg in merged]
             else:
                 lam, handle = device_sym_eig_tridiag(factors)
+            mark("setup_eigvals")
             eig_pos, log_lam = self._select(lam)
             Sp = [SelectionMatrixSparse((col, lam[i].shape[0])) for i, col in enumerate(eig_pos.T)]
+            mark("setup_select")
             if self._separated(lam, [S.unique for S in Sp]):
                 if split:
                     qsel_dev, qperm = self._centro_vectors(handle, merged,
@@ -521,6 +526,7 @@ class GriefKernel(GridKernel):
                     qsel_dev = device_sym_eig_tridiag_vectors(handle, [S.unique for S in Sp])
                 self._Quu_factors = factors
                 self._Quu_full = None
+                mark("setup_vectors")
         if qsel_dev is None:
             Q, lam = self._factor_eigs(base)
             eig_pos, log_lam = self._select(lam)
