@@ -1,0 +1,12 @@
+#!/bin/bash
+# The remaining sharded tests (fused 32^4 onwards, IPC processes), per-rank
+# compute by recurrence, then the bimodality diagnostic.
+set -o pipefail
+cd "$(dirname "$0")/../.."
+O=gpurun_out/r04_m
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py -k "fused_cg_virtual_ranks and 32 or refusal or ipc" > $O/dist.log 2>&1 || { tail -40 $O/dist.log; exit 1; }
+tail -3 $O/dist.log
+timeout -k 10 400 python -u tools/shard_compute.py --reps 5 > $O/shard.jsonl 2> $O/shard.err || { tail -20 $O/shard.err; exit 1; }
+cat $O/shard.jsonl
+bash scripts/r04/k_bimodal.sh
