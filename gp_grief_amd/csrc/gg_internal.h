@@ -107,6 +107,9 @@ struct MpFuse {
   // back) and the block's partial r.r goes to rr_part.
   double* r = nullptr;
   const double* q_old = nullptr;
+  // q_old holds K p_old without the shift (sharded fused CG, whose post pass
+  // then only reads): the prologue uses q_old + qshift * p_old (0 = off)
+  double qshift = 0.0;
   double* p_out = nullptr;
   const CgScalars* sc = nullptr;
   double* rr_part = nullptr;

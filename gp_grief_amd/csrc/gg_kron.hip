@@ -1751,8 +1751,8 @@ static int dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_
 // factors 1..d-1 and d >= 4 only (the caller checks gg_kron_dist_fold_mask).
 static int dist_phase1_fused(const gg_kron_dist* D, const double* p_old, double* p_new,
                              double* send_dev, double* work_dev, double* r_dev,
-                             const double* q_old, double* x_dev, gg_cgs* cgs, int push,
-                             gg_stream stream) {
+                             const double* q_old, double* x_dev, gg_cgs* cgs, double shift,
+                             int push, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(D && p_old && p_new && send_dev && work_dev && r_dev && q_old && x_dev && cgs,
                GG_ERR_VALUE, "NULL argument");
@@ -1809,6 +1809,7 @@ static int dist_phase1_fused(const gg_kron_dist* D, const double* p_old, double*
         fz.pqo_stride = cap;
         fz.r = r_dev;
         fz.q_old = q_old;
+        fz.qshift = shift;   // q_old = K p_old: gg_cgs_fused_post does not shift it
         fz.p_out = p_new;
         fz.sc = sc;
         gg::cgs_set_pro_blocks(cgs, nblk);
@@ -1838,10 +1839,10 @@ static int dist_phase1_fused(const gg_kron_dist* D, const double* p_old, double*
 
 int gg_kron_dist_phase1_fused(const gg_kron_dist* D, const double* p_old_dev, double* p_new_dev,
                               double* send_dev, double* work_dev, double* r_dev,
-                              const double* q_old_dev, double* x_dev, gg_cgs* cgs, int push,
-                              gg_stream stream) {
+                              const double* q_old_dev, double* x_dev, gg_cgs* cgs,
+                              double shift, int push, gg_stream stream) {
   return dist_phase1_fused(D, p_old_dev, p_new_dev, send_dev, work_dev, r_dev, q_old_dev, x_dev,
-                           cgs, push, stream);
+                           cgs, shift, push, stream);
 }
 
 int gg_kron_dist_phase1(const gg_kron_dist* D, double* x_local_dev, double* send_dev,

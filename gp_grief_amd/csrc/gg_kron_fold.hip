@@ -123,7 +123,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
   double* Pout = fz.p_out;
 
   bool cg_first = false, cg_pending = false, pqo_on = false;
-  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
+  double cg_beta = 0.0, cg_alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0, cg_qs = 0.0;
   double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
   if (CGP == 3) {
     lz_cy = fz.coef[2];
@@ -135,6 +135,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     if (CGP == 2) {
       cg_pending = fz.sc->pending != 0;
       cg_alpha = fz.sc->alpha;
+      cg_qs = fz.qshift;
       // p_new.q_old (conjugacy r.q); q_old is not A p_old on the first step
       pqo_on = fz.pqo_stride > 0 && !cg_first;
     }
@@ -221,6 +222,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
         rr_acc = fma(v, v, rr_acc);
       }
     } else if (CGP) {
+      if (CGP == 2 && cg_qs != 0.0) q = fma(cg_qs, v, q);   // (K + s I) p_old
       if (CGP == 2 && cg_pending) {
         r = r - cg_alpha * q;
         if (ok) {

@@ -698,13 +698,22 @@ int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream 
   });
 }
 
+// diagnostic knob GG_CG_VEC_PAD (elements, even): the CG vectors sit n + pad
+// apart in the workspace instead of n (HBM placement experiments)
+static int64_t cg_vec_pad() {
+  const char* e = getenv("GG_CG_VEC_PAD");
+  const int64_t v = e ? atoll(e) : 0;
+  return v > 0 ? 2 * (v / 2) : 0;
+}
+
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
     // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
     // product's own output for an odd number of factors, MpFuse::first_dst)
-    *elems = 6 * n + gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
+    *elems = 6 * (n + cg_vec_pad()) + gg::kron_work_elems(K, false) +
+             (gg::kron_d(K) % 2 == 1 ? n : 0);
   });
 }
 
@@ -719,13 +728,14 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->K = K;
       cg->shift = shift;
       cg->n = nr;
+      const int64_t vs = nr + cg_vec_pad();
       cg->r = work_dev;
-      cg->p = work_dev + nr;
-      cg->q = work_dev + 2 * nr;
-      cg->p2 = work_dev + 3 * nr;
-      cg->p3 = work_dev + 4 * nr;
-      cg->p4 = work_dev + 5 * nr;
-      cg->mv_work = work_dev + 6 * nr;
+      cg->p = work_dev + vs;
+      cg->q = work_dev + 2 * vs;
+      cg->p2 = work_dev + 3 * vs;
+      cg->p3 = work_dev + 4 * vs;
+      cg->p4 = work_dev + 5 * vs;
+      cg->mv_work = work_dev + 6 * vs;
       if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
       const char* xd = getenv("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
       if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
@@ -1318,22 +1328,22 @@ __global__ void cgs_init_kernel(CgScalars* sc, const double* rr, double rtol, do
 // doubles per iteration, red = [r.r, p.q_old, p.q, 0, q.q] (the caller
 // all-reduces it between gg_cgs_fused_post and gg_cgs_fused_scalars)
 
-// q = Y + shift p in place (Y = K p after the exchanges), block partials of
-// p.q and q.q -- 16-byte lanes (n even, 16-byte aligned vectors)
+// block partials of p.q' and q'.q', q' = Y + shift p (Y = K p after the
+// exchanges, left unshifted: the next prologue adds shift p_old itself) --
+// two read streams, 16-byte lanes (n even, 16-byte aligned vectors)
 __global__ __launch_bounds__(kVecThreads) void cgs_post_kernel(
-    double* __restrict__ q, const double* __restrict__ p, int64_t n, double shift,
+    const double* __restrict__ q, const double* __restrict__ p, int64_t n, double shift,
     const CgScalars* __restrict__ sc, double* __restrict__ part, int64_t pstride) {
   if (sc->done) return;
   double pq = 0.0, qq = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  double2* q2 = reinterpret_cast<double2*>(q);
+  const double2* q2 = reinterpret_cast<const double2*>(q);
   const double2* p2 = reinterpret_cast<const double2*>(p);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n / 2; i += stride) {
     const double2 pv = p2[i];
     double2 v = q2[i];
     v.x = fma(shift, pv.x, v.x);
     v.y = fma(shift, pv.y, v.y);
-    q2[i] = v;
     pq = fma(pv.x, v.x, pq);
     pq = fma(pv.y, v.y, pq);
     qq = fma(v.x, v.x, qq);
@@ -1374,6 +1384,23 @@ __global__ __launch_bounds__(1024) void cgs_fused_red_kernel(
     red[3] = 0.0;
     red[4] = t[3];
   }
+}
+
+// the closing pending update r -= alpha (q + shift p), partial r.r
+__global__ __launch_bounds__(kVecThreads) void cgs_close_r_kernel(
+    double* __restrict__ r, const double* __restrict__ q, const double* __restrict__ p, int64_t n,
+    double shift, const CgScalars* __restrict__ sc, double* __restrict__ partials) {
+  if (sc->done || !sc->pending) return;
+  const double a = sc->alpha;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const double rv = r[i] - a * fma(shift, p[i], q[i]);
+    r[i] = rv;
+    acc = fma(rv, rv, acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
 // the closing textbook step (cg_rho_kernel's need_pending 1) from the global
@@ -1546,8 +1573,8 @@ int gg_cgs_rho(gg_cgs* c, const double* rr_dev, gg_stream stream) {
   });
 }
 
-int gg_cgs_fused_post(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, double shift,
-                      double* red_dev, gg_stream stream) {
+int gg_cgs_fused_post(gg_cgs* c, const double* q_dev, const double* p_dev, int64_t n,
+                      double shift, double* red_dev, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(c && q_dev && p_dev && red_dev && n >= 2 && n % 2 == 0, GG_ERR_VALUE,
                "bad argument");
@@ -1581,11 +1608,12 @@ int gg_cgs_fused_scalars(gg_cgs* c, const double* red_dev, const double* p_new_d
   });
 }
 
-int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_dev, int64_t n,
-                       int64_t half, double* rr_dev, gg_stream stream) {
+int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_dev,
+                       const double* p_dev, int64_t n, int64_t half, double shift,
+                       double* rr_dev, gg_stream stream) {
   return gg::guard([&] {
-    GG_REQUIRE(c && x_dev && r_dev && q_dev && rr_dev && half >= 0 && half <= n, GG_ERR_VALUE,
-               "bad argument");
+    GG_REQUIRE(c && x_dev && r_dev && q_dev && p_dev && rr_dev && half >= 0 && half <= n,
+               GG_ERR_VALUE, "bad argument");
     hipStream_t s = gg::as_stream(stream);
     const int nb = gg::vec_blocks(n);
     // the deferred x steps, then the pending r update with its r.r partials
@@ -1595,8 +1623,8 @@ int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_
     hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, c->sc);
     GG_LAUNCH_CHECK();
     GG_HIP(hipMemsetAsync(c->partials, 0, nb * sizeof(double), s));
-    hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, nullptr,
-                       r_dev, nullptr, q_dev, n, c->sc, c->partials, 1);
+    hipLaunchKernelGGL(gg::cgs_close_r_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, r_dev,
+                       q_dev, p_dev, n, shift, c->sc, c->partials);
     GG_LAUNCH_CHECK();
     gg::launch_reduce_to(c->partials, nb, rr_dev, s);
   });

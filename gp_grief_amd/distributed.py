@@ -204,11 +204,11 @@ class HipEngine(object):
         d = len(self.m)
         return d >= 4 and (self.fold_mask >> 1) == (1 << (d - 1)) - 1 and self.n_local % 2 == 0
 
-    def phase1_fused(self, p_old, p_new, send, r, q_old, x, push):
+    def phase1_fused(self, p_old, p_new, send, r, q_old, x, shift, push):
         native.check(native.lib().gg_kron_dist_phase1_fused(
             self.h, native.dptr(p_old), native.dptr(p_new), native.dptr(send),
             native.dptr(self.work), native.dptr(r), native.dptr(q_old), native.dptr(x), self.cgs,
-            int(bool(push)), native.stream_ptr()), "gg_kron_dist_phase1_fused")
+            float(shift), int(bool(push)), native.stream_ptr()), "gg_kron_dist_phase1_fused")
 
     def fused_post(self, q, p, shift):
         native.check(native.lib().gg_cgs_fused_post(
@@ -220,11 +220,12 @@ class HipEngine(object):
             self.cgs, native.dptr(self.red5), native.dptr(p_new), native.stream_ptr()),
             "gg_cgs_fused_scalars")
 
-    def fused_close(self, x, r, q):
+    def fused_close(self, x, r, q, p, shift):
         half = 2 * ((self.n_local + 3) // 4)
         native.check(native.lib().gg_cgs_fused_close(
-            self.cgs, native.dptr(x), native.dptr(r), native.dptr(q), self.n_local, half,
-            native.dptr(self.red), native.stream_ptr()), "gg_cgs_fused_close")
+            self.cgs, native.dptr(x), native.dptr(r), native.dptr(q), native.dptr(p),
+            self.n_local, half, float(shift), native.dptr(self.red), native.stream_ptr()),
+            "gg_cgs_fused_close")
 
     def fused_close_rho(self):
         native.check(native.lib().gg_cgs_fused_close_rho(self.cgs, native.dptr(self.red),
@@ -419,16 +420,17 @@ class DistKronCG(object):
 
     def _iterate_fused(self, n_iter):
         """The fused recurrence: per iteration phase 1 (prologue, x side job),
-        the exchanges and phase 2 (K p_new lands in q), q += shift p_new with
-        p.q / q.q, ONE all-reduce of five doubles, the scalars; leaving, the
-        deferred x and pending r update and one all-reduce of r.r -- the
-        textbook state (gg_cg_iterate's contract)."""
+        the exchanges and phase 2 (K p_new lands in q, kept unshifted), a
+        read-only pass for p.q' and q'.q' (q' = q + shift p_new), ONE
+        all-reduce of five doubles, the scalars; leaving, the deferred x and
+        pending r update and one all-reduce of r.r -- the textbook state
+        (gg_cg_iterate's contract), with q = K p."""
         push = self.mode == "push"
         pb = self.pbuf
         for _ in range(int(n_iter)):
             self._mark("start")
             p_old, p_new = pb[0], pb[1]
-            self.e.phase1_fused(p_old, p_new, self.send, self.r, self.q, self.x, push)
+            self.e.phase1_fused(p_old, p_new, self.send, self.r, self.q, self.x, self.shift, push)
             self._mark("phase1")
             if push:
                 self.x_ex.barrier()
@@ -453,7 +455,7 @@ class DistKronCG(object):
             # (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2})
             pb[0], pb[1], pb[2], pb[3] = p_new, pb[3], p_old, pb[2]
         self.p = pb[0]
-        self.e.fused_close(self.x, self.r, self.q)
+        self.e.fused_close(self.x, self.r, self.q, self.p, self.shift)
         self._allreduce()
         self.e.fused_close_rho()
 

@@ -148,10 +148,11 @@ SIGNATURES = {
     "gg_cgs_update": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64, _c_dp, _vp],
     "gg_cgs_rho": [_vp, _c_dp, _vp],
     "gg_kron_dist_phase1_fused": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp, _vp,
-                                  ctypes.c_int, _vp],
+                                  ctypes.c_double, ctypes.c_int, _vp],
     "gg_cgs_fused_post": [_vp, _c_dp, _c_dp, ctypes.c_int64, ctypes.c_double, _c_dp, _vp],
     "gg_cgs_fused_scalars": [_vp, _c_dp, _c_dp, _vp],
-    "gg_cgs_fused_close": [_vp, _c_dp, _c_dp, _c_dp, ctypes.c_int64, ctypes.c_int64, _c_dp, _vp],
+    "gg_cgs_fused_close": [_vp, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64, ctypes.c_int64,
+                           ctypes.c_double, _c_dp, _vp],
     "gg_cgs_fused_close_rho": [_vp, _c_dp, _vp],
     "gg_cgs_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                       ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],

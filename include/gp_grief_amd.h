@@ -393,31 +393,34 @@ int gg_cgs_status(gg_cgs* c, int* iters, int* done, double* rho, double* tol,
 /* Fused sharded CG: the single-GPU fused recurrence (gg_cg_*, recurrence
  * "fused") across ranks, ONE all-reduce of five doubles per iteration.  Per
  * iteration j: gg_kron_dist_phase1_fused (mode product 1 carries the
- * prologue -- r -= alpha q_old when pending, p_new = r + beta p_old into its
- * own buffer, r.r and p_new.q_old partials; mode product 2 the balanced
+ * prologue -- with q_old = K p_old (unshifted) and s = shift: r -= alpha
+ * (q_old + s p_old) when pending, p_new = r + beta p_old into its own buffer,
+ * r.r and p_new.(q_old + s p_old) partials; mode product 2 the balanced
  * deferred x update, half of x per iteration; the last one the all-to-all /
  * push epilogue; push != 0: scratch as in phase1_push), the exchanges and
- * phase 2 as for the textbook CG (K p lands in q), gg_cgs_fused_post (q +=
- * shift p_new, p.q and q.q; writes red[5] = [r.r, p_new.q_old, p.q, 0, q.q]
- * local), the caller's all-reduce of red, gg_cgs_fused_scalars (alpha, beta
- * by the |r - alpha q|^2 expansion with r.q = p.q - beta p.q_old, the x
- * deferral).  Leaving the iterations: gg_cgs_fused_close (deferred x steps,
- * pending r update, local r.r into rr_dev; half = 2 ceil(n_local / 4)), the
- * caller's all-reduce of rr_dev, gg_cgs_fused_close_rho -- the textbook
- * state, as gg_cg_iterate leaves it.  Needs d >= 4, folded factors 1..d-1,
+ * phase 2 as for the textbook CG (K p lands in q), gg_cgs_fused_post (reads
+ * only: p.(q + s p) and |q + s p|^2; writes red[5] = [r.r, p_new.q_old',
+ * p.q', 0, q'.q'] local, q' = q + s p), the caller's all-reduce of red,
+ * gg_cgs_fused_scalars (alpha, beta by the |r - alpha q'|^2 expansion with
+ * r.q' = p.q' - beta p.q_old', the x deferral).  Leaving the iterations:
+ * gg_cgs_fused_close (deferred x steps, pending r -= alpha (q + s p) with p
+ * the last direction, local r.r into rr_dev; half = 2 ceil(n_local / 4)),
+ * the caller's all-reduce of rr_dev, gg_cgs_fused_close_rho -- the textbook
+ * state, as gg_cg_iterate leaves it (q stays K p, unshifted).  Needs d >= 4, folded factors 1..d-1,
  * 16-byte aligned even-length vectors.  Reference: the CG the reference's
  * GP solves need on the operator of
  * kron_matrix.py:52-97; no reference counterpart for the sharding.         */
 int gg_kron_dist_phase1_fused(const gg_kron_dist* D, const double* p_old_dev, double* p_new_dev,
                               double* send_dev, double* work_dev, double* r_dev,
-                              const double* q_old_dev, double* x_dev, gg_cgs* cgs, int push,
-                              gg_stream stream);
-int gg_cgs_fused_post(gg_cgs* c, double* q_dev, const double* p_dev, int64_t n, double shift,
-                      double* red_dev, gg_stream stream);
+                              const double* q_old_dev, double* x_dev, gg_cgs* cgs,
+                              double shift, int push, gg_stream stream);
+int gg_cgs_fused_post(gg_cgs* c, const double* q_dev, const double* p_dev, int64_t n,
+                      double shift, double* red_dev, gg_stream stream);
 int gg_cgs_fused_scalars(gg_cgs* c, const double* red_dev, const double* p_new_dev,
                          gg_stream stream);
-int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_dev, int64_t n,
-                       int64_t half, double* rr_dev, gg_stream stream);
+int gg_cgs_fused_close(gg_cgs* c, double* x_dev, double* r_dev, const double* q_dev,
+                       const double* p_dev, int64_t n, int64_t half, double shift,
+                       double* rr_dev, gg_stream stream);
 int gg_cgs_fused_close_rho(gg_cgs* c, const double* rr_dev, gg_stream stream);
 
 #ifdef __cplusplus

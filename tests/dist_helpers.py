@@ -57,16 +57,17 @@ class NumpyEngine(object):
     # x deferral; partial sums are plain local dot products here
     supports_fused = True
 
-    def phase1_fused(self, p_old, p_new, send, r, q_old, x, push):
+    def phase1_fused(self, p_old, p_new, send, r, q_old, x, shift, push):
         sc = self.sc
         if sc["done"]:
             return
         rv, pn = r.numpy(), p_new.numpy()
+        qe = q_old.numpy() + shift * p_old.numpy()     # q_old = K p_old, unshifted
         if sc["pending"]:
-            rv -= sc["alpha"] * q_old.numpy()
+            rv -= sc["alpha"] * qe
         self.rr_local = float(np.dot(rv, rv))
         pn[:] = rv + sc["beta"] * p_old.numpy()
-        self.pqo_local = float(np.dot(pn, q_old.numpy()))
+        self.pqo_local = float(np.dot(pn, qe))
         h = sc["xh"]
         if h < 2:   # the side job: half h of the active pair
             H = self.half()
@@ -83,8 +84,7 @@ class NumpyEngine(object):
         self.red5 = getattr(self, "red5", torch.zeros(5, dtype=torch.float64))
         if self.sc["done"]:
             return
-        qv = q.numpy()
-        qv += shift * p.numpy()
+        qv = q.numpy() + shift * p.numpy()   # q itself stays K p
         self.red5[:] = torch.tensor([self.rr_local, self.pqo_local, float(np.dot(p.numpy(), qv)),
                                      0.0, float(np.dot(qv, qv))], dtype=torch.float64)
 
@@ -117,7 +117,7 @@ class NumpyEngine(object):
         else:
             sc.update(xc=[sc["xsc"], alpha], xp=[sc["xsp"], p_new], xh=0, xs=False)
 
-    def fused_close(self, x, r, q):
+    def fused_close(self, x, r, q, p, shift):
         sc = self.sc
         xv = x.numpy()
         if sc["xs"]:
@@ -130,7 +130,7 @@ class NumpyEngine(object):
         self.red[0] = 0.0
         if not sc["done"] and sc["pending"]:
             rv = r.numpy()
-            rv -= sc["alpha"] * q.numpy()
+            rv -= sc["alpha"] * (q.numpy() + shift * p.numpy())
             self.red[0] = float(np.dot(rv, rv))
 
     def fused_close_rho(self):

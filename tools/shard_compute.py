@@ -81,11 +81,11 @@ def run_one(a, eng, G, rec, m, d, torch, bench, dev):
         ev[0].record()
         if rec == "fused":
             p_old, p_new = pb[0], pb[1]
-            eng.phase1_fused(p_old, p_new, send, r, q, xs, False)   # prologue + x side job
+            eng.phase1_fused(p_old, p_new, send, r, q, xs, 0.01, False)   # prologue + x side
             ev[1].record()
             eng.phase2(recv, q)                                     # factor 0 on N/G
             ev[2].record()
-            eng.fused_post(q, p_new, 0.01)                          # q += s p ; p.q, q.q
+            eng.fused_post(q, p_new, 0.01)                          # p.q', q'.q' (reads)
             ev[3].record()
             eng.fused_scalars(p_new)                                # (after the all-reduce)
             ev[4].record()
