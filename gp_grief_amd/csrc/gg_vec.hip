@@ -698,13 +698,20 @@ int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream 
   });
 }
 
-// diagnostic knob GG_CG_VEC_PAD (elements, even): the CG vectors sit n + pad
-// apart in the workspace instead of n (HBM placement experiments)
+// The CG vectors start on 256-byte boundaries: the workspace base is rounded
+// up and every vector's stride is a multiple of 32 doubles.  A vector off a
+// 128-byte line costs the fused prologue (six streams) 13.0 -> 15.4 ms at
+// 200^4 -- the "slow level" of rounds 3-4, reproduced by the diagnostic knob
+// GG_CG_VEC_PAD (elements, even; added to the stride: pad 2 = every vector
+// 16 bytes further off the line than the previous; tools/prologue_levels.py,
+// profiles/r04/n_levels.jsonl).
 static int64_t cg_vec_pad() {
   const char* e = getenv("GG_CG_VEC_PAD");
   const int64_t v = e ? atoll(e) : 0;
   return v > 0 ? 2 * (v / 2) : 0;
 }
+static int64_t cg_vec_stride(int64_t n) { return (n + 31) / 32 * 32 + cg_vec_pad(); }
+constexpr int64_t kCgAlignSlack = 32;   // doubles: room to round the base up to 256 B
 
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
@@ -712,7 +719,7 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
     const int64_t n = gg::kron_n(K);
     // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
     // product's own output for an odd number of factors, MpFuse::first_dst)
-    *elems = 6 * (n + cg_vec_pad()) + gg::kron_work_elems(K, false) +
+    *elems = kCgAlignSlack + 6 * cg_vec_stride(n) + gg::kron_work_elems(K, false) +
              (gg::kron_d(K) % 2 == 1 ? n : 0);
   });
 }
@@ -728,7 +735,11 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->K = K;
       cg->shift = shift;
       cg->n = nr;
-      const int64_t vs = nr + cg_vec_pad();
+      const int64_t vs = cg_vec_stride(nr);
+      GG_REQUIRE((reinterpret_cast<uintptr_t>(work_dev) & 7) == 0, GG_ERR_VALUE,
+                 "the CG workspace must hold doubles (8-byte aligned)");
+      work_dev = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(work_dev) + 255) &
+                                           ~static_cast<uintptr_t>(255));
       cg->r = work_dev;
       cg->p = work_dev + vs;
       cg->q = work_dev + 2 * vs;
