@@ -432,11 +432,11 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
     return roof, extra
 
 
-PMC_JSON = os.path.join("profiles", "r03", "pmc_mode_product.json")
+PMC_JSON = os.path.join("profiles", "r04", "pmc_mode_product.json")
 # the sources that decide the CG mode products' HBM traffic
 KERNEL_SOURCES = ["gp_grief_amd/csrc/gg_kron.hip", "gp_grief_amd/csrc/gg_kron_fold.hip",
                   "gp_grief_amd/csrc/gg_mp.h", "gp_grief_amd/csrc/gg_internal.h",
-                  "gp_grief_amd/csrc/gg_vec.hip"]
+                  "gp_grief_amd/csrc/gg_vec.hip", "gp_grief_amd/csrc/gg_kron_ring.hip"]
 
 
 def kernel_source_hash():
