@@ -74,7 +74,7 @@ def test_pmc_traffic_requires_matching_sources(tmp_path, monkeypatch):
     rec = {"recurrence": "fused", "fusion_layout": 0, "fold_mask": 15, "x_deferred": True,
            "source_sha256": bench.kernel_source_hash(), "calibrated_on_own_pattern": True,
            "per_position": [{"position": k, "traffic_bytes": 1e10 * (k + 1)} for k in range(4)]}
-    os.makedirs(tmp_path / "profiles" / "r03")
+    os.makedirs(os.path.dirname(tmp_path / bench.PMC_JSON))
     path = tmp_path / bench.PMC_JSON
     json.dump(rec, open(path, "w"))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
