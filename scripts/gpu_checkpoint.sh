@@ -16,7 +16,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('s
 tail -1 $O/smoke.log
 # HBM traffic of the fused-CG mode products: two separate PMC passes (kernel
 # trace only), reads by request size and writes (tools/pmc_traffic.py)
-B="python3 bench.py --steps 4 --warmup 2 --cpu-baseline off --lanczos 0 --grief off"
+B="python3 bench.py --steps 4 --warmup 2 --cpu-baseline off --lanczos 0 --grief off --matvec 0"
 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --kernel-trace -d $O/mp_rd -o run --output-format csv -- $B > $O/mp_rd.log 2>&1 || { tail -5 $O/mp_rd.log; exit 1; }
 timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --kernel-trace -d $O/mp_wr -o run --output-format csv -- $B > $O/mp_wr.log 2>&1 || { tail -5 $O/mp_wr.log; exit 1; }
 python3 tools/pmc_traffic.py $O/mp_rd $O/mp_wr $O/pmc_mode_product.json
