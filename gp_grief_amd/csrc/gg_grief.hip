@@ -125,6 +125,10 @@ __global__ __launch_bounds__(256) void grief_tables_kernel(
     if (t % kTQ == q && t < nu) {
       const double v = acc[t];
       const int64_t o = a * U + col0 + ug + t;
+      if (Stab == nullptr) {   // value table: X itself
+        Ltab[o] = v;
+        continue;
+      }
       Stab[o] = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
       Ltab[o] = log(fabs(v == 0.0 ? 1.0 : v));
     }
@@ -215,6 +219,10 @@ __device__ __forceinline__ void tables_mfma_body(const TabFactor& F, int grp,
         if (uu < nu) {
           const double v = acc[r];
           const int64_t o = a * U + F.col0 + ug + uu;
+          if (Stab == nullptr) {   // value table: X itself (half the table bytes)
+            Ltab[o] = v;
+            continue;
+          }
           Stab[o] = v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0);
           Ltab[o] = log(fabs(v == 0.0 ? 1.0 : v));
         }
@@ -317,7 +325,7 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_kernel(
   const int j = j0 + threadIdx.x;
   const int rows = (int)min<int64_t>(kR, n - a0);
   for (int e = threadIdx.x; e < rows * U; e += blockDim.x)
-    sT[e] = Stab[a0 * U + e] * exp(Ltab[a0 * U + e]);
+    sT[e] = Stab ? Stab[a0 * U + e] * exp(Ltab[a0 * U + e]) : Ltab[a0 * U + e];
   if (kD == 0 && j < p)
     for (int f = 0; f < d; ++f) sC[f * kPhiCols + threadIdx.x] = cidx[(int64_t)j * d + f];
   int creg[kD > 0 ? kD : 1];
@@ -369,7 +377,7 @@ __global__ __launch_bounds__(kPhiCols) void grief_phi_pair_kernel(
   const int64_t a0 = (int64_t)blockIdx.x * kR;
   const int rows = (int)min<int64_t>(kR, n - a0);
   for (int e = threadIdx.x; e < rows * U; e += blockDim.x)
-    sT[e] = Stab[a0 * U + e] * exp(Ltab[a0 * U + e]);
+    sT[e] = Stab ? Stab[a0 * U + e] * exp(Ltab[a0 * U + e]) : Ltab[a0 * U + e];
   __syncthreads();
   const int pairs = p >> 1;
   for (int jp = threadIdx.x; jp < pairs; jp += kPhiCols) {
@@ -522,7 +530,7 @@ int gg_grief_tables(int kind, double variance, double lengthscale, const double*
                     int col0, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(kind >= 0 && kind <= 3, GG_ERR_VALUE, "unknown kernel kind");
-    GG_REQUIRE(x_dev && xg_dev && qsel_dev && ltab_dev && stab_dev, GG_ERR_VALUE, "NULL");
+    GG_REQUIRE(x_dev && xg_dev && qsel_dev && ltab_dev, GG_ERR_VALUE, "NULL");
     GG_REQUIRE(m >= 1 && u >= 1 && col0 >= 0 && col0 + u <= U && n >= 0, GG_ERR_VALUE,
                "bad table geometry");
     if (n == 0) return;
@@ -552,7 +560,7 @@ int gg_grief_tables_all(int nf, const int* kinds, const double* variances,
                         gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(nf >= 1 && kinds && variances && lengthscales && x_dev && x_offsets && xg_devs &&
-                   ms && qsel_devs && us && ltab_dev && stab_dev && col0s && n >= 0,
+                   ms && qsel_devs && us && ltab_dev && col0s && n >= 0,
                GG_ERR_VALUE, "bad argument");
     for (int f = 0; f < nf; ++f) {
       GG_REQUIRE(kinds[f] >= 0 && kinds[f] <= 3, GG_ERR_VALUE, "unknown kernel kind");
@@ -585,7 +593,7 @@ int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t 
                  const int* cidx_dev, int d, const double* log_lam_dev, int p, int transposed,
                  double* phi_dev, gg_stream stream) {
   return gg::guard([&] {
-    GG_REQUIRE(ltab_dev && stab_dev && cidx_dev && log_lam_dev && phi_dev, GG_ERR_VALUE, "NULL");
+    GG_REQUIRE(ltab_dev && cidx_dev && log_lam_dev && phi_dev, GG_ERR_VALUE, "NULL");
     GG_REQUIRE(d >= 1 && d <= gg::kMaxDim && U >= 1 && p >= 1 && n >= 0, GG_ERR_VALUE,
                "bad Phi geometry");
     if (n == 0) return;

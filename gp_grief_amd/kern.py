@@ -397,8 +397,13 @@ class GriefKernel(GridKernel):
         n = xd.numel() // self.grid_dim
         d = self.grid_dim
         L = native.lib()
+        # the value table X (gg_grief_tables_all with stab NULL): one double per
+        # entry, where the log / sign pair of the reference's expand_SKC costs
+        # two -- Phi takes the product of the values, the same numbers up to
+        # rounding (GG_GRIEF_LOGTAB=1: the log / sign tables, A/B)
         ltab = dev.empty(max(n * B["U"], 1))
-        stab = dev.empty(max(n * B["U"], 1))
+        stab = dev.empty(max(n * B["U"], 1)) if os.environ.get("GG_GRIEF_LOGTAB") == "1" \
+            else None
         # every dimension's table in one launch (factor f reads input dim d-1-f);
         # the host argument arrays are built once per basis
         a = B.get("tab_args")
@@ -407,11 +412,14 @@ class GriefKernel(GridKernel):
             B["tab_args"] = a
         native.check(L.gg_grief_tables_all(d, a["kinds"], a["var"], a["ls"], native.dptr(xd), d,
                                            a["xoff"], n, a["xgp"], a["ms"], a["qsp"], a["us"],
-                                           native.dptr(ltab), native.dptr(stab), B["U"], a["c0"],
+                                           native.dptr(ltab),
+                                           native.dptr(stab) if stab is not None else None,
+                                           B["U"], a["c0"],
                                            native.stream_ptr()), "gg_grief_tables_all")
         p = self.n_eigs
         phi = dev.empty(n * p)
-        native.check(L.gg_grief_phi(native.dptr(ltab), native.dptr(stab), B["U"], n,
+        native.check(L.gg_grief_phi(native.dptr(ltab),
+                                    native.dptr(stab) if stab is not None else None, B["U"], n,
                                     native.dptr(B["cidx"]), d, native.dptr(B["log_lam"]), p,
                                     int(bool(transposed)), native.dptr(phi),
                                     native.stream_ptr()), "gg_grief_phi")

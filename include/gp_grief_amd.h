@@ -233,7 +233,9 @@ int gg_cov(int kind, double variance, double lengthscale, int dims, const double
            gg_stream stream);
 /* Per-dimension tables of expand_SKC (gp_grief/tensors/tensors.py:97-128):
  * X[u][a] = sum_k qsel[u][k] k(xg[k], x[a * x_stride]); writes
- * ltab[a*U + col0 + u] = log|X| (0 where X == 0) and stab = sign(X).        */
+ * ltab[a*U + col0 + u] = log|X| (0 where X == 0) and stab = sign(X), or with
+ * stab_dev == NULL the value table ltab[a*U + col0 + u] = X (half the bytes;
+ * what gg_grief_phi needs).                                                  */
 int gg_grief_tables(int kind, double variance, double lengthscale, const double* x_dev,
                     int64_t x_stride, int64_t n, const double* xg_dev, int m,
                     const double* qsel_dev, int u, double* ltab_dev, double* stab_dev, int U,
@@ -250,7 +252,9 @@ int gg_grief_tables_all(int nf, const int* kinds, const double* variances,
                         gg_stream stream);
 /* Phi[a][j] = prod_f stab[a][c_jf] * exp(sum_f ltab[a][c_jf] - log_lam[j] / 2)
  * (GriefKernel.cov, gp_grief/kern/grief_kernel.py:96-104); cidx: p x d int32.
- * transposed != 0 writes Phi^T (p x n).                                      */
+ * stab_dev == NULL: ltab is the value table (X itself) and Phi[a][j] =
+ * prod_f ltab[a][c_jf] * exp(-log_lam[j] / 2).  transposed != 0 writes Phi^T
+ * (p x n).                                                                   */
 int gg_grief_phi(const double* ltab_dev, const double* stab_dev, int U, int64_t n,
                  const int* cidx_dev, int d, const double* log_lam_dev, int p, int transposed,
                  double* phi_dev, gg_stream stream);

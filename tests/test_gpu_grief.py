@@ -484,3 +484,29 @@ def test_grief_subset_falls_back_on_clusters(gg, monkeypatch):
     kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
     kern._setup_inducing_cov()
     assert kern._Quu_full is not None
+
+
+@pytest.mark.parametrize("d,kind", [(3, "RBF"), (6, "Matern52")])
+def test_grief_phi_value_table_matches_log_table(gg, monkeypatch, d, kind):
+    """Phi from the value table (default: gg_grief_tables_all / gg_grief_phi
+    with stab NULL) against the log / sign tables of the reference's
+    expand_SKC (GG_GRIEF_LOGTAB=1), row-major and transposed: the same numbers
+    up to the exp(log|X|) rounding, 1e-13 relative."""
+    import torch
+    rng = np.random.default_rng(3)
+    n, m, p = 2000, 24, 200
+    x = rng.random((n, d))
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GG_GRIEF_LOGTAB", flag)
+        kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=0.2 + 0.02 * i)
+              for i in range(d)]
+        grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1)] * d)
+        kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+        P = kern.phi_device(x).cpu().numpy()
+        PT = kern.phi_device(x, transposed=True).cpu().numpy()
+        torch.cuda.synchronize()
+        out.append((P, PT))
+    (P0, T0), (P1, T1) = out
+    assert np.abs(T0 - P0.T).max() == 0.0
+    assert rel(P0, P1) < 1e-13 and rel(T0, T1) < 1e-13
