@@ -65,6 +65,22 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
   static_assert(!kMap || kEpi == 0, "the mapped epilogue stores only");
   constexpr bool kLean = (kOpt & 4) != 0;
   constexpr bool kBdb = (kOpt & 8) != 0;
+  // kOpt bits 5-7 (GG_FOLD_PRO_NT mask 1 / 2 / 4): non-temporal A-operand /
+  // r / q_old loads, non-temporal p_new / r stores (CG prologue), and
+  // non-temporal stores of the plain epilogue
+  constexpr bool kNTl = (kOpt & 32) != 0, kNTs = (kOpt & 64) != 0, kNTy = (kOpt & 128) != 0;
+  auto ldg = [](const double* p) -> double {
+    if constexpr (kNTl) return __builtin_nontemporal_load(p);
+    return *p;
+  };
+  auto stg = [](double* p, double v) {
+    if constexpr (kNTs) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  };
+  auto sty = [](double* p, double v) {
+    if constexpr (kNTy) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  };
   static_assert(!(kMap && kStg), "staged epilogue: identity layout only");
   constexpr int kWaves = kWv;   // waves per workgroup (A/B variants: 6, 12)
   constexpr int kThreads = 64 * kWv;
@@ -193,15 +209,15 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     for (int s = 0; s < kKC; ++s) {
       const int64_t l_ = last ? (ol < alast ? ol : alast) : ol;
       const int64_t h_ = last ? (oh > bclamp ? oh : bclamp) : oh;
-      a[0][s] = X[l_];
-      a[1][s] = X[h_];
+      a[0][s] = ldg(X + l_);
+      a[1][s] = ldg(X + h_);
       if (CGP) {
-        r[0][s] = Rg[l_];
-        r[1][s] = Rg[h_];
+        r[0][s] = ldg(Rg + l_);
+        r[1][s] = ldg(Rg + h_);
       }
       if (CGP >= 2) {
-        q[0][s] = Qa[l_];
-        q[1][s] = Qa[h_];
+        q[0][s] = ldg(Qa + l_);
+        q[1][s] = ldg(Qa + h_);
       }
       ol += m4;
       oh -= m4;
@@ -218,7 +234,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     if (CGP == 3) {
       v = fma(lz_cp, q, fma(lz_cu, r, lz_cy * v));
       if (ok) {
-        *at(Pout) = v;
+        stg(at(Pout), v);
         rr_acc = fma(v, v, rr_acc);
       }
     } else if (CGP) {
@@ -226,12 +242,12 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
       if (CGP == 2 && cg_pending) {
         r = r - cg_alpha * q;
         if (ok) {
-          *at(Rg) = r;
+          stg(at(Rg), r);
           rr_acc = fma(r, r, rr_acc);
         }
       }
       v = cg_first ? r : fma(cg_beta, v, r);
-      if (Pout != nullptr && ok) *at(Pout) = v;
+      if (Pout != nullptr && ok) stg(at(Pout), v);
       if (CGP == 2 && pqo_on && ok) pqo_acc = fma(v, q, pqo_acc);
     }
     return v;
@@ -544,7 +560,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (cok && (lane >> 4) + 4 * r < rows_left)
-          *reinterpret_cast<double*>(ybase + boff_of(r, e)) = value(e, r);
+          sty(reinterpret_cast<double*>(ybase + boff_of(r, e)), value(e, r));
     }
   } else {
     // shift / dots: the loads of half-tile e + 1 are issued before e's stores
@@ -780,7 +796,21 @@ static FoldConfig fold_by_kind(int kind, bool lean_ok) {
     if (kind == 2) {
       const int lp = env_int("GG_FOLD_LEAN_PRO");
       if (lean_ok && (lp == 1 || lp == 2)) return lean_pro_cfg(lp);
-      if (env_int("GG_FOLD_PRO_W", 12) == 12) return wide_cfg(2);
+      if (env_int("GG_FOLD_PRO_W", 12) == 12) {
+        // non-temporal prologue streams (default mask 3: the operand / r /
+        // q_old loads and the p_new / r stores; Y, read by the next launch,
+        // stays a normal store) -- 200^4, interleaved processes on two boxes:
+        // prologue 13.90 -> 13.63 ms, iteration 40.62 -> 40.36 ms (mask 7,
+        // Y too: mixed, the side launches +0.1 ms; profiles/r04/t_pro_nt*)
+        switch (env_int("GG_FOLD_PRO_NT", 3)) {
+          case 1: return cfg_fold<7, 1, 2, false, 32, 0, 12>();
+          case 2: return cfg_fold<7, 1, 2, false, 64, 0, 12>();
+          case 3: return cfg_fold<7, 1, 2, false, 96, 0, 12>();
+          case 6: return cfg_fold<7, 1, 2, false, 192, 0, 12>();
+          case 7: return cfg_fold<7, 1, 2, false, 224, 0, 12>();
+          default: return wide_cfg(2);
+        }
+      }
       const char* e = getenv("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }

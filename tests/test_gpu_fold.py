@@ -110,6 +110,21 @@ def test_fold_lean_matches_clamped(gg, monkeypatch, m0):
     assert rel(out["1"][0], oracle.kron_matvec(F, x[:, 0])) < 1e-13
 
 
+def test_fold_prologue_nontemporal_bitwise(gg, monkeypatch):
+    """The CG prologue with non-temporal loads / stores (GG_FOLD_PRO_NT=1,
+    A/B knob) runs the same arithmetic: a fused CG at 200^3 agrees bitwise."""
+    F = [grid_factor(200, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
+    x = np.random.default_rng(5).standard_normal((200 ** 3, 1))
+    out = {}
+    for nt in ("0", "1", "2", "3", "6", "7"):
+        monkeypatch.setenv("GG_FOLD_PRO_NT", nt)
+        K = kron(gg, F)
+        xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=6, recurrence="fused")
+        out[nt] = np.asarray(xs)
+    for nt in ("1", "2", "3", "6", "7"):
+        assert np.array_equal(out["0"], out[nt])
+
+
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
     """A centrosymmetric but non-symmetric factor: the transposed operator's
     split is packed from F^T."""
