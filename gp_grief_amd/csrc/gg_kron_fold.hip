@@ -65,9 +65,10 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
   static_assert(!kMap || kEpi == 0, "the mapped epilogue stores only");
   constexpr bool kLean = (kOpt & 4) != 0;
   constexpr bool kBdb = (kOpt & 8) != 0;
-  // kOpt bits 5-7 (GG_FOLD_PRO_NT mask 1 / 2 / 4): non-temporal A-operand /
-  // r / q_old loads, non-temporal p_new / r stores (CG prologue), and
-  // non-temporal stores of the plain epilogue
+  // kOpt bits 5-7 (GG_FOLD_*_NT masks 1 / 2 / 4): bit 5 non-temporal A-operand
+  // (+ r / q_old) loads; bit 6 non-temporal p_new / r stores (CG prologue),
+  // epilogue operand loads (p, r) and the x side job's streams; bit 7
+  // non-temporal output stores
   constexpr bool kNTl = (kOpt & 32) != 0, kNTs = (kOpt & 64) != 0, kNTy = (kOpt & 128) != 0;
   auto ldg = [](const double* p) -> double {
     if constexpr (kNTl) return __builtin_nontemporal_load(p);
@@ -189,8 +190,8 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
       for (int s = 0; s < kKC; ++s) {
         const int64_t t = (int64_t)c * kKC + s;
         const int64_t lb = lrow_b(t), hb = hrow_b(t);
-        a[0][s] = *reinterpret_cast<const double*>(sbase(X, lb) + loff);
-        a[1][s] = *reinterpret_cast<const double*>(sbase(X, hb) + hoff);
+        a[0][s] = ldg(reinterpret_cast<const double*>(sbase(X, lb) + loff));
+        a[1][s] = ldg(reinterpret_cast<const double*>(sbase(X, hb) + hoff));
         if (CGP) {
           r[0][s] = *reinterpret_cast<const double*>(sbase(Rg, lb) + loff);
           r[1][s] = *reinterpret_cast<const double*>(sbase(Rg, hb) + hoff);
@@ -482,9 +483,8 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
           const bool ok = i2 < tot2;
           const int64_t g = g0 + 2 * (int64_t)i2;
           av[u] = ok ? *reinterpret_cast<const double2*>(wl + 2 * i2) : double2{0.0, 0.0};
-          pv[u] = (ok && xs != nullptr) ? *reinterpret_cast<const double2*>(xs + g)
-                                        : double2{0.0, 0.0};
-          ev[u] = (ok && rq_on) ? *reinterpret_cast<const double2*>(er + g) : double2{0.0, 0.0};
+          pv[u] = (ok && xs != nullptr) ? ld2<kNTs>(xs + g) : double2{0.0, 0.0};
+          ev[u] = (ok && rq_on) ? ld2<kNTs>(er + g) : double2{0.0, 0.0};
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
           if (i2 >= tot2) continue;
           const int64_t g = g0 + 2 * (int64_t)i2;
           if (xs == nullptr) {
-            *reinterpret_cast<double2*>(Y + g) = av[u];
+            st2<kNTy>(Y + g, av[u]);
             continue;
           }
           double2 p2 = pv[u];
@@ -511,8 +511,8 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
             qqsum = fma(v.x, v.x, qqsum);
             qqsum = fma(v.y, v.y, qqsum);
           }
-          *reinterpret_cast<double2*>(Y + g) = v;
-          if (kRecomp) *reinterpret_cast<double2*>(epo + g) = p2;
+          st2<kNTy>(Y + g, v);
+          if (kRecomp) st2<kNTy>(epo + g, p2);
         }
       }
     }
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
   mp_block_sums<kWaves, CGP, edots, false>(dsum, edots ? rqsum : pqo_acc, qqsum, rr_acc,
                                            dot_partials, fz, kStg ? lds + 4 * kWaves * m : lds,
                                            blockIdx.x);
-  if (kEpi >= 1) mp_side_job<kThreads>(fz, blockIdx.x);
+  if (kEpi >= 1) mp_side_job<kThreads, kNTs>(fz, blockIdx.x);
 }
 
 // kind (kron_apply's launch kind) -> the folded kernel; kind 5 (fusion
@@ -666,14 +666,30 @@ static FoldConfig lean_cfg(int kind, bool staged) {
   constexpr int JT = 7, TT = 1;
   if (staged) {
     switch (kind) {
-      case 3: return cfg_fold<JT, TT, 3, true, 4>();
+      case 3:
+        // GG_FOLD_EPI_NT (A/B): non-temporal streams of the CG epilogue
+        switch (env_int("GG_FOLD_EPI_NT")) {
+          case 1: return cfg_fold<JT, TT, 3, true, 4 | 32>();
+          case 2: return cfg_fold<JT, TT, 3, true, 4 | 64>();
+          case 4: return cfg_fold<JT, TT, 3, true, 4 | 128>();
+          case 6: return cfg_fold<JT, TT, 3, true, 4 | 192>();
+          case 7: return cfg_fold<JT, TT, 3, true, 4 | 224>();
+          default: return cfg_fold<JT, TT, 3, true, 4>();
+        }
       case 6: return cfg_fold<JT, TT, 6, true, 4>();
       default: return cfg_fold<JT, TT, 0, true, 4>();
     }
   }
   switch (kind) {
     case 3: return cfg_fold<JT, TT, 3, false, 4>();
-    case 4: return cfg_fold<JT, TT, 4, false, 4>();
+    case 4:
+      // GG_FOLD_SIDE_NT (A/B): non-temporal streams of the side-job launches
+      switch (env_int("GG_FOLD_SIDE_NT")) {
+        case 1: return cfg_fold<JT, TT, 4, false, 4 | 32>();
+        case 2: return cfg_fold<JT, TT, 4, false, 4 | 64>();
+        case 3: return cfg_fold<JT, TT, 4, false, 4 | 96>();
+        default: return cfg_fold<JT, TT, 4, false, 4>();
+      }
     case 6: return cfg_fold<JT, TT, 6, false, 4>();
     default: return cfg_fold<JT, TT, 0, false, 4>();
   }

@@ -56,7 +56,27 @@ __device__ __forceinline__ void mp_block_sums(double dsum, double rqsum, double 
 // Side job (fused CG, second / third mode product): x += alpha p_old over
 // this workgroup's slice, 16-byte lanes.  The mode product has HBM headroom;
 // the other workgroups of the CU keep the matrix cores busy meanwhile.
-template <int kThreads>
+// 16-byte loads / stores, non-temporal when kNT (streams read or written once
+// per iteration)
+typedef double nt_d2 __attribute__((ext_vector_type(2)));
+template <bool kNT>
+__device__ __forceinline__ double2 ld2(const double* p) {
+  if constexpr (kNT) {
+    const nt_d2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_d2*>(p));
+    return double2{v.x, v.y};
+  }
+  return *reinterpret_cast<const double2*>(p);
+}
+template <bool kNT>
+__device__ __forceinline__ void st2(double* p, double2 v) {
+  if constexpr (kNT) {
+    __builtin_nontemporal_store(nt_d2{v.x, v.y}, reinterpret_cast<nt_d2*>(p));
+  } else {
+    *reinterpret_cast<double2*>(p) = v;
+  }
+}
+
+template <int kThreads, bool kNT = false>
 __device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
   if (fz.sx == nullptr) return;
   int64_t lo = blk * fz.schunk;
@@ -81,15 +101,15 @@ __device__ __forceinline__ void mp_side_job(const MpFuse& fz, int64_t blk) {
       double2 xv2[kB2], a2[kB2], b2[kB2];
 #pragma unroll
       for (int u = 0; u < kB2; ++u) {
-        xv2[u] = *reinterpret_cast<const double2*>(xo + i + 2 * kThreads * u);
-        a2[u] = *reinterpret_cast<const double2*>(p0 + i + 2 * kThreads * u);
-        b2[u] = *reinterpret_cast<const double2*>(p1 + i + 2 * kThreads * u);
+        xv2[u] = ld2<kNT>(xo + i + 2 * kThreads * u);
+        a2[u] = ld2<kNT>(p0 + i + 2 * kThreads * u);
+        b2[u] = ld2<kNT>(p1 + i + 2 * kThreads * u);
       }
 #pragma unroll
       for (int u = 0; u < kB2; ++u) {
         xv2[u].x += c0 * a2[u].x + c1 * b2[u].x;
         xv2[u].y += c0 * a2[u].y + c1 * b2[u].y;
-        *reinterpret_cast<double2*>(xo + i + 2 * kThreads * u) = xv2[u];
+        st2<kNT>(xo + i + 2 * kThreads * u, xv2[u]);
       }
     }
     for (; i < hi; i += 2 * kThreads) {

@@ -110,19 +110,28 @@ def test_fold_lean_matches_clamped(gg, monkeypatch, m0):
     assert rel(out["1"][0], oracle.kron_matvec(F, x[:, 0])) < 1e-13
 
 
-def test_fold_prologue_nontemporal_bitwise(gg, monkeypatch):
-    """The CG prologue with non-temporal loads / stores (GG_FOLD_PRO_NT=1,
-    A/B knob) runs the same arithmetic: a fused CG at 200^3 agrees bitwise."""
+def test_fold_nontemporal_variants_bitwise(gg, monkeypatch):
+    """Non-temporal loads / stores in the CG launches (GG_FOLD_PRO_NT,
+    GG_FOLD_EPI_NT, GG_FOLD_SIDE_NT masks) run the same arithmetic: a fused
+    CG at 200^3 agrees bitwise with every mask off."""
     F = [grid_factor(200, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
     x = np.random.default_rng(5).standard_normal((200 ** 3, 1))
-    out = {}
-    for nt in ("0", "1", "2", "3", "6", "7"):
-        monkeypatch.setenv("GG_FOLD_PRO_NT", nt)
+    knobs = ["GG_FOLD_PRO_NT", "GG_FOLD_EPI_NT", "GG_FOLD_SIDE_NT"]
+    cases = [{"GG_FOLD_PRO_NT": "0"}] + \
+        [{"GG_FOLD_PRO_NT": v} for v in ("1", "2", "3", "6", "7")] + \
+        [{"GG_FOLD_PRO_NT": "0", "GG_FOLD_EPI_NT": v} for v in ("1", "2", "4", "6", "7")] + \
+        [{"GG_FOLD_PRO_NT": "0", "GG_FOLD_SIDE_NT": v} for v in ("1", "2", "3")]
+    out = []
+    for case in cases:
+        for k in knobs:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in case.items():
+            monkeypatch.setenv(k, v)
         K = kron(gg, F)
         xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=6, recurrence="fused")
-        out[nt] = np.asarray(xs)
-    for nt in ("1", "2", "3", "6", "7"):
-        assert np.array_equal(out["0"], out[nt])
+        out.append(np.asarray(xs))
+    for o in out[1:]:
+        assert np.array_equal(out[0], o)
 
 
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
