@@ -667,8 +667,10 @@ static FoldConfig lean_cfg(int kind, bool staged) {
   if (staged) {
     switch (kind) {
       case 3:
-        // GG_FOLD_EPI_NT (A/B): non-temporal streams of the CG epilogue
-        switch (env_int("GG_FOLD_EPI_NT")) {
+        // GG_FOLD_EPI_NT: non-temporal streams of the CG epilogue (default 6:
+        // the p operand loads and the q stores; epilogue 8.66-8.76 -> 8.59-8.64
+        // ms at 200^4, interleaved, profiles/r04/u_nt)
+        switch (env_int("GG_FOLD_EPI_NT", 6)) {
           case 1: return cfg_fold<JT, TT, 3, true, 4 | 32>();
           case 2: return cfg_fold<JT, TT, 3, true, 4 | 64>();
           case 4: return cfg_fold<JT, TT, 3, true, 4 | 128>();
@@ -683,8 +685,10 @@ static FoldConfig lean_cfg(int kind, bool staged) {
   switch (kind) {
     case 3: return cfg_fold<JT, TT, 3, false, 4>();
     case 4:
-      // GG_FOLD_SIDE_NT (A/B): non-temporal streams of the side-job launches
-      switch (env_int("GG_FOLD_SIDE_NT")) {
+      // GG_FOLD_SIDE_NT: non-temporal streams of the side-job launches
+      // (default 3: A-operand loads and the x side job's loads / stores;
+      // 7.89-7.96 -> 7.84-7.89 ms per launch, profiles/r04/u_nt)
+      switch (env_int("GG_FOLD_SIDE_NT", 3)) {
         case 1: return cfg_fold<JT, TT, 4, false, 4 | 32>();
         case 2: return cfg_fold<JT, TT, 4, false, 4 | 64>();
         case 3: return cfg_fold<JT, TT, 4, false, 4 | 96>();
