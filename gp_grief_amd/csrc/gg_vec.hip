@@ -340,6 +340,49 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
   }
 }
 
+// a sharded CG rank's local sums of one fused iteration, red = [r.r (of the
+// prologue's r update), p.q_old, p.q, r.q, q.q] (gg_cg_iterate_partial); the
+// caller all-reduces red and cg_fused_scalars_kernel takes it as one-element
+// partial arrays
+__global__ __launch_bounds__(1024) void cg_local_red_kernel(
+    const double* __restrict__ rr_part, int64_t nrr, int64_t rr_stride,
+    const double* __restrict__ mv_part, int64_t nmv, int64_t pstride, int rq_ident,
+    double* __restrict__ red) {
+  double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) {
+    a[0] += rr_part[i];
+    if (rq_ident) a[1] += rr_part[rr_stride + i];
+  }
+  for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
+    a[2] += mv_part[i];
+    if (!rq_ident) a[3] += mv_part[pstride + i];
+    a[4] += mv_part[2 * pstride + i];
+  }
+  double t[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    t[k] = block_sum(a[k]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < 5; ++k) red[k] = t[k];
+}
+
+// the closing step of a sharded rank: rho from the all-reduced r.r
+__global__ void cg_close_rho_kernel(CgScalars* sc, const double* rr) {
+  if (sc->done || !sc->pending) return;
+  const double s = *rr;
+  sc->rho_prev = sc->rho;
+  sc->rho = s;
+  sc->beta = s / sc->rho_prev;
+  sc->iters += 1;
+  sc->first = 0;
+  sc->pending = 0;
+  sc->repair = 0;
+  if (!(sqrt(s) >= sc->tol)) sc->done = 1;
+}
+
 __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t count,
                                CgScalars* sc, double rtol, double atol) {
   double acc = 0.0;
@@ -589,6 +632,9 @@ struct gg_cg {
   const double* b = nullptr;
   double* x = nullptr;
   int64_t mv_partials = 0;
+  // rank of a sharded CG (gg_cg_*_partial / _finish): an iteration's local
+  // sums await the caller's all-reduce (the p_new of that iteration)
+  bool await_finish = false;
   // live timing of the mode products (gg_cg_profile): d + 1 events per
   // profiled iteration, recorded on the CG stream, read back on demand
   bool profiling = false;
@@ -1053,6 +1099,162 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
                          (int64_t)nb, cg->sc, 1);
       GG_LAUNCH_CHECK();
     }
+  });
+}
+
+// ---- a rank of a sharded CG (include/gp_grief_amd.h, gg_cg_*_partial):
+// the fused recurrence on this rank's block of a block-diagonal operator,
+// every dot product reduced by the caller between _partial and _finish
+int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* rr_dev,
+                        gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && b_dev && x_dev && rr_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(cg->fused, GG_ERR_VALUE, "the sharded rank runs the fused recurrence");
+    hipStream_t s = gg::as_stream(stream);
+    cg->b = b_dev;
+    cg->x = x_dev;
+    cg->await_finish = false;
+    const int64_t n = cg->n;
+    GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    GG_HIP(hipMemsetAsync(x_dev, 0, n * sizeof(double), s));
+    const int nb = gg::vec_blocks(n);
+    gg::launch_dot_partials(cg->r, cg->r, n, cg->partials, nb, s);
+    gg::launch_reduce_to(cg->partials, nb, rr_dev, s);
+  });
+}
+
+int gg_cg_start_finish(gg_cg* cg, const double* rr_dev, double rtol, double atol,
+                       gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cg->x && rr_dev, GG_ERR_VALUE, "CG not started (gg_cg_start_partial)");
+    GG_REQUIRE(rtol >= 0 && atol >= 0, GG_ERR_VALUE,
+               "tolerances must be real, non-negative numbers");
+    hipLaunchKernelGGL(gg::cg_init_kernel, dim3(1), dim3(1024), 0, gg::as_stream(stream), rr_dev,
+                       (int64_t)1, cg->sc, rtol, atol);
+    GG_LAUNCH_CHECK();
+  });
+}
+
+int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cg->x && red_dev, GG_ERR_VALUE, "CG not started");
+    GG_REQUIRE(cg->fused && cg->fusion == 0, GG_ERR_VALUE,
+               "the sharded rank runs the fused recurrence, layout 0");
+    GG_REQUIRE(!cg->await_finish, GG_ERR_VALUE, "gg_cg_iterate_finish first");
+    hipStream_t s = gg::as_stream(stream);
+    const int64_t n = cg->n;
+    int64_t nparts = 0;
+    hipEvent_t* ev = nullptr;
+    if (cg->profiling) {
+      const size_t need = cg->events_used + (size_t)gg::kron_d(cg->K) + 1;
+      while (cg->events.size() < need) {
+        hipEvent_t e;
+        GG_HIP(hipEventCreate(&e));
+        cg->events.push_back(e);
+      }
+      ev = cg->events.data() + cg->events_used;
+      cg->events_used = need;
+    }
+    // no repair kernels: a cancelled beta (set to 0 by the scalars) restarts
+    // the recurrence with p = r instead of a second all-reduce
+    const int xmode = cg->xdefer;
+    gg::MpFuse fz;
+    fz.r = cg->r;
+    fz.q_old = cg->q;
+    fz.p_out = cg->p2;
+    fz.sc = cg->sc;
+    fz.rr_part = cg->rr_part;
+    fz.rr_cap = cg->rr_count;
+    int64_t pro_blocks = 0;
+    fz.pro_blocks = &pro_blocks;
+    fz.sx = cg->x;
+    fz.sp = cg->p;
+    fz.sn = n;
+    fz.xdefer = xmode;
+    fz.first_dst = cg->first_dst;
+    const bool rq_ident = cg->rq != 0;
+    fz.er = rq_ident ? nullptr : cg->r;
+    fz.pqo_stride = rq_ident ? cg->rr_count : 0;
+    fz.pstride = cg->mv_partials;
+    gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                   &cg->sc->done, s, &nparts, &fz, 2, ev);
+    GG_REQUIRE(pro_blocks > 0 && pro_blocks <= cg->rr_count, GG_ERR_RUNTIME,
+               "fused CG: no prologue launch recorded");
+    hipLaunchKernelGGL(gg::cg_local_red_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
+                       pro_blocks, cg->rr_count, cg->partials, nparts, cg->mv_partials,
+                       rq_ident ? 1 : 0, red_dev);
+    GG_LAUNCH_CHECK();
+    cg->await_finish = true;
+  });
+}
+
+int gg_cg_iterate_finish(gg_cg* cg, const double* red_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && red_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(cg->await_finish, GG_ERR_VALUE, "gg_cg_iterate_partial first");
+    hipStream_t s = gg::as_stream(stream);
+    const int xmode = cg->xdefer;
+    const bool rq_ident = cg->rq != 0;
+    // red = [rr, p.q_old | p.q, r.q, q.q]: one-element partial arrays
+    hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, red_dev,
+                       (int64_t)1, (int64_t)1, red_dev + 2, (int64_t)1, (int64_t)1, cg->sc,
+                       xmode ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
+    GG_LAUNCH_CHECK();
+    if (xmode == 2) {
+      double* cur = cg->p;
+      double* o2 = cg->p3;
+      cg->p = cg->p2;
+      cg->p2 = cg->p4;
+      cg->p3 = cur;
+      cg->p4 = o2;
+    } else if (xmode == 1) {
+      double* old_ = cg->p3;
+      cg->p3 = cg->p;
+      cg->p = cg->p2;
+      cg->p2 = old_;
+    } else {
+      std::swap(cg->p, cg->p2);
+    }
+    cg->await_finish = false;
+  });
+}
+
+int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cg->x && rr_dev, GG_ERR_VALUE, "CG not started");
+    GG_REQUIRE(!cg->await_finish, GG_ERR_VALUE, "gg_cg_iterate_finish first");
+    hipStream_t s = gg::as_stream(stream);
+    const int64_t n = cg->n;
+    const int nb = gg::vec_blocks(n);
+    if (cg->xdefer == 2) {
+      hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
+                         gg::kron_side_half(cg->K, n), cg->sc);
+      GG_LAUNCH_CHECK();
+    } else if (cg->xdefer == 1) {
+      hipLaunchKernelGGL(gg::cg_x_flush_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
+                         cg->sc);
+      GG_LAUNCH_CHECK();
+    }
+    if (cg->xdefer) {
+      hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+      GG_LAUNCH_CHECK();
+    }
+    // the pending r update (x: the x_defer bookkeeping above, or here)
+    GG_HIP(hipMemsetAsync(cg->partials, 0, nb * sizeof(double), s));
+    hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                       cg->xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                       cg->partials, 1);
+    GG_LAUNCH_CHECK();
+    gg::launch_reduce_to(cg->partials, nb, rr_dev, s);
+  });
+}
+
+int gg_cg_close_finish(gg_cg* cg, const double* rr_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && rr_dev, GG_ERR_VALUE, "NULL argument");
+    hipLaunchKernelGGL(gg::cg_close_rho_kernel, dim3(1), dim3(1), 0, gg::as_stream(stream),
+                       cg->sc, rr_dev);
+    GG_LAUNCH_CHECK();
   });
 }
 

@@ -492,3 +492,268 @@ class DistKronCG(object):
                 break
         it, done, rho, tol = self.status()
         return self.x, (0 if done and np.sqrt(max(rho, 0.0)) < tol else it)
+
+
+# ------------------------------------------------------------ parity sharding
+# A centrosymmetric factor F (J F J = F, J the index reversal; every
+# stationary kernel on an evenly spaced grid) of even order m = 2h is
+# block-diagonal in the even / odd basis: with u_i = (x_i + x_{m-1-i}) / sqrt 2
+# and v_i = (x_i - x_{m-1-i}) / sqrt 2 (an orthogonal change of basis P),
+# P F P^T = diag(S, T), S[j, i] = F[j, i] + F[j, m-1-i], T[j, i] = F[j, i] -
+# F[j, m-1-i] (i, j < h; both symmetric when F is).  Taking the grid vector to
+# that basis along factors 0..K-1 makes K = F_0 x ... x F_{d-1} block-diagonal
+# with 2^K blocks X_0 x ... x X_{K-1} x F_K x ... x F_{d-1}, X_k in {S_k, T_k}:
+# with one block per rank (G = 2^K), the matvec needs no exchange at all and
+# the CG's dot products are the only collective -- ONE all-reduce of five
+# doubles per iteration (the north star's "single RCCL all-reduce for the CG
+# dot product").  P is orthogonal, so the CG on the transformed system takes
+# the same iterates (x~ = P x) up to rounding; the per-iteration work is the
+# single-GPU fused CG's (the folded kernel applies S and T to u and v; here the
+# folding of factors 0..K-1 happens once, in the right-hand side and the
+# solution).
+
+def centro_split(F, rtol=16.0):
+    """(S, T) of a square, even-order, centrosymmetric factor; None when F is
+    not one (max |F - J F J| > rtol eps max |F|, the test gg_kron_create
+    applies before folding)."""
+    F = np.asarray(F, dtype=np.float64)
+    if F.ndim != 2 or F.shape[0] != F.shape[1] or F.shape[0] % 2:
+        return None
+    m = F.shape[0]
+    scale = float(np.abs(F).max()) if F.size else 0.0
+    if np.abs(F - F[::-1, ::-1]).max() > rtol * np.finfo(np.float64).eps * max(scale, 1e-300):
+        return None
+    C = 0.5 * (F + F[::-1, ::-1])      # the centrosymmetric part
+    h = m // 2
+    A, B = C[:h, :h], C[:h, m - 1:h - 1:-1]   # B[j, i] = C[j, m-1-i]
+    return np.ascontiguousarray(A + B), np.ascontiguousarray(A - B)
+
+
+def parity_ok(factors, world):
+    """world = 2^K with K <= d and factors 0..K-1 centrosymmetric of even order."""
+    world = int(world)
+    if world < 1 or world & (world - 1):
+        return False
+    K = world.bit_length() - 1
+    if K > len(factors):
+        return False
+    return all(centro_split(factors[k]) is not None for k in range(K))
+
+
+def parity_local_factors(factors, world, rank):
+    """Rank g's block: X_k = S_k (bit k of g clear, bit 0 = the most
+    significant of K) or T_k for k < K, F_k beyond."""
+    K = int(world).bit_length() - 1
+    out = []
+    for k, F in enumerate(factors):
+        if k < K:
+            S, T = centro_split(F)
+            out.append(T if (int(rank) >> (K - 1 - k)) & 1 else S)
+        else:
+            out.append(np.ascontiguousarray(np.asarray(F, dtype=np.float64)))
+    return out
+
+
+def _parity_transform(X, K, inverse=False):
+    """Apply (or undo) the even / odd basis change along axes 0..K-1 of the
+    d-dimensional array X (host)."""
+    r2 = np.sqrt(0.5)
+    for k in range(K):
+        X = np.moveaxis(X, k, 0)
+        m = X.shape[0]
+        h = m // 2
+        if not inverse:
+            lo, hi = X[:h], X[m - 1:h - 1:-1]
+            X = np.concatenate([(lo + hi) * r2, (lo - hi) * r2], axis=0)
+        else:
+            u, v = X[:h], X[h:]
+            lo, hi = (u + v) * r2, (u - v) * r2
+            X = np.concatenate([lo, hi[::-1]], axis=0)
+        X = np.moveaxis(X, 0, k)
+    return X
+
+
+def parity_fold(vec, m, world):
+    """Host: the global vector (C order over factors of sizes m) -> every
+    rank's local block in the even / odd basis (flattened, C order over the
+    local factor sizes)."""
+    m = [int(v) for v in m]
+    K = int(world).bit_length() - 1
+    X = _parity_transform(np.asarray(vec, dtype=np.float64).reshape(m), K)
+    out = []
+    for g in range(int(world)):
+        sl = tuple(slice(((g >> (K - 1 - k)) & 1) * (m[k] // 2),
+                         (((g >> (K - 1 - k)) & 1) + 1) * (m[k] // 2)) if k < K else slice(None)
+                   for k in range(len(m)))
+        out.append(np.ascontiguousarray(X[sl]).reshape(-1))
+    return out
+
+
+def parity_unfold(locals_, m):
+    """Host: every rank's local block -> the global vector."""
+    m = [int(v) for v in m]
+    world = len(locals_)
+    K = world.bit_length() - 1
+    X = np.empty(m)
+    lshape = [m[k] // 2 if k < K else m[k] for k in range(len(m))]
+    for g, loc in enumerate(locals_):
+        sl = tuple(slice(((g >> (K - 1 - k)) & 1) * (m[k] // 2),
+                         (((g >> (K - 1 - k)) & 1) + 1) * (m[k] // 2)) if k < K else slice(None)
+                   for k in range(len(m)))
+        X[sl] = np.asarray(loc).reshape(lshape)
+    return _parity_transform(X, K, inverse=True).reshape(-1)
+
+
+class ParityHipEngine(object):
+    """This rank's block of the parity-sharded operator as a resident fused CG
+    (linalg.KronCG on the local factors) driven through the C ABI's
+    gg_cg_*_partial / _finish split."""
+
+    def __init__(self, factors, world, rank, shift):
+        from . import linalg, tensors
+        self.local_factors = parity_local_factors(factors, world, rank)
+        self.K = tensors.KronMatrix(self.local_factors)
+        self.cg = linalg.KronCG(self.K, shift, recurrence="fused")
+        if self.cg.recurrence != "fused" or self.cg.fusion != 0:
+            raise ValueError("the parity-sharded rank needs the fused recurrence (layout 0)")
+        self.n_local = int(self.cg.n)
+        self.red5 = dev.zeros(5)
+        self.red1 = dev.zeros(1)
+
+    def empty(self):
+        return dev.empty(self.n_local)
+
+    def zeros(self):
+        return dev.zeros(self.n_local)
+
+    def apply(self, x, y):
+        self.K._device().matvec(x, out=y)
+
+    def _c(self, name, *args):
+        native.check(getattr(native.lib(), name)(self.cg.h, *args, native.stream_ptr()), name)
+
+    def start_partial(self, b, x):
+        self._c("gg_cg_start_partial", native.dptr(b), native.dptr(x), native.dptr(self.red1))
+        return self.red1
+
+    def start_finish(self, rtol, atol):
+        self._c("gg_cg_start_finish", native.dptr(self.red1), float(rtol), float(atol))
+
+    def iterate_partial(self):
+        self._c("gg_cg_iterate_partial", native.dptr(self.red5))
+        return self.red5
+
+    def iterate_finish(self):
+        self._c("gg_cg_iterate_finish", native.dptr(self.red5))
+
+    def close_partial(self):
+        self._c("gg_cg_close_partial", native.dptr(self.red1))
+        return self.red1
+
+    def close_finish(self):
+        self._c("gg_cg_close_finish", native.dptr(self.red1))
+
+    def status(self):
+        return self.cg.status()
+
+    def profile(self, enable):
+        self.cg.profile(enable)
+
+    def profile_read(self):
+        return self.cg.profile_read()
+
+
+class ParityShardCG(object):
+    """CG on (K + shift I) x = b with K's factors 0..K-1 parity-sharded over
+    2^K ranks (module notes above): no exchange in the matvec, one all-reduce
+    of five doubles per iteration (+ one scalar each at start and when
+    leaving iterate()).  Vectors are this rank's block in the even / odd
+    basis (parity_fold / parity_unfold; bench.py builds it on the device).
+    engine: ParityHipEngine (default) or a test engine with its methods."""
+
+    def __init__(self, factors, world, rank, exchange, shift, engine=None):
+        if not parity_ok(factors, world):
+            raise ValueError("parity sharding needs 2^K ranks and factors 0..K-1 "
+                             "centrosymmetric of even order")
+        self.world, self.rank = int(world), int(rank)
+        self.x_ex = exchange
+        self.shift = float(shift)
+        self.e = engine if engine is not None else ParityHipEngine(factors, world, rank, shift)
+        self.n_local = self.e.n_local
+        self.x = None
+        self._prof = None
+        self.mode = "parity"
+        self.recurrence = "fused"
+
+    # per-phase timing on the compute stream (as DistKronCG.profile)
+    def profile(self, enable, iterations=64):
+        self._prof = [] if enable else None
+        self.e.profile(enable)
+        if enable:
+            import torch
+            pool = getattr(self, "_ev_pool", [])
+            while len(pool) < 4 * max(1, int(iterations)) + 1:
+                pool.append(torch.cuda.Event(enable_timing=True))
+            self._ev_pool = pool
+
+    def _mark(self, name):
+        if self._prof is not None:
+            import torch
+            k = len(self._prof)
+            if k < len(self._ev_pool):
+                e = self._ev_pool[k]
+            else:
+                e = torch.cuda.Event(enable_timing=True)
+                self._ev_pool.append(e)
+            e.record()
+            self._prof.append((name, e))
+
+    def profile_read(self):
+        import torch
+        torch.cuda.synchronize()
+        out = {}
+        ev = self._prof or []
+        for (_, e0), (n1, e1) in zip(ev[:-1], ev[1:]):
+            if n1 == "start":
+                continue
+            out[n1] = out.get(n1, 0.0) + e0.elapsed_time(e1)
+        return out
+
+    def apply(self, x, y):
+        """y = (this rank's block of K) x (no shift)."""
+        self.e.apply(x, y)
+
+    def start(self, b, rtol=1e-5, atol=0.0, x_out=None):
+        self.x = self.e.zeros() if x_out is None else x_out
+        self.x_ex.all_reduce(self.e.start_partial(b, self.x))
+        self.e.start_finish(rtol, atol)
+
+    def iterate(self, n_iter):
+        for _ in range(int(n_iter)):
+            self._mark("start")
+            red = self.e.iterate_partial()
+            self._mark("launches")
+            self.x_ex.all_reduce(red)
+            self._mark("allreduce")
+            self.e.iterate_finish()
+            self._mark("scalars")
+        self.x_ex.all_reduce(self.e.close_partial())
+        self.e.close_finish()
+
+    def status(self):
+        """(iterations, converged, residual norm, tolerance) -- gg_cg_status."""
+        return self.e.status()
+
+    def solve(self, b, rtol=1e-5, atol=0.0, maxiter=None, check_every=20):
+        self.start(b, rtol, atol)
+        maxiter = 10 * self.n_local * self.world if maxiter is None else maxiter
+        done_iters = 0
+        while done_iters < maxiter:
+            k = min(check_every, maxiter - done_iters)
+            self.iterate(k)
+            done_iters += k
+            it, conv, res, tol = self.status()
+            if conv or not np.isfinite(res):
+                break
+        it, conv, res, tol = self.status()
+        return self.x, (0 if conv else it)

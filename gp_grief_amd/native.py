@@ -66,6 +66,12 @@ SIGNATURES = {
     "gg_cg_get_xdefer": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_rq": [_vp, ctypes.c_int],
     "gg_cg_get_rq": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_start_partial": [_vp, _c_dp, _c_dp, _c_dp, _vp],
+    "gg_cg_start_finish": [_vp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
+    "gg_cg_iterate_partial": [_vp, _c_dp, _vp],
+    "gg_cg_iterate_finish": [_vp, _c_dp, _vp],
+    "gg_cg_close_partial": [_vp, _c_dp, _vp],
+    "gg_cg_close_finish": [_vp, _c_dp, _vp],
     "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
     "gg_cg_profile": [_vp, ctypes.c_int],

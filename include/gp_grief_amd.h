@@ -151,6 +151,29 @@ int gg_cg_get_rq(const gg_cg* cg, int* mode);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
+/* A rank of a sharded CG whose operator is block-diagonal across ranks (the
+ * parity sharding of gp_grief_amd/distributed.py: this handle's operator is
+ * the rank's block, (K + shift I) restricted to it), every dot product
+ * summed over ranks by the caller -- ONE all-reduce per iteration.
+ * start_partial: r = b, x = 0, local r.r into rr_dev[0]; the caller
+ * all-reduces rr_dev; start_finish: tolerances from the global norm.
+ * iterate_partial: one fused iteration (layout 0: prologue, x side job,
+ * epilogue on the mode products, as gg_cg_iterate) writing the local sums
+ * red_dev[5] = [r.r, p.q_old, p.q, r.q, q.q]; the caller all-reduces red_dev;
+ * iterate_finish: the scalar step (cg_fused_scalars on the global sums).  A
+ * cancelled beta restarts with p = r (no repair pass: it would need a second
+ * all-reduce).  close_partial: the deferred x steps and the pending r update,
+ * local r.r into rr_dev; after the all-reduce, close_finish -- the textbook
+ * state.  Reference: scipy's cg recurrence on kron_matrix.py:52-97's
+ * operator (e); no reference counterpart for sharding. */
+int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* rr_dev,
+                        gg_stream stream);
+int gg_cg_start_finish(gg_cg* cg, const double* rr_dev, double rtol, double atol,
+                       gg_stream stream);
+int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream);
+int gg_cg_iterate_finish(gg_cg* cg, const double* red_dev, gg_stream stream);
+int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream);
+int gg_cg_close_finish(gg_cg* cg, const double* rr_dev, gg_stream stream);
 /* Live timing: while enabled, every gg_cg_iterate matvec records HIP events
  * around each of its d mode products on the CG stream.  profile_read
  * (synchronising) returns the number of profiled matvecs and, per mode

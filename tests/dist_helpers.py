@@ -281,3 +281,107 @@ def reference_factors(m, d, seed=0):
 def make_factors(m, d):
     """bench.py's GG_BENCH_ENGINE hook: the factors of the CPU rehearsal."""
     return reference_factors(m, d)
+
+
+class ParityNumpyEngine(object):
+    """distributed.ParityHipEngine restated with NumPy on torch CPU tensors:
+    this rank's block of the parity-sharded operator (oracle.kron_matvec on
+    the local factors) and the fused CG recurrence split at its one
+    reduction (gg_cg_iterate_partial / _finish: r -= alpha q_old and r.r,
+    p = r + beta p and p.q_old, q = A p + s p with p.q and q.q; the scalars
+    from the global sums with beta from the |r - alpha q|^2 expansion and
+    r.q from the conjugacy identity; a cancelled beta restarts with p = r).
+    x is updated one step late (no deferred pairs)."""
+
+    def __init__(self, factors, world, rank, shift):
+        from gp_grief_amd.distributed import parity_local_factors
+        self.F = parity_local_factors(factors, world, rank)
+        self.shift = float(shift)
+        self.n_local = int(np.prod([f.shape[0] for f in self.F]))
+        self.red5 = torch.zeros(5, dtype=torch.float64)
+        self.red1 = torch.zeros(1, dtype=torch.float64)
+        self.sc = {}
+
+    def empty(self):
+        return torch.empty(self.n_local, dtype=torch.float64)
+
+    def zeros(self):
+        return torch.zeros(self.n_local, dtype=torch.float64)
+
+    def apply(self, x, y):
+        y.numpy()[:] = oracle.kron_matvec(self.F, x.numpy())
+
+    def _A(self, v):
+        return oracle.kron_matvec(self.F, v) + self.shift * v
+
+    def start_partial(self, b, x):
+        self.x = x
+        self.r = b.numpy().copy()
+        x.numpy()[:] = 0.0
+        self.p = np.zeros(self.n_local)
+        self.q = np.zeros(self.n_local)
+        self.red1[0] = float(self.r @ self.r)
+        return self.red1
+
+    def start_finish(self, rtol, atol):
+        s = float(self.red1[0])
+        tol = max(atol, rtol * np.sqrt(s))
+        self.sc = dict(rho=s, tol=tol, iters=0, pending=False, alpha=0.0, beta=0.0,
+                       done=(s == 0.0 or not np.sqrt(s) >= tol))
+
+    def iterate_partial(self):
+        sc = self.sc
+        if sc["done"]:
+            return self.red5
+        if sc["pending"]:
+            self.x.numpy()[:] += sc["alpha"] * self.p
+            self.r -= sc["alpha"] * self.q
+        pn = self.r + sc["beta"] * self.p
+        pqo = float(pn @ self.q)
+        qn = self._A(pn)
+        self.red5[:] = torch.tensor([float(self.r @ self.r), pqo, float(pn @ qn), 0.0,
+                                     float(qn @ qn)], dtype=torch.float64)
+        self.p, self.q = pn, qn
+        return self.red5
+
+    def iterate_finish(self):
+        sc = self.sc
+        if sc["done"]:
+            return
+        rr, pqo, pq, _, qq = [float(v) for v in self.red5]
+        if sc["pending"]:
+            sc.update(rho=rr, iters=sc["iters"] + 1)
+            if not np.sqrt(rr) >= sc["tol"]:
+                sc.update(done=True, pending=False)
+                return
+        rho = sc["rho"]
+        alpha = rho / pq
+        rq = pq - sc["beta"] * pqo
+        rt = rho - 2.0 * alpha * rq + alpha * alpha * qq
+        sc.update(alpha=alpha, beta=0.0 if rt < 1e-6 * rho else rt / rho, pending=True)
+
+    def close_partial(self):
+        sc = self.sc
+        self.red1[0] = 0.0
+        if sc["pending"] and not sc["done"]:
+            self.x.numpy()[:] += sc["alpha"] * self.p
+            self.r -= sc["alpha"] * self.q
+            self.red1[0] = float(self.r @ self.r)
+        return self.red1
+
+    def close_finish(self):
+        sc = self.sc
+        if sc["done"] or not sc["pending"]:
+            return
+        s = float(self.red1[0])
+        sc.update(beta=s / sc["rho"], rho=s, iters=sc["iters"] + 1, pending=False)
+        if not np.sqrt(s) >= sc["tol"]:
+            sc["done"] = True
+
+    def status(self):
+        sc = self.sc
+        res = np.sqrt(max(sc["rho"], 0.0))
+        return sc["iters"], bool(sc["done"] and res < sc["tol"]), res, sc["tol"]
+
+    def profile(self, enable):
+        pass

@@ -195,3 +195,44 @@ def test_push_exchange_over_ipc_processes(gpu, tmp_path, monkeypatch, world, m, 
                                    rtol=1e-10)
     assert all(int(r["info"]) == 0 for r in res)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+
+
+@pytest.mark.parametrize("world,m,d,shift", [(2, 16, 4, 0.05), (4, 16, 4, 0.05),
+                                             (8, 16, 4, 0.05), (8, 24, 3, 0.05),
+                                             (4, 32, 4, 1.0), (2, 200, 2, 0.05)])
+def test_parity_sharded_cg_virtual_ranks(gpu, world, m, d, shift):
+    """The parity-sharded CG (ParityShardCG on ParityHipEngine: each rank's
+    even / odd block as a resident fused CG split at its one all-reduce,
+    gg_cg_*_partial / _finish) on virtual ranks: the blocks' matvecs unfold to
+    the oracle's K x, the solution to the oracle CG's (iterations within 2 %,
+    x to 1e-8)."""
+    import torch
+    from gp_grief_amd.distributed import ParityShardCG, parity_fold, parity_unfold
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(9).standard_normal(m ** d)
+    ex = ThreadExchange(world)
+    cgs = [ParityShardCG(F, world, g, ex, shift) for g in range(world)]
+    bl = parity_fold(xg, [m] * d, world)
+
+    def body(g):
+        ex.bind(g)
+        cg = cgs[g]
+        b = torch.from_numpy(bl[g].copy()).cuda()
+        y = cg.e.empty()
+        cg.apply(b, y)
+        x, info = cg.solve(b, rtol=1e-10, maxiter=4000, check_every=9)
+        torch.cuda.synchronize()
+        return y.cpu().numpy(), x.cpu().numpy(), info, cg.status()[0]
+
+    res = run_threads(world, body)
+    y = parity_unfold([r[0] for r in res], [m] * d)
+    ref = oracle.kron_matvec(F, xg)
+    assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < 1e-12
+    x = parity_unfold([r[1] for r in res], [m] * d)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, xg,
+                                   rtol=1e-10)
+    assert all(r[2] == 0 for r in res)
+    assert len({r[3] for r in res}) == 1
+    slack = 0.05 if m == 200 else 0.02
+    assert abs(res[0][3] - it) <= max(2, slack * it)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
