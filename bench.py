@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--recurrence", default="fused", choices=["fused", "textbook"])
+    # multi-GPU decomposition: parity blocks (no exchange) where the factors
+    # allow it, else factor 0 sharded with two exchanges per matvec
+    ap.add_argument("--shard", default="auto", choices=["auto", "parity", "transpose"])
     ap.add_argument("--lanczos", type=int, default=30,
                     help="also time this many device Lanczos steps (one probe; 0 = off; "
                          "single GPU only)")
@@ -157,6 +160,44 @@ def local_rhs(m, d, world, rank, torch, dev):
     return y
 
 
+def parity_local_rhs(m, d, world, rank, torch, dev):
+    """This rank's block of the same right-hand side in the even / odd basis
+    of factors 0..K-1 (G = 2^K; distributed.parity_fold, on the device): local
+    index = C order over (h, ..., h, m, ..., m), h = m / 2, and b~ = 2^(-K/2)
+    sum over the 2^K mirror choices s of sign(s) y[g(s)] -- axis k takes
+    digit i (s_k = 0) or m - 1 - i (s_k = 1, sign -1 when bit k of the rank,
+    counted from the most significant, is set)."""
+    K = world.bit_length() - 1
+    h = m // 2
+    sizes = [h] * K + [m] * (d - K)
+    nl = int(np.prod(sizes))
+    y = torch.empty(nl, dtype=torch.float64, device=dev)
+    chunk = 1 << 24
+    scale = 2.0 ** (-0.5 * K)
+    for i in range(0, nl, chunk):
+        k = min(chunk, nl - i)
+        rest = torch.arange(i, i + k, dtype=torch.int64, device=dev)
+        digits = [None] * d
+        for ax in range(d - 1, -1, -1):
+            digits[ax] = torch.remainder(rest, sizes[ax])
+            rest = torch.div(rest, sizes[ax], rounding_mode="floor")
+        acc = torch.zeros(k, dtype=torch.float64, device=dev)
+        for sgn_bits in range(1 << K):
+            g = torch.zeros(k, dtype=torch.int64, device=dev)
+            sign = 1.0
+            for ax in range(d):
+                if ax < K and (sgn_bits >> (K - 1 - ax)) & 1:
+                    idx = (m - 1) - digits[ax]
+                    if (rank >> (K - 1 - ax)) & 1:
+                        sign = -sign
+                else:
+                    idx = digits[ax]
+                g = g * m + idx
+            acc += sign * rhs_at(g, m, d, torch)
+        y[i:i + k] = acc * scale
+    return y
+
+
 # ---------------------------------------------------------------- sharded
 def _engine_factory():
     """HipEngine, or (tests only) GG_BENCH_ENGINE=module:Class, whose module
@@ -178,6 +219,12 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     m, d, s = a.grid, a.dims, a.sigma2
     Engine, make_factors = _engine_factory()
     F = make_factors(m, d) if make_factors is not None else grid_factors(m, d)[1]
+    shard = os.environ.get("GG_DIST_SHARD", a.shard)
+    from gp_grief_amd.distributed import parity_ok
+    if shard in ("auto", "parity") and parity_ok(F, world):
+        return run_parity(a, world, rank, torch, dev, dist, on_gpu, F)
+    if shard == "parity":
+        raise SystemExit("bench.py: parity sharding needs 2^K GPUs and centrosymmetric factors")
     eng = Engine(F, world, rank)
     y = local_rhs(m, d, world, rank, torch, dev)
     ex = TorchExchange()
@@ -275,6 +322,89 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         res["local_roofline"] = sharded_roofline(phases, n, m, d, world,
                                                  getattr(eng, "fold_mask", 0))
     return res
+
+
+def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
+    """Strong scaling by parity sharding (distributed.ParityShardCG): rank g
+    owns one block of the operator in the even / odd basis of factors
+    0..K-1 -- no exchange, one all-reduce of five doubles per iteration."""
+    from gp_grief_amd.distributed import ParityShardCG, TorchExchange
+    m, d, s = a.grid, a.dims, a.sigma2
+    ex = TorchExchange()
+    spec = os.environ.get("GG_BENCH_PARITY_ENGINE")   # tests: module:Class
+    eng = None
+    if spec:
+        import importlib
+        mod_name, cls_name = spec.split(":")
+        eng = getattr(importlib.import_module(mod_name), cls_name)(F, world, rank, s)
+    cg = ParityShardCG(F, world, rank, ex, s, engine=eng)
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    if on_gpu:
+        y = parity_local_rhs(m, d, world, rank, torch, dev)
+    else:
+        from gp_grief_amd.distributed import parity_fold
+        yg = rhs_at(torch.arange(m ** d, dtype=torch.int64), m, d, torch).numpy()
+        y = torch.from_numpy(parity_fold(yg, [m] * d, world)[rank].copy())
+    cg.start(y, rtol=0.0, atol=0.0)
+    cg.iterate(a.warmup)
+    sync()
+    dist.barrier()
+    sync()
+    if on_gpu:
+        cg.profile(True, a.steps)
+    t0 = time.perf_counter()
+    cg.iterate(a.steps)
+    sync()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    it, conv, res, tol = cg.status()
+    assert it == a.warmup + a.steps and np.isfinite(res), (it, res)
+    n = m ** d
+    K = world.bit_length() - 1
+    res_ = {
+        "metric": METRIC,
+        "value": a.steps / dt,
+        "unit": "CG iters/s",
+        "n_gpus": dist.get_world_size(),
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1e3 * dt / a.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d, "
+                               "parity-sharded over %d GPUs" % (m, d, s, n, world),
+                   "grid": m, "dims": d, "sigma2": s, "n": n,
+                   "exchange": "none",
+                   "cg_recurrence": "fused",
+                   "local_factor_orders": [f.shape[0] for f in cg.e.local_factors]
+                   if hasattr(cg.e, "local_factors") else None,
+                   "parallelism": ("parity-shard factors 0..%d over %d GPUs: the operator is "
+                                   "block-diagonal in their even / odd basis, each rank owns "
+                                   "one block; no exchange, one 5-double all-reduce per "
+                                   "iteration (RCCL)" % (K - 1, world))},
+    }
+    if on_gpu:
+        ph = cg.profile_read()
+        nm, per = cg.e.profile_read()
+        cg.profile(False)
+        keys = sorted(ph)
+        v = torch.tensor([ph[k] / a.steps for k in keys] + [x / max(nm, 1) for x in per],
+                         dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        vals = [float(u) for u in v.tolist()]
+        res_["phase_ms_per_iteration"] = dict(zip(keys, vals[:len(keys)]))
+        res_["local_launch_ms"] = vals[len(keys):]
+        nl = n / world
+        res_["local_passes_per_iteration"] = 15
+        res_["local_gbs"] = 15 * 8.0 * nl / (res_["phase_ms_per_iteration"].get("launches", 0)
+                                             * 1e-3 or 1) / 1e9
+    return res_
 
 
 def sharded_roofline(phases, n, m, d, world, fold_mask):

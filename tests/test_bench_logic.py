@@ -8,6 +8,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
+import numpy as np  # noqa: E402
+import pytest  # noqa: E402
 
 
 def test_launch_passes_fused_layout0_d4():
@@ -97,3 +99,16 @@ def test_cpu_share_reports_its_limit():
     assert threads >= 1 and share["limited_by"] in ("affinity_mask", "cgroup_cpu_quota",
                                                     "OMP_NUM_THREADS")
     assert threads <= share["affinity_cpus"]
+
+
+@pytest.mark.parametrize("world,m,d", [(2, 8, 3), (4, 6, 3), (8, 4, 4)])
+def test_parity_local_rhs_matches_host_fold(world, m, d):
+    """bench.parity_local_rhs (device formula of every rank's even / odd block
+    of the right-hand side) equals distributed.parity_fold of the global one."""
+    import torch
+    from gp_grief_amd.distributed import parity_fold
+    yg = bench.rhs_at(torch.arange(m ** d, dtype=torch.int64), m, d, torch).numpy()
+    ref = parity_fold(yg, [m] * d, world)
+    for g in range(world):
+        loc = bench.parity_local_rhs(m, d, world, g, torch, torch.device("cpu")).numpy()
+        assert np.abs(loc - ref[g]).max() < 1e-13 * np.abs(yg).max()
