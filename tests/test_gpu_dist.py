@@ -240,3 +240,48 @@ def test_parity_sharded_cg_virtual_ranks(gpu, world, m, d, shift):
     slack = 0.07 if m == 200 else 0.02
     assert abs(res[0][3] - it) <= max(2, slack * it)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+
+
+def _parity_worker(rank, world, port, m, d, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from dist_helpers import bind_device, reference_factors
+    bind_device(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from gp_grief_amd.distributed import ParityShardCG, TorchExchange, parity_fold
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(13).standard_normal(m ** d)
+    cg = ParityShardCG(F, world, rank, TorchExchange(), 0.05)
+    b = torch.from_numpy(parity_fold(xg, [m] * d, world)[rank].copy()).cuda()
+    x, info = cg.solve(b, rtol=1e-10, maxiter=3000, check_every=11)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), x=x.cpu().numpy(), info=info,
+             iters=cg.status()[0])
+    dist.barrier()
+    del cg
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,m,d", [(2, 16, 3), (4, 12, 3)])
+def test_parity_sharded_cg_processes(gpu, tmp_path, world, m, d):
+    """One process per rank (rank g on device g % count), the five-double
+    all-reduce through TorchExchange (gloo here; RCCL on a multi-GPU node)."""
+    import torch.multiprocessing as mp
+    from gp_grief_amd.distributed import parity_unfold
+    port = _free_port()
+    mp.start_processes(_parity_worker, args=(world, port, m, d, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(world)]
+    F = reference_factors(m, d)
+    xg = np.random.default_rng(13).standard_normal(m ** d)
+    x = parity_unfold([r["x"] for r in res], [m] * d)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + 0.05 * v, xg,
+                                   rtol=1e-10)
+    assert all(int(r["info"]) == 0 for r in res)
+    assert len({int(r["iters"]) for r in res}) == 1
+    assert abs(int(res[0]["iters"]) - it) <= max(2, 0.02 * it)
+    assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
