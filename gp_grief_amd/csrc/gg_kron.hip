@@ -1053,6 +1053,8 @@ static bool ring_side_env() {
   return e && atoi(e) == 1;
 }
 
+int64_t kron_side_half(const gg_kron* K, int64_t n);
+
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
                 double* work, double* dot_partials, const int* skip, hipStream_t stream,
                 int64_t* n_partials_out, const MpFuse* cg, int cgp, hipEvent_t* ev) {
@@ -1082,6 +1084,10 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   int64_t size = n_in;
   const double* src = x;
   int64_t np_total = 0;
+  // the x side job as a concurrent kernel on the CG's side stream (balanced
+  // x_defer, d >= 3): mode products 1..d-2 run plain (the ring kernel)
+  const bool side_async = cgp == 2 && cg->side_stream != nullptr && cg->sx != nullptr &&
+                          cg->xdefer == 2 && d >= 3 && cg->sc != nullptr;
   if (ev) GG_HIP(hipEventRecord(ev[0], stream));
   for (int k = 0; k < d; ++k) {
     const Factor& f = fs[k];
@@ -1117,7 +1123,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // the x side job rides on the second mode product; with d >= 4 the
         // third (also a plain, MFMA-bound one) takes the second half of x
         const bool split_side = cgp == 2 && d >= 4 && cg->sx != nullptr;
-        const bool side = cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
+        const bool side = !side_async && cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
                           (k == 1 || (split_side && k == 2));
         const int epi_kind = !epi ? 0 : cg->ep_out == nullptr ? 3 : cg->ex != nullptr ? 5 : 6;
         const int kind = epi ? epi_kind : side ? 4 : pro;
@@ -1146,13 +1152,12 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
               rv > 0 && xs_ == nullptr && f.rfrag != nullptr && M % 2 == 0 && M >= 2 &&
               ((reinterpret_cast<uintptr_t>(step_src) | reinterpret_cast<uintptr_t>(dst)) & 15) ==
                   0;
-          if (ring_ok && kind == 0 && skip == nullptr) {
+          if (ring_ok && kind == 0 && (skip == nullptr || side_async)) {
             const RingConfig rc = select_ring(f.fJT, f.fTT, rv);
             const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
             const int grid = ring_grid(rc, cu_count(), nb);
             hipLaunchKernelGGL(rc.fn, dim3((unsigned)grid), dim3(64 * rc.waves), rc.lds, stream,
-                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb, nullptr,
-                               MpFuse());
+                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb, skip, MpFuse());
             GG_LAUNCH_CHECK();
             continue;
           }
@@ -1288,6 +1293,15 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
       }
     }
     (void)out_size;
+    if (side_async && k == 0) {
+      // after the prologue (which read the x_defer state the previous scalars
+      // wrote): half sc->xh of the active pair, beside mode products 1..d-2
+      GG_HIP(hipEventRecord(cg->side_ev[0], stream));
+      GG_HIP(hipStreamWaitEvent(cg->side_stream, cg->side_ev[0], 0));
+      launch_x_half(cg->sx, cg->sn, kron_side_half(K, cg->sn), cg->sc, cg->side_stream);
+      GG_HIP(hipEventRecord(cg->side_ev[1], cg->side_stream));
+    }
+    if (side_async && k == d - 1) GG_HIP(hipStreamWaitEvent(stream, cg->side_ev[1], 0));
     if (ev) GG_HIP(hipEventRecord(ev[k + 1], stream));
     size = out_size;
     src = dst;

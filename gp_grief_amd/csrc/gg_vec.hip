@@ -205,6 +205,58 @@ __global__ __launch_bounds__(kVecThreads) void cg_x_flush_kernel(double* __restr
     x[i] += c0 * p0[i] + c1 * p1[i];
 }
 
+// x_defer mode 2 on its own stream: half sc->xh of the active pair, x += c0
+// p0 + c1 p1 over [0, H) or [H, n) -- no state change (the scalars kernel
+// advances xh).  One 256-thread workgroup per CU, few registers, no LDS: it
+// fits beside a ring mode product's workgroup (2 waves / SIMD at 226 VGPRs,
+// 131 KB of LDS) and streams while that one computes.  Non-temporal: every
+// element is touched once per iteration.
+__global__ __launch_bounds__(256) void cg_x_half_kernel(double* __restrict__ x, int64_t n,
+                                                        int64_t H,
+                                                        const CgScalars* __restrict__ sc) {
+  if (sc->done) return;
+  const int h = sc->xh;
+  if (h >= 2) return;
+  const int64_t lo = h ? H : 0, hi = h ? n : H;
+  const double c0 = sc->xc[0], c1 = sc->xc[1];
+  const double* __restrict__ p0 = sc->xp[0];
+  const double* __restrict__ p1 = sc->xp[1];
+  typedef double v2 __attribute__((ext_vector_type(2)));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 2;
+  int64_t i = lo + 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  constexpr int kU = 2;
+  for (; i + (kU - 1) * stride + 1 < hi; i += kU * stride) {
+    v2 xv[kU], a[kU], b[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      xv[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(x + i + u * stride));
+      a[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p0 + i + u * stride));
+      b[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p1 + i + u * stride));
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      xv[u] += c0 * a[u] + c1 * b[u];
+      __builtin_nontemporal_store(xv[u], reinterpret_cast<v2*>(x + i + u * stride));
+    }
+  }
+  for (; i < hi; i += stride) {
+    x[i] += c0 * p0[i] + c1 * p1[i];
+    if (i + 1 < hi) x[i + 1] += c0 * p0[i + 1] + c1 * p1[i + 1];
+  }
+}
+
+void launch_x_half(double* x, int64_t n, int64_t H, const CgScalars* sc, hipStream_t s) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    GG_HIP(hipGetDevice(&dev));
+    GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  hipLaunchKernelGGL(cg_x_half_kernel, dim3((unsigned)std::max(cus, 1)), dim3(256), 0, s, x, n,
+                     H, sc);
+  GG_LAUNCH_CHECK();
+}
+
 // x_defer mode 2: x += xsc xsp (the waiting single step) + the active pair
 // on the halves not yet applied (half 0 = [0, H), half 1 = [H, n))
 __global__ __launch_bounds__(kVecThreads) void cg_x_flush2_kernel(double* __restrict__ x,
@@ -635,6 +687,9 @@ struct gg_cg {
   // rank of a sharded CG (gg_cg_*_partial / _finish): an iteration's local
   // sums await the caller's all-reduce (the p_new of that iteration)
   bool await_finish = false;
+  // the x side job's own stream and its two ordering events (MpFuse)
+  hipStream_t side_stream = nullptr;
+  hipEvent_t side_ev[2] = {nullptr, nullptr};
   // live timing of the mode products (gg_cg_profile): d + 1 events per
   // profiled iteration, recorded on the CG stream, read back on demand
   bool profiling = false;
@@ -815,6 +870,12 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
       GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
+      // the concurrent x side job (GG_CG_SIDE_ASYNC=0: in the mode products)
+      const char* sa = getenv("GG_CG_SIDE_ASYNC");
+      if (cg->fused && !(sa && atoi(sa) == 0)) {
+        GG_HIP(hipStreamCreateWithFlags(&cg->side_stream, hipStreamNonBlocking));
+        for (hipEvent_t& e : cg->side_ev) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      }
     } catch (...) {
       gg_cg_destroy(cg);
       throw;
@@ -831,6 +892,9 @@ int gg_cg_destroy(gg_cg* cg) {
     if (cg->sc) (void)hipFree(cg->sc);
     if (cg->sc_host) (void)hipHostFree(cg->sc_host);
     for (hipEvent_t e : cg->events) (void)hipEventDestroy(e);
+    for (hipEvent_t e : cg->side_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (cg->side_stream) (void)hipStreamDestroy(cg->side_stream);
     delete cg;
   });
 }
@@ -1016,6 +1080,11 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         fz.sn = n;
         fz.xdefer = xmode;
         fz.first_dst = cg->first_dst;
+        if (xmode == 2) {
+          fz.side_stream = cg->side_stream;
+          fz.side_ev[0] = cg->side_ev[0];
+          fz.side_ev[1] = cg->side_ev[1];
+        }
         // r.q: conjugacy identity (layout 0: the prologue adds p_new.q_old
         // partials, the epilogue skips its pass over r) or read in the epilogue
         const bool rq_ident = cg->rq != 0 && cg->fusion == 0;
@@ -1172,6 +1241,11 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     fz.sn = n;
     fz.xdefer = xmode;
     fz.first_dst = cg->first_dst;
+    if (xmode == 2) {
+      fz.side_stream = cg->side_stream;
+      fz.side_ev[0] = cg->side_ev[0];
+      fz.side_ev[1] = cg->side_ev[1];
+    }
     const bool rq_ident = cg->rq != 0;
     fz.er = rq_ident ? nullptr : cg->r;
     fz.pqo_stride = rq_ident ? cg->rr_count : 0;

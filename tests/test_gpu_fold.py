@@ -134,6 +134,27 @@ def test_fold_nontemporal_variants_bitwise(gg, monkeypatch):
         assert np.array_equal(out[0], o)
 
 
+@pytest.mark.parametrize("d", [3, 4])
+def test_cg_side_job_stream_matches_inline(gg, monkeypatch, d):
+    """The x side job as a concurrent kernel on the CG's side stream (default,
+    beside ring mode products) and inside the mode products
+    (GG_CG_SIDE_ASYNC=0): the same iterates (r and p do not depend on x) and x
+    to rounding."""
+    m = 200 if d == 3 else 40
+    F = [grid_factor(m, 0.1 + 0.02 * k) for k in range(d)]
+    x = np.random.default_rng(6).standard_normal((m ** d, 1))
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GG_CG_SIDE_ASYNC", flag)
+        K = kron(gg, F)
+        for maxiter in (7, 8):
+            xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=maxiter,
+                                    recurrence="fused")
+            out[(flag, maxiter)] = np.asarray(xs)
+    for maxiter in (7, 8):
+        assert rel(out[("1", maxiter)], out[("0", maxiter)]) < 1e-14
+
+
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
     """A centrosymmetric but non-symmetric factor: the transposed operator's
     split is packed from F^T."""
