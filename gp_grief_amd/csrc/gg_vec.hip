@@ -870,9 +870,13 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
       GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
-      // the concurrent x side job (GG_CG_SIDE_ASYNC=0: in the mode products)
+      // the concurrent x side job (GG_CG_SIDE_ASYNC=1, opt-in): at 200^4 the
+      // streaming kernel (50 VGPRs) cannot sit beside a ring workgroup (2 x
+      // 232 of 512 VGPRs per SIMD), so it holds CUs the ring needs: mode
+      // products 1-2 7.7 -> 11.0-11.5 ms, the iteration 38.8 -> 46-47.5 ms
+      // (profiles/r04/w_side_async)
       const char* sa = getenv("GG_CG_SIDE_ASYNC");
-      if (cg->fused && !(sa && atoi(sa) == 0)) {
+      if (cg->fused && sa && atoi(sa) == 1) {
         GG_HIP(hipStreamCreateWithFlags(&cg->side_stream, hipStreamNonBlocking));
         for (hipEvent_t& e : cg->side_ev) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }

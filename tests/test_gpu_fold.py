@@ -145,7 +145,7 @@ def test_cg_side_job_stream_matches_inline(gg, monkeypatch, d):
     x = np.random.default_rng(6).standard_normal((m ** d, 1))
     out = {}
     for flag in ("1", "0"):
-        monkeypatch.setenv("GG_CG_SIDE_ASYNC", flag)
+        monkeypatch.setenv("GG_CG_SIDE_ASYNC", flag)   # 1: opt-in stream
         K = kron(gg, F)
         for maxiter in (7, 8):
             xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=maxiter,
