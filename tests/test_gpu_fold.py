@@ -136,7 +136,7 @@ def test_fold_nontemporal_variants_bitwise(gg, monkeypatch):
 
 @pytest.mark.parametrize("d", [3, 4])
 def test_cg_side_job_stream_matches_inline(gg, monkeypatch, d):
-    """The x side job as a concurrent kernel on the CG's side stream (default,
+    """The x side job as a concurrent kernel on the CG's side stream (opt-in,
     beside ring mode products) and inside the mode products
     (GG_CG_SIDE_ASYNC=0): the same iterates (r and p do not depend on x) and x
     to rounding."""
