@@ -446,6 +446,26 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     const int rl = lane >> 4;
     static_assert(TS == TA, "staged epilogue: equal S / T tails");
     constexpr int JFULL = JS - (TS > 0 ? 1 : 0);   // 16x16 tiles per half
+    constexpr int kU = 4;
+    // kOpt bit 8 (GG_FOLD_EPI_PRE): p of batch t + 1 prefetched (m <= 256:
+    // at most two batches of 64 kU double2 per 4-row round)
+    constexpr bool kPre = (kOpt & 256) != 0;
+    constexpr int kUP = 2;                          // double2 per lane per prefetched batch
+    constexpr int kNB = 4;                          // batches per 4-row round (m <= 256)
+    static_assert(!kPre || kNB * 64 * kUP * 2 >= 4 * 32 * JS, "prefetch: batches per round");
+    double2 pc[kUP], pn[kUP];
+    auto pre_fetch = [&](int t, double2 (&pv)[kUP]) {
+      const int r = t / kNB, base = (t % kNB) * 64 * kUP;
+      const int nr = min(4, max(0, rows_left - 4 * r));
+      const int tot2 = (nr * m) >> 1;
+      const int64_t g0 = (b0u + 4 * r) * m;
+#pragma unroll
+      for (int u = 0; u < kUP; ++u) {
+        const int i2 = base + lane + 64 * u;
+        pv[u] = i2 < tot2 ? ld2<kNTs>(xs + g0 + 2 * (int64_t)i2) : double2{0.0, 0.0};
+      }
+    };
+    if (kPre && !rq_on && xs != nullptr) pre_fetch(0, pc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -474,46 +494,81 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
       const int nr = min(4, max(0, rows_left - 4 * r));
       const int tot2 = (nr * m) >> 1;              // double2 of this round (m even)
       const int64_t g0 = (b0u + 4 * r) * m;        // first element (16-B aligned)
-      constexpr int kU = 4;
-      for (int base = 0; base < tot2; base += 64 * kU) {
-        double2 av[kU], pv[kU], ev[kU];
+      if (!kPre || rq_on || xs == nullptr) {
+        for (int base = 0; base < tot2; base += 64 * kU) {
+          double2 av[kU], pv[kU], ev[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int i2 = base + lane + 64 * u;
-          const bool ok = i2 < tot2;
-          const int64_t g = g0 + 2 * (int64_t)i2;
-          av[u] = ok ? *reinterpret_cast<const double2*>(wl + 2 * i2) : double2{0.0, 0.0};
-          pv[u] = (ok && xs != nullptr) ? ld2<kNTs>(xs + g) : double2{0.0, 0.0};
-          ev[u] = (ok && rq_on) ? ld2<kNTs>(er + g) : double2{0.0, 0.0};
+          for (int u = 0; u < kU; ++u) {
+            const int i2 = base + lane + 64 * u;
+            const bool ok = i2 < tot2;
+            const int64_t g = g0 + 2 * (int64_t)i2;
+            av[u] = ok ? *reinterpret_cast<const double2*>(wl + 2 * i2) : double2{0.0, 0.0};
+            pv[u] = (ok && xs != nullptr) ? ld2<kNTs>(xs + g) : double2{0.0, 0.0};
+            ev[u] = (ok && rq_on) ? ld2<kNTs>(er + g) : double2{0.0, 0.0};
+          }
+#pragma unroll
+          for (int u = 0; u < kU; ++u) {
+            const int i2 = base + lane + 64 * u;
+            if (i2 >= tot2) continue;
+            const int64_t g = g0 + 2 * (int64_t)i2;
+            if (xs == nullptr) {
+              st2<kNTy>(Y + g, av[u]);
+              continue;
+            }
+            double2 p2 = pv[u];
+            if (kRecomp) {
+              p2.x = first ? ev[u].x : fma(beta, p2.x, ev[u].x);
+              p2.y = first ? ev[u].y : fma(beta, p2.y, ev[u].y);
+            }
+            double2 v;
+            v.x = fma(shift, p2.x, av[u].x);
+            v.y = fma(shift, p2.y, av[u].y);
+            dsum = fma(p2.x, v.x, dsum);
+            dsum = fma(p2.y, v.y, dsum);
+            if (edots) {
+              rqsum = fma(ev[u].x, v.x, rqsum);
+              rqsum = fma(ev[u].y, v.y, rqsum);
+              qqsum = fma(v.x, v.x, qqsum);
+              qqsum = fma(v.y, v.y, qqsum);
+            }
+            st2<kNTy>(Y + g, v);
+            if (kRecomp) st2<kNTy>(epo + g, p2);
+          }
+        }
+        continue;
+      }
+      // kPre (the conjugacy r.q path: p the only global operand): the p
+      // values of the next batch -- the next round's first while this round's
+      // last is processed -- are loaded before this batch's arithmetic and
+      // stores, so one HBM latency per block is exposed instead of one per
+      // batch (CDNA4 retires vmcnt in order, stores included)
+#pragma unroll
+      for (int b = 0; b < kNB; ++b) {
+        const int base = b * 64 * kUP;
+        const int t = kNB * r + b;
+        if (t + 1 < 4 * kNB) pre_fetch(t + 1, pn);
+        if (base < tot2) {
+#pragma unroll
+          for (int u = 0; u < kUP; ++u) {
+            const int i2 = base + lane + 64 * u;
+            if (i2 >= tot2) continue;
+            const int64_t g = g0 + 2 * (int64_t)i2;
+            const double2 av = *reinterpret_cast<const double2*>(wl + 2 * i2);
+            const double2 p2 = pc[u];
+            double2 v;
+            v.x = fma(shift, p2.x, av.x);
+            v.y = fma(shift, p2.y, av.y);
+            dsum = fma(p2.x, v.x, dsum);
+            dsum = fma(p2.y, v.y, dsum);
+            if (edots) {
+              qqsum = fma(v.x, v.x, qqsum);
+              qqsum = fma(v.y, v.y, qqsum);
+            }
+            st2<kNTy>(Y + g, v);
+          }
         }
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int i2 = base + lane + 64 * u;
-          if (i2 >= tot2) continue;
-          const int64_t g = g0 + 2 * (int64_t)i2;
-          if (xs == nullptr) {
-            st2<kNTy>(Y + g, av[u]);
-            continue;
-          }
-          double2 p2 = pv[u];
-          if (kRecomp) {
-            p2.x = first ? ev[u].x : fma(beta, p2.x, ev[u].x);
-            p2.y = first ? ev[u].y : fma(beta, p2.y, ev[u].y);
-          }
-          double2 v;
-          v.x = fma(shift, p2.x, av[u].x);
-          v.y = fma(shift, p2.y, av[u].y);
-          dsum = fma(p2.x, v.x, dsum);
-          dsum = fma(p2.y, v.y, dsum);
-          if (edots) {
-            rqsum = fma(ev[u].x, v.x, rqsum);
-            rqsum = fma(ev[u].y, v.y, rqsum);
-            qqsum = fma(v.x, v.x, qqsum);
-            qqsum = fma(v.y, v.y, qqsum);
-          }
-          st2<kNTy>(Y + g, v);
-          if (kRecomp) st2<kNTy>(epo + g, p2);
-        }
+        for (int u = 0; u < kUP; ++u) pc[u] = pn[u];
       }
     }
   } else if (kMap) {
@@ -670,6 +725,7 @@ static FoldConfig lean_cfg(int kind, bool staged) {
         // GG_FOLD_EPI_NT: non-temporal streams of the CG epilogue (default 6:
         // the p operand loads and the q stores; epilogue 8.66-8.76 -> 8.59-8.64
         // ms at 200^4, interleaved, profiles/r04/u_nt)
+        if (env_int("GG_FOLD_EPI_PRE") == 1) return cfg_fold<JT, TT, 3, true, 4 | 192 | 256>();
         switch (env_int("GG_FOLD_EPI_NT", 6)) {
           case 1: return cfg_fold<JT, TT, 3, true, 4 | 32>();
           case 2: return cfg_fold<JT, TT, 3, true, 4 | 64>();

@@ -116,11 +116,11 @@ def test_fold_nontemporal_variants_bitwise(gg, monkeypatch):
     CG at 200^3 agrees bitwise with every mask off."""
     F = [grid_factor(200, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
     x = np.random.default_rng(5).standard_normal((200 ** 3, 1))
-    knobs = ["GG_FOLD_PRO_NT", "GG_FOLD_EPI_NT", "GG_FOLD_SIDE_NT"]
+    knobs = ["GG_FOLD_PRO_NT", "GG_FOLD_EPI_NT", "GG_FOLD_SIDE_NT", "GG_FOLD_EPI_PRE"]
     cases = [{"GG_FOLD_PRO_NT": "0", "GG_FOLD_EPI_NT": "0", "GG_FOLD_SIDE_NT": "0"}] + \
         [{"GG_FOLD_PRO_NT": v} for v in ("1", "2", "3", "6", "7")] + \
         [{"GG_FOLD_EPI_NT": v} for v in ("1", "2", "4", "6", "7")] + \
-        [{"GG_FOLD_SIDE_NT": v} for v in ("1", "2", "3")] + [{}]
+        [{"GG_FOLD_SIDE_NT": v} for v in ("1", "2", "3")] + [{}, {"GG_FOLD_EPI_PRE": "1"}]
     out = []
     for case in cases:
         for k in knobs:
