@@ -447,8 +447,9 @@ __global__ __launch_bounds__(64 * kWv, kMinW) void mode_product_fold_kernel(
     static_assert(TS == TA, "staged epilogue: equal S / T tails");
     constexpr int JFULL = JS - (TS > 0 ? 1 : 0);   // 16x16 tiles per half
     constexpr int kU = 4;
-    // kOpt bit 8 (GG_FOLD_EPI_PRE): p of batch t + 1 prefetched (m <= 256:
-    // at most two batches of 64 kU double2 per 4-row round)
+    // kOpt bit 8 (GG_FOLD_EPI_PRE=1, opt-in): p of batch t + 1 prefetched
+    // (m <= 256: four batches of 64 kUP double2 per 4-row round); spills 6
+    // VGPRs at the 3-wave budget, epilogue +0.25 ms (profiles/r04/x_epi_pre)
     constexpr bool kPre = (kOpt & 256) != 0;
     constexpr int kUP = 2;                          // double2 per lane per prefetched batch
     constexpr int kNB = 4;                          // batches per 4-row round (m <= 256)
