@@ -143,9 +143,40 @@ def _stationary_host(kind, var, ls, d2):
     raise NotImplementedError(kind)
 
 
+def _stationary_grad_host(kind, var, ls, diff):
+    """d k(x, z) / d x for 1-D inputs, diff = x - z: the analytic gradients of
+    _stationary_host (the reference takes them from GPy's gradients_X,
+    grid_kernel.py:196-199; its native kernels have none)."""
+    if kind == "RBF":
+        if ls < 1e-6:
+            return np.zeros_like(diff)
+        return -diff / (ls * ls) * var * np.exp(-0.5 * diff * diff / (ls * ls))
+    r = np.abs(diff) / ls
+    if kind == "Exponential":
+        return -var * np.exp(-r) * np.sign(diff) / ls
+    if kind == "Matern32":
+        s3 = 1.7320508075688772
+        return -3.0 * var * np.exp(-s3 * r) * diff / (ls * ls)
+    if kind == "Matern52":
+        s5 = 2.23606797749979
+        return -(5.0 / 3) * var * (1.0 + s5 * r) * np.exp(-s5 * r) * diff / (ls * ls)
+    raise NotImplementedError(kind)
+
+
 class Stationary(BaseKernel):
     """Stationary kernels evaluated on the device (stationary.py:9-76)."""
     _kind = None
+
+    def cov_grad_x(self, x, z):
+        """(N, M) matrix of d k(x_a, z_j) / d x_a for a 1-D kernel (host) --
+        GPy's gradients_X(1, x, z_j) column by column in the reference."""
+        if self._children or self.active_dims.size != 1:
+            raise NotImplementedError("input gradients need a plain 1-D stationary kernel")
+        x = np.asarray(x, dtype=np.float64).reshape(-1, self.n_dims)[:, self.active_dims]
+        z = np.asarray(z, dtype=np.float64).reshape(-1, self.n_dims)[:, self.active_dims]
+        return _stationary_grad_host(self._kind, float(np.asarray(self.variance).reshape(-1)[0]),
+                                     float(np.asarray(self.lengthscale).reshape(-1)[0]),
+                                     x[:, :1] - z[:, 0][None, :])
 
     def _device_cov(self, x, z, mode, out, lengthscale=None):
         """Evaluate into the device matrix `out` (N x M); mode 0/1/2 = set/mul/add."""
@@ -309,7 +340,18 @@ class GridKernel(object):
         return Kxz
 
     def cov_kr_grad(self, x, z, grad_dim):
-        raise NotImplementedError  # needs GPyKernel in the reference (grid_kernel.py:196-199)
+        """Gradient of cov_kr w.r.t. x[:, grad_dim] (grid_kernel.py:181-209):
+        the grad_dim factor replaced by d k / d x (analytic for the stationary
+        kernels; the reference needs GPy kernels here), factors reversed."""
+        (N, d) = x.shape
+        assert self.grid_dim == d
+        Kxz = []
+        for i, kern in enumerate(self.kern_list):
+            if i == grad_dim:
+                Kxz.append(kern.cov_grad_x(x[:, (i,)], np.asarray(z[i])))
+            else:
+                Kxz.append(kern.cov(x=x[:, (i,)], z=z[i]))
+        return Kxz[::-1]
 
     @property
     def parameters(self):
@@ -449,7 +491,31 @@ class GriefKernel(GridKernel):
         return a
 
     def cov_grad(self, x, grad_dim):
-        raise NotImplementedError  # needs GPyKernel gradients (grid_kernel.py:196-199)
+        """d Phi_L / d x[:, grad_dim] (grief_kernel.py:113-126), n x p (host),
+        on the SAME selected eigenvectors as Phi (the device basis: qsel,
+        cidx, log_lam), so it pairs with the fit's alpha.  Per factor f the
+        selected rows X_f = Qsel_f K_ux,f (d k / d x for the input dimension
+        grad_dim), Phi_jk = prod_f X_f[c_jf] exp(-log_lam_j / 2)."""
+        self._setup_inducing_cov()
+        B = self._dev_basis
+        x = np.asarray(x, dtype=np.float64)
+        n, d = x.shape
+        assert d == self.grid_dim
+        rows = []
+        for f in range(d):
+            i = d - 1 - f                      # factor f = input dimension d - 1 - f
+            kern = self.kern_list[i]
+            xg = np.asarray(self.grid.xg[i], dtype=np.float64).reshape(-1, 1)
+            if i == grad_dim:
+                Kux = kern.cov_grad_x(x[:, (i,)], xg).T
+            else:
+                Kux = np.asarray(kern.cov(x=x[:, (i,)], z=xg)).T
+            rows.append(dev.to_host(B["qsel"][f]).reshape(int(B["u"][f]), -1).dot(Kux))
+        X = np.concatenate(rows, axis=0)       # U x n, factor f's rows from col0_f
+        cidx = dev.to_host(B["cidx"]).reshape(self.n_eigs, d)
+        dPhi = np.exp(-0.5 * np.asarray(self._log_lam, dtype=np.float64)).reshape(-1, 1) * \
+            np.prod(np.stack([X[cidx[:, f], :] for f in range(d)]), axis=0)
+        return np.ascontiguousarray(dPhi.T)
 
     # ------------------------------------------------------------ parameters
     @property

@@ -463,7 +463,12 @@ class GPGriefModel(BaseModel):
         return dense.host(yhat).reshape((-1, 1)), dense.host(var)
 
     def d_Yhat_d_x(self, Xnew, dim):
-        raise NotImplementedError  # needs GriefKernel.cov_grad (GPyKernel only)
+        """d Yhat / d Xnew[:, dim] (gp_grief_model.py:127-134): dPhi* alpha_p,
+        dPhi* from GriefKernel.cov_grad on the fit's basis; a host array as
+        the reference's dot product, (M, 1)."""
+        self.predict_precompute(Xnew)
+        dPhi = self.kern.cov_grad(Xnew, dim)
+        return dPhi.dot(dense.host(self._alpha_p).reshape(-1, 1))
 
     def _phi_setup(self):
         self._w = self.kern.w

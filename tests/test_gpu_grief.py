@@ -510,3 +510,30 @@ def test_grief_phi_value_table_matches_log_table(gg, monkeypatch, d, kind):
     (P0, T0), (P1, T1) = out
     assert np.abs(T0 - P0.T).max() == 0.0
     assert rel(P0, P1) < 1e-13 and rel(T0, T1) < 1e-13
+
+
+@pytest.mark.parametrize("kind", ["RBF", "Matern52"])
+def test_d_yhat_d_x_matches_finite_differences(gg, kind):
+    """GPGriefModel.d_Yhat_d_x (gp_grief_model.py:127-134 via
+    GriefKernel.cov_grad, on the fit's own eigenvector basis) against central
+    differences of the predictive mean.  The reference needs GPy kernels for
+    it (grid_kernel.py:196-199): parity unpinned, checked by differences."""
+    rng = np.random.default_rng(11)
+    d, m, n, p = 2, 32, 600, 60
+    x = rng.random((n, d))
+    y = (np.sin(5 * x).sum(axis=1) + 0.05 * rng.standard_normal(n)).reshape(-1, 1)
+    kl = [getattr(gg.kern, kind)(1, variance=1.0, lengthscale=0.2 + 0.05 * i) for i in range(d)]
+    grid = gg.grid.InducingGrid(xg=[np.linspace(0, 1, m).reshape(-1, 1)] * d)
+    kern = gg.kern.GriefKernel(kern_list=kl, grid=grid, n_eigs=p)
+    model = gg.models.GPGriefModel(x, y, kern, noise_var=0.01)
+    xt = 0.1 + 0.8 * rng.random((40, d))
+    h = 1e-5
+    for dim in range(d):
+        g = np.asarray(model.d_Yhat_d_x(xt, dim))
+        assert g.shape == (40, 1)
+        e = np.zeros(d)
+        e[dim] = h
+        fp = np.asarray(model.predict(xt + e)[0])
+        fm = np.asarray(model.predict(xt - e)[0])
+        fd = (fp - fm) / (2 * h)
+        assert np.abs(g - fd).max() < 1e-5 * max(1.0, np.abs(fd).max())
