@@ -163,13 +163,17 @@ def local_rhs(m, d, world, rank, torch, dev):
 def parity_local_rhs(m, d, world, rank, torch, dev):
     """This rank's block of the same right-hand side in the even / odd basis
     of factors 0..K-1 (G = 2^K; distributed.parity_fold, on the device): local
-    index = C order over (h, ..., h, m, ..., m), h = m / 2, and b~ = 2^(-K/2)
+    index = C order over the local axes (distributed.parity_local_axes: the
+    unsharded axes K..d-1 of size m, then the sharded 0..K-1 of size h = m / 2),
+    and b~ = 2^(-K/2)
     sum over the 2^K mirror choices s of sign(s) y[g(s)] -- axis k takes
     digit i (s_k = 0) or m - 1 - i (s_k = 1, sign -1 when bit k of the rank,
     counted from the most significant, is set)."""
+    from gp_grief_amd.distributed import parity_local_axes
     K = world.bit_length() - 1
     h = m // 2
-    sizes = [h] * K + [m] * (d - K)
+    axes = parity_local_axes(d, world)            # global axis of each local axis
+    sizes = [h if a < K else m for a in axes]
     nl = int(np.prod(sizes))
     y = torch.empty(nl, dtype=torch.float64, device=dev)
     chunk = 1 << 24
@@ -177,10 +181,10 @@ def parity_local_rhs(m, d, world, rank, torch, dev):
     for i in range(0, nl, chunk):
         k = min(chunk, nl - i)
         rest = torch.arange(i, i + k, dtype=torch.int64, device=dev)
-        digits = [None] * d
-        for ax in range(d - 1, -1, -1):
-            digits[ax] = torch.remainder(rest, sizes[ax])
-            rest = torch.div(rest, sizes[ax], rounding_mode="floor")
+        digits = [None] * d                       # by global axis
+        for pos in range(d - 1, -1, -1):
+            digits[axes[pos]] = torch.remainder(rest, sizes[pos])
+            rest = torch.div(rest, sizes[pos], rounding_mode="floor")
         acc = torch.zeros(k, dtype=torch.float64, device=dev)
         for sgn_bits in range(1 << K):
             g = torch.zeros(k, dtype=torch.int64, device=dev)

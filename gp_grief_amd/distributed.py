@@ -541,17 +541,30 @@ def parity_ok(factors, world):
 
 
 def parity_local_factors(factors, world, rank):
-    """Rank g's block: X_k = S_k (bit k of g clear, bit 0 = the most
-    significant of K) or T_k for k < K, F_k beyond."""
+    """Rank g's block as the factor list of its local operator: the
+    unsharded factors F_K .. F_{d-1} first, then X_k = S_k (bit k of g clear,
+    bit 0 = the most significant of K) or T_k for k < K.  The order is the
+    local vector layout (C order over m_K .. m_{d-1}, h_0 .. h_{K-1}): the
+    first mode product, which carries the CG prologue (six streams), then runs
+    on a centrosymmetric factor's tuned folded kernel -- per-rank iteration at
+    G = 8 5.55-5.70 -> 5.27-5.28 ms against the sharded factors first
+    (profiles/r04/y_parity_order.jsonl)."""
     K = int(world).bit_length() - 1
-    out = []
+    head, tail = [], []
     for k, F in enumerate(factors):
         if k < K:
             S, T = centro_split(F)
-            out.append(T if (int(rank) >> (K - 1 - k)) & 1 else S)
+            tail.append(T if (int(rank) >> (K - 1 - k)) & 1 else S)
         else:
-            out.append(np.ascontiguousarray(np.asarray(F, dtype=np.float64)))
-    return out
+            head.append(np.ascontiguousarray(np.asarray(F, dtype=np.float64)))
+    return head + tail
+
+
+def parity_local_axes(d, world):
+    """Global axis of each local axis (the local layout of
+    parity_local_factors)."""
+    K = int(world).bit_length() - 1
+    return list(range(K, d)) + list(range(K))
 
 
 def _parity_transform(X, K, inverse=False):
@@ -580,12 +593,13 @@ def parity_fold(vec, m, world):
     m = [int(v) for v in m]
     K = int(world).bit_length() - 1
     X = _parity_transform(np.asarray(vec, dtype=np.float64).reshape(m), K)
+    axes = parity_local_axes(len(m), world)
     out = []
     for g in range(int(world)):
         sl = tuple(slice(((g >> (K - 1 - k)) & 1) * (m[k] // 2),
                          (((g >> (K - 1 - k)) & 1) + 1) * (m[k] // 2)) if k < K else slice(None)
                    for k in range(len(m)))
-        out.append(np.ascontiguousarray(X[sl]).reshape(-1))
+        out.append(np.ascontiguousarray(np.transpose(X[sl], axes)).reshape(-1))
     return out
 
 
@@ -595,12 +609,14 @@ def parity_unfold(locals_, m):
     world = len(locals_)
     K = world.bit_length() - 1
     X = np.empty(m)
-    lshape = [m[k] // 2 if k < K else m[k] for k in range(len(m))]
+    axes = parity_local_axes(len(m), world)
+    lshape = [m[a] // 2 if a < K else m[a] for a in axes]
+    inv = np.argsort(axes)
     for g, loc in enumerate(locals_):
         sl = tuple(slice(((g >> (K - 1 - k)) & 1) * (m[k] // 2),
                          (((g >> (K - 1 - k)) & 1) + 1) * (m[k] // 2)) if k < K else slice(None)
                    for k in range(len(m)))
-        X[sl] = np.asarray(loc).reshape(lshape)
+        X[sl] = np.transpose(np.asarray(loc).reshape(lshape), inv)
     return _parity_transform(X, K, inverse=True).reshape(-1)
 
 

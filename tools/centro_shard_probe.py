@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--dims", type=int, default=4)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--rotate", type=int, default=0,
+                    help="1: the unsharded (folded) factors first in the local operator")
     a = ap.parse_args()
     import torch
     import bench
@@ -49,6 +51,8 @@ def main():
                     loc.append(T if (g >> (K - 1 - k)) & 1 else S)
                 else:
                     loc.append(F[k])
+            if a.rotate:
+                loc = loc[K:] + loc[:K]
             Kl = gg.tensors.KronMatrix([np.ascontiguousarray(f) for f in loc])
             n = int(np.prod([f.shape[0] for f in loc]))
             y = torch.ones(n, dtype=torch.float64, device="cuda")
@@ -64,7 +68,7 @@ def main():
             torch.cuda.synchronize()
             nm, per = cg.profile_read()
             fm = Kl._device().fold_mask()
-            print(json.dumps({"G": G, "rank": g, "local_shape": [f.shape[0] for f in loc],
+            print(json.dumps({"G": G, "rank": g, "rotate": a.rotate, "local_shape": [f.shape[0] for f in loc],
                               "fold_mask": fm, "ms_per_iteration": e0.elapsed_time(e1) / a.steps,
                               "launch_ms": [v / max(nm, 1) for v in per]}), flush=True)
             del cg, Kl, y
