@@ -1036,6 +1036,11 @@ int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
 // Leaving gg_cg_iterate applies the pending x / r update with the textbook
 // kernels, so the state it leaves (x, r, iteration count) is the textbook's.
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
+  const int st = gg_cg_iterate_open(cg, max_iters, check_every, stream);
+  return st != GG_OK ? st : gg_cg_close(cg, stream);
+}
+
+int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
     hipStream_t s = gg::as_stream(stream);
@@ -1146,6 +1151,17 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
         if (cg->sc_host->done) break;
       }
     }
+  });
+}
+
+// leaving the fused recurrence: the deferred x steps and the pending r update
+// (no-op for the textbook recurrence or when nothing is pending)
+int gg_cg_close(gg_cg* cg, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
+    hipStream_t s = gg::as_stream(stream);
+    const int64_t n = cg->n;
+    const int nb = gg::vec_blocks(n);
     if (cg->fused) {
       const bool xdefer = cg->xdefer != 0 && cg->fusion != 2;
       // closing update (no-op unless pending): x += alpha p, r -= alpha q,

@@ -418,7 +418,7 @@ class DistKronCG(object):
         if self.recurrence == "fused":
             self.e.zero(self.q)   # q_old of the first prologue (not pending)
 
-    def _iterate_fused(self, n_iter):
+    def _iterate_fused(self, n_iter, close=True):
         """The fused recurrence: per iteration phase 1 (prologue, x side job),
         the exchanges and phase 2 (K p_new lands in q, kept unshifted), a
         read-only pass for p.q' and q'.q' (q' = q + shift p_new), ONE
@@ -455,13 +455,22 @@ class DistKronCG(object):
             # (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2})
             pb[0], pb[1], pb[2], pb[3] = p_new, pb[3], p_old, pb[2]
         self.p = pb[0]
+        if close:
+            self.close()
+
+    def close(self):
+        """Leave the fused recurrence (deferred x steps, pending r update):
+        the textbook state; a no-op for the textbook recurrence."""
+        if self.recurrence != "fused":
+            return
         self.e.fused_close(self.x, self.r, self.q, self.p, self.shift)
         self._allreduce()
         self.e.fused_close_rho()
 
-    def iterate(self, n_iter):
+    def iterate(self, n_iter, close=True):
+        """close=False (fused recurrence) leaves it open for the next call."""
         if self.recurrence == "fused":
-            return self._iterate_fused(n_iter)
+            return self._iterate_fused(n_iter, close)
         for _ in range(int(n_iter)):
             self._mark("start")
             self._matvec_into_q(self.p, fuse_cg=True)        # p = r + beta p ; q = K p
@@ -744,7 +753,9 @@ class ParityShardCG(object):
         self.x_ex.all_reduce(self.e.start_partial(b, self.x))
         self.e.start_finish(rtol, atol)
 
-    def iterate(self, n_iter):
+    def iterate(self, n_iter, close=True):
+        """close=False leaves the recurrence open (the next call continues
+        it); close() applies the pending updates before x or counts are read."""
         for _ in range(int(n_iter)):
             self._mark("start")
             red = self.e.iterate_partial()
@@ -753,6 +764,10 @@ class ParityShardCG(object):
             self._mark("allreduce")
             self.e.iterate_finish()
             self._mark("scalars")
+        if close:
+            self.close()
+
+    def close(self):
         self.x_ex.all_reduce(self.e.close_partial())
         self.e.close_finish()
 

@@ -172,11 +172,21 @@ class KronCG(object):
                                               float(rtol), float(atol), native.stream_ptr()),
                      "gg_cg_start")
 
-    def iterate(self, n_iter, check_every=0):
+    def iterate(self, n_iter, check_every=0, close=True):
+        """n_iter iterations; close=False leaves the fused recurrence open
+        (its last r update and deferred x steps pending, continued by the next
+        call) -- close() (or a later iterate(close=True)) restores the
+        textbook state before x or the counts are read."""
         from . import native
         n_iter = min(int(n_iter), 2 ** 31 - 1)
-        native.check(native.lib().gg_cg_iterate(self.h, n_iter, min(int(check_every), n_iter),
-                                                native.stream_ptr()), "gg_cg_iterate")
+        name = "gg_cg_iterate" if close else "gg_cg_iterate_open"
+        native.check(getattr(native.lib(), name)(self.h, n_iter, min(int(check_every), n_iter),
+                                                 native.stream_ptr()), name)
+
+    def close(self):
+        """Apply the pending r update and deferred x steps (gg_cg_close)."""
+        from . import native
+        native.check(native.lib().gg_cg_close(self.h, native.stream_ptr()), "gg_cg_close")
 
     def status(self):
         from . import native

@@ -58,6 +58,8 @@ SIGNATURES = {
     "gg_cg_destroy": [_vp],
     "gg_cg_start": [_vp, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
     "gg_cg_iterate": [_vp, ctypes.c_int, ctypes.c_int, _vp],
+    "gg_cg_iterate_open": [_vp, ctypes.c_int, ctypes.c_int, _vp],
+    "gg_cg_close": [_vp, _vp],
     "gg_cg_set_recurrence": [_vp, ctypes.c_int],
     "gg_cg_get_recurrence": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_fusion": [_vp, ctypes.c_int],

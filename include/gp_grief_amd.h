@@ -149,6 +149,13 @@ int gg_cg_get_xdefer(const gg_cg* cg, int* on);
 int gg_cg_set_rq(gg_cg* cg, int mode);
 int gg_cg_get_rq(const gg_cg* cg, int* mode);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
+/* gg_cg_iterate = gg_cg_iterate_open + gg_cg_close.  _open leaves the fused
+ * recurrence open (the last iteration's r update and the deferred x steps
+ * pending; the next _open continues it seamlessly, the device stopping test
+ * and done flag stay exact); gg_cg_close applies them -- the textbook state
+ * (x, r, iteration count).  Read x or gg_cg_status's counts after a close. */
+int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
+int gg_cg_close(gg_cg* cg, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
 /* A rank of a sharded CG whose operator is block-diagonal across ranks (the

@@ -155,6 +155,26 @@ def test_cg_side_job_stream_matches_inline(gg, monkeypatch, d):
         assert rel(out[("1", maxiter)], out[("0", maxiter)]) < 1e-14
 
 
+def test_cg_open_iterations_chain_bitwise(gg):
+    """iterate(close=False) calls continue one open fused recurrence: open(5)
+    + open(7) + close() is the same launch sequence as iterate(12), bitwise;
+    the counts and x are the textbook state after the close."""
+    import torch
+    F = [grid_factor(200, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
+    K = kron(gg, F)
+    b = torch.from_numpy(np.random.default_rng(8).standard_normal(200 ** 3)).cuda()
+    out = []
+    for chain in ([12], [5, 7]):
+        cg = gg.linalg.KronCG(K, 0.05)
+        cg.start(b, rtol=0.0, atol=0.0)
+        for k in chain:
+            cg.iterate(k, close=False)
+        cg.close()
+        out.append((cg.x.cpu().numpy().copy(), cg.status()))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1][0] == out[1][1][0] == 12 and out[0][1][2] == out[1][1][2]
+
+
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
     """A centrosymmetric but non-symmetric factor: the transposed operator's
     split is packed from F^T."""
