@@ -446,3 +446,4 @@ def test_cg_prologue_shape_change_on_live_handle(gg, monkeypatch):
     assert it0 == it1 == 9
     assert abs(r1 - r0) <= 1e-8 * abs(r0)
     assert rel(sw.x.cpu().numpy(), ref.x.cpu().numpy()) < 1e-10
+
