@@ -217,6 +217,17 @@ def _engine_factory():
     return getattr(mod, cls_name), getattr(mod, "make_factors", None)
 
 
+def _all_reduce(dist, t, op):
+    """All-reduce of a small tensor; through the host when the process group
+    is gloo and the tensor lives on a GPU (the gloo-gpu rehearsal)."""
+    if t.is_cuda and str(dist.get_backend()) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op)
+
+
 def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     """Strong scaling: one CG on the full grid, factor 0 sharded over ranks."""
     from gp_grief_amd.distributed import DistKronCG, TorchExchange
@@ -251,7 +262,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
               file=sys.stderr, flush=True)
         cg, ok = None, 0.0
     flag = torch.tensor([ok], dtype=torch.float64, device=dev)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    _all_reduce(dist, flag, dist.ReduceOp.MIN)
     if float(flag.item()) < 1.0:
         cg = DistKronCG(eng, ex, s, mode="a2a", recurrence=rec)
     if cg.mode == "push":
@@ -262,7 +273,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         ref.apply(y.clone(), ya)
         cg.apply(y.clone(), yp)
         err = torch.stack([(ya - yp).abs().max(), ya.abs().max()])
-        dist.all_reduce(err, op=dist.ReduceOp.MAX)
+        _all_reduce(dist, err, dist.ReduceOp.MAX)
         del ref, ya, yp
         if not float(err[0]) <= 1e-12 * float(err[1]):
             cg = DistKronCG(eng, ex, s, mode="a2a", recurrence=rec)
@@ -281,7 +292,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     dist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _all_reduce(dist, t, dist.ReduceOp.MAX)
     dt = float(t.item())
     phases = None
     if on_gpu:
@@ -295,7 +306,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         # max over ranks of each phase's mean per iteration
         keys = sorted(ph)
         v = torch.tensor([ph[k] / a.steps for k in keys], dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        _all_reduce(dist, v, dist.ReduceOp.MAX)
         phases = dict(zip(keys, [float(u) for u in v.tolist()]))
     res = {
         "metric": METRIC,
@@ -364,7 +375,7 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
     dist.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _all_reduce(dist, t, dist.ReduceOp.MAX)
     dt = float(t.item())
     if on_gpu:
         ph = cg.profile_read()
@@ -404,7 +415,7 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
         keys = sorted(ph)
         v = torch.tensor([ph[k] / a.steps for k in keys] + [x / max(nm, 1) for x in per],
                          dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        _all_reduce(dist, v, dist.ReduceOp.MAX)
         vals = [float(u) for u in v.tolist()]
         res_["phase_ms_per_iteration"] = dict(zip(keys, vals[:len(keys)]))
         res_["local_launch_ms"] = vals[len(keys):]
@@ -836,12 +847,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     backend = os.environ.get("GG_BENCH_BACKEND", "nccl")
-    on_gpu = backend == "nccl"
+    # gloo-gpu (rehearsal on a box with fewer GPUs than ranks): the ranks'
+    # work on the GPUs (rank % count), their collectives over gloo
+    on_gpu = backend in ("nccl", "gloo-gpu")
     if world > 1:
         import torch.distributed as dist
         if on_gpu:
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+            torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dist.init_process_group("gloo" if backend == "gloo-gpu" else backend)
         dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu \
             else torch.device("cpu")
         res = run_sharded(a, world, rank, torch, dev, dist, on_gpu)
