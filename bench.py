@@ -420,9 +420,12 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
         res_["phase_ms_per_iteration"] = dict(zip(keys, vals[:len(keys)]))
         res_["local_launch_ms"] = vals[len(keys):]
         nl = n / world
-        res_["local_passes_per_iteration"] = 15
-        res_["local_gbs"] = 15 * 8.0 * nl / (res_["phase_ms_per_iteration"].get("launches", 0)
-                                             * 1e-3 or 1) / 1e9
+        passes = float(sum(launch_passes(d, "fused", 0, True, True)))
+        res_["local_passes_per_iteration"] = passes
+        lm = res_["phase_ms_per_iteration"].get("launches", 0.0)
+        if lm > 0:
+            res_["local_gbs"] = passes * 8.0 * nl / (lm * 1e-3) / 1e9
+            res_["local_frac_hbm"] = res_["local_gbs"] / HBM_PEAK_GBS
     return res_
 
 
