@@ -891,6 +891,19 @@ static FoldConfig fold_by_kind(int kind, bool lean_ok) {
       const char* e = getenv("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }
+    if (kind == 7) {
+      // the fused Lanczos prologue: 12-wave workgroups with non-temporal
+      // streams, as the CG prologue (default 2) -- 200^4 Lanczos step 34.1-35.1
+      // -> 33.47-33.50 ms, prologue 11.9-12.5 -> 11.3 ms, tridiagonal
+      // bitwise unchanged (profiles/r04/zf_lz).  GG_FOLD_LZ: 0 = 4-wave plain,
+      // 1 = 12-wave, 3 = 4-wave non-temporal (A/B)
+      switch (env_int("GG_FOLD_LZ", 2)) {
+        case 1: return cfg_fold<7, 1, 7, false, 0, 0, 12>();
+        case 2: return cfg_fold<7, 1, 7, false, 96, 0, 12>();
+        case 3: return cfg_fold<7, 1, 7, false, 96>();
+        default: break;
+      }
+    }
     if (lean_ok && kind == 4 && env_int("GG_FOLD_SIDE_W") == 12) return wide_cfg(4);
     if (lean_ok && env_int("GG_FOLD_LEAN", 1) == 1 && lean_kind(kind, false))
       return lean_cfg(kind, false);
