@@ -736,7 +736,13 @@ static FoldConfig lean_cfg(int kind, bool staged) {
           default: return cfg_fold<JT, TT, 3, true, 4>();
         }
       case 6: return cfg_fold<JT, TT, 6, true, 4>();
-      default: return cfg_fold<JT, TT, 0, true, 4>();
+      default:
+        // the shift / dot epilogue of a plain launch (the fused Lanczos
+        // step's last mode product): non-temporal operand loads and output
+        // stores (default; GG_FOLD_LZE=0 restores normal ones) -- 200^4
+        // Lanczos epilogue 8.54-8.64 -> 8.38-8.47 ms (profiles/r04/zf_lz)
+        if (env_int("GG_FOLD_LZE", 1) == 1) return cfg_fold<JT, TT, 0, true, 4 | 192>();
+        return cfg_fold<JT, TT, 0, true, 4>();
     }
   }
   switch (kind) {

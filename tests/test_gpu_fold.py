@@ -175,6 +175,24 @@ def test_cg_open_iterations_chain_bitwise(gg):
     assert out[0][1][0] == out[1][1][0] == 12 and out[0][1][2] == out[1][1][2]
 
 
+def test_lanczos_launch_variants_bitwise(gg, monkeypatch):
+    """The fused Lanczos step's prologue shapes (GG_FOLD_LZ: 4- / 12-wave,
+    non-temporal) and its epilogue's non-temporal streams (GG_FOLD_LZE) give
+    the same tridiagonal, bitwise."""
+    F = [grid_factor(200, 0.1), grid_factor(16, 0.3), grid_factor(16, 0.25),
+         grid_factor(200, 0.2, "Matern52")]
+    K = kron(gg, F)
+    assert fold_mask(K) & 0b1001 == 0b1001
+    out = []
+    for lz, lze in (("0", "0"), ("1", "0"), ("2", "1"), ("3", "1"), ("2", "0")):
+        monkeypatch.setenv("GG_FOLD_LZ", lz)
+        monkeypatch.setenv("GG_FOLD_LZE", lze)
+        a, b = gg.linalg.lanczos_tridiag(K, 0.01, 12, seed=3, probe=1)
+        out.append((np.asarray(a), np.asarray(b)))
+    for a, b in out[1:]:
+        assert np.array_equal(a, out[0][0]) and np.array_equal(b, out[0][1])
+
+
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):
     """A centrosymmetric but non-symmetric factor: the transposed operator's
     split is packed from F^T."""
