@@ -825,7 +825,19 @@ hipStream_t aux_stream(int which) {
   int least = 0, greatest = 0;
   GG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t st;
-  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 1 ? least : greatest));
+  if (which >= 16) {
+    // which = 16 + R: a CU-masked stream without the CUs whose bit index i
+    // has i % 32 < R (R of every 32 -- R per XCD whether the mask's words or
+    // its bits modulo 8 follow the XCDs)
+    int cus = 0;
+    GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<uint32_t> mask((size_t)ceil_div(cus, 32), 0u);
+    for (int i = 0; i < cus; ++i)
+      if (i % 32 >= which - 16) mask[(size_t)(i / 32)] |= 1u << (i % 32);
+    GG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  } else {
+    GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 1 ? least : greatest));
+  }
   streams[{dev, which}] = st;
   return st;
 }
@@ -1945,7 +1957,12 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     const char* la = getenv("GG_POTRF_LOOKAHEAD");
     const bool lookahead = !(la != nullptr && atoi(la) == 0);
     hipStream_t cs = lookahead ? gg::aux_stream(0) : s;   // factor chain, high priority
-    hipStream_t ws = lookahead ? gg::aux_stream(1) : s;   // wide updates, low priority
+    // GG_POTRF_CUMASK=R (1..31, A/B): the wide updates on a CU-masked stream
+    // that leaves R CUs of every 32 to the chain, instead of the low-priority
+    // stream (whose workgroups hold every CU until they drain)
+    const char* cm = getenv("GG_POTRF_CUMASK");
+    const int cu_res = cm ? std::max(0, std::min(31, atoi(cm))) : 0;
+    hipStream_t ws = lookahead ? gg::aux_stream(cu_res > 0 ? 16 + cu_res : 1) : s;
     hipStream_t us = lookahead ? gg::aux_stream(2) : s;   // in-panel updates, high priority
     std::vector<hipEvent_t> evs;
     auto new_event = [&]() {
