@@ -181,6 +181,25 @@ def test_cholesky_solve_logdet(gg, n):
     assert np.all(np.triu(Xi, 1) == 0)
 
 
+@pytest.mark.parametrize("reserve", ["2", "8"])
+def test_cholesky_cu_masked_wide_updates(gg, monkeypatch, reserve):
+    """GG_POTRF_CUMASK=R (opt-in A/B): the wide trailing updates on a
+    CU-masked stream give the same factor as the default look-ahead streams
+    (the same kernels on the same operands: bitwise)."""
+    import torch
+    from gp_grief_amd import dense
+    n = 4500   # 512-column panels: several wide updates
+    rng = np.random.default_rng(7)
+    G = rng.standard_normal((n, n + 10))
+    P = torch.from_numpy(G.dot(G.T) / n + 0.1 * np.eye(n)).cuda()
+    monkeypatch.delenv("GG_POTRF_CUMASK", raising=False)
+    ref = dense.Cholesky(P.clone())
+    monkeypatch.setenv("GG_POTRF_CUMASK", reserve)
+    ch = dense.Cholesky(P.clone())
+    assert torch.equal(torch.tril(ch.L), torch.tril(ref.L))
+    assert ch.logdet == ref.logdet
+
+
 def test_cholesky_not_spd_raises(gg):
     import torch
     from gp_grief_amd import dense
