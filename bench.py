@@ -489,6 +489,39 @@ def launch_passes(d, recurrence, fusion=0, xdefer=False, rq=False):
     return passes
 
 
+def block_launch_passes(d):
+    """Passes over N of each launch of the fused CG iteration in the
+    parity-block basis (gg_kronb.hip block_apply; d - 1 launches): the first
+    (axis 0, in place) carries the prologue -- p_old (its MFMA operand), r and
+    q_old read, r, p_new and the output written; the second (d >= 4) the
+    balanced x side job (half of x per iteration: x, p_{j-2}, p_{j-1} read, x
+    written = 2 passes); the last (the pair of innermost axes) reads its input
+    and p_new, writes q."""
+    passes = [2.0] * (d - 1)
+    passes[0] += 4.0
+    if d >= 4:
+        passes[1] += 2.0
+    passes[-1] += 1.0
+    return passes
+
+
+def block_launch_kernels(d):
+    kinds = ["plain"] * (d - 1)
+    kinds[0] = "prologue"
+    if d >= 4:
+        kinds[1] = "side"
+    kinds[-1] = "pair-epilogue"
+    return kinds
+
+
+def block_launch_flops(n, m, d):
+    """MFMA FLOP per launch: an h x h factor (h = m / 2) per element of its
+    axis is 2 n h = n m; the pair launch applies two."""
+    fl = [1.0 * n * m] * (d - 1)
+    fl[-1] = 2.0 * n * m
+    return fl
+
+
 def launch_kernels(d, recurrence, fusion=0):
     """The kernel instantiation of each launch position (gg_kron.hip kron_apply
     selects it per position): positions that share one are one rocprof row."""
@@ -515,13 +548,20 @@ def dominant_group(per_pos, kinds):
 
 
 def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0,
-                    xdefer=False, rq=False):
+                    xdefer=False, rq=False, block=False):
     """fold_mask bit k: mode product k runs on the centrosymmetric split
     (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
-    the roofline prices the work the kernel actually does."""
-    flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
-    passes = launch_passes(d, recurrence, fusion, xdefer, rq)
-    kinds = launch_kernels(d, recurrence, fusion)
+    the roofline prices the work the kernel actually does.  block: the CG runs
+    in the parity-block basis (d - 1 launches)."""
+    if block:
+        flops = block_launch_flops(n, m, d)
+        passes = block_launch_passes(d)
+        kinds = block_launch_kernels(d)
+    else:
+        flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
+        passes = launch_passes(d, recurrence, fusion, xdefer, rq)
+        kinds = launch_kernels(d, recurrence, fusion)
+    L = len(kinds)
     group, kind = dominant_group(per_pos, kinds)
     dom = group[0]
     flop = flops[dom]
@@ -542,8 +582,9 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
         "unit": "TFLOP/s" if bound == "mfma" else "GB/s",
         "frac": (f_mfma if bound == "mfma" else f_hbm) / t,
         "traffic": None, "traffic_unit": "bytes per launch",
-        "kernel": "mode product, %s kernel (launch position%s %s of %d; %s CG, layout %d)"
-                  % (kind, "s" if len(group) > 1 else "", ", ".join(str(i) for i in group), d,
+        "kernel": "%s, %s kernel (launch position%s %s of %d; %s CG, layout %d)"
+                  % ("parity-block launch" if block else "mode product", kind,
+                     "s" if len(group) > 1 else "", ", ".join(str(i) for i in group), L,
                      recurrence, fusion),
         "selection": "the kernel with the largest total time per iteration (rocprof "
                      "groups launches by kernel); per-launch averages over its positions",
@@ -552,7 +593,9 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
         "launch_ms_source": "HIP events the library records around each launch, on the "
                             "stream it launches on, over the timed iterations",
         "flop_per_launch": flop, "algorithmic_bytes_per_launch": byts,
-        "flop_rule": ("n m MFMA FLOP (centrosymmetric even/odd split: two h x h GEMMs, "
+        "flop_rule": ("parity-block basis: n m MFMA FLOP per h x h factor applied (h = m/2), "
+                      "2 n m for the pair launch" if block else
+                      "n m MFMA FLOP (centrosymmetric even/odd split: two h x h GEMMs, "
                       "h = m/2; the dense product is 2 n m)" if (fold_mask >> dom) & 1
                       else "2 n m (dense factor)"),
         "passes_per_launch": byts / (8.0 * n),
@@ -567,14 +610,15 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
                            / (per_pos[big] * 1e-3),
                            "frac_mfma": f_mfma / (per_pos[big] * 1e-3)},
         "mode_product_ms_by_position": per_pos,
+        "launch_kinds": kinds,
         "passes_by_position": passes,
         "matvec_ms": 1e3 * mv_s,
         "matvec_tflops": sum(flops) / mv_s / 1e12,
         "matvec_frac": sum(flops) / mv_s / 1e12 / FP64_MFMA_PEAK_TFLOPS,
         "matvec_dense_equivalent_tflops": d * 2.0 * n * m / mv_s / 1e12,
         "fold_mask": fold_mask,
-        "matvec_hbm_gbs": 8.0 * n * (2 * d + 1) / mv_s / 1e9,
-        "matvec_hbm_frac": 8.0 * n * (2 * d + 1) / mv_s / 1e9 / HBM_PEAK_GBS,
+        "matvec_hbm_gbs": 8.0 * n * (2 * L + 1) / mv_s / 1e9,
+        "matvec_hbm_frac": 8.0 * n * (2 * L + 1) / mv_s / 1e9 / HBM_PEAK_GBS,
         "iteration_algorithmic_bytes": it_bytes,
         "iteration_hbm_gbs": it_bytes / (ms_per_step * 1e-3) / 1e9,
         "iteration_floor_ms": 1e3 * floor_it,
@@ -600,7 +644,8 @@ def kernel_source_hash():
     return h.hexdigest()
 
 
-def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True, rq=False):
+def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True, rq=False,
+                block=False):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
     positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
     when they were taken on this workload, recurrence, fusion layout and fold
@@ -613,6 +658,8 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
     if not os.path.exists(path):
         return None, "no PMC passes committed (%s)" % PMC_JSON
     rec = json.load(open(path))
+    if bool(rec.get("block_basis", False)) != bool(block):
+        return None, "PMC passes taken in another CG basis"
     if rec.get("recurrence") != recurrence or rec.get("fusion_layout", 0) != fusion:
         return None, "PMC passes taken with another recurrence / fusion layout"
     if rec.get("fold_mask", 0) != fold_mask:
@@ -837,6 +884,39 @@ def time_matvec(K, n, m, d, fold_mask, torch, dev, reps=5):
             "launch_frac_hbm": [16.0 * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS for t in pos]}
 
 
+def time_block_matvec(K, n, m, d, torch, dev, reps=5):
+    """The same operator in the parity-block basis (what the CG iterations
+    apply): y_b = (P K P^T) x_b with x_b resident in
+    the block layout, d - 1 launches (gg_kron_block_matvec_timed, HIP events
+    per launch).  Bytes: 2 passes per launch (in place; the pair launch reads
+    its slab once and writes it once) = 16 N (d - 1); FLOP n m per h x h
+    factor applied (the same MFMA work as the folded grid-basis matvec)."""
+    dk = K._device()
+    x = grid_rhs_device(m, d, torch, dev)
+    y = torch.empty_like(x)
+    dk.block_matvec(x, out=y)    # warm-up (and the scratch allocation)
+    torch.cuda.synchronize()
+    per, tot = dk.block_matvec_timed(x, y, reps)
+    del x, y
+    dk.release_work()
+    L = d - 1
+    ms = tot / reps
+    byts = 16.0 * n * L
+    flop = float(sum(block_launch_flops(n, m, d)))
+    pos = [t / reps for t in per]
+    return {"reps": reps, "ms": ms, "launch_ms": pos, "launches": L,
+            "ms_source": "HIP events around every launch on the library's stream "
+                         "(gg_kron_block_matvec_timed)",
+            "algorithmic_bytes": byts, "passes": 2 * L, "flop": flop,
+            "achieved_gbs": byts / (ms * 1e-3) / 1e9,
+            "frac_hbm": byts / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "achieved_tflops": flop / (ms * 1e-3) / 1e12,
+            "frac_mfma": flop / (ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+            "launch_frac_mfma": [f / (t * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS
+                                 for f, t in zip(block_launch_flops(n, m, d), pos)],
+            "launch_frac_hbm": [16.0 * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS for t in pos]}
+
+
 # ---------------------------------------------------------------- main
 def main():
     a = parse()
@@ -909,10 +989,11 @@ def main():
     ms_per_step = 1e3 * dt / a.steps
     per_pos = [t / n_mv for t in mode_ms]
     fold_mask = K._device().fold_mask()
+    block = solver.basis == "block"
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
-                                  solver.fusion, fold_mask, solver.xdefer, solver.rq)
+                                  solver.fusion, fold_mask, solver.xdefer, solver.rq, block)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
-                               fold_mask, solver.xdefer, solver.rq)
+                               fold_mask, solver.xdefer, solver.rq, block)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -934,6 +1015,8 @@ def main():
                    "cg_fusion_layout": solver.fusion,
                    "cg_x_deferred": solver.xdefer,
                    "cg_rq_identity": solver.rq,
+                   "cg_basis": solver.basis,
+                   "launches_per_iteration": solver.launches(),
                    "fold_mask": fold_mask,
                    "timed_region": "exactly `steps` fused CG iterations continuing the "
                                    "warm-up's open recurrence; the once-per-solve closing "
@@ -948,6 +1031,9 @@ def main():
     if a.matvec > 0:
         result["matvec"] = time_matvec(K, n, m, d, fold_mask, torch, dev, a.matvec)
         torch.cuda.empty_cache()
+        if K._device().block_info()[0]:
+            result["block_matvec"] = time_block_matvec(K, n, m, d, torch, dev, a.matvec)
+            torch.cuda.empty_cache()
     if a.lanczos > 0:
         result["lanczos"] = time_lanczos(K, s, a.lanczos, torch, n, m, d, fold_mask)
         torch.cuda.empty_cache()

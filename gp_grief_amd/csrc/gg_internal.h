@@ -161,6 +161,9 @@ struct MpFuse {
   // w = coef[2] Y + coef[3] u + coef[4] u_prev, stored to p_out (over u_prev,
   // element-wise in place), its block partial |w|^2 to rr_part
   const double* coef = nullptr;
+  // block-basis CG (gg_kronb.hip): the pair launch's output q (the chain runs
+  // in place on q_old, the last launch cannot)
+  double* blk_q_out = nullptr;
 };
 
 // Output address map of a mode product (see gg_kron.hip epilogue):
@@ -196,5 +199,28 @@ void launch_reduce_to(const double* partials, int64_t count, double* out, hipStr
 // x_defer 2, one half of the active pair (sc->xh; [0, H) or [H, n)) as a
 // streaming kernel sized to sit beside the ring mode products (gg_vec.hip)
 void launch_x_half(double* x, int64_t n, int64_t H, const CgScalars* sc, hipStream_t s);
+
+// ---- the Kronecker operator in its parity-block basis (gg_kronb.hip) ----
+struct BlockOp;
+// nullptr when the operator has no block form (a factor not square, of odd
+// order or not centrosymmetric; d outside 2..6; the last two orders unequal or
+// without a pair kernel; GG_KRON_BLOCK=0 at creation)
+BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
+                      const double* const* factors);
+void block_destroy(BlockOp* B);
+int64_t block_n(const BlockOp* B);
+int block_d(const BlockOp* B);
+int block_launches(const BlockOp* B);   // launches per matvec (d - 1)
+// x (C order over the factors) -> P x in the block layout (inverse: back);
+// sq_part (forward only, may be NULL): block_fold_partials(B) partials of |P x|^2
+void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, double* sq_part,
+                hipStream_t s);
+int64_t block_fold_partials(const BlockOp* B);
+void block_apply(const BlockOp* B, const double* x, double* y, double shift, double* work,
+                 double* dot_partials, const int* skip, hipStream_t stream, int64_t* n_partials,
+                 const MpFuse* cg, int cgp, hipEvent_t* ev);
+int64_t block_prologue_blocks(const BlockOp* B);
+int64_t block_partials_needed(const BlockOp* B);
+int64_t block_side_half(int64_t n);
 
 }  // namespace gg

@@ -1027,6 +1027,7 @@ static void pack_fold(const double* K, int64_t m, bool transpose, Factor& f) {
 struct gg_kron {
   int d = 0;
   std::vector<gg::Factor> fwd, bwd;  // operator and transposed operator
+  gg::BlockOp* blk = nullptr;        // parity-block basis (gg_kronb.hip), when it exists
   int64_t n_rows = 1, n_cols = 1;
   int64_t max_inter_fwd = 0, max_inter_bwd = 0;
   bool square_steps_fwd = true, square_steps_bwd = true;
@@ -1339,6 +1340,7 @@ int64_t kron_work_elems(const gg_kron* K, bool transpose) {
 bool kron_first_single_launch(const gg_kron* K) { return K->fwd[0].JT <= kMaxJT; }
 
 int64_t kron_n(const gg_kron* K) { return K->n_rows; }
+const BlockOp* kron_block(const gg_kron* K) { return K->blk; }
 int kron_d(const gg_kron* K) { return K->d; }
 // x_defer mode 2: the side jobs' half boundary of an n-vector (d >= 4: two
 // launches per half, quarters of 2 ceil(n / 8) elements; else one launch per
@@ -1400,6 +1402,7 @@ int gg_kron_create(int d, const int64_t* rows, const int64_t* cols,
       }
       gg::plan_sizes(K->fwd, K->n_cols, K->max_inter_fwd, K->square_steps_fwd);
       gg::plan_sizes(K->bwd, K->n_rows, K->max_inter_bwd, K->square_steps_bwd);
+      K->blk = gg::block_create(d, rows, cols, factors_host);
     } catch (...) {
       gg_kron_destroy(K);
       throw;
@@ -1418,6 +1421,7 @@ int gg_kron_destroy(gg_kron* K) {
         if (f.ffrag) (void)hipFree(f.ffrag);
         if (f.rfrag) (void)hipFree(f.rfrag);
       }
+    gg::block_destroy(K->blk);
     delete K;
   });
 }
@@ -1480,6 +1484,75 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
           float ms = 0.f;
           GG_HIP(hipEventElapsedTime(&ms, ev[(size_t)r * (d + 1) + k],
                                      ev[(size_t)r * (d + 1) + k + 1]));
+          launch_ms_host[k] += ms;
+        }
+      float tot = 0.f;
+      GG_HIP(hipEventElapsedTime(&tot, ev.front(), ev.back()));
+      *total_ms_host = tot;
+    } catch (...) {
+      release();
+      throw;
+    }
+    release();
+  });
+}
+
+// ------------------------------------------------ parity-block basis (P1)
+int gg_kron_block_info(const gg_kron* K, int* available, int64_t* n, int* launches) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && available != nullptr, GG_ERR_VALUE, "NULL argument");
+    *available = K->blk != nullptr ? 1 : 0;
+    if (n) *n = K->blk ? gg::block_n(K->blk) : 0;
+    if (launches) *launches = K->blk ? gg::block_launches(K->blk) : 0;
+  });
+}
+
+int gg_kron_block_fold(const gg_kron* K, int inverse, const double* x_dev, double* y_dev,
+                       gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(K->blk != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    GG_REQUIRE(x_dev != y_dev, GG_ERR_VALUE, "x and y must not alias");
+    gg::block_fold(K->blk, inverse != 0, x_dev, y_dev, nullptr, gg::as_stream(stream));
+  });
+}
+
+int gg_kron_block_matvec(const gg_kron* K, const double* x_dev, double* y_dev, double shift,
+                         double* work_dev, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(K->blk != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    gg::block_apply(K->blk, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
+                    gg::as_stream(stream), nullptr, nullptr, 0, nullptr);
+  });
+}
+
+int gg_kron_block_matvec_timed(const gg_kron* K, const double* x_dev, double* y_dev,
+                               double shift, double* work_dev, int reps, double* launch_ms_host,
+                               double* total_ms_host, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev && launch_ms_host && total_ms_host && reps >= 1,
+               GG_ERR_VALUE, "bad argument");
+    GG_REQUIRE(K->blk != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    hipStream_t s = gg::as_stream(stream);
+    const int L = gg::block_launches(K->blk);
+    std::vector<hipEvent_t> ev((size_t)reps * (L + 1), nullptr);
+    auto release = [&] {
+      for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    };
+    try {
+      for (auto& e : ev) GG_HIP(hipEventCreate(&e));
+      for (int r = 0; r < reps; ++r)
+        gg::block_apply(K->blk, x_dev, y_dev, shift, work_dev, nullptr, nullptr, s, nullptr,
+                        nullptr, 0, ev.data() + (size_t)r * (L + 1));
+      GG_HIP(hipStreamSynchronize(s));
+      for (int k = 0; k < L; ++k) launch_ms_host[k] = 0.0;
+      for (int r = 0; r < reps; ++r)
+        for (int k = 0; k < L; ++k) {
+          float ms = 0.f;
+          GG_HIP(hipEventElapsedTime(&ms, ev[(size_t)r * (L + 1) + k],
+                                     ev[(size_t)r * (L + 1) + k + 1]));
           launch_ms_host[k] += ms;
         }
       float tot = 0.f;

@@ -1,0 +1,1446 @@
+// The Kronecker operator in its parity-block basis.
+//
+// Reference: KronMatrix.kronvec_prod, gp_grief/tensors/kron_matrix.py:52-97
+// (y = (K_0 (x) ... (x) K_{d-1}) x, one BLAS3 product per factor).  This
+// translation unit applies the SAME operator after an orthogonal change of
+// basis; the change is an execution detail of that product.
+//
+// A centrosymmetric factor F (J F J = F, J the index reversal -- every
+// stationary kernel on an evenly spaced grid) of even order m = 2h commutes
+// with J, so in the basis u_i = (x_i + x_{m-1-i}) / sqrt 2, v_i = (x_i -
+// x_{m-1-i}) / sqrt 2 (i < h) it is block diagonal: diag(S, T) with
+//     S[j][i] = F[j][i] + F[j][m-1-i],   T[j][i] = F[j][i] - F[j][m-1-i].
+// With every factor in that basis the whole operator is block diagonal over
+// the 2^d parity patterns beta = (beta_0 .. beta_{d-1}):
+//     P K P^T = diag_beta( F_0^{beta_0} (x) ... (x) F_{d-1}^{beta_{d-1}} ),
+// F^0 = S, F^1 = T, each block a Kronecker product of h x h matrices.  P is
+// orthogonal, so a CG run in this basis takes the same iterates (P x) up to
+// rounding; the fold x -> P x and the unfold run once per solve.
+//
+// Layout in HBM ("block layout"): block beta (index B = sum_k beta_k 2^{d-1-k},
+// slowest) of n_b = prod h_k elements, C order over (i'_0, ..., i'_{d-1}).
+//
+// Why: the fold makes each factor's h x h matrix an ordinary dense GEMM (no
+// mirrored rows inside the kernels), and it makes the two innermost axes of a
+// block one contiguous h x h SLAB (80 KB at h = 100) -- small enough that one
+// launch applies BOTH of their factors, Z = F_{d-2} X F_{d-1}^T, with the
+// intermediate held in registers.  A matvec is then d - 1 launches over the
+// vector instead of d (6 passes instead of 8 at d = 4), every one in place
+// (no rotation of axes, no scratch buffer for the chain):
+//   * blk_mode_kernel, axes 0 .. d-3: Y[o][j][c] = sum_i F[j][i] X[o][i][c]
+//     per block (the axis's rows strided by the inner extent); a wave owns 16
+//     columns c and every output row j, the factor's A fragments sit in LDS,
+//     the column data streams from HBM straight into the B operand;
+//   * blk_pair_kernel, axes d-2, d-1: per slab Z = F_{d-2} X F_{d-1}^T, two
+//     waves per slab (each half of the output columns), W = X F^T in
+//     registers feeding the second GEMM as its B operand.
+// Both run FP64 MFMA (v_mfma_f64_16x16x4_f64, the 4-row / 4-column tails of
+// h = 16 TF + 4 on v_mfma_f64_4x4x4_4b_f64) and carry the fused CG's vector
+// work like the folded kernels do (prologue on the first launch, the x side
+// job on the second, q = K p + s p with the dots on the last).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <vector>
+
+#include "gg_internal.h"
+
+namespace gg {
+
+typedef double bd4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlkMaxD = 6;        // 2^d corner values per fold thread
+constexpr int kBlkModeWaves = 12;  // waves per blk_mode_kernel workgroup (3 / SIMD)
+constexpr int kBlkPairWaves = 4;   // waves per blk_pair_kernel workgroup (2 slabs)
+
+struct BlockOp {
+  int d = 0;
+  int64_t m[kBlkMaxD] = {}, h[kBlkMaxD] = {};
+  int64_t nb = 0, n = 0;          // block size, vector length (2^d nb)
+  // A / B fragments of S (parity 0) and T (1) per axis: [KS][JT][64] doubles,
+  // frag(s, t, l) = F[16 t + (l & 15)][4 s + (l >> 4)] for full tiles, the tail
+  // tile (T4) F[16 (JT-1) + (l & 3)][4 s + (l >> 4)] (rows replicated over the
+  // four 4x4 blocks of v_mfma_f64_4x4x4_4b_f64); zero outside h x h
+  double* frag[kBlkMaxD][2] = {};
+  int KS[kBlkMaxD] = {}, JT[kBlkMaxD] = {};
+  bool T4[kBlkMaxD] = {};
+  int pTF = 0;   // pair axes: h = 16 pTF + 4
+  int cus = 256;
+  bool fast = true;   // blk_mode_fast_kernel where instantiated (GG_BLK_MODE_FAST=0: off)
+};
+
+// ------------------------------------------------------------------ fold
+// Thread per mirror group (i'_0 .. i'_{d-1}): the 2^d corners x[..., i_k or
+// m_k-1-i_k, ...] -> the 2^d blocks at offset i' by a Walsh-Hadamard
+// transform over the d parity bits, scaled by 2^{-d/2} (orthogonal; its own
+// inverse).  Consecutive threads take consecutive i'_{d-1}: the corner reads
+// are ascending or descending runs, the block writes ascending runs.
+struct FoldGeom {
+  int d;
+  int64_t m[kBlkMaxD], h[kBlkMaxD], stride[kBlkMaxD];
+  int64_t nb;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void blk_fold_kernel(const double* __restrict__ x,
+                                                       double* __restrict__ y, FoldGeom g,
+                                                       int inverse, double scale,
+                                                       double* __restrict__ sq_part) {
+  constexpr int C = 1 << D;
+  double acc = 0.0;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.nb;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, span[D];
+    int64_t rem = t;
+#pragma unroll
+    for (int k = D - 1; k >= 0; --k) {
+      const int64_t i = rem % g.h[k];
+      rem /= g.h[k];
+      lo += i * g.stride[k];
+      span[k] = (g.m[k] - 1 - 2 * i) * g.stride[k];   // low -> mirrored corner
+    }
+    double v[C];
+    if (!inverse) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        int64_t o = lo;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          if ((c >> (D - 1 - k)) & 1) o += span[k];
+        v[c] = x[o];
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) v[c] = x[(int64_t)c * g.nb + t];
+    }
+#pragma unroll
+    for (int b = 1; b < C; b <<= 1)
+#pragma unroll
+      for (int c = 0; c < C; ++c)
+        if (!(c & b)) {
+          const double a0 = v[c], a1 = v[c | b];
+          v[c] = a0 + a1;
+          v[c | b] = a0 - a1;
+        }
+    if (!inverse) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const double w = v[c] * scale;
+        y[(int64_t)c * g.nb + t] = w;
+        acc = fma(w, w, acc);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        int64_t o = lo;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+          if ((c >> (D - 1 - k)) & 1) o += span[k];
+        y[o] = v[c] * scale;
+      }
+    }
+  }
+  if (sq_part != nullptr) {
+    // deterministic per-block partial of |P x|^2 (the CG's starting r.r)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) sq_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
+}
+
+// wave-uniform byte address (SGPRs through readfirstlane) -- loads and
+// stores below take the form base (SGPR pair) + a 32-bit lane byte offset, so
+// the per-access address arithmetic is scalar and the few lane offsets are
+// the only address VGPRs (the accumulators of W fill the register budget)
+__device__ __forceinline__ char* ubase(const void* p, int64_t off) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p) + (uint64_t)off;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<char*>(((uint64_t)hi << 32) | lo);
+}
+// through address-space-1 pointers: global_load / global_store (a generic
+// pointer gives FLAT instructions, whose out-of-order completion makes the
+// compiler wait for vmcnt(0) and lgkmcnt(0) before every use)
+typedef __attribute__((address_space(1))) char gchar;
+typedef __attribute__((address_space(1))) double gdouble;
+__device__ __forceinline__ double ldu(const void* p, int64_t uoff, uint32_t voff) {
+  gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
+  return *reinterpret_cast<const gdouble*>(b + voff);
+}
+__device__ __forceinline__ void stu(void* p, int64_t uoff, uint32_t voff, double v) {
+  gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
+  *reinterpret_cast<gdouble*>(b + voff) = v;
+}
+// 16-byte global accesses (per-lane addresses)
+typedef double gd2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) gd2v gd2;
+__device__ __forceinline__ double2 ld2g(const double* p) {
+  const gd2v v = *reinterpret_cast<const gd2*>(reinterpret_cast<uintptr_t>(p));
+  return double2{v.x, v.y};
+}
+__device__ __forceinline__ void st2g(double* p, double2 v) {
+  *reinterpret_cast<gd2*>(reinterpret_cast<uintptr_t>(p)) = gd2v{v.x, v.y};
+}
+
+// ------------------------------------------------- in-place mode product
+// Axis k <= d-3 of every block, in place: Y[o][j][c] = sum_i F[j][i] X[o][i][c]
+// (F = S_k or T_k by the block's parity bit for axis k; X may equal Y).
+//
+// A wave owns a strip of 16 columns c (inner % 16 == 0) and all h output
+// rows: MFMA A = F fragments (LDS), B = the strip's rows 4 s .. 4 s + 3
+// (lane l reads X[4 s + (l >> 4)][c0 + (l & 15)]: four 128-B row segments per
+// wave instruction, every byte used once), D tile t: lane 16 g + n holds
+// rows 16 t + 4 r + g (r = 0..3) of column c0 + n.  The k-steps of the
+// wave's strips form one stream, loaded kDepth steps ahead into a register
+// ring, so HBM latency spans strip boundaries.
+//
+// Work: groups of kBlkModeWaves strips inside one block (one factor per
+// group); each workgroup takes a contiguous range of groups (it crosses at
+// most a block boundary or two) and restages the factor's fragments into LDS
+// when the parity changes.  One workgroup per CU (the fragments: KS x JT x
+// 512 B, 89.6 KB at h = 100).
+//
+// KIND 0: plain.  KIND 1: the fused CG prologue (gg_vec.hip layout 0): X holds
+// p_old; per element r -= alpha q_old when pending (written back, r.r
+// partial), p_new = r + beta p_old (first: r) written to fz.p_out, p_new.q_old
+// partial; the MFMA B operand is p_new; Y (the q buffer) is written over
+// q_old at the same positions after this wave has read them.  KIND 2: plain
+// plus the balanced x side job (x += c0 p0 + c1 p1 over half sc->xh of x),
+// one slice of it per strip.
+struct ModeArgs {
+  const double* X;
+  double* Y;
+  const double* fS;
+  const double* fT;
+  int h, KS;
+  int64_t inner;    // elements per row of the axis (product of the later h)
+  int64_t spb;      // strips per block
+  int64_t gpb;      // strip groups per block
+  int64_t ngroups;  // 2^d gpb
+  int64_t per_wg;   // groups per workgroup (contiguous ranges)
+  int64_t nb;       // block size
+  int bitpos;       // parity bit of the axis in the block index
+  const int* skip;
+  // CG prologue (KIND 1)
+  double* r;
+  const double* q_old;
+  double* p_out;
+  const CgScalars* sc;
+  double* rr_part;    // [grid] r.r, [pqo_stride + grid] p_new.q_old
+  int64_t pqo_stride;
+  // side job (KIND 2): x += c0 p0 + c1 p1 over [soff, soff + sn) (half 0) or
+  // [soff_h1, soff_h1 + sn_h1) (half 1); each strip slot takes sstep elements
+  double* sx;
+  int64_t soff, sn, soff_h1, sn_h1, sstep;
+};
+
+template <int JT, bool T4, int KIND>
+__global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArgs a) {
+  constexpr int W = kBlkModeWaves;
+  constexpr int TF = T4 ? JT - 1 : JT;   // full 16-row tiles
+  constexpr int kDepth = 8;              // k-steps in flight per wave
+  constexpr int NV = KIND == 1 ? 3 : 1;  // streams per element
+  constexpr int kSD = 2;                 // side-job k-steps in flight
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (a.skip != nullptr && *a.skip) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n16 = lane & 15, kq = lane >> 4;
+  const int64_t g0 = (int64_t)blockIdx.x * a.per_wg;
+  const int64_t g1 = min(a.ngroups, g0 + a.per_wg);
+  const int KS = a.KS;
+  const int64_t cpr = a.inner >> 4;   // strips per row of the axis
+  // lane byte offset of element (row kq, column n16) from a strip's row 4 s
+  uint32_t o_e = (uint32_t)(((int64_t)kq * a.inner + n16) * 8);
+  asm volatile("" : "+v"(o_e));
+  const int64_t rstep = a.inner * 32;   // bytes from k-step s to s + 1
+
+  // a strip cursor: group g -> (block B, local group lg, outer o, column
+  // strip cs); advanced one group at a time without divisions
+  struct Cur {
+    int64_t B, lg, o, cs;
+  };
+  auto cur_at = [&](int64_t g) {
+    Cur c;
+    c.B = g / a.gpb;
+    c.lg = g - c.B * a.gpb;
+    const int64_t ls = c.lg * W + wave;
+    c.o = ls / cpr;
+    c.cs = ls - c.o * cpr;
+    return c;
+  };
+  auto cur_next = [&](Cur& c) {
+    if (++c.lg == a.gpb) {
+      c.lg = 0;
+      ++c.B;
+      c.o = 0;
+      c.cs = wave;   // W < cpr (inner >= 400)
+    } else {
+      c.cs += W;
+      if (c.cs >= cpr) {
+        c.cs -= cpr;
+        ++c.o;
+      }
+    }
+  };
+  // element offset of the strip (row 0, column 0); a strip past the block's
+  // last one (a partial last group) reads the last valid strip, never stored
+  auto cur_base = [&](const Cur& c) -> int64_t {
+    int64_t o = c.o, cs = c.cs;
+    if (c.lg * W + wave >= a.spb) {
+      o = (a.spb - 1) / cpr;
+      cs = (a.spb - 1) - o * cpr;
+    }
+    return c.B * a.nb + o * (int64_t)a.h * a.inner + (cs << 4);
+  };
+  auto cur_valid = [&](const Cur& c) -> bool { return c.lg * W + wave < a.spb; };
+
+  // CG prologue state
+  bool first = false, pending = false, pqo_on = false;
+  double beta = 0.0, alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
+  if (KIND == 1) {
+    first = a.sc->first != 0;
+    beta = a.sc->beta;
+    pending = a.sc->pending != 0;
+    alpha = a.sc->alpha;
+    pqo_on = a.pqo_stride > 0 && !first;
+  }
+  // side job state
+  double sc0 = 0.0, sc1 = 0.0;
+  const double* sp0 = nullptr;
+  const double* sp1 = nullptr;
+  double* sxo = nullptr;
+  int64_t slen = 0;
+  if (KIND == 2) {
+    const int xh = a.sc->xh;
+    if (xh < 2) {
+      const int64_t off = xh ? a.soff_h1 : a.soff;
+      slen = xh ? a.sn_h1 : a.sn;
+      sc0 = a.sc->xc[0];
+      sc1 = a.sc->xc[1];
+      sp0 = a.sc->xp[0] + off;
+      sp1 = a.sc->xp[1] + off;
+      sxo = a.sx + off;
+    }
+  }
+
+  bd4 acc[TF > 0 ? TF : 1];
+  double acc4 = 0.0;
+  auto zero = [&] {
+#pragma unroll
+    for (int t = 0; t < (TF > 0 ? TF : 1); ++t) acc[t] = bd4{0.0, 0.0, 0.0, 0.0};
+    acc4 = 0.0;
+  };
+
+  // segments of groups whose blocks share the axis's parity: the factor
+  // fragments are staged once per segment, the k-step pipeline runs inside
+  int64_t sg0 = g0;
+  while (sg0 < g1) {
+    const int64_t B0 = sg0 / a.gpb;
+    const int par = (int)((B0 >> a.bitpos) & 1);
+    const int64_t Bend = ((B0 >> a.bitpos) + 1) << a.bitpos;   // first block of the next parity run
+    const int64_t sg1 = min(g1, Bend * a.gpb);
+    // stage the factor (every wave done with the previous one)
+    __syncthreads();
+    {
+      const double* src = par ? a.fT : a.fS;
+      const int nd = KS * JT * 64;
+      for (int i = threadIdx.x * 2; i < nd; i += 64 * W * 2)
+        *reinterpret_cast<double2*>(lds + i) = *reinterpret_cast<const double2*>(src + i);
+    }
+    __syncthreads();
+
+    const int64_t nsteps = (sg1 - sg0) * KS;
+    // load cursor
+    Cur lc = cur_at(sg0);
+    int ld_s = 0;
+    int64_t ld_n = 0;   // steps issued
+    double ring[kDepth][NV];
+    auto issue = [&](int slot) {
+      const int64_t base = cur_base(lc);
+      // rows past h (a partial last k-step) read row 0: zeroed when consumed
+      const bool in = 4 * ld_s + kq < a.h;
+      const int64_t ub = base * 8 + (int64_t)ld_s * rstep;
+      const int64_t ubr = in ? ub : base * 8;
+      const uint32_t vo = in ? o_e : (uint32_t)(n16 * 8);
+      ring[slot][0] = ldu(a.X, ubr, vo);
+      if (KIND == 1) {
+        ring[slot][1] = ldu(a.r, ubr, vo);
+        ring[slot][2] = ldu(a.q_old, ubr, vo);
+      }
+      ++ld_n;
+      if (++ld_s == KS) {
+        ld_s = 0;
+        cur_next(lc);
+      }
+    };
+    // side ring: slot q = g W + wave owns [q sstep, (q + 1) sstep) of the
+    // half; k-step s of the strip carries the double2 at q sstep + 128 s + 2 lane
+    double2 sring[kSD][3];
+    int64_t sl_g = sg0;
+    int sl_s = 0;
+    auto side_elem = [&](int64_t g, int s) -> int64_t {
+      const int64_t q0 = (g * W + wave) * a.sstep;
+      const int64_t e = q0 + 128 * (int64_t)s + 2 * lane;
+      const int64_t hi = min(slen, q0 + a.sstep);
+      return (e + 1 < hi) ? e : -1;
+    };
+    auto side_issue = [&](int slot) {
+      const int64_t e = (KIND == 2 && slen > 0 && sl_g < sg1) ? side_elem(sl_g, sl_s) : -1;
+      if (e >= 0) {
+        sring[slot][0] = *reinterpret_cast<const double2*>(sxo + e);
+        sring[slot][1] = *reinterpret_cast<const double2*>(sp0 + e);
+        sring[slot][2] = *reinterpret_cast<const double2*>(sp1 + e);
+      }
+      if (++sl_s == KS) {
+        sl_s = 0;
+        ++sl_g;
+      }
+    };
+
+#pragma unroll
+    for (int u = 0; u < kDepth; ++u)
+      if ((int64_t)u < nsteps) issue(u);
+    if (KIND == 2) {
+#pragma unroll
+      for (int u = 0; u < kSD; ++u) side_issue(u);
+    }
+    zero();
+    Cur cc = cur_at(sg0);   // consume cursor
+    int cs_s = 0;
+    int64_t cs_g = sg0;
+    int64_t cs_base = cur_base(cc);
+    bool cs_valid = cur_valid(cc);
+
+    for (int64_t c0 = 0; c0 < nsteps; c0 += kDepth) {
+#pragma unroll
+      for (int u = 0; u < kDepth; ++u) {
+        if (c0 + u < nsteps) {
+          // B operand of k-step cs_s
+          const int i = 4 * cs_s + kq;
+          double xb = i < a.h ? ring[u][0] : 0.0;
+          if (KIND == 1) {
+            const bool ok = cs_valid && i < a.h;
+            double r = i < a.h ? ring[u][1] : 0.0;
+            const double q = i < a.h ? ring[u][2] : 0.0;
+            const int64_t ub = (cs_base + (int64_t)4 * cs_s * a.inner) * 8;
+            if (pending) {
+              r = r - alpha * q;
+              if (ok) {
+                stu(a.r, ub, o_e, r);
+                rr_acc = fma(r, r, rr_acc);
+              }
+            }
+            xb = first ? r : fma(beta, xb, r);
+            if (ok) {
+              stu(a.p_out, ub, o_e, xb);
+              if (pqo_on) pqo_acc = fma(xb, q, pqo_acc);
+            }
+            if (!(i < a.h)) xb = 0.0;
+          }
+          const double* fs = lds + ((int64_t)cs_s * JT) * 64 + lane;
+#pragma unroll
+          for (int t = 0; t < TF; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fs[t * 64], xb, acc[t], 0, 0, 0);
+          if (T4) acc4 = __builtin_amdgcn_mfma_f64_4x4x4f64(fs[TF * 64], xb, acc4, 0, 0, 0);
+          if (ld_n < nsteps) issue(u);
+          if (KIND == 2) {
+            // the side element of this k-step (loaded kSD steps ago; c0 is a
+            // multiple of kDepth, so the slot is u mod kSD)
+            const int64_t e = slen > 0 ? side_elem(cs_g, cs_s) : -1;
+            const double2 xv = sring[u & 1][0], p0 = sring[u & 1][1], p1 = sring[u & 1][2];
+            if (e >= 0) {
+              double2 o;
+              o.x = xv.x + (sc0 * p0.x + sc1 * p1.x);   // mp_side_job's expression
+              o.y = xv.y + (sc0 * p0.y + sc1 * p1.y);
+              *reinterpret_cast<double2*>(sxo + e) = o;
+            }
+            side_issue(u & 1);
+          }
+          if (++cs_s == KS) {
+            // epilogue: D tile t lane 16 g + n elem r -> row 16 t + 4 r + g;
+            // the 4x4 tail lane 16 r + n -> row 16 TF + r (column c0 + n)
+            if (cs_valid) {
+#pragma unroll
+              for (int t = 0; t < TF; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  // with a 4x4 tail every full tile is inside h; without,
+                  // the last tile may be padded
+                  if (T4 || 16 * t + 4 * r + kq < a.h)
+                    stu(a.Y, (cs_base + (int64_t)(16 * t + 4 * r) * a.inner) * 8, o_e,
+                        acc[t][r]);
+                }
+              if (T4 && 16 * TF + kq < a.h)
+                stu(a.Y, (cs_base + (int64_t)16 * TF * a.inner) * 8, o_e, acc4);
+            }
+            zero();
+            cs_s = 0;
+            ++cs_g;
+            cur_next(cc);
+            cs_base = cur_base(cc);
+            cs_valid = cur_valid(cc);
+          }
+        }
+      }
+    }
+    sg0 = sg1;
+  }
+  if (KIND == 1) {
+    __shared__ double red[2 * kBlkModeWaves];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      rr_acc += __shfl_xor(rr_acc, off, 64);
+      pqo_acc += __shfl_xor(pqo_acc, off, 64);
+    }
+    if (lane == 0) {
+      red[wave] = rr_acc;
+      red[W + wave] = pqo_acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < W; ++w) {
+        s0 += red[w];
+        s1 += red[W + w];
+      }
+      if (a.rr_part != nullptr) {
+        a.rr_part[blockIdx.x] = s0;
+        if (a.pqo_stride > 0) a.rr_part[a.pqo_stride + blockIdx.x] = s1;
+      }
+    }
+  }
+}
+
+// The production shape of blk_mode_kernel: h = 16 TF + 4 (KS = 4 TF + 1
+// k-steps, a 4-row tail), every memory operation unconditional so that the
+// compiler's wait counting stays exact across the whole stream (a wave-uniform
+// branch around a store or load makes it fall back to vmcnt(0) at the next
+// merge): strips past a block's end read a valid strip and store to a trash
+// slot, the prologue always stores r (unchanged when nothing is pending), the
+// side job's spare lanes store to the trash slot.  The k-step ring is kD =
+// KS mod-free deep (kD divides KS), so a step's slot is compile-time across
+// strips.  Work split, LDS fragments and fusions as blk_mode_kernel.
+__device__ __attribute__((aligned(16))) double g_blk_trash[6 * 64];
+
+// waves per workgroup of the fast kernel: 12 (3 per SIMD) for the plain
+// launch, 8 (2 per SIMD, 256 registers) for the fused ones
+template <int KIND>
+constexpr int fast_waves() {
+  return KIND == 0 ? 12 : 8;
+}
+
+template <int TF, int KIND>
+__global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kernel(ModeArgs a) {
+  constexpr int W = fast_waves<KIND>();
+  constexpr int JT = TF + 1;
+  constexpr int KS = 4 * TF + 1;
+  constexpr int kD = (KS % 5 == 0) ? 5 : (KS % 3 == 0) ? 3 : KS;   // ring depth, divides KS
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  if (a.skip != nullptr && *a.skip) return;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n16 = lane & 15, kq = lane >> 4;
+  const int64_t g0 = (int64_t)blockIdx.x * a.per_wg;
+  const int64_t g1 = min(a.ngroups, g0 + a.per_wg);
+  const int64_t cpr = a.inner >> 4;
+  uint32_t o_e = (uint32_t)(((int64_t)kq * a.inner + n16) * 8);
+  asm volatile("" : "+v"(o_e));
+  const int64_t rstep = a.inner * 32;
+  double* trash = g_blk_trash + 2 * lane;   // 16 bytes per lane: spare stores land here
+  // a store whose wave-uniform `valid` sends it to the trash slot instead:
+  // one store instruction either way (the wait counts stay fixed)
+  const uint32_t o_t = (uint32_t)(lane * 16);
+  auto stq = [&](bool valid, void* p, int64_t uoff, uint32_t voff, double v) {
+    void* bp = valid ? p : static_cast<void*>(g_blk_trash);
+    stu(bp, valid ? uoff : 0, valid ? voff : o_t, v);
+  };
+
+  struct Cur {
+    int64_t B, lg, o, cs;
+  };
+  auto cur_at = [&](int64_t g) {
+    Cur c;
+    c.B = g / a.gpb;
+    c.lg = g - c.B * a.gpb;
+    const int64_t ls = c.lg * W + wave;
+    c.o = ls / cpr;
+    c.cs = ls - c.o * cpr;
+    return c;
+  };
+  auto cur_next = [&](Cur& c) {
+    if (++c.lg == a.gpb) {
+      c.lg = 0;
+      ++c.B;
+      c.o = 0;
+      c.cs = wave;
+    } else {
+      c.cs += W;
+      if (c.cs >= cpr) {
+        c.cs -= cpr;
+        ++c.o;
+      }
+    }
+  };
+  // a strip past the block's last one reads the last valid strip
+  auto cur_base = [&](const Cur& c) -> int64_t {
+    int64_t o = c.o, cs = c.cs;
+    if (c.lg * W + wave >= a.spb) {
+      o = (a.spb - 1) / cpr;
+      cs = (a.spb - 1) - o * cpr;
+    }
+    return c.B * a.nb + o * (int64_t)a.h * a.inner + (cs << 4);
+  };
+  auto cur_valid = [&](const Cur& c) -> bool { return c.lg * W + wave < a.spb; };
+
+  bool first = false, pqo_on = false;
+  double beta = 0.0, alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
+  if (KIND == 1) {
+    first = a.sc->first != 0;
+    beta = a.sc->beta;
+    alpha = a.sc->pending != 0 ? a.sc->alpha : 0.0;   // not pending: r stays r
+    pqo_on = a.pqo_stride > 0 && !first;
+  }
+  const bool pending = KIND == 1 && a.sc->pending != 0;
+  double sc0 = 0.0, sc1 = 0.0;
+  const double* sp0 = a.sx;
+  const double* sp1 = a.sx;
+  double* sxo = a.sx;
+  int64_t slen = 0;
+  if (KIND == 2) {
+    const int xh = a.sc->xh;
+    if (xh < 2) {
+      const int64_t off = xh ? a.soff_h1 : a.soff;
+      slen = xh ? a.sn_h1 : a.sn;
+      sc0 = a.sc->xc[0];
+      sc1 = a.sc->xc[1];
+      sp0 = a.sc->xp[0] + off;
+      sp1 = a.sc->xp[1] + off;
+      sxo = a.sx + off;
+    }
+  }
+  // side element of (group g, step s): a valid even index (clamped) and
+  // whether this lane owns it
+  auto side_at = [&](int64_t g, int s, bool& own) -> int64_t {
+    const int64_t q0 = (g * W + wave) * a.sstep;
+    const int64_t e = q0 + 128 * (int64_t)s + 2 * lane;
+    const int64_t hi = min(slen, q0 + a.sstep);
+    own = e + 1 < hi;
+    return own ? e : 0;
+  };
+
+  int64_t sg0 = g0;
+  while (sg0 < g1) {
+    const int64_t B0 = sg0 / a.gpb;
+    const int par = (int)((B0 >> a.bitpos) & 1);
+    const int64_t Bend = ((B0 >> a.bitpos) + 1) << a.bitpos;
+    const int64_t sg1 = min(g1, Bend * a.gpb);
+    __syncthreads();
+    {
+      const double* src = par ? a.fT : a.fS;
+      constexpr int nd = KS * JT * 64;
+      for (int i = threadIdx.x * 2; i < nd; i += 64 * W * 2)
+        *reinterpret_cast<double2*>(lds + i) = *reinterpret_cast<const double2*>(src + i);
+    }
+    __syncthreads();
+
+    // load cursor: strip lc, its base; past the segment the last strip again
+    Cur lc = cur_at(sg0);
+    int64_t lg_n = sg0;
+    int64_t l_base = cur_base(lc);
+    double ring[kD][3];
+    double2 sring[kD][3];
+    auto issue = [&](int slot, int s) {
+      // k-step s of the load cursor's strip (s compile-time)
+      const int64_t ub = l_base * 8 + (int64_t)s * rstep;
+      ring[slot][0] = ldu(a.X, ub, o_e);
+      if (KIND == 1) {
+        ring[slot][1] = ldu(a.r, ub, o_e);
+        ring[slot][2] = ldu(a.q_old, ub, o_e);
+      }
+      if (KIND == 2) {
+        bool own;
+        const int64_t e = side_at(lg_n < sg1 ? lg_n : sg1 - 1, s, own);
+        sring[slot][0] = ld2g(sxo + e);
+        sring[slot][1] = ld2g(sp0 + e);
+        sring[slot][2] = ld2g(sp1 + e);
+      }
+    };
+    auto load_next_strip = [&] {
+      if (lg_n + 1 < sg1) {
+        cur_next(lc);
+        l_base = cur_base(lc);
+      }
+      ++lg_n;
+    };
+#pragma unroll
+    for (int u = 0; u < kD; ++u) issue(u, u);
+
+    Cur cc = cur_at(sg0);
+#pragma unroll 1
+    for (int64_t g = sg0; g < sg1; ++g) {
+      const int64_t cbase = cur_base(cc);
+      const bool cvalid = cur_valid(cc);
+      // the fragments' LDS offset, opaque per strip: the reads are not loop
+      // invariant (hoisted, 175 of them would not fit the registers)
+      uint32_t lo = (uint32_t)(lane * 8);
+      asm volatile("" : "+v"(lo));
+      const char* lb = reinterpret_cast<const char*>(lds) + lo;
+      bd4 acc[TF];
+      double acc4 = 0.0;
+#pragma unroll
+      for (int t = 0; t < TF; ++t) acc[t] = bd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int slot = s % kD;
+        // h = 16 TF + 4: every row 4 s + kq of the strip is inside h
+        double xb = ring[slot][0];
+        if (KIND == 1) {
+          double r = ring[slot][1];
+          const double q = ring[slot][2];
+          const int64_t ub = (cbase + (int64_t)4 * s * a.inner) * 8;
+          r = r - alpha * q;
+          const double rr = fma(r, r, rr_acc);
+          xb = first ? r : fma(beta, xb, r);
+          const double pqo = fma(xb, q, pqo_acc);
+          if (cvalid) {   // wave-uniform
+            if (pending) rr_acc = rr;
+            if (pqo_on) pqo_acc = pqo;
+          }
+          // stores unconditional: a spare strip's go to the trash slot
+          stq(cvalid, a.r, ub, o_e, r);
+          stq(cvalid, a.p_out, ub, o_e, xb);
+        }
+        const double* fs = reinterpret_cast<const double*>(lb + (s * JT) * 512);
+#pragma unroll
+        for (int t = 0; t < TF; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fs[t * 64], xb, acc[t], 0, 0, 0);
+        acc4 = __builtin_amdgcn_mfma_f64_4x4x4f64(fs[TF * 64], xb, acc4, 0, 0, 0);
+        if (KIND == 2) {
+          bool own;
+          const int64_t e = side_at(g, s, own);
+          const double2 xv = sring[slot][0], p0 = sring[slot][1], p1 = sring[slot][2];
+          double2 o;
+          o.x = xv.x + (sc0 * p0.x + sc1 * p1.x);   // mp_side_job's expression
+          o.y = xv.y + (sc0 * p0.y + sc1 * p1.y);
+          st2g(own ? sxo + e : trash, o);
+        }
+        // refill this slot with the step kD ahead (the next strip's when
+        // it wraps)
+        if (s + kD < KS) {
+          issue(slot, s + kD);
+        } else {
+          if (s + kD == KS) load_next_strip();
+          issue(slot, s + kD - KS);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // one k-step per scheduling region
+      }
+      // epilogue: tile t lane 16 g + n elem r -> row 16 t + 4 r + g; the tail
+      // lane 16 r + n -> row 16 TF + r (column c0 + n); spare strips to trash
+#pragma unroll
+      for (int t = 0; t < TF; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stq(cvalid, a.Y, (cbase + (int64_t)(16 * t + 4 * r) * a.inner) * 8, o_e, acc[t][r]);
+      stq(cvalid, a.Y, (cbase + (int64_t)16 * TF * a.inner) * 8, o_e, acc4);
+      cur_next(cc);
+    }
+    sg0 = sg1;
+  }
+  if (KIND == 1) {
+    __shared__ double red[2 * W];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      rr_acc += __shfl_xor(rr_acc, off, 64);
+      pqo_acc += __shfl_xor(pqo_acc, off, 64);
+    }
+    if (lane == 0) {
+      red[wave] = rr_acc;
+      red[W + wave] = pqo_acc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < W; ++w) {
+        s0 += red[w];
+        s1 += red[W + w];
+      }
+      if (a.rr_part != nullptr) {
+        a.rr_part[blockIdx.x] = s0;
+        if (a.pqo_stride > 0) a.rr_part[a.pqo_stride + blockIdx.x] = s1;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------- pair (slab) kernel
+// Axes d-2 and d-1 of every block together: slab s (h x h, contiguous) ->
+// Z = F2 X F3^T, F2 = F_{d-2}^{beta}, F3 = F_{d-1}^{beta}.  h = 16 TF + 4.
+//
+// Two waves per slab, each owning a set of output columns j: role 0 the full
+// 16-column tiles [0, JA) and the 4-column tail, role 1 the tiles [JA, TF).
+// GEMM 1, W[a][j] = sum_c X[a][c] F3[j][c] for the role's columns j and all
+// rows a: A = X rows (lane l: X[16 t + (l & 15)][4 s + (l >> 4)]; the 4-row
+// tail with its rows replicated over the 4x4 blocks), B = F3 fragments; W
+// stays in registers.  GEMM 2, Z[i][j] = sum_a F2[i][a] W[a][j]: a W tile's
+// accumulator IS the B operand of k-step s = 4 t_a + r (element r of lane
+// 16 g + n holds W[16 t_a + 4 r + g][16 t_j + n]), A = F2 fragments, one
+// 16-row strip of Z at a time.  The 4-column tail of W (lane 16 r + 4 g + c:
+// W[16 t_a + 4 g + r][16 TF + c]) becomes the tail's B operand by a 4-lane
+// group broadcast inside each 16-lane row (ds_swizzle).  Roles alternate per
+// slab so each wave averages the two.  Epilogue: Z (+ shift p, p.q and q.q
+// partials) straight from the accumulators.  Not in place (the two roles
+// read X while the other stores Z).
+struct PairArgs {
+  const double* X;
+  double* Y;
+  const double* f3S;   // F_{d-1} fragments [KS][TF+1][64]
+  const double* f3T;
+  const double* f2S;   // F_{d-2} fragments [KS][TF+1][64]
+  const double* f2T;
+  int64_t nslab;       // 2^d * slabs per block
+  int64_t spb;         // slabs per block
+  const double* P;     // epilogue: q = Z + shift * P, partials (nullptr: plain)
+  double shift;
+  double* partials;    // [grid] p.q, [pstride + grid] r.q (0), [2 pstride + grid] q.q
+  int64_t pstride;
+  const int* skip;
+};
+
+// swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
+// (b4, R1 R0, b1 b0) -- the 4-lane group R of its 16-lane row
+template <int R>
+__device__ __forceinline__ double bcast_group(double v) {
+  constexpr int pat = (R << 7) | 0x13;   // bitmask mode: and 0x13, or R << 2, xor 0
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+  return __hiloint2double(hi, lo);
+}
+
+template <int TF, int J0, int NJ, bool TJ>
+__device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, double& pq,
+                                          double& qq, float& junk) {
+  constexpr int H = 16 * TF + 4;
+  constexpr int KS = 4 * TF + 1;
+  constexpr int NJB = NJ + (TJ ? 1 : 0);   // B fragments per k-step
+  constexpr int64_t FS = (int64_t)(TF + 1) * 64 * 8;   // bytes per fragment k-step
+  const int lane = threadIdx.x & 63;
+  const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
+  // lane byte offsets (opaque: recomputed per slab, never hoisted as a set)
+  uint32_t o_x = (uint32_t)((n16 * H + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
+  uint32_t o_xt = (uint32_t)((l3 * H + kq) * 8);        // X tail rows 16 TF + l3
+  uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
+  uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
+  uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
+  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f), "+v"(o_z), "+v"(o_zt));
+  const int64_t blk = slab / A.spb;
+  const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
+  const double* f3 = par3 ? A.f3T : A.f3S;
+  const double* f2 = par2 ? A.f2T : A.f2S;
+  const int64_t sbyte = slab * (int64_t)H * H * 8;
+
+  // ---- GEMM 1: W = X F3^T (the role's columns)
+  bd4 W[TF][NJ > 0 ? NJ : 1];
+  double Wta[NJ > 0 ? NJ : 1];   // tail rows a = 16 TF .. +3, full column tiles
+  double Wj[TF];                 // full row tiles, tail columns (TJ)
+  double Wc = 0.0;               // corner (TJ)
+#pragma unroll
+  for (int t = 0; t < TF; ++t) {
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) W[t][u] = bd4{0.0, 0.0, 0.0, 0.0};
+    Wj[t] = 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) Wta[u] = 0.0;
+
+  auto ld1 = [&](int s, double (&xa)[TF + 1], double (&fb)[NJB > 0 ? NJB : 1]) {
+    const int64_t xs = sbyte + (int64_t)s * 32;
+#pragma unroll
+    for (int t = 0; t < TF; ++t) xa[t] = ldu(A.X, xs + (int64_t)t * 16 * H * 8, o_x);
+    xa[TF] = ldu(A.X, xs + (int64_t)TF * 16 * H * 8, o_xt);
+    const int64_t fs = (int64_t)s * FS;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) fb[u] = ldu(f3, fs + (int64_t)(J0 + u) * 512, o_f);
+    if (TJ) fb[NJ] = ldu(f3, fs + (int64_t)TF * 512, o_f);
+  };
+  auto mm1 = [&](const double (&xa)[TF + 1], const double (&fb)[NJB > 0 ? NJB : 1]) {
+#pragma unroll
+    for (int t = 0; t < TF; ++t)
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+        W[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[t], fb[u], W[t][u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < NJ; ++u)
+      Wta[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[u], Wta[u], 0, 0, 0);
+    if (TJ) {
+#pragma unroll
+      for (int t = 0; t < TF; ++t)
+        Wj[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[t], fb[NJ], Wj[t], 0, 0, 0);
+      Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
+    }
+  };
+  // L2 prefetch of X: k-step s reads columns 4 s .. 4 s + 3 of every row, so
+  // a row's 128-B line is first touched every fourth k-step -- one k-step of
+  // register prefetch does not cover that HBM miss.  Every pair of k-steps
+  // touches the lines two line columns ahead (4-byte loads, rows lane and
+  // 64 + lane); a touch's value is folded into a junk sum two pairs later,
+  // so it never makes a k-step wait (the sum is stored once per kernel)
+  auto touch = [&](int s, float& t0, float& t1) {
+    int cb = (s >> 2) + 2;
+    cb = cb < (H + 15) / 16 ? cb : (H + 15) / 16 - 1;
+    const int r1 = 64 + lane < H ? 64 + lane : H - 1;
+    t0 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
+        reinterpret_cast<uintptr_t>(A.X) + sbyte + ((int64_t)lane * H + 16 * cb) * 8);
+    t1 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
+        reinterpret_cast<uintptr_t>(A.X) + sbyte + ((int64_t)r1 * H + 16 * cb) * 8);
+  };
+  {
+    double xa0[TF + 1], fb0[NJB > 0 ? NJB : 1], xa1[TF + 1], fb1[NJB > 0 ? NJB : 1];
+    float ta0, ta1, tb0, tb1, tc0, tc1;
+    touch(0, ta0, ta1);
+    touch(4, tb0, tb1);
+    ld1(0, xa0, fb0);
+#pragma unroll 1
+    for (int s = 0; s + 1 < KS; s += 2) {
+      touch(s + 2, tc0, tc1);
+      ld1(s + 1, xa1, fb1);
+      mm1(xa0, fb0);
+      if (s + 2 < KS) ld1(s + 2, xa0, fb0);
+      mm1(xa1, fb1);
+      junk += (ta0 + ta1) * 0.0f;   // the touch of two pairs ago
+      ta0 = tb0;
+      ta1 = tb1;
+      tb0 = tc0;
+      tb1 = tc1;
+    }
+    junk += (ta0 + ta1 + tb0 + tb1) * 0.0f;
+    mm1(xa0, fb0);   // KS odd: the last k-step (loaded by the loop's last pass)
+  }
+
+  // ---- GEMM 2: Z = F2 W, one 16-row strip t_i at a time
+  const bool epi = A.P != nullptr;
+  const double sh = A.shift;
+  // k-step s: B operands from the accumulators
+  auto bfull = [&](int s, int u) -> double {
+    return s < 4 * TF ? W[s >> 2][u][s & 3] : Wta[u];
+  };
+  auto btail = [&](int s) -> double {
+    if (s >= 4 * TF) return Wc;
+    switch (s & 3) {
+      case 0: return bcast_group<0>(Wj[s >> 2]);
+      case 1: return bcast_group<1>(Wj[s >> 2]);
+      case 2: return bcast_group<2>(Wj[s >> 2]);
+      default: return bcast_group<3>(Wj[s >> 2]);
+    }
+  };
+  // one output element: q = Z (+ shift p, dots)
+  auto put = [&](int64_t ub, uint32_t vo, double z, double p) {
+    double q = z;
+    if (epi) {
+      q = fma(sh, p, q);
+      pq = fma(p, q, pq);
+      qq = fma(q, q, qq);
+    }
+    stu(A.Y, ub, vo, q);
+  };
+#pragma unroll 1
+  for (int ti = 0; ti < TF; ++ti) {
+    bd4 Z[NJ > 0 ? NJ : 1];
+    double Zt = 0.0;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) Z[u] = bd4{0.0, 0.0, 0.0, 0.0};
+    const int64_t zrow = sbyte + (int64_t)16 * ti * H * 8;   // row 16 ti
+    // epilogue operands issued now, consumed after the k-loop
+    double pv[NJ > 0 ? NJ : 1][4], pvt = 0.0;
+    if (epi) {
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pv[u][r] = ldu(A.P, zrow + (int64_t)(4 * r * H + 16 * (J0 + u)) * 8, o_z);
+      if (TJ) pvt = ldu(A.P, zrow + (int64_t)16 * TF * 8, o_zt);
+    }
+    const int64_t fti = (int64_t)ti * 512;
+    // A fragments kPF k-steps ahead; the scheduling barriers keep each step's
+    // loads / MFMAs in place
+    constexpr int kPF = 4;
+    double fr[kPF];
+#pragma unroll
+    for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const double f = fr[s % kPF];
+      if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+        Z[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, bfull(s, u), Z[u], 0, 0, 0);
+      if (TJ) Zt = __builtin_amdgcn_mfma_f64_4x4x4f64(f, btail(s), Zt, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // Z[u] lane 16 g + n elem r -> row 16 ti + 4 r + g, column 16 (J0 + u) + n;
+    // Zt lane 16 r + 4 b + c -> row 16 ti + 4 b + r, column 16 TF + c
+#pragma unroll
+    for (int u = 0; u < NJ; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        put(zrow + (int64_t)(4 * r * H + 16 * (J0 + u)) * 8, o_z, Z[u][r], epi ? pv[u][r] : 0.0);
+    if (TJ) put(zrow + (int64_t)16 * TF * 8, o_zt, Zt, pvt);
+  }
+  // tail rows i = 16 TF + r: A = F2's replicated tail fragment; the outputs of
+  // v_mfma_f64_4x4x4_4b_f64: lane 16 r + 4 b + c -> row 16 TF + r, column
+  // 16 (J0 + u) + 4 b + c; the corner (TJ) is replicated over b (b = 0 stores)
+  {
+    double Z4[NJ > 0 ? NJ : 1], Z4t = 0.0;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) Z4[u] = 0.0;
+    const int64_t zrow = sbyte + (int64_t)16 * TF * H * 8;
+    const int64_t fti = (int64_t)TF * 512;
+    constexpr int kPF = 4;
+    double fr[kPF];
+#pragma unroll
+    for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const double f = fr[s % kPF];
+      if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+        Z4[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(f, bfull(s, u), Z4[u], 0, 0, 0);
+      if (TJ) Z4t = __builtin_amdgcn_mfma_f64_4x4x4f64(f, btail(s), Z4t, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+      const int64_t ub = zrow + (int64_t)16 * (J0 + u) * 8;
+      put(ub, o_z, Z4[u], epi ? ldu(A.P, ub, o_z) : 0.0);
+    }
+    if (TJ && b4 == 0) {
+      // lane 16 r + c (b = 0): row 16 TF + r, column 16 TF + c
+      const int64_t ub = zrow + (int64_t)16 * TF * 8;
+      put(ub, o_zt, Z4t, epi ? ldu(A.P, ub, o_zt) : 0.0);
+    }
+  }
+}
+
+template <int TF, int JA>
+__global__ __launch_bounds__(64 * kBlkPairWaves, 2) void blk_pair_kernel(PairArgs A) {
+  if (A.skip != nullptr && *A.skip) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // wave pairs (2 w, 2 w + 1) share a slab; roles alternate per slab
+  const int64_t npairs = (int64_t)gridDim.x * (kBlkPairWaves / 2);
+  const int64_t pair = (int64_t)blockIdx.x * (kBlkPairWaves / 2) + (wave >> 1);
+  double pq = 0.0, qq = 0.0;
+  float junk = 0.0f;   // L2-prefetch touches (pair_slab)
+  int it = 0;
+  for (int64_t slab = pair; slab < A.nslab; slab += npairs, ++it) {
+    const int role = ((wave & 1) + it) & 1;
+    if (JA == TF) {
+      // a single role (TF = 1): the second wave of the pair idles
+      if ((wave & 1) == 0) pair_slab<TF, 0, JA, true>(A, slab, pq, qq, junk);
+    } else if (role == 0) {
+      pair_slab<TF, 0, JA, true>(A, slab, pq, qq, junk);
+    } else {
+      pair_slab<TF, JA, TF - JA, false>(A, slab, pq, qq, junk);
+    }
+  }
+  // keep the touches alive: one store per lane to the junk slot
+  reinterpret_cast<float*>(g_blk_trash)[lane] = junk;
+  if (A.partials != nullptr) {
+    __shared__ double red[2 * kBlkPairWaves];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      pq += __shfl_xor(pq, off, 64);
+      qq += __shfl_xor(qq, off, 64);
+    }
+    if (lane == 0) {
+      red[wave] = pq;
+      red[kBlkPairWaves + wave] = qq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < kBlkPairWaves; ++w) {
+        s0 += red[w];
+        s1 += red[kBlkPairWaves + w];
+      }
+      A.partials[blockIdx.x] = s0;
+      A.partials[A.pstride + blockIdx.x] = 0.0;
+      A.partials[2 * A.pstride + blockIdx.x] = s1;
+    }
+  }
+}
+
+// ------------------------------------------------------------- host side
+typedef void (*blk_mode_fn)(ModeArgs);
+typedef void (*blk_pair_fn)(PairArgs);
+
+
+
+template <int KIND>
+static blk_mode_fn mode_fn(int JT, bool T4) {
+#define GG_BLK_MODE(jt)                                                    \
+  case jt:                                                                 \
+    return T4 ? blk_mode_kernel<jt, true, KIND> : blk_mode_kernel<jt, false, KIND>;
+  switch (JT) {
+    GG_BLK_MODE(1)
+    GG_BLK_MODE(2)
+    GG_BLK_MODE(3)
+    GG_BLK_MODE(4)
+    GG_BLK_MODE(5)
+    GG_BLK_MODE(6)
+    GG_BLK_MODE(7)
+    default: return nullptr;
+  }
+#undef GG_BLK_MODE
+}
+template <int KIND>
+static blk_mode_fn mode_fast_fn(int JT) {
+  switch (JT) {
+    case 2: return blk_mode_fast_kernel<1, KIND>;
+    case 3: return blk_mode_fast_kernel<2, KIND>;
+    case 7: return blk_mode_fast_kernel<6, KIND>;
+    default: return nullptr;
+  }
+}
+// the fast (fixed-count) kernel where instantiated: a 4-row tail and
+// h = 16 (JT - 1) + 4 exactly (KS = 4 JT - 3)
+static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast = false) {
+  if (T4 && h == 16 * (JT - 1) + 4 && fast) {
+    const blk_mode_fn f = kind == 1 ? mode_fast_fn<1>(JT)
+                                    : kind == 2 ? mode_fast_fn<2>(JT) : mode_fast_fn<0>(JT);
+    if (f != nullptr) return f;
+  }
+  return kind == 1 ? mode_fn<1>(JT, T4) : kind == 2 ? mode_fn<2>(JT, T4) : mode_fn<0>(JT, T4);
+}
+
+// pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
+static blk_pair_fn select_pair(int TF) {
+  switch (TF) {
+    case 1: return blk_pair_kernel<1, 1>;
+    case 2: return blk_pair_kernel<2, 1>;
+    case 6: return blk_pair_kernel<6, 3>;
+    default: return nullptr;
+  }
+}
+
+static int blk_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    GG_HIP(hipGetDevice(&dev));
+    GG_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+static void blk_set_lds_limits(const BlockOp* B) {
+  for (int k = 0; k + 2 < B->d; ++k) {
+    const size_t bytes = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
+    for (int kind = 0; kind < 3; ++kind)
+      GG_HIP(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(
+              select_mode(kind, B->JT[k], B->T4[k], (int)B->h[k], B->fast)),
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  }
+}
+
+BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
+                      const double* const* factors) {
+  if (d < 2 || d > kBlkMaxD) return nullptr;
+  const char* env = getenv("GG_KRON_BLOCK");   // read once, at handle creation
+  if (env && atoi(env) == 0) return nullptr;
+  for (int k = 0; k < d; ++k) {
+    if (rows[k] != cols[k] || rows[k] % 2 != 0 || rows[k] < 2) return nullptr;
+    if (rows[k] / 2 > 112) return nullptr;   // blk_mode_kernel: JT <= 7
+  }
+  const int64_t hp = rows[d - 1] / 2;
+  if (rows[d - 2] != rows[d - 1] || (hp - 4) % 16 != 0) return nullptr;
+  const int TF = (int)((hp - 4) / 16);
+  if (select_pair(TF) == nullptr) return nullptr;
+  // centrosymmetric factors only (the test of gg_kron.hip pack_fold)
+  for (int k = 0; k < d; ++k) {
+    const int64_t m = rows[k];
+    const double* F = factors[k];
+    double amax = 0.0, dmax = 0.0;
+    for (int64_t j = 0; j < m; ++j)
+      for (int64_t i = 0; i < m; ++i) {
+        amax = std::max(amax, std::fabs(F[j * m + i]));
+        dmax = std::max(dmax, std::fabs(F[j * m + i] - F[(m - 1 - j) * m + (m - 1 - i)]));
+      }
+    if (!(dmax <= 16.0 * 2.220446049250313e-16 * amax) || !(amax > 0.0)) return nullptr;
+  }
+  BlockOp* B = new BlockOp();
+  try {
+    B->d = d;
+    B->nb = 1;
+    for (int k = 0; k < d; ++k) {
+      B->m[k] = rows[k];
+      B->h[k] = rows[k] / 2;
+      B->nb *= B->h[k];
+    }
+    B->n = B->nb << d;
+    B->pTF = TF;
+    B->cus = blk_cus();
+    const char* fe = getenv("GG_BLK_MODE_FAST");   // A/B knob, read at creation only
+    B->fast = !(fe && atoi(fe) == 0);
+    for (int k = 0; k < d; ++k) {
+      const int64_t m = B->m[k], h = B->h[k];
+      const double* F = factors[k];
+      // the centrosymmetric part (F + J F J) / 2, then S / T
+      auto Fc = [&](int64_t j, int64_t i) {
+        return 0.5 * (F[j * m + i] + F[(m - 1 - j) * m + (m - 1 - i)]);
+      };
+      int JT, KS;
+      bool T4;
+      if (k >= d - 2) {
+        JT = TF + 1;
+        T4 = true;
+      } else {
+        const int64_t tail = h % 16;
+        T4 = tail != 0 && tail <= 4;
+        JT = (int)ceil_div(h, 16);
+      }
+      KS = (int)ceil_div(h, 4);
+      B->JT[k] = JT;
+      B->KS[k] = KS;
+      B->T4[k] = T4;
+      const int TFk = T4 ? JT - 1 : JT;
+      for (int par = 0; par < 2; ++par) {
+        std::vector<double> hb((size_t)KS * JT * 64, 0.0);
+        for (int s = 0; s < KS; ++s)
+          for (int t = 0; t < JT; ++t)
+            for (int l = 0; l < 64; ++l) {
+              const bool tail = T4 && t == TFk;
+              const int64_t j = tail ? 16 * (int64_t)t + (l & 3) : 16 * (int64_t)t + (l & 15);
+              const int64_t i = 4 * (int64_t)s + (l >> 4);
+              double v = 0.0;
+              if (j < h && i < h)
+                v = par == 0 ? Fc(j, i) + Fc(j, m - 1 - i) : Fc(j, i) - Fc(j, m - 1 - i);
+              hb[((size_t)s * JT + t) * 64 + l] = v;
+            }
+        GG_HIP(hipMalloc(&B->frag[k][par], hb.size() * sizeof(double)));
+        GG_HIP(hipMemcpy(B->frag[k][par], hb.data(), hb.size() * sizeof(double),
+                         hipMemcpyHostToDevice));
+      }
+    }
+    for (int k = 0; k + 2 < d; ++k)
+      GG_REQUIRE(select_mode(0, B->JT[k], B->T4[k]) != nullptr, GG_ERR_RUNTIME,
+                 "no block mode kernel for this factor order");
+    blk_set_lds_limits(B);
+  } catch (...) {
+    block_destroy(B);
+    throw;
+  }
+  return B;
+}
+
+void block_destroy(BlockOp* B) {
+  if (!B) return;
+  for (int k = 0; k < kBlkMaxD; ++k)
+    for (int p = 0; p < 2; ++p)
+      if (B->frag[k][p]) (void)hipFree(B->frag[k][p]);
+  delete B;
+}
+
+int64_t block_n(const BlockOp* B) { return B->n; }
+int block_d(const BlockOp* B) { return B->d; }
+int block_launches(const BlockOp* B) { return B->d - 1; }
+
+static int fold_grid(const BlockOp* B) {
+  return (int)std::min<int64_t>(ceil_div(B->nb, 256), (int64_t)B->cus * 8);
+}
+int64_t block_fold_partials(const BlockOp* B) { return fold_grid(B); }
+
+void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, double* sq_part,
+                hipStream_t s) {
+  FoldGeom g{};
+  g.d = B->d;
+  g.nb = B->nb;
+  int64_t st = 1;
+  for (int k = B->d - 1; k >= 0; --k) {
+    g.m[k] = B->m[k];
+    g.h[k] = B->h[k];
+    g.stride[k] = st;
+    st *= B->m[k];
+  }
+  const double scale = std::ldexp(1.0, -B->d / 2) * ((B->d & 1) ? M_SQRT1_2 : 1.0);
+  const int grid = fold_grid(B);
+  double* sp = inverse ? nullptr : sq_part;
+  switch (B->d) {
+#define GG_BLK_FOLD(D)                                                                      \
+  case D:                                                                                   \
+    hipLaunchKernelGGL(blk_fold_kernel<D>, dim3(grid), dim3(256), 0, s, x, y, g,           \
+                       inverse ? 1 : 0, scale, sp);                                         \
+    break;
+    GG_BLK_FOLD(2)
+    GG_BLK_FOLD(3)
+    GG_BLK_FOLD(4)
+    GG_BLK_FOLD(5)
+    GG_BLK_FOLD(6)
+#undef GG_BLK_FOLD
+    default: GG_REQUIRE(false, GG_ERR_VALUE, "block basis: 2 <= d <= 6");
+  }
+  GG_LAUNCH_CHECK();
+}
+
+// grid of the mode-product launch of axis k (one workgroup per CU)
+// waves per workgroup of the launch select_mode picks
+static int mode_waves(int kind, const BlockOp* B, int k) {
+  const int JT = B->JT[k];
+  const bool fast = B->T4[k] && B->h[k] == 16 * (JT - 1) + 4 && B->fast &&
+                    (kind == 1 ? mode_fast_fn<1>(JT) : kind == 2 ? mode_fast_fn<2>(JT)
+                                                                : mode_fast_fn<0>(JT)) != nullptr;
+  if (!fast) return kBlkModeWaves;
+  return kind == 0 ? fast_waves<0>() : kind == 1 ? fast_waves<1>() : fast_waves<2>();
+}
+
+static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* grid_out) {
+  const int d = B->d;
+  int64_t inner = 1, outer = 1;
+  for (int i = k + 1; i < d; ++i) inner *= B->h[i];
+  for (int i = 0; i < k; ++i) outer *= B->h[i];
+  GG_REQUIRE(inner % 16 == 0, GG_ERR_VALUE, "block basis: inner extent not a multiple of 16");
+  a.h = (int)B->h[k];
+  a.KS = B->KS[k];
+  a.inner = inner;
+  a.spb = outer * (inner / 16);
+  a.gpb = ceil_div(a.spb, (int64_t)W);
+  a.ngroups = a.gpb << d;
+  const int64_t grid = std::min<int64_t>(a.ngroups, (int64_t)B->cus);
+  a.per_wg = ceil_div(a.ngroups, grid);
+  a.nb = B->nb;
+  a.bitpos = d - 1 - k;
+  a.fS = B->frag[k][0];
+  a.fT = B->frag[k][1];
+  const int64_t g = ceil_div(a.ngroups, a.per_wg);
+  *grid_out = (int)g;
+  return g;
+}
+
+int64_t block_prologue_blocks(const BlockOp* B) {
+  ModeArgs a{};
+  int g = 0;
+  if (B->d < 3) return 1;
+  mode_geometry(B, 0, mode_waves(1, B, 0), a, &g);
+  return g;
+}
+
+static int pair_grid(const BlockOp* B) {
+  int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) << B->d;
+  return (int)std::min<int64_t>(ceil_div(nslab, kBlkPairWaves / 2), (int64_t)B->cus * 2);
+}
+int64_t block_partials_needed(const BlockOp* B) { return pair_grid(B); }
+
+// y = (P K P^T + shift I) x in the block layout (x, y distinct; `work`: n
+// doubles of scratch when d >= 3 -- the in-place chain of axes 0..d-3 runs
+// there, x stays intact for the shift).  With the fused CG (cgp 2, layout 0,
+// cg != nullptr): the chain runs in place on y == cg->q_old (the prologue of
+// the first launch reads q_old before it writes the launch's output over it:
+// same positions, same wave), x = p_old, p_new -> cg->p_out, the second
+// launch (d >= 4) carries the balanced x side job, and the pair launch writes
+// q = Z + shift p_new into cg->blk_q_out (not y: the two waves of a slab read
+// its input while storing) with the p.q / q.q partials.
+void block_apply(const BlockOp* B, const double* x, double* y, double shift, double* work,
+                 double* dot_partials, const int* skip, hipStream_t stream, int64_t* n_partials,
+                 const MpFuse* cg, int cgp, hipEvent_t* ev) {
+  const int d = B->d;
+  if (cg == nullptr) cgp = 0;
+  GG_REQUIRE(cgp == 0 || cgp == 2, GG_ERR_VALUE, "block basis: plain or fused CG only");
+  GG_REQUIRE(cgp == 0 || d >= 3, GG_ERR_VALUE, "block basis CG: d >= 3");
+  GG_REQUIRE(x != y, GG_ERR_VALUE, "x and y must not alias");
+  if (cgp == 2)
+    GG_REQUIRE(cg->q_old == y && cg->p_out != nullptr && cg->p_out != x &&
+                   cg->blk_q_out != nullptr && cg->blk_q_out != y,
+               GG_ERR_VALUE, "block CG: buffer roles");
+  else if (d >= 3)
+    GG_REQUIRE(work != nullptr && work != x && work != y, GG_ERR_VALUE,
+               "block basis: scratch required");
+  if (ev) GG_HIP(hipEventRecord(ev[0], stream));
+  const double* src = x;
+  double* chain = cgp == 2 ? y : work;
+  int pos = 0;
+  for (int k = 0; k + 2 < d; ++k) {
+    ModeArgs a{};
+    int grid = 0;
+    int kind = 0;
+    if (cgp == 2 && k == 0)
+      kind = 1;
+    else if (cgp == 2 && k == 1 && cg->sx != nullptr && cg->xdefer == 2)
+      kind = 2;
+    const int W = mode_waves(kind, B, k);
+    mode_geometry(B, k, W, a, &grid);
+    a.X = src;
+    a.Y = chain;
+    a.skip = skip;
+    if (kind == 1) {
+      a.r = cg->r;
+      a.q_old = cg->q_old;
+      a.p_out = cg->p_out;
+      a.sc = cg->sc;
+      a.rr_part = cg->rr_part;
+      a.pqo_stride = cg->pqo_stride;
+      GG_REQUIRE(grid <= cg->rr_cap, GG_ERR_VALUE, "prologue partial array too short");
+      if (cg->pro_blocks != nullptr) *cg->pro_blocks = grid;
+    } else if (kind == 2) {
+      a.sc = cg->sc;
+      a.sx = cg->sx;
+      const int64_t sn = cg->sn;
+      const int64_t H = block_side_half(sn);
+      a.soff = 0;
+      a.sn = std::min(H, sn);
+      a.soff_h1 = a.sn;
+      a.sn_h1 = sn - a.sn;
+      const int64_t slots = a.ngroups * W;
+      a.sstep = 2 * ceil_div(std::max<int64_t>(std::max(a.sn, a.sn_h1), 1), 2 * slots);
+      GG_REQUIRE(a.sstep <= 128 * (int64_t)a.KS, GG_ERR_VALUE,
+                 "block CG: x side job larger than its k-steps");
+    }
+    const blk_mode_fn fn = select_mode(kind, B->JT[k], B->T4[k], (int)B->h[k], B->fast);
+    const size_t lds = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), lds, stream, a);
+    GG_LAUNCH_CHECK();
+    if (cgp == 2 && k == 0 && d == 3 && cg->sx != nullptr && cg->xdefer == 2)
+      // no second launch to carry the x side job: its half as a streaming kernel
+      launch_x_half(cg->sx, cg->sn, block_side_half(cg->sn), cg->sc, stream);
+    if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
+    src = chain;
+  }
+  // the pair launch
+  PairArgs p{};
+  p.X = src;
+  p.Y = cgp == 2 ? cg->blk_q_out : y;
+  const int k3 = d - 1, k2 = d - 2;
+  p.f3S = B->frag[k3][0];
+  p.f3T = B->frag[k3][1];
+  p.f2S = B->frag[k2][0];
+  p.f2T = B->frag[k2][1];
+  p.spb = B->nb / (B->h[k3] * B->h[k2]);
+  p.nslab = p.spb << d;
+  p.skip = skip;
+  const int grid = pair_grid(B);
+  if (cgp == 2) {
+    p.P = cg->p_out;
+    p.shift = shift;
+    p.partials = dot_partials;
+    p.pstride = cg->pstride;
+  } else if (shift != 0.0) {
+    p.P = x;
+    p.shift = shift;
+  }
+  hipLaunchKernelGGL(select_pair(B->pTF), dim3(grid), dim3(64 * kBlkPairWaves), 0, stream, p);
+  GG_LAUNCH_CHECK();
+  if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
+  if (n_partials) *n_partials = (cgp == 2) ? grid : 0;
+}
+
+// the x side job's half boundary in the block path (the closing flush uses it)
+int64_t block_side_half(int64_t n) { return 2 * ceil_div(n, (int64_t)4); }
+
+}  // namespace gg

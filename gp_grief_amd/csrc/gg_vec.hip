@@ -24,6 +24,7 @@ int64_t kron_n(const gg_kron* K);
 int kron_d(const gg_kron* K);
 bool kron_first_single_launch(const gg_kron* K);
 int64_t kron_side_half(const gg_kron* K, int64_t n);
+const BlockOp* kron_block(const gg_kron* K);
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -695,6 +696,17 @@ struct gg_cg {
   bool profiling = false;
   std::vector<hipEvent_t> events;
   size_t events_used = 0;
+  // parity-block basis (gg_kronb.hip): the recurrence runs on P b, P x, ...
+  // in the block layout -- xb the iterate, q2 the pair launch's q (swapped
+  // with q every iteration); x (the caller's) is written by the unfold of
+  // each close.  basis: requested (gg_cg_set_basis); block: in effect for the
+  // current solve (fixed at gg_cg_start: fused, layout 0, x_defer 2, rq 1)
+  const gg::BlockOp* blk = nullptr;
+  int basis = 1;
+  bool block = false;
+  double* xb = nullptr;
+  double* q2 = nullptr;
+  int launches() const { return block ? gg::block_launches(blk) : gg::kron_d(K); }
 };
 
 extern "C" {
@@ -819,9 +831,11 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
     const int64_t n = gg::kron_n(K);
     // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
-    // product's own output for an odd number of factors, MpFuse::first_dst)
-    *elems = kCgAlignSlack + 6 * cg_vec_stride(n) + gg::kron_work_elems(K, false) +
-             (gg::kron_d(K) % 2 == 1 ? n : 0);
+    // product's own output for an odd number of factors, MpFuse::first_dst);
+    // the block basis (gg_kronb.hip) takes the scratch region for xb and q2
+    const int64_t scratch = gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
+    const int64_t blk = gg::kron_block(K) != nullptr ? 2 * cg_vec_stride(n) : 0;
+    *elems = kCgAlignSlack + 6 * cg_vec_stride(n) + std::max(scratch, blk);
   });
 }
 
@@ -849,11 +863,21 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->p4 = work_dev + 5 * vs;
       cg->mv_work = work_dev + 6 * vs;
       if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
+      cg->blk = gg::kron_block(K);
+      if (cg->blk != nullptr) {
+        cg->xb = work_dev + 6 * vs;
+        cg->q2 = work_dev + 7 * vs;
+        const char* be = getenv("GG_CG_BASIS");   // read once per handle
+        if (be) cg->basis = atoi(be) != 0 ? 1 : 0;
+      } else {
+        cg->basis = 0;
+      }
       const char* xd = getenv("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
       if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
       const char* rqe = getenv("GG_CG_RQ");       // A/B knob: 0 (epilogue reads r) or 1
       if (rqe) cg->rq = std::min(2, std::max(0, atoi(rqe)));   // 2: diagnostic
       cg->mv_partials = gg::kron_partials_needed(K, false);
+      if (cg->blk) cg->mv_partials = std::max(cg->mv_partials, gg::block_partials_needed(cg->blk));
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
       GG_HIP(hipMalloc(&cg->partials, np * sizeof(double)));
       // the fused recurrence needs d >= 2 and 16-byte aligned vectors (its
@@ -864,6 +888,7 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
         // capacity for any prologue launch shape; each iteration sums exactly
         // the partials its prologue launch wrote (MpFuse::pro_blocks)
         cg->rr_count = gg::kron_prologue_blocks(K);
+        if (cg->blk) cg->rr_count = std::max(cg->rr_count, gg::block_prologue_blocks(cg->blk));
         GG_HIP(hipMalloc(&cg->rr_part, 2 * cg->rr_count * sizeof(double)));
         GG_HIP(hipMemset(cg->rr_part, 0, 2 * cg->rr_count * sizeof(double)));
       }
@@ -914,7 +939,7 @@ int gg_cg_profile(gg_cg* cg, int enable) {
 int gg_cg_profile_read(gg_cg* cg, int* n_matvecs, double* mode_ms, int mode_ms_len) {
   return gg::guard([&] {
     GG_REQUIRE(cg && n_matvecs, GG_ERR_VALUE, "NULL argument");
-    const int d = gg::kron_d(cg->K);
+    const int d = cg->launches();
     GG_REQUIRE(mode_ms == nullptr || mode_ms_len >= d, GG_ERR_VALUE, "mode_ms too short");
     const size_t per = (size_t)d + 1;
     const int nm = (int)(cg->events_used / per);
@@ -943,8 +968,19 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
     cg->b = b_dev;
     cg->x = x_dev;
     const int64_t n = cg->n;
-    GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
+    cg->block = cg->blk != nullptr && cg->basis != 0 && cg->fused && cg->fusion == 0 &&
+                cg->xdefer == 2 && cg->rq == 1 && gg::block_d(cg->blk) >= 3;
     GG_HIP(hipMemsetAsync(x_dev, 0, n * sizeof(double), s));
+    if (cg->block) {
+      // r = P b (the fold, with its |P b|^2 partials), x_b = 0
+      gg::block_fold(cg->blk, false, b_dev, cg->r, cg->partials, s);
+      GG_HIP(hipMemsetAsync(cg->xb, 0, n * sizeof(double), s));
+      hipLaunchKernelGGL(gg::cg_init_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                         gg::block_fold_partials(cg->blk), cg->sc, rtol, atol);
+      GG_LAUNCH_CHECK();
+      return;
+    }
+    GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     const int nb = gg::vec_blocks(n);
     gg::launch_dot_partials(cg->r, cg->r, n, cg->partials, nb, s);
     hipLaunchKernelGGL(gg::cg_init_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
@@ -1016,6 +1052,38 @@ int gg_cg_get_rq(const gg_cg* cg, int* mode) {
   });
 }
 
+int gg_cg_set_basis(gg_cg* cg, int block) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set the basis before gg_cg_start");
+    GG_REQUIRE(block == 0 || cg->blk != nullptr, GG_ERR_VALUE,
+               "the operator has no parity-block basis");
+    cg->basis = block != 0 ? 1 : 0;
+  });
+}
+
+int gg_cg_get_basis(const gg_cg* cg, int* block) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && block, GG_ERR_VALUE, "NULL argument");
+    // in effect once started; before, what gg_cg_start will choose
+    *block = cg->x != nullptr ? (cg->block ? 1 : 0)
+                              : (cg->blk != nullptr && cg->basis != 0 && cg->fused &&
+                                 cg->fusion == 0 && cg->xdefer == 2 && cg->rq == 1 &&
+                                 gg::block_d(cg->blk) >= 3)
+                                    ? 1
+                                    : 0;
+  });
+}
+
+int gg_cg_launches(const gg_cg* cg, int* launches) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && launches, GG_ERR_VALUE, "NULL argument");
+    int b = 0;
+    gg_cg_get_basis(cg, &b);
+    *launches = b ? gg::block_launches(cg->blk) : gg::kron_d(cg->K);
+  });
+}
+
 int gg_cg_get_recurrence(const gg_cg* cg, int* fused) {
   return gg::guard([&] {
     GG_REQUIRE(cg && fused, GG_ERR_VALUE, "NULL argument");
@@ -1051,7 +1119,7 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
       int64_t nparts = 0;
       hipEvent_t* ev = nullptr;
       if (cg->profiling) {
-        const size_t need = cg->events_used + (size_t)gg::kron_d(cg->K) + 1;
+        const size_t need = cg->events_used + (size_t)cg->launches() + 1;
         while (cg->events.size() < need) {
           hipEvent_t e;
           GG_HIP(hipEventCreate(&e));
@@ -1100,8 +1168,16 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         fz.er = (rq_ident && cg->rq != 2) ? nullptr : cg->r;
         fz.pqo_stride = rq_ident ? cg->rr_count : 0;
         fz.pstride = cg->mv_partials;
-        gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
-                       &cg->sc->done, s, &nparts, &fz, 2, ev);
+        if (cg->block) {
+          // the block basis: d - 1 launches, q2 <- (K + s I) p_new
+          fz.sx = cg->xb;
+          fz.blk_q_out = cg->q2;
+          gg::block_apply(cg->blk, cg->p, cg->q, cg->shift, nullptr, cg->partials,
+                          &cg->sc->done, s, &nparts, &fz, 2, ev);
+        } else {
+          gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                         &cg->sc->done, s, &nparts, &fz, 2, ev);
+        }
         GG_REQUIRE(pro_blocks > 0 && pro_blocks <= cg->rr_count, GG_ERR_RUNTIME,
                    "fused CG: no prologue launch recorded");
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
@@ -1109,6 +1185,7 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
                            cg->sc,
                            xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
         GG_LAUNCH_CHECK();
+        if (cg->block) std::swap(cg->q, cg->q2);
         if (xmode == 2) {
           // (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2}): the
           // active pair (at most p_{j-1}, p_{j-2} next iteration) stays alive
@@ -1168,8 +1245,10 @@ int gg_cg_close(gg_cg* cg, gg_stream stream) {
       // rho = r.r, beta, iteration count -- the textbook state.  x_defer: the
       // deferred steps first (also after convergence), then r only
       if (xdefer && cg->xdefer == 2) {
-        hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x,
-                           n, gg::kron_side_half(cg->K, n), cg->sc);
+        hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           cg->block ? cg->xb : cg->x, n,
+                           cg->block ? gg::block_side_half(n) : gg::kron_side_half(cg->K, n),
+                           cg->sc);
         GG_LAUNCH_CHECK();
         hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
         GG_LAUNCH_CHECK();
@@ -1188,6 +1267,8 @@ int gg_cg_close(gg_cg* cg, gg_stream stream) {
                          (int64_t)nb, cg->sc, 1);
       GG_LAUNCH_CHECK();
     }
+    // the block basis: the caller's x = P^T x_b
+    if (cg->block) gg::block_fold(cg->blk, true, cg->xb, cg->x, nullptr, s);
   });
 }
 
@@ -1202,6 +1283,7 @@ int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* r
     hipStream_t s = gg::as_stream(stream);
     cg->b = b_dev;
     cg->x = x_dev;
+    cg->block = false;   // the sharded rank: the handle's own operator layout
     cg->await_finish = false;
     const int64_t n = cg->n;
     GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1235,7 +1317,7 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     int64_t nparts = 0;
     hipEvent_t* ev = nullptr;
     if (cg->profiling) {
-      const size_t need = cg->events_used + (size_t)gg::kron_d(cg->K) + 1;
+      const size_t need = cg->events_used + (size_t)cg->launches() + 1;
       while (cg->events.size() < need) {
         hipEvent_t e;
         GG_HIP(hipEventCreate(&e));

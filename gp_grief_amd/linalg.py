@@ -123,7 +123,8 @@ class KronCG(object):
     iterate() in the textbook state.
     """
 
-    def __init__(self, K, shift, recurrence="fused", fusion=None, xdefer=None, rq=None):
+    def __init__(self, K, shift, recurrence="fused", fusion=None, xdefer=None, rq=None,
+                 basis=None):
         from . import device as dev
         from . import native
         self.K = K
@@ -158,6 +159,13 @@ class KronCG(object):
             native.check(L.gg_cg_set_rq(h, int(bool(rq))), "gg_cg_set_rq")
         native.check(L.gg_cg_get_rq(h, ctypes.byref(f)))
         self.rq = f.value
+        if basis is not None:
+            # "block": the parity-block basis (default where it exists), "grid": off
+            if basis not in ("block", "grid"):
+                raise ValueError("basis must be 'block' or 'grid'")
+            native.check(L.gg_cg_set_basis(h, int(basis == "block")), "gg_cg_set_basis")
+        native.check(L.gg_cg_get_basis(h, ctypes.byref(f)))
+        self.basis = "block" if f.value else "grid"
         self.n = int(K.shape[0])
         self.x = None
 
@@ -202,10 +210,17 @@ class KronCG(object):
         from . import native
         native.check(native.lib().gg_cg_profile(self.h, int(bool(enable))), "gg_cg_profile")
 
-    def profile_read(self):
-        """(profiled matvecs, [summed ms per mode-product position]) (synchronising)."""
+    def launches(self):
+        """Kernel launches per matvec (d; d - 1 in the block basis)."""
         from . import native
-        d = len(self._dk._keep)
+        v = ctypes.c_int()
+        native.check(native.lib().gg_cg_launches(self.h, ctypes.byref(v)))
+        return v.value
+
+    def profile_read(self):
+        """(profiled matvecs, [summed ms per launch position]) (synchronising)."""
+        from . import native
+        d = self.launches()
         nm = ctypes.c_int()
         buf = (ctypes.c_double * 16)()
         native.check(native.lib().gg_cg_profile_read(self.h, ctypes.byref(nm), buf, 16),
@@ -222,7 +237,7 @@ class KronCG(object):
 
 
 def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None,
-       recurrence="fused", fusion=None):
+       recurrence="fused", fusion=None, basis=None):
     """Solve (K + shift I) x = b with CG on the device (x0 = 0).
 
     Same stopping rule and iterates as scipy.sparse.linalg.cg (recurrence:
@@ -243,7 +258,7 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         maxiter = n * 10
     if check_every is None:
         check_every = 10 if n >= 1 << 20 else 50
-    solver = KronCG(K, shift, recurrence, fusion=fusion)
+    solver = KronCG(K, shift, recurrence, fusion=fusion, basis=basis)
     solver.start(bd, rtol, atol)
     # one call: the library polls the device's done flag every check_every
     # iterations and stops issuing work once converged

@@ -45,6 +45,13 @@ SIGNATURES = {
     "gg_kron_matvec_timed": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_double, _c_dp,
                              ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                              ctypes.POINTER(ctypes.c_double), _vp],
+    "gg_kron_block_info": [_vp, ctypes.POINTER(ctypes.c_int), _c_i64p,
+                           ctypes.POINTER(ctypes.c_int)],
+    "gg_kron_block_fold": [_vp, ctypes.c_int, _c_dp, _c_dp, _vp],
+    "gg_kron_block_matvec": [_vp, _c_dp, _c_dp, ctypes.c_double, _c_dp, _vp],
+    "gg_kron_block_matvec_timed": [_vp, _c_dp, _c_dp, ctypes.c_double, _c_dp, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), _vp],
     "gg_kron_diag_scale": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double, ctypes.c_int, _c_dp,
                            _c_dp, _vp],
     "gg_kron_logdet_shifted": [ctypes.c_int, _c_i64p, _c_dp, ctypes.c_double,
@@ -68,6 +75,9 @@ SIGNATURES = {
     "gg_cg_get_xdefer": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_rq": [_vp, ctypes.c_int],
     "gg_cg_get_rq": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_set_basis": [_vp, ctypes.c_int],
+    "gg_cg_get_basis": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_launches": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_start_partial": [_vp, _c_dp, _c_dp, _c_dp, _vp],
     "gg_cg_start_finish": [_vp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
     "gg_cg_iterate_partial": [_vp, _c_dp, _vp],

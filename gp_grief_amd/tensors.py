@@ -69,6 +69,49 @@ class _DeviceKron(object):
         native.check(native.lib().gg_kron_fold_mask(self.h, int(transpose), ctypes.byref(v)))
         return v.value
 
+    def block_info(self):
+        """(available, n, launches per matvec) of the parity-block basis
+        (gg_kron_block_info)."""
+        a, n, l = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int()
+        native.check(native.lib().gg_kron_block_info(self.h, ctypes.byref(a), ctypes.byref(n),
+                                                     ctypes.byref(l)))
+        return bool(a.value), n.value, l.value
+
+    def block_fold(self, xd, inverse=False, out=None):
+        """P x (inverse: P^T x) between the grid and the block layout."""
+        y = dev.empty(self.n_rows) if out is None else out
+        native.check(native.lib().gg_kron_block_fold(self.h, int(bool(inverse)),
+                                                     native.dptr(xd), native.dptr(y),
+                                                     native.stream_ptr()), "gg_kron_block_fold")
+        return y
+
+    def _block_work(self):
+        if "block" not in self._work:
+            self._work["block"] = dev.empty(self.n_rows)
+        return self._work["block"]
+
+    def block_matvec(self, xd, shift=0.0, out=None):
+        """(P K P^T + shift I) x in the block layout (gg_kron_block_matvec)."""
+        y = dev.empty(self.n_rows) if out is None else out
+        native.check(native.lib().gg_kron_block_matvec(self.h, native.dptr(xd), native.dptr(y),
+                                                       float(shift),
+                                                       native.dptr(self._block_work()),
+                                                       native.stream_ptr()),
+                     "gg_kron_block_matvec")
+        return y
+
+    def block_matvec_timed(self, xd, out, reps, shift=0.0):
+        """reps block-basis matvecs with HIP events around every launch
+        (gg_kron_block_matvec_timed): (per-launch summed ms, total ms)."""
+        _, _, L = self.block_info()
+        lm = (ctypes.c_double * max(L, 1))()
+        tot = ctypes.c_double()
+        native.check(native.lib().gg_kron_block_matvec_timed(
+            self.h, native.dptr(xd), native.dptr(out), float(shift),
+            native.dptr(self._block_work()), int(reps), lm, ctypes.byref(tot),
+            native.stream_ptr()), "gg_kron_block_matvec_timed")
+        return [lm[k] for k in range(L)], tot.value
+
     def work(self, transpose):
         key = bool(transpose)
         if key not in self._work:

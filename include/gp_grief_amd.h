@@ -78,6 +78,34 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
                          double shift, double* work_dev, int reps, double* launch_ms_host,
                          double* total_ms_host, gg_stream stream);
 
+/* The parity-block basis of a centrosymmetric operator: with
+ * every factor square, of even order m_k = 2 h_k and centrosymmetric (J F J =
+ * F: every stationary kernel on an evenly spaced grid), the orthogonal change
+ * of basis P (per axis u_i = (x_i + x_{m-1-i}) / sqrt 2, v_i = (x_i -
+ * x_{m-1-i}) / sqrt 2) makes the operator block diagonal over the 2^d parity
+ * patterns, each block a Kronecker product of h_k x h_k matrices
+ * S = F[j][i] + F[j][m-1-i], T = F[j][i] - F[j][m-1-i].  Block layout: block
+ * B = sum_k beta_k 2^{d-1-k} (slowest) of prod h_k elements, C order inside.
+ * A matvec there is d - 1 launches (the last two axes of a block share one
+ * launch): the CG (gg_cg_*) runs in this basis by default when it exists
+ * (gg_cg_set_basis), folding b at start and unfolding x at every close.
+ * Existence: 2 <= d <= 6, h_{d-2} = h_{d-1} in {20, 36, 100}, every h <= 112
+ * (GG_KRON_BLOCK=0 at gg_kron_create disables it).  No reference counterpart:
+ * an execution detail of kron_matrix.py:52-97.                              */
+int gg_kron_block_info(const gg_kron* K, int* available, int64_t* n, int* launches);
+/* y = P x (inverse: x = P^T y, the unfold); x, y distinct n-vectors.        */
+int gg_kron_block_fold(const gg_kron* K, int inverse, const double* x_dev, double* y_dev,
+                       gg_stream stream);
+/* y = (P K P^T + shift I) x in the block layout; work_dev: n doubles (d >= 3).
+ * The operator of kron_matrix.py:52-97 in the parity-block basis.           */
+int gg_kron_block_matvec(const gg_kron* K, const double* x_dev, double* y_dev, double shift,
+                         double* work_dev, gg_stream stream);
+/* reps of gg_kron_block_matvec with HIP events around each of its d - 1
+ * launches (synchronising; as gg_kron_matvec_timed).                       */
+int gg_kron_block_matvec_timed(const gg_kron* K, const double* x_dev, double* y_dev,
+                               double shift, double* work_dev, int reps, double* launch_ms_host,
+                               double* total_ms_host, gg_stream stream);
+
 /* y = x / (prod_k lam_k[i_k] + shift), the eigenvalue product decoded from
  * the flat index on the fly (never expanded).  solve_schur's divide,
  * kron_matrix.py:349-350.  lam_dev: concatenated per-factor eigenvalues.   */
@@ -148,6 +176,17 @@ int gg_cg_get_xdefer(const gg_cg* cg, int* on);
  * set: before gg_cg_start; get: 1 when the identity is in effect.         */
 int gg_cg_set_rq(gg_cg* cg, int mode);
 int gg_cg_get_rq(const gg_cg* cg, int* mode);
+/* The recurrence's basis (before gg_cg_start): 1 (default where the operator
+ * has one, GG_CG_BASIS=0 at gg_cg_create turns it off) runs the fused
+ * recurrence (layout 0, x_defer 2, r.q identity) in the parity-block basis of
+ * gg_kron_block_info: b folded at start, the iterate kept folded, the
+ * caller's x written by the unfold at every close; 0 the original layout.
+ * get: 1 when the block basis is (or will be, at start) in effect.
+ * gg_cg_launches: kernel launches per matvec (d, or d - 1 in the block
+ * basis): the positions of gg_cg_profile_read.                              */
+int gg_cg_set_basis(gg_cg* cg, int block);
+int gg_cg_get_basis(const gg_cg* cg, int* block);
+int gg_cg_launches(const gg_cg* cg, int* launches);
 int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream);
 /* gg_cg_iterate = gg_cg_iterate_open + gg_cg_close.  _open leaves the fused
  * recurrence open (the last iteration's r update and the deferred x steps

@@ -273,3 +273,71 @@ def rowcol_kr_expand(R, K, C, logged=False):
         else:
             prod = prod * X
     return (log, sign) if logged else prod
+
+
+# ---------------------------------------------------------- parity-block basis
+# No reference routine: the build's change of basis for centrosymmetric
+# factors.  Restated here (test infrastructure) so the
+# device fold / block operator can be checked against the dense product of
+# kron_matvec (kron_matrix.py:52-97), which itself is reference-pinned.
+
+def block_fold(x, ms, inverse=False):
+    """P x for the orthogonal per-axis butterfly u_i = (x_i + x_{m-1-i}) / sqrt 2,
+    v_i = (x_i - x_{m-1-i}) / sqrt 2 (i < m/2) on every axis (C order, factor 0
+    slowest).  Block layout: parity pattern beta (bit d-1-k for axis k) slowest,
+    then (i'_0 .. i'_{d-1}) C order.  inverse=True applies P^T (block -> grid).
+    """
+    ms = [int(m) for m in ms]
+    d = len(ms)
+    hs = [m // 2 for m in ms]
+    s = 1.0 / np.sqrt(2.0)
+    if not inverse:
+        t = np.asarray(x, dtype=np.float64).reshape(ms)
+        # per axis: [lo half ; reversed hi half] -> (even, odd) stacked on a new
+        # leading parity axis; the parity axes collect in front in axis order
+        parts = [t]
+        for k in range(d):
+            nxt = []
+            for a in parts:
+                lo = np.take(a, np.arange(hs[k]), axis=k)
+                hi = np.take(a, np.arange(ms[k] - 1, hs[k] - 1, -1), axis=k)
+                nxt.append((lo + hi) * s)
+                nxt.append((lo - hi) * s)
+            parts = nxt
+        return np.concatenate([p.reshape(-1) for p in parts])
+    nb = int(np.prod(hs))
+    y = np.asarray(x, dtype=np.float64).reshape(-1)
+    parts = [y[b * nb:(b + 1) * nb].reshape(hs) for b in range(2 ** d)]
+    for k in reversed(range(d)):
+        nxt = []
+        for j in range(0, len(parts), 2):
+            e, o = parts[j], parts[j + 1]
+            lo = (e + o) * s
+            hi = (e - o) * s
+            nxt.append(np.concatenate([lo, np.flip(hi, axis=k)], axis=k))
+        parts = nxt
+    return parts[0].reshape(-1)
+
+
+def block_factors(F):
+    """(S, T) of a centrosymmetric factor of even order: S[j][i] = F[j][i] +
+    F[j][m-1-i], T[j][i] = F[j][i] - F[j][m-1-i] (j, i < m/2)."""
+    F = np.asarray(F, dtype=np.float64)
+    m = F.shape[0]
+    h = m // 2
+    Fr = F[:h, ::-1][:, :h]          # F[j][m-1-i]
+    return F[:h, :h] + Fr, F[:h, :h] - Fr
+
+
+def block_matvec(factors, xb):
+    """(P K P^T) x_b in the block layout: block beta is the Kronecker product of
+    S_k (beta_k = 0) / T_k (beta_k = 1) (kron_matvec on each block)."""
+    d = len(factors)
+    st = [block_factors(F) for F in factors]
+    nb = int(np.prod([np.shape(F)[0] // 2 for F in factors]))
+    xb = np.asarray(xb, dtype=np.float64).reshape(-1)
+    out = np.empty_like(xb)
+    for b in range(2 ** d):
+        fs = [st[k][(b >> (d - 1 - k)) & 1] for k in range(d)]
+        out[b * nb:(b + 1) * nb] = kron_matvec(fs, xb[b * nb:(b + 1) * nb])
+    return out

@@ -1,0 +1,233 @@
+"""The Kronecker operator in its parity-block basis on the MI355X (gg_kronb.hip).
+
+Every factor F of a stationary kernel on an evenly spaced grid is
+centrosymmetric (J F J = F); in the orthogonal basis P of per-axis
+even / odd butterflies the operator is block diagonal over the 2^d parity
+patterns.  The device computes P x (the fold), the
+block operator P K P^T (d - 1 launches: in-place mode products on axes
+0..d-3 and one launch for the two innermost axes of every block), and runs
+the fused CG there.  Parity is against the reference's product
+KronMatrix.kronvec_prod (gp_grief/tensors/kron_matrix.py:52-97) through the
+oracle: unfold(block_matvec(fold x)) vs oracle.kron_matvec at 1e-13
+relative, the device fold vs the oracle's restatement at 1e-15, and CG
+solves vs the oracle CG (iterations within 2 %, x to 1e-8).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64).reshape(-1)
+    b = np.asarray(b, dtype=np.float64).reshape(-1)
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+@pytest.fixture(scope="module")
+def gg(gpu):
+    import gp_grief_amd
+    return gp_grief_amd
+
+
+def grid_factor(m, ell=0.15, kind="RBF"):
+    g = np.linspace(0.0, 1.0, m)
+    return oracle.cov_1d(kind, g, g, 1.0, ell) + 1e-12 * np.eye(m)
+
+
+def factors(ms, seed=0):
+    kinds = ["RBF", "Matern52", "RBF", "Matern32", "RBF", "Exponential"]
+    return [grid_factor(m, 0.1 + 0.03 * k + 0.01 * seed, kinds[k % len(kinds)])
+            for k, m in enumerate(ms)]
+
+
+def dev(gg, x):
+    return gg.device.to_device(np.ascontiguousarray(x, dtype=np.float64).reshape(-1))
+
+
+def host(gg, xd):
+    return gg.device.to_host(xd).reshape(-1)
+
+
+# shapes: d = 2 .. 5; the pair orders 40 / 72 / 200 (h = 20 / 36 / 100) and
+# leading orders with h = 1..100 (full tiles, 4-row tails, padded tiles)
+SHAPES = [
+    (200, 200),
+    (40, 40),
+    (8, 72, 72),
+    (12, 40, 40),
+    (10, 200, 200),
+    (6, 14, 40, 40),
+    (2, 34, 40, 40),
+    (40, 8, 72, 72),
+    (4, 6, 8, 40, 40),
+    (200, 6, 40, 40),
+]
+
+
+@pytest.mark.parametrize("ms", SHAPES)
+def test_block_info(gg, ms):
+    K = gg.tensors.KronMatrix(factors(ms), sym=True)
+    ok, n, L = K._device().block_info()
+    assert ok and n == int(np.prod(ms)) and L == len(ms) - 1
+
+
+@pytest.mark.parametrize("ms,why", [
+    ((9, 40, 40), "odd order"),
+    ((8, 40, 72), "unequal pair orders"),
+    ((8, 48, 48), "no pair kernel for h = 24"),
+    ((8, 240, 40, 40), "h > 112"),
+])
+def test_block_unavailable(gg, ms, why):
+    K = gg.tensors.KronMatrix(factors(ms), sym=True)
+    assert not K._device().block_info()[0], why
+
+
+def test_block_unavailable_not_centrosymmetric(gg):
+    F = factors((8, 40, 40))
+    F[0] = F[0] + np.diag(np.linspace(0.0, 0.1, 8))   # breaks J F J = F
+    K = gg.tensors.KronMatrix(F, sym=True)
+    assert not K._device().block_info()[0]
+
+
+@pytest.mark.parametrize("ms", SHAPES)
+def test_block_fold_vs_oracle(gg, ms):
+    K = gg.tensors.KronMatrix(factors(ms), sym=True)
+    dk = K._device()
+    x = np.random.default_rng(1).standard_normal(int(np.prod(ms)))
+    xb = host(gg, dk.block_fold(dev(gg, x)))
+    ref = oracle.kron.block_fold(x, ms)
+    assert rel(xb, ref) < 1e-15
+    back = host(gg, dk.block_fold(dev(gg, xb), inverse=True))
+    assert rel(back, x) < 1e-15
+    assert abs(np.linalg.norm(xb) - np.linalg.norm(x)) < 1e-13 * np.linalg.norm(x)
+
+
+@pytest.mark.parametrize("ms", SHAPES)
+@pytest.mark.parametrize("shift", [0.0, 0.05])
+def test_block_matvec_vs_oracle(gg, ms, shift):
+    F = factors(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    dk = K._device()
+    n = int(np.prod(ms))
+    x = np.random.default_rng(2).standard_normal(n)
+    xb = oracle.kron.block_fold(x, ms)
+    yb = host(gg, dk.block_matvec(dev(gg, xb), shift=shift))
+    refb = oracle.kron.block_matvec(F, xb) + shift * xb
+    assert rel(yb, refb) < 1e-13
+    # through the fold: the reference's product
+    y = oracle.kron.block_fold(yb, ms, inverse=True)
+    assert rel(y, oracle.kron_matvec(F, x) + shift * x) < 1e-13
+
+
+@pytest.mark.parametrize("ms", [(40, 40, 40, 40), (200, 6, 40, 40), (40, 8, 72, 72),
+                                (72, 36, 72, 72)])
+def test_block_fast_kernels_match_generic(gg, monkeypatch, ms):
+    """The fixed-count mode kernels (h = 16 TF + 4: blk_mode_fast_kernel) and
+    the generic ones compute the same k-step sums in the same order: the block
+    matvec is bitwise equal; a fused CG (prologue and side-job launches) over
+    a few iterations agrees to 1e-12 (the fused launches run 8-wave
+    workgroups, so the r.r partials group differently)."""
+    F = factors(ms)
+    n = int(np.prod(ms))
+    x = np.random.default_rng(8).standard_normal(n)
+    out = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("GG_BLK_MODE_FAST", fast)
+        K = gg.tensors.KronMatrix(F, sym=True)
+        y = host(gg, K._device().block_matvec(dev(gg, x), shift=0.03))
+        s = gg.linalg.KronCG(K, 0.03)
+        s.start(dev(gg, x), rtol=1e-14)
+        s.iterate(9)
+        out.append((y, host(gg, s.x), s.status()))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert rel(out[0][1], out[1][1]) < 1e-12
+    assert out[0][2][0] == out[1][2][0] == 9
+
+
+def test_block_matvec_repeatable(gg):
+    """Bitwise repeatable (no atomics; fixed slab / strip assignment)."""
+    ms = (12, 72, 72)
+    K = gg.tensors.KronMatrix(factors(ms), sym=True)
+    dk = K._device()
+    xd = dev(gg, np.random.default_rng(3).standard_normal(int(np.prod(ms))))
+    a = host(gg, dk.block_matvec(xd, shift=0.01))
+    b = host(gg, dk.block_matvec(xd, shift=0.01))
+    assert np.array_equal(a, b)
+
+
+def oracle_cg(F, b, shift, rtol, maxiter):
+    return oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b, rtol=rtol,
+                           maxiter=maxiter)
+
+
+@pytest.mark.parametrize("ms,shift", [((10, 40, 40), 0.05), ((6, 12, 40, 40), 0.05),
+                                      ((4, 8, 72, 72), 0.2), ((8, 6, 8, 40, 40), 0.1),
+                                      ((40, 40, 40, 40), 0.5), ((40, 72, 72), 0.2)])
+def test_block_cg_vs_oracle(gg, ms, shift):
+    F = factors(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(4).standard_normal((n, 1))
+    solver = gg.linalg.KronCG(K, shift)
+    assert solver.basis == "block" and solver.launches() == len(ms) - 1
+    x, info = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, maxiter=20000)
+    it = gg.linalg.cg.last.iters
+    xs, _, its = oracle_cg(F, b[:, 0], shift, 1e-10, 20000)
+    assert info == 0
+    assert abs(it - its) <= max(2, 0.02 * its), (it, its)
+    assert rel(x, xs) < 1e-8
+    r = oracle.kron_matvec(F, x[:, 0]) + shift * x[:, 0] - b[:, 0]
+    assert np.linalg.norm(r) <= 1.5e-10 * np.linalg.norm(b)
+
+
+def test_block_cg_matches_grid_basis(gg):
+    ms, shift = (6, 14, 40, 40), 0.05
+    K = gg.tensors.KronMatrix(factors(ms, 1), sym=True)
+    b = np.random.default_rng(5).standard_normal((int(np.prod(ms)), 1))
+    xb, ib = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, basis="block")
+    itb = gg.linalg.cg.last.iters
+    xg, ig = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, basis="grid")
+    itg = gg.linalg.cg.last.iters
+    assert ib == 0 and ig == 0
+    assert abs(itb - itg) <= max(2, 0.02 * itg)
+    assert rel(xb, xg) < 1e-8
+
+
+def test_block_cg_open_chain_bitwise(gg):
+    """Open iterations chain into one closed call bitwise (the recurrence's
+    pending update and deferred x steps carry across calls), as in the grid
+    basis (test_gpu_fold.py test_cg_open_iterations_chain_bitwise)."""
+    ms, shift = (6, 12, 40, 40), 0.05
+    K = gg.tensors.KronMatrix(factors(ms, 2), sym=True)
+    bd = dev(gg, np.random.default_rng(6).standard_normal(int(np.prod(ms))))
+    a = gg.linalg.KronCG(K, shift)
+    a.start(bd, rtol=1e-14)
+    a.iterate(37)
+    xa = host(gg, a.x)
+    c = gg.linalg.KronCG(K, shift)
+    c.start(bd, rtol=1e-14)
+    for k in (5, 11, 1, 20):
+        c.iterate(k, close=False)
+    c.close()
+    assert np.array_equal(host(gg, c.x), xa)
+    assert a.status()[0] == c.status()[0] == 37
+
+
+def test_block_cg_state_textbook_after_close(gg):
+    """After a close the caller's x is P^T x_b: the true residual of x
+    matches the recurrence's |r| (the textbook state)."""
+    ms, shift = (8, 72, 72), 0.05
+    F = factors(ms, 3)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    b = np.random.default_rng(7).standard_normal(int(np.prod(ms)))
+    s = gg.linalg.KronCG(K, shift)
+    s.start(dev(gg, b), rtol=1e-14)
+    s.iterate(30)
+    it, conv, res, tol = s.status()
+    x = host(gg, s.x)
+    r = b - (oracle.kron_matvec(F, x) + shift * x)
+    assert it == 30 and not conv
+    assert abs(np.linalg.norm(r) - res) <= 1e-6 * np.linalg.norm(b)
