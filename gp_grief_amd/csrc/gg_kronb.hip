@@ -66,6 +66,9 @@ struct BlockOp {
   bool T4[kBlkMaxD] = {};
   int pTF = 0;   // pair axes: h = 16 pTF + 4
   int cus = 256;
+  int pair_abl = 0;   // diag ablation of the pair kernel's memory streams (GG_BLK_PAIR_ABL)
+  // blk_pair_lds_kernel (TF 2 and 6; GG_BLK_PAIR_LDS=0: blk_pair_kernel)
+  bool pair_lds = false;
   bool fast = true;   // blk_mode_fast_kernel where instantiated (GG_BLK_MODE_FAST=0: off)
 };
 
@@ -159,7 +162,18 @@ __device__ __forceinline__ char* ubase(const void* p, int64_t off) {
   const uint64_t v = reinterpret_cast<uint64_t>(p) + (uint64_t)off;
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return reinterpret_cast<char*>(((uint64_t)hi << 32) | lo);
+  uint64_t u = ((uint64_t)hi << 32) | lo;
+  // opaque in SGPRs: otherwise (base + uniform) + lane offset is reassociated
+  // into a 64-bit VGPR address per access (no saddr form, two VGPRs each)
+  asm("" : "+s"(u));
+  return reinterpret_cast<char*>(u);
+}
+// a wave-uniform 64-bit integer held in SGPRs (values the compiler computes
+// in VGPRs, e.g. after a 64-bit division, though every lane agrees)
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 // through address-space-1 pointers: global_load / global_store (a generic
 // pointer gives FLAT instructions, whose out-of-order completion makes the
@@ -594,9 +608,11 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
       o = (a.spb - 1) / cpr;
       cs = (a.spb - 1) - o * cpr;
     }
-    return c.B * a.nb + o * (int64_t)a.h * a.inner + (cs << 4);
+    return uni64(c.B * a.nb + o * (int64_t)a.h * a.inner + (cs << 4));
   };
-  auto cur_valid = [&](const Cur& c) -> bool { return c.lg * W + wave < a.spb; };
+  auto cur_valid = [&](const Cur& c) -> bool {
+    return __builtin_amdgcn_readfirstlane((int)(c.lg * W + wave < a.spb)) != 0;
+  };
 
   bool first = false, pqo_on = false;
   double beta = 0.0, alpha = 0.0, rr_acc = 0.0, pqo_acc = 0.0;
@@ -810,6 +826,7 @@ struct PairArgs {
   double* partials;    // [grid] p.q, [pstride + grid] r.q (0), [2 pstride + grid] q.q
   int64_t pstride;
   const int* skip;
+  int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -822,107 +839,24 @@ __device__ __forceinline__ double bcast_group(double v) {
   return __hiloint2double(hi, lo);
 }
 
+// GEMM 2 and the epilogue of one slab (both pair kernels): Z = F2 W from the
+// role's W accumulators, q = Z (+ shift p, the p.q / q.q partials) stored.
 template <int TF, int J0, int NJ, bool TJ>
-__device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, double& pq,
-                                          double& qq, float& junk) {
+__device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, const double* f2,
+                                           const bd4 (&W)[TF][NJ > 0 ? NJ : 1],
+                                           const double (&Wta)[NJ > 0 ? NJ : 1],
+                                           const double (&Wj)[TF], const double Wc, double& pq,
+                                           double& qq) {
   constexpr int H = 16 * TF + 4;
   constexpr int KS = 4 * TF + 1;
-  constexpr int NJB = NJ + (TJ ? 1 : 0);   // B fragments per k-step
   constexpr int64_t FS = (int64_t)(TF + 1) * 64 * 8;   // bytes per fragment k-step
   const int lane = threadIdx.x & 63;
   const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
-  // lane byte offsets (opaque: recomputed per slab, never hoisted as a set)
-  uint32_t o_x = (uint32_t)((n16 * H + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
-  uint32_t o_xt = (uint32_t)((l3 * H + kq) * 8);        // X tail rows 16 TF + l3
   uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
   uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
   uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
-  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f), "+v"(o_z), "+v"(o_zt));
-  const int64_t blk = slab / A.spb;
-  const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
-  const double* f3 = par3 ? A.f3T : A.f3S;
-  const double* f2 = par2 ? A.f2T : A.f2S;
-  const int64_t sbyte = slab * (int64_t)H * H * 8;
-
-  // ---- GEMM 1: W = X F3^T (the role's columns)
-  bd4 W[TF][NJ > 0 ? NJ : 1];
-  double Wta[NJ > 0 ? NJ : 1];   // tail rows a = 16 TF .. +3, full column tiles
-  double Wj[TF];                 // full row tiles, tail columns (TJ)
-  double Wc = 0.0;               // corner (TJ)
-#pragma unroll
-  for (int t = 0; t < TF; ++t) {
-#pragma unroll
-    for (int u = 0; u < NJ; ++u) W[t][u] = bd4{0.0, 0.0, 0.0, 0.0};
-    Wj[t] = 0.0;
-  }
-#pragma unroll
-  for (int u = 0; u < NJ; ++u) Wta[u] = 0.0;
-
-  auto ld1 = [&](int s, double (&xa)[TF + 1], double (&fb)[NJB > 0 ? NJB : 1]) {
-    const int64_t xs = sbyte + (int64_t)s * 32;
-#pragma unroll
-    for (int t = 0; t < TF; ++t) xa[t] = ldu(A.X, xs + (int64_t)t * 16 * H * 8, o_x);
-    xa[TF] = ldu(A.X, xs + (int64_t)TF * 16 * H * 8, o_xt);
-    const int64_t fs = (int64_t)s * FS;
-#pragma unroll
-    for (int u = 0; u < NJ; ++u) fb[u] = ldu(f3, fs + (int64_t)(J0 + u) * 512, o_f);
-    if (TJ) fb[NJ] = ldu(f3, fs + (int64_t)TF * 512, o_f);
-  };
-  auto mm1 = [&](const double (&xa)[TF + 1], const double (&fb)[NJB > 0 ? NJB : 1]) {
-#pragma unroll
-    for (int t = 0; t < TF; ++t)
-#pragma unroll
-      for (int u = 0; u < NJ; ++u)
-        W[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[t], fb[u], W[t][u], 0, 0, 0);
-#pragma unroll
-    for (int u = 0; u < NJ; ++u)
-      Wta[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[u], Wta[u], 0, 0, 0);
-    if (TJ) {
-#pragma unroll
-      for (int t = 0; t < TF; ++t)
-        Wj[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[t], fb[NJ], Wj[t], 0, 0, 0);
-      Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
-    }
-  };
-  // L2 prefetch of X: k-step s reads columns 4 s .. 4 s + 3 of every row, so
-  // a row's 128-B line is first touched every fourth k-step -- one k-step of
-  // register prefetch does not cover that HBM miss.  Every pair of k-steps
-  // touches the lines two line columns ahead (4-byte loads, rows lane and
-  // 64 + lane); a touch's value is folded into a junk sum two pairs later,
-  // so it never makes a k-step wait (the sum is stored once per kernel)
-  auto touch = [&](int s, float& t0, float& t1) {
-    int cb = (s >> 2) + 2;
-    cb = cb < (H + 15) / 16 ? cb : (H + 15) / 16 - 1;
-    const int r1 = 64 + lane < H ? 64 + lane : H - 1;
-    t0 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
-        reinterpret_cast<uintptr_t>(A.X) + sbyte + ((int64_t)lane * H + 16 * cb) * 8);
-    t1 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
-        reinterpret_cast<uintptr_t>(A.X) + sbyte + ((int64_t)r1 * H + 16 * cb) * 8);
-  };
-  {
-    double xa0[TF + 1], fb0[NJB > 0 ? NJB : 1], xa1[TF + 1], fb1[NJB > 0 ? NJB : 1];
-    float ta0, ta1, tb0, tb1, tc0, tc1;
-    touch(0, ta0, ta1);
-    touch(4, tb0, tb1);
-    ld1(0, xa0, fb0);
-#pragma unroll 1
-    for (int s = 0; s + 1 < KS; s += 2) {
-      touch(s + 2, tc0, tc1);
-      ld1(s + 1, xa1, fb1);
-      mm1(xa0, fb0);
-      if (s + 2 < KS) ld1(s + 2, xa0, fb0);
-      mm1(xa1, fb1);
-      junk += (ta0 + ta1) * 0.0f;   // the touch of two pairs ago
-      ta0 = tb0;
-      ta1 = tb1;
-      tb0 = tc0;
-      tb1 = tc1;
-    }
-    junk += (ta0 + ta1 + tb0 + tb1) * 0.0f;
-    mm1(xa0, fb0);   // KS odd: the last k-step (loaded by the loop's last pass)
-  }
-
-  // ---- GEMM 2: Z = F2 W, one 16-row strip t_i at a time
+  asm volatile("" : "+v"(o_f), "+v"(o_z), "+v"(o_zt));
+  // one 16-row strip t_i at a time
   const bool epi = A.P != nullptr;
   const double sh = A.shift;
   // k-step s: B operands from the accumulators
@@ -1027,6 +961,110 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   }
 }
 
+template <int TF, int J0, int NJ, bool TJ>
+__device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, double& pq,
+                                          double& qq, float& junk) {
+  constexpr int H = 16 * TF + 4;
+  constexpr int KS = 4 * TF + 1;
+  constexpr int NJB = NJ + (TJ ? 1 : 0);   // B fragments per k-step
+  constexpr int64_t FS = (int64_t)(TF + 1) * 64 * 8;   // bytes per fragment k-step
+  const int lane = threadIdx.x & 63;
+  const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
+  // lane byte offsets (opaque: recomputed per slab, never hoisted as a set)
+  uint32_t o_x = (uint32_t)((n16 * H + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
+  uint32_t o_xt = (uint32_t)((l3 * H + kq) * 8);        // X tail rows 16 TF + l3
+  uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
+  uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
+  uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
+  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f), "+v"(o_z), "+v"(o_zt));
+  const int64_t blk = slab / A.spb;
+  const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
+  const double* f3 = par3 ? A.f3T : A.f3S;
+  const double* f2 = par2 ? A.f2T : A.f2S;
+  const int64_t sbyte = ((A.abl & 2) ? slab % 16 : slab) * (int64_t)H * H * 8;
+  const int64_t xbyte = ((A.abl & 1) ? slab % 16 : slab) * (int64_t)H * H * 8;
+
+  // ---- GEMM 1: W = X F3^T (the role's columns)
+  bd4 W[TF][NJ > 0 ? NJ : 1];
+  double Wta[NJ > 0 ? NJ : 1];   // tail rows a = 16 TF .. +3, full column tiles
+  double Wj[TF];                 // full row tiles, tail columns (TJ)
+  double Wc = 0.0;               // corner (TJ)
+#pragma unroll
+  for (int t = 0; t < TF; ++t) {
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) W[t][u] = bd4{0.0, 0.0, 0.0, 0.0};
+    Wj[t] = 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) Wta[u] = 0.0;
+
+  auto ld1 = [&](int s, double (&xa)[TF + 1], double (&fb)[NJB > 0 ? NJB : 1]) {
+    const int64_t xs = xbyte + (int64_t)s * 32;
+#pragma unroll
+    for (int t = 0; t < TF; ++t) xa[t] = ldu(A.X, xs + (int64_t)t * 16 * H * 8, o_x);
+    xa[TF] = ldu(A.X, xs + (int64_t)TF * 16 * H * 8, o_xt);
+    const int64_t fs = (int64_t)s * FS;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) fb[u] = ldu(f3, fs + (int64_t)(J0 + u) * 512, o_f);
+    if (TJ) fb[NJ] = ldu(f3, fs + (int64_t)TF * 512, o_f);
+  };
+  auto mm1 = [&](const double (&xa)[TF + 1], const double (&fb)[NJB > 0 ? NJB : 1]) {
+#pragma unroll
+    for (int t = 0; t < TF; ++t)
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+        W[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[t], fb[u], W[t][u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < NJ; ++u)
+      Wta[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[u], Wta[u], 0, 0, 0);
+    if (TJ) {
+#pragma unroll
+      for (int t = 0; t < TF; ++t)
+        Wj[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[t], fb[NJ], Wj[t], 0, 0, 0);
+      Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
+    }
+  };
+  // L2 prefetch of X: k-step s reads columns 4 s .. 4 s + 3 of every row, so
+  // a row's 128-B line is first touched every fourth k-step -- one k-step of
+  // register prefetch does not cover that HBM miss.  Every pair of k-steps
+  // touches the lines two line columns ahead (4-byte loads, rows lane and
+  // 64 + lane); a touch's value is folded into a junk sum two pairs later,
+  // so it never makes a k-step wait (the sum is stored once per kernel)
+  auto touch = [&](int s, float& t0, float& t1) {
+    int cb = (s >> 2) + 2;
+    cb = cb < (H + 15) / 16 ? cb : (H + 15) / 16 - 1;
+    const int r1 = 64 + lane < H ? 64 + lane : H - 1;
+    t0 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
+        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)lane * H + 16 * cb) * 8);
+    t1 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
+        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)r1 * H + 16 * cb) * 8);
+  };
+  {
+    double xa0[TF + 1], fb0[NJB > 0 ? NJB : 1], xa1[TF + 1], fb1[NJB > 0 ? NJB : 1];
+    float ta0, ta1, tb0, tb1, tc0, tc1;
+    touch(0, ta0, ta1);
+    touch(4, tb0, tb1);
+    ld1(0, xa0, fb0);
+#pragma unroll 1
+    for (int s = 0; s + 1 < KS; s += 2) {
+      touch(s + 2, tc0, tc1);
+      ld1(s + 1, xa1, fb1);
+      mm1(xa0, fb0);
+      if (s + 2 < KS) ld1(s + 2, xa0, fb0);
+      mm1(xa1, fb1);
+      junk += (ta0 + ta1) * 0.0f;   // the touch of two pairs ago
+      ta0 = tb0;
+      ta1 = tb1;
+      tb0 = tc0;
+      tb1 = tc1;
+    }
+    junk += (ta0 + ta1 + tb0 + tb1) * 0.0f;
+    mm1(xa0, fb0);   // KS odd: the last k-step (loaded by the loop's last pass)
+  }
+
+  pair_gemm2<TF, J0, NJ, TJ>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
+}
+
 template <int TF, int JA>
 __global__ __launch_bounds__(64 * kBlkPairWaves, 2) void blk_pair_kernel(PairArgs A) {
   if (A.skip != nullptr && *A.skip) return;
@@ -1076,6 +1114,242 @@ __global__ __launch_bounds__(64 * kBlkPairWaves, 2) void blk_pair_kernel(PairArg
   }
 }
 
+// ------------------------------------------- pair kernel, LDS-staged X ring
+// The same slab product with GEMM 1's operands moving global -> LDS by
+// LDS-DMA (global_load_lds_dwordx4) through a ring of kPairNS stages shared by
+// the two waves of a slab, instead of straight into registers: there
+// (blk_pair_kernel) the register prefetch is one k-step deep -- W holds 164
+// of the 256 registers -- and HBM latency stays exposed (MFMA busy ~0.60).
+// Here kPairNS - 1 k-steps stay in flight without registers, each X byte
+// crosses L2 -> CU once per slab (both waves read the LDS copy), and the ring
+// runs straight across slab boundaries (the next slab's first stages land
+// while GEMM 2 of this one runs).
+//
+// Stage = one k-step s: [X image][F_{d-1} fragment image].  X image: 16-byte
+// pieces (row, column pair c) of columns 4 s .. 4 s + 3, position
+// 32 t + 16 c + r16 for row 16 t + r16 (XG row groups, rows past h re-read
+// row h - 1): lane (n16, kq) reads piece c = kq >> 1, half kq & 1 with one
+// ds_read_b64 per row tile (a 16-row tile is 512 contiguous bytes over the
+// wave: conflict-free).  Fragment image: the k-step's JT fragments as packed
+// (BlockOp::frag, padded to an even count).  Each stage is XI + FI 1-KiB DMAs,
+// DPW per wave.
+//
+// GEMM 1 issues nothing but these DMAs, so the only vector-memory waits there
+// are the counted ones: a wait on an ordinary load while an LDS-DMA younger
+// than it is in flight is compiled as vmcnt(0) (the pending events are mixed),
+// which is why the fragments ride in the ring too.  Per stage: s_waitcnt
+// vmcnt((kPairNS - 2) DPW) (this wave's DMAs of the stage landed), s_barrier
+// (the partner's have, and both finished reading the previous stage), then
+// the DMAs of stage + kPairNS - 1 into the freed slot.  Past the workgroup's
+// last slab the DMAs re-read its last stage, so the count holds everywhere.
+// GEMM 2 keeps its ordinary loads (F_{d-2} fragments, p): its first wait
+// drains the next slab's DMAs once per slab.
+constexpr int kPairNS = 4;
+
+template <int N>
+__device__ __forceinline__ void blk_wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt holds 6 bits");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int TF>
+struct PairRing {
+  static constexpr int H = 16 * TF + 4;
+  static constexpr int KS = 4 * TF + 1;     // stages per slab (k-steps)
+  static constexpr int JT = TF + 1;         // fragments per k-step
+  static constexpr int XG = ((TF + 1) + 1) / 2 * 2;   // row groups, even
+  static constexpr int XI = XG / 2;         // X DMAs per stage (1 KiB: 2 groups)
+  static constexpr int FI = (JT + 1) / 2;   // fragment DMAs (1 KiB: 2 fragments)
+  static constexpr int DPW = (XI + FI) / 2; // DMAs per wave per stage
+  static constexpr int XD = XG * 64;        // doubles of the X image
+  static constexpr int STAGE = XD + 2 * FI * 64;   // doubles per stage
+  static_assert((XI + FI) % 2 == 0, "equal DMA counts per wave");
+};
+
+// where a slab's operands live: X byte offset, F_{d-1} fragments (parity)
+struct PairSlabSrc {
+  int64_t xoff;
+  const double* f3;
+};
+
+template <int TF, int J0, int NJ, bool TJ, typename Issue>
+__device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, int cslot,
+                                              bool early, PairSlabSrc cur, PairSlabSrc nxt,
+                                              bool nxt_valid, const double* ring, Issue&& issue,
+                                              double& pq, double& qq) {
+  typedef PairRing<TF> R;
+  constexpr int KS = R::KS;
+  constexpr int NS = kPairNS;
+  static_assert((NS & (NS - 1)) == 0, "ring slots: a power of two");
+  constexpr int NJB = NJ + (TJ ? 1 : 0);
+  constexpr int Y = (NS - 2) * R::DPW;
+  static_assert(Y <= 63, "ring too deep for the counted wait");
+  const int lane = threadIdx.x & 63;
+  const int n16 = lane & 15, kq = lane >> 4;
+  // LDS byte offsets within a stage: X rows 16 t + n16 (piece kq >> 1, half
+  // kq & 1), the tail rows 16 TF + (n16 & 3), the role's fragments
+  uint32_t o_x = (uint32_t)((((kq >> 1) * 16 + n16) * 2 + (kq & 1)) * 8);
+  uint32_t o_xt = (uint32_t)((((kq >> 1) * 16 + (n16 & 3)) * 2 + (kq & 1)) * 8);
+  uint32_t o_f = (uint32_t)((R::XD + lane) * 8);
+  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f));
+  const int64_t blk = slab / A.spb;
+  const double* f2 = ((blk >> 1) & 1) ? A.f2T : A.f2S;
+  const int64_t sbyte = slab * (int64_t)R::H * R::H * 8;
+
+  bd4 W[TF][NJ > 0 ? NJ : 1];
+  double Wta[NJ > 0 ? NJ : 1];
+  double Wj[TF];
+  double Wc = 0.0;
+#pragma unroll
+  for (int t = 0; t < TF; ++t) {
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) W[t][u] = bd4{0.0, 0.0, 0.0, 0.0};
+    Wj[t] = 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) Wta[u] = 0.0;
+
+  const char* rb = reinterpret_cast<const char*>(ring);   // __shared__: ds_read
+  int slot = cslot;
+#pragma unroll 1
+  for (int s = 0; s < KS; ++s) {
+    // the stage's DMAs landed (this wave's: counted; the partner's: barrier)
+    if (early && s < NS - 1)
+      blk_wait_vm<0>();   // the workgroup's first stages: fewer younger DMAs than Y
+    else
+      blk_wait_vm<Y>();
+    __builtin_amdgcn_s_barrier();
+    // stage s + NS - 1 (this slab's, else the next slab's; past the last
+    // slab this one's last stage again) into the slot every wave is done with
+    {
+      const int sn = s + NS - 1;
+      const bool in_next = sn >= KS;
+      const PairSlabSrc src = in_next && nxt_valid ? nxt : cur;
+      const int st = in_next ? (nxt_valid ? sn - KS : KS - 1) : sn;
+      issue(src, st, (slot + NS - 1) & (NS - 1));
+    }
+    const char* sb = rb + slot * (R::STAGE * 8);
+    double xa[TF + 1], fb[NJB];
+#pragma unroll
+    for (int t = 0; t < TF; ++t) xa[t] = *reinterpret_cast<const double*>(sb + o_x + t * 512);
+    xa[TF] = *reinterpret_cast<const double*>(sb + o_xt + TF * 512);
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) fb[u] = *reinterpret_cast<const double*>(sb + o_f + (J0 + u) * 512);
+    if (TJ) fb[NJ] = *reinterpret_cast<const double*>(sb + o_f + TF * 512);
+#pragma unroll
+    for (int t = 0; t < TF; ++t)
+#pragma unroll
+      for (int u = 0; u < NJ; ++u)
+        W[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[t], fb[u], W[t][u], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < NJ; ++u)
+      Wta[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[u], Wta[u], 0, 0, 0);
+    if (TJ) {
+#pragma unroll
+      for (int t = 0; t < TF; ++t)
+        Wj[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[t], fb[NJ], Wj[t], 0, 0, 0);
+      Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
+    }
+    slot = (slot + 1) & (NS - 1);
+  }
+  pair_gemm2<TF, J0, NJ, TJ>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
+}
+
+template <int TF, int JA>
+__global__ __launch_bounds__(128, 2) void blk_pair_lds_kernel(PairArgs A) {
+  typedef PairRing<TF> R;
+  constexpr int NS = kPairNS;
+  constexpr int H = R::H;
+  constexpr int64_t FSK = (int64_t)R::JT * 64 * 8;   // fragment bytes per k-step
+  __shared__ __attribute__((aligned(16))) double ring[NS * R::STAGE];
+  if (A.skip != nullptr && *A.skip) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t G = gridDim.x;
+  // slabs of this workgroup: blockIdx.x + it G, it < nmine (grid <= nslab)
+  const int nmine = __builtin_amdgcn_readfirstlane(
+      (int)((A.nslab - (int64_t)blockIdx.x + G - 1) / G));
+  // this wave's DMAs: global index i = wave DPW + j; i < XI: X pieces of row
+  // groups 2 i, 2 i + 1 (lane -> group 2 i + (lane >> 5), column pair
+  // (lane >> 4) & 1, row r16 = lane & 15); else fragments 2 (i - XI), +1
+  uint32_t dlane[R::DPW];
+#pragma unroll
+  for (int j = 0; j < R::DPW; ++j) {
+    const int i = wave * R::DPW + j;
+    if (i < R::XI) {
+      const int t = 2 * i + (lane >> 5);
+      const int row = min(16 * t + (lane & 15), H - 1);
+      dlane[j] = (uint32_t)((row * H + 2 * ((lane >> 4) & 1)) * 8);
+    } else {
+      dlane[j] = (uint32_t)((2 * (i - R::XI) * 64 + 2 * lane) * 8);
+    }
+  }
+  auto src_at = [&](int it) {
+    const int64_t slab = (int64_t)blockIdx.x + (int64_t)it * G;
+    PairSlabSrc p;
+    p.xoff = uni64(slab * (int64_t)H * H * 8);
+    const int par = __builtin_amdgcn_readfirstlane((int)((slab / A.spb) & 1));
+    p.f3 = par ? A.f3T : A.f3S;
+    return p;
+  };
+  // k-step st of a slab into ring slot `slot`
+  auto issue = [&](const PairSlabSrc& p, int st, int slot) {
+    const char* xb = ubase(A.X, p.xoff + (int64_t)st * 32);
+    const char* fbs = ubase(p.f3, (int64_t)st * FSK);
+    double* dst = ring + slot * R::STAGE;
+#pragma unroll
+    for (int j = 0; j < R::DPW; ++j) {
+      const int i = wave * R::DPW + j;   // wave-uniform
+      const char* src = i < R::XI ? xb : fbs;
+      __builtin_amdgcn_global_load_lds(
+          reinterpret_cast<const __attribute__((address_space(1))) void*>(
+              reinterpret_cast<uintptr_t>(src + dlane[j])),
+          (__attribute__((address_space(3))) void*)(dst + i * 128), 16, 0, 0);
+    }
+  };
+  PairSlabSrc cur = src_at(0);
+#pragma unroll
+  for (int j = 0; j + 1 < NS; ++j) issue(cur, min(j, R::KS - 1), j);   // stages 0 .. NS - 2
+  double pq = 0.0, qq = 0.0;
+  int cslot = 0;   // slot of the current slab's k-step 0
+  for (int it = 0; it < nmine; ++it) {
+    const int64_t slab = (int64_t)blockIdx.x + (int64_t)it * G;
+    const bool nv = it + 1 < nmine;
+    const PairSlabSrc nxt = nv ? src_at(it + 1) : cur;
+    const int role = (wave + it) & 1;
+    if (role == 0)
+      pair_slab_lds<TF, 0, JA, true>(A, slab, cslot, it == 0, cur, nxt, nv, ring, issue, pq, qq);
+    else
+      pair_slab_lds<TF, JA, TF - JA, false>(A, slab, cslot, it == 0, cur, nxt, nv, ring, issue,
+                                            pq, qq);
+    cslot = (cslot + R::KS) & (NS - 1);
+    cur = nxt;
+  }
+  blk_wait_vm<0>();   // the DMAs past the last slab land before the wave ends
+  if (A.partials != nullptr) {
+    // the reduction reuses the ring (one LDS object in this kernel: a second
+    // one gets alias scopes, and the compiler then waits vmcnt(0) between
+    // every DMA and the next ds_read)
+    __syncthreads();
+    double* red = ring;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      pq += __shfl_xor(pq, off, 64);
+      qq += __shfl_xor(qq, off, 64);
+    }
+    if (lane == 0) {
+      red[wave] = pq;
+      red[2 + wave] = qq;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      A.partials[blockIdx.x] = red[0] + red[1];
+      A.partials[A.pstride + blockIdx.x] = 0.0;
+      A.partials[2 * A.pstride + blockIdx.x] = red[2] + red[3];
+    }
+  }
+}
+
 // ------------------------------------------------------------- host side
 typedef void (*blk_mode_fn)(ModeArgs);
 typedef void (*blk_pair_fn)(PairArgs);
@@ -1120,7 +1394,14 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
 }
 
 // pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
-static blk_pair_fn select_pair(int TF) {
+static blk_pair_fn select_pair(int TF, bool lds = false) {
+  if (lds) {
+    switch (TF) {
+      case 2: return blk_pair_lds_kernel<2, 1>;
+      case 6: return blk_pair_lds_kernel<6, 3>;
+      default: return nullptr;
+    }
+  }
   switch (TF) {
     case 1: return blk_pair_kernel<1, 1>;
     case 2: return blk_pair_kernel<2, 1>;
@@ -1190,6 +1471,10 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     B->cus = blk_cus();
     const char* fe = getenv("GG_BLK_MODE_FAST");   // A/B knob, read at creation only
     B->fast = !(fe && atoi(fe) == 0);
+    const char* pe = getenv("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
+    B->pair_abl = pe ? atoi(pe) : 0;
+    const char* le = getenv("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
+    B->pair_lds = select_pair(TF, true) != nullptr && !(le && atoi(le) == 0);
     for (int k = 0; k < d; ++k) {
       const int64_t m = B->m[k], h = B->h[k];
       const double* F = factors[k];
@@ -1213,7 +1498,8 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
       B->T4[k] = T4;
       const int TFk = T4 ? JT - 1 : JT;
       for (int par = 0; par < 2; ++par) {
-        std::vector<double> hb((size_t)KS * JT * 64, 0.0);
+        // + 128 zeros: blk_pair_lds_kernel stages an even fragment count
+        std::vector<double> hb((size_t)KS * JT * 64 + 128, 0.0);
         for (int s = 0; s < KS; ++s)
           for (int t = 0; t < JT; ++t)
             for (int l = 0; l < 64; ++l) {
@@ -1332,8 +1618,12 @@ int64_t block_prologue_blocks(const BlockOp* B) {
   return g;
 }
 
+// workgroups of the pair launch: blk_pair_kernel 2 slabs each, 2 per CU;
+// blk_pair_lds_kernel one slab each, 4 per CU (28 KiB of LDS ring apiece at
+// h = 100), persistent
 static int pair_grid(const BlockOp* B) {
   int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) << B->d;
+  if (B->pair_lds) return (int)std::min<int64_t>(nslab, (int64_t)B->cus * 4);
   return (int)std::min<int64_t>(ceil_div(nslab, kBlkPairWaves / 2), (int64_t)B->cus * 2);
 }
 int64_t block_partials_needed(const BlockOp* B) { return pair_grid(B); }
@@ -1424,6 +1714,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   p.spb = B->nb / (B->h[k3] * B->h[k2]);
   p.nslab = p.spb << d;
   p.skip = skip;
+  p.abl = B->pair_abl;
   const int grid = pair_grid(B);
   if (cgp == 2) {
     p.P = cg->p_out;
@@ -1434,7 +1725,8 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     p.P = x;
     p.shift = shift;
   }
-  hipLaunchKernelGGL(select_pair(B->pTF), dim3(grid), dim3(64 * kBlkPairWaves), 0, stream, p);
+  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds), dim3(grid),
+                     dim3(B->pair_lds ? 128 : 64 * kBlkPairWaves), 0, stream, p);
   GG_LAUNCH_CHECK();
   if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
   if (n_partials) *n_partials = (cgp == 2) ? grid : 0;
