@@ -66,7 +66,11 @@ def parse():
     ap.add_argument("--recurrence", default="fused", choices=["fused", "textbook"])
     # multi-GPU decomposition: parity blocks (no exchange) where the factors
     # allow it, else factor 0 sharded with two exchanges per matvec
-    ap.add_argument("--shard", default="auto", choices=["auto", "parity", "transpose"])
+    # multi-GPU decomposition: "block" = the parity-block basis's 2^d blocks
+    # over 2^K ranks (no exchange); "parity" = factors 0..K-1 in the even /
+    # odd basis (no exchange); "transpose" = factor 0 sharded (two exchanges
+    # per matvec); "auto" = the first that applies, in that order
+    ap.add_argument("--shard", default="auto", choices=["auto", "block", "parity", "transpose"])
     ap.add_argument("--lanczos", type=int, default=30,
                     help="also time this many device Lanczos steps (one probe; 0 = off; "
                          "single GPU only)")
@@ -228,16 +232,43 @@ def _all_reduce(dist, t, op):
         dist.all_reduce(t, op=op)
 
 
-def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
-    """Strong scaling: one CG on the full grid, factor 0 sharded over ranks."""
+def backend_fields(backend, world, torch, on_gpu):
+    """How the ranks ran: the collective backend, the GPUs the box has, and
+    the scaling label -- "rehearsal" when every rank shares fewer physical
+    GPUs than ranks over gloo (GG_BENCH_BACKEND=gloo-gpu: a correctness and
+    plumbing run, not a scaling result)."""
+    phys = torch.cuda.device_count() if on_gpu else 0
+    rehearsal = backend != "nccl" or phys < world
+    return {"backend": "nccl (RCCL)" if backend == "nccl" else backend,
+            "physical_gpus": phys,
+            "scaling": "rehearsal" if rehearsal else "strong",
+            "collectives": "RCCL" if backend == "nccl" else "gloo"}
+
+
+def run_sharded(a, world, rank, torch, dev, dist, on_gpu, backend="nccl"):
+    """Strong scaling: one CG on the full grid, sharded over the ranks."""
     from gp_grief_amd.distributed import DistKronCG, TorchExchange
     m, d, s = a.grid, a.dims, a.sigma2
     Engine, make_factors = _engine_factory()
-    F = make_factors(m, d) if make_factors is not None else grid_factors(m, d)[1]
+    K = None
+    if make_factors is not None:
+        F = make_factors(m, d)
+    else:
+        K, F = grid_factors(m, d)
     shard = os.environ.get("GG_DIST_SHARD", a.shard)
-    from gp_grief_amd.distributed import parity_ok
+    from gp_grief_amd.distributed import block_shard_ok, parity_ok
+    if shard in ("auto", "block"):
+        blk_spec = os.environ.get("GG_BENCH_BLOCK_ENGINE")   # tests: module:Class
+        if K is None:
+            from gp_grief_amd.tensors import KronMatrix
+            K = KronMatrix(F, sym=True)
+        if blk_spec or (on_gpu and block_shard_ok(K, world)):
+            return run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend)
+        if shard == "block":
+            raise SystemExit("bench.py: block sharding needs 2^K <= 2^d GPUs and a parity-block "
+                             "basis")
     if shard in ("auto", "parity") and parity_ok(F, world):
-        return run_parity(a, world, rank, torch, dev, dist, on_gpu, F)
+        return run_parity(a, world, rank, torch, dev, dist, on_gpu, F, backend)
     if shard == "parity":
         raise SystemExit("bench.py: parity sharding needs 2^K GPUs and centrosymmetric factors")
     eng = Engine(F, world, rank)
@@ -308,6 +339,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         v = torch.tensor([ph[k] / a.steps for k in keys], dtype=torch.float64, device=dev)
         _all_reduce(dist, v, dist.ReduceOp.MAX)
         phases = dict(zip(keys, [float(u) for u in v.tolist()]))
+    bf = backend_fields(backend, world, torch, on_gpu)
     res = {
         "metric": METRIC,
         "value": a.steps / dt,
@@ -317,22 +349,24 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": bf["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
+        "backend": bf["backend"],
+        "physical_gpus": bf["physical_gpus"],
         "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d, factor 0 "
-                               "sharded over %d GPUs" % (m, d, s, n, world),
+                               "sharded over %d ranks" % (m, d, s, n, world),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
                    "exchange": cg.mode,
                    "cg_recurrence": cg.recurrence,
                    "parallelism": ("shard factor-0 x%d: matvec exchange by %s, %s per "
-                                   "iteration (RCCL)"
+                                   "iteration (%s)"
                                    % (world, "peer-memory stores in the mode-product "
-                                             "epilogues + 2 RCCL barriers"
-                                      if cg.mode == "push" else "2 RCCL all-to-all",
+                                             "epilogues + 2 barriers"
+                                      if cg.mode == "push" else "2 all-to-all",
                                       "one 5-double all-reduce" if cg.recurrence == "fused"
-                                      else "2 scalar all-reduces"))},
+                                      else "2 scalar all-reduces", bf["collectives"]))},
     }
     if phases is not None:
         res["phase_ms_per_iteration"] = phases
@@ -341,7 +375,7 @@ def run_sharded(a, world, rank, torch, dev, dist, on_gpu):
     return res
 
 
-def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
+def run_parity(a, world, rank, torch, dev, dist, on_gpu, F, backend="nccl"):
     """Strong scaling by parity sharding (distributed.ParityShardCG): rank g
     owns one block of the operator in the even / odd basis of factors
     0..K-1 -- no exchange, one all-reduce of five doubles per iteration."""
@@ -386,6 +420,7 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
     assert it == a.warmup + a.steps and np.isfinite(res), (it, res)
     n = m ** d
     K = world.bit_length() - 1
+    bf = backend_fields(backend, world, torch, on_gpu)
     res_ = {
         "metric": METRIC,
         "value": a.steps / dt,
@@ -395,21 +430,23 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
         "warmup": a.warmup,
         "ms_per_step": 1e3 * dt / a.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": bf["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
+        "backend": bf["backend"],
+        "physical_gpus": bf["physical_gpus"],
         "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d, "
-                               "parity-sharded over %d GPUs" % (m, d, s, n, world),
+                               "parity-sharded over %d ranks" % (m, d, s, n, world),
                    "grid": m, "dims": d, "sigma2": s, "n": n,
                    "exchange": "none",
                    "cg_recurrence": "fused",
                    "local_factor_orders": [f.shape[0] for f in cg.e.local_factors]
                    if hasattr(cg.e, "local_factors") else None,
-                   "parallelism": ("parity-shard factors 0..%d over %d GPUs: the operator is "
+                   "parallelism": ("parity-shard factors 0..%d over %d ranks: the operator is "
                                    "block-diagonal in their even / odd basis, each rank owns "
                                    "one block; no exchange, one 5-double all-reduce per "
-                                   "iteration (RCCL)" % (K - 1, world))},
+                                   "iteration (%s)" % (K - 1, world, bf["collectives"]))},
     }
     if on_gpu:
         keys = sorted(ph)
@@ -426,6 +463,152 @@ def run_parity(a, world, rank, torch, dev, dist, on_gpu, F):
         if lm > 0:
             res_["local_gbs"] = passes * 8.0 * nl / (lm * 1e-3) / 1e9
             res_["local_frac_hbm"] = res_["local_gbs"] / HBM_PEAK_GBS
+    return res_
+
+
+def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
+    """Strong scaling by block sharding (distributed.BlockHipEngine): the
+    operator in its parity-block basis is block diagonal over the 2^d parity
+    patterns; rank g of G = 2^K owns blocks [g 2^d / G, (g + 1) 2^d / G) and
+    runs the single-GPU block kernels on them (d - 1 launches per iteration).
+    No exchange; one all-reduce of five doubles per iteration.  The right-hand
+    side is folded on the device from the grid vector into the rank's blocks
+    (gg_kron_block_fold_range) and the solution unfolded the same way; both are
+    once per solve, timed beside the iterations."""
+    from gp_grief_amd.distributed import BlockHipEngine, ParityShardCG, TorchExchange
+    m, d, s = a.grid, a.dims, a.sigma2
+    n = m ** d
+    spec = os.environ.get("GG_BENCH_BLOCK_ENGINE")   # tests: module:Class (host arrays)
+    if spec:
+        import importlib
+        mod_name, cls_name = spec.split(":")
+        Engine = getattr(importlib.import_module(mod_name), cls_name)
+    else:
+        Engine = BlockHipEngine
+    eng = Engine(K, world, rank, s)
+    ex = TorchExchange()
+    sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+    fold_ms = unfold_ms = xred_ms = None
+    if on_gpu:
+        yg = grid_rhs_device(m, d, torch, dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        y = eng.fold(yg)
+        e1.record()
+        sync()
+        fold_ms = e0.elapsed_time(e1)
+        del yg
+        torch.cuda.empty_cache()
+    else:
+        y = eng.fold(rhs_at(torch.arange(n, dtype=torch.int64), m, d, torch).numpy())
+    cg = ParityShardCG(F, world, rank, ex, s, engine=eng)
+    cg.start(y, rtol=0.0, atol=0.0)
+    cg.iterate(a.warmup, close=False)
+    sync()
+    dist.barrier()
+    sync()
+    # HIP events on the GPU (host timestamps in the CPU rehearsal)
+    cg.profile(True, a.steps)
+    t0 = time.perf_counter()
+    cg.iterate(a.steps, close=False)
+    sync()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    _all_reduce(dist, t, dist.ReduceOp.MAX)
+    dt = float(t.item())
+    ph = cg.profile_read()
+    nm, per = eng.profile_read()
+    cg.profile(False)
+    cg.close()                       # the once-per-solve closing update
+    it, conv, res, tol = cg.status()
+    assert it == a.warmup + a.steps and np.isfinite(res), (it, res)
+    if on_gpu:
+        # the solution's way back: this rank's contribution to P^T x (one
+        # pass over N), summed over the ranks by one all-reduce of N doubles
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        xg = eng.unfold(cg.x)
+        e1.record()
+        sync()
+        unfold_ms = e0.elapsed_time(e1)
+        if backend == "nccl":
+            e0.record()
+            dist.all_reduce(xg)
+            e1.record()
+            sync()
+            xred_ms = e0.elapsed_time(e1)
+        del xg
+        torch.cuda.empty_cache()
+    nl = n // world
+    bf = backend_fields(backend, world, torch, on_gpu)
+    ms_per_step = 1e3 * dt / a.steps
+    res_ = {
+        "metric": METRIC,
+        "value": a.steps / dt,
+        "unit": "CG iters/s",
+        "n_gpus": dist.get_world_size(),
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": bf["scaling"],
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "backend": bf["backend"],
+        "physical_gpus": bf["physical_gpus"],
+        "config": {"workload": "4D RBF grid %d^%d, CG on (K + %g I) x = y, N = %d, "
+                               "block-sharded over %d ranks" % (m, d, s, n, world),
+                   "grid": m, "dims": d, "sigma2": s, "n": n,
+                   "exchange": "none",
+                   "cg_recurrence": "fused",
+                   "cg_basis": "block",
+                   "blocks_per_rank": (1 << d) // world,
+                   "n_per_rank": nl,
+                   "launches_per_iteration": d - 1,
+                   "timed_region": "exactly `steps` fused CG iterations continuing the "
+                                   "warm-up's open recurrence; fold, closing update and "
+                                   "unfold (once per solve) outside it",
+                   "parallelism": ("block-shard: the operator's 2^%d parity blocks, %d per "
+                                   "rank (factors 0..%d's parity bits = the rank); no "
+                                   "exchange, one 5-double all-reduce per iteration (%s)"
+                                   % (d, (1 << d) // world, world.bit_length() - 2,
+                                      bf["collectives"]))},
+        "cpu_baseline": {"value": None, "unit": "CG iters/s",
+                         "reference": "the n_gpus = 1 line's cpu_baseline (the bench contract "
+                                      "times the CPU baseline on rank 0 at N = 1 only); the "
+                                      "same single CG on the same grid"},
+    }
+    if ph:
+        keys = sorted(ph)
+        v = torch.tensor([ph[k] / a.steps for k in keys] + [x / max(nm, 1) for x in per] +
+                         [fold_ms or 0.0, unfold_ms or 0.0],
+                         dtype=torch.float64, device=dev)
+        _all_reduce(dist, v, dist.ReduceOp.MAX)
+        vals = [float(u) for u in v.tolist()]
+        phases = dict(zip(keys, vals[:len(keys)]))
+        per_pos = vals[len(keys):len(keys) + len(per)]
+        res_["phase_ms_per_iteration"] = phases
+        res_["local_launch_ms"] = per_pos
+        # the dominant kernel of a rank (its blocks are whole blocks: the
+        # single-GPU block roofline with n -> N / G)
+        roof, extra = roofline_report(per_pos, nl, m, d, "fused", ms_per_step, block=True)
+        roof["scope"] = "per rank: the rank's dominant launch on its N / G elements " \
+                        "(max over ranks of the per-launch %s means)" \
+                        % ("HIP-event" if on_gpu else "host-timer (CPU rehearsal engine)")
+        roof["traffic_source"] = "no PMC passes for the sharded layout"
+        res_["roofline"] = roof
+        res_["local_matvec_ms"] = extra["matvec_ms"]
+        res_["local_iteration_floor_ms"] = extra["iteration_floor_ms"]
+        ar = phases.get("allreduce", 0.0)
+        res_["allreduce"] = {"ms_per_iteration": ar, "share_of_iteration": ar / ms_per_step,
+                             "doubles_per_iteration": 5, "collectives": bf["collectives"]}
+        res_["fold_ms"] = vals[-2] if on_gpu else None
+        res_["unfold_ms"] = vals[-1] if on_gpu else None
+        res_["fold_unfold_bytes_per_rank"] = 8.0 * (n + nl)
+        if xred_ms is not None:
+            res_["solution_allreduce_ms"] = xred_ms
     return res_
 
 
@@ -768,21 +951,26 @@ def cpu_baseline(F, sigma2, iters):
                          share["physical_cores"], per_it[0], iters, float(np.mean(timed)))}
 
 
-def grief_leg(names, torch, cpu):
+def grief_leg(names, torch, cpu, dist=None, world=1, rank=0):
     """P2 beside the headline: one cold GPGriefModel fit per config through the
     public API, stage-timed with HIP events (bench_grief.run_config: best of
     2), the Gram's MFMA and the Phi writer's HBM fractions, and for C2 the
-    oracle's NumPy fit (oracle/grief.py) on the host as its CPU baseline."""
+    oracle's NumPy fit (oracle/grief.py) on the host as its CPU baseline.
+    world > 1: data rows sharded over the ranks (bench_grief.rows_of), the
+    Gram and Phi^T y all-reduced, times the max over ranks."""
     import bench_grief
     import gp_grief_amd as gg
     import gp_grief_amd.grid  # noqa: F401
     import gp_grief_amd.kern  # noqa: F401
     import gp_grief_amd.models  # noqa: F401
-    ctx = bench_grief.Ctx(torch, None, 1, 0)
+    ctx = bench_grief.Ctx(torch, dist if world > 1 else None, world, rank)
     out = {}
     for name in names:
         r = bench_grief.run_config(gg, ctx, name, 2, cpu and name == "C2", False)
         keep = {k: r[k] for k in ("fit_ms", "stage_ms", "gram", "phi", "lml") if k in r}
+        keep["n_gpus"] = world
+        keep["parallelism"] = r["config"]["parallelism"]
+        keep["rows_per_rank"] = r["config"]["rows_per_rank"]
         keep["workload"] = r["config"]
         if "cpu_baseline" in r:
             keep["cpu_baseline"] = r["cpu_baseline"]
@@ -940,7 +1128,15 @@ def main():
         dist.init_process_group("gloo" if backend == "gloo-gpu" else backend)
         dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu \
             else torch.device("cpu")
-        res = run_sharded(a, world, rank, torch, dev, dist, on_gpu)
+        res = run_sharded(a, world, rank, torch, dev, dist, on_gpu, backend)
+        if on_gpu and a.grief != "off":
+            # P2 beside it: BASELINE C4 is the 4-GPU GRIEF config, C5 the
+            # 8-GPU one -- data rows sharded, Gram / Phi^T y all-reduced
+            names = {4: ["C4"], 8: ["C5"]}.get(world, [])
+            torch.cuda.empty_cache()
+            res["grief"] = grief_leg(names, torch, False, dist=dist, world=world, rank=rank) \
+                if names else {"skipped": "the sharded GRIEF leg runs C4 at N = 4 and C5 at "
+                                          "N = 8 (BASELINE configs[3], [4])"}
         if rank == 0:
             print(json.dumps(res), flush=True)
         dist.destroy_process_group()

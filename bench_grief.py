@@ -116,7 +116,10 @@ class Ctx(object):
     def max(self, v):
         if self.dist is None:
             return float(v)
-        t = self.torch.tensor([float(v)], dtype=self.torch.float64, device="cuda")
+        # through the host under gloo (the gloo-gpu rehearsal of bench.py)
+        gloo = str(self.dist.get_backend()) == "gloo"
+        t = self.torch.tensor([float(v)], dtype=self.torch.float64,
+                              device="cpu" if gloo else "cuda")
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -260,7 +263,8 @@ def run_config(gg, ctx, name, repeats, cpu, with_cg, s=0.01):
                    "rows_per_rank": n_rank, "sigma2": s, "U_selected_rows": U,
                    "repeats": repeats,
                    "parallelism": "single-gpu" if ctx.world == 1 else
-                   "data rows x%d, Gram all-reduce (RCCL), replicated potrf" % ctx.world},
+                   "data rows x%d, Gram all-reduce (%s), replicated potrf"
+                   % (ctx.world, "RCCL" if str(ctx.dist.get_backend()) == "nccl" else "gloo")},
         "stage_ms": best,
         "gram": {"bound": "mfma", "flop": gram_flop,
                  "flop_rule": "n p^2 per rank (lower triangle only)" if uplo

@@ -211,14 +211,20 @@ void block_destroy(BlockOp* B);
 int64_t block_n(const BlockOp* B);
 int block_d(const BlockOp* B);
 int block_launches(const BlockOp* B);   // launches per matvec (d - 1)
+int64_t block_nb(const BlockOp* B);   // elements per block
 // x (C order over the factors) -> P x in the block layout (inverse: back);
-// sq_part (forward only, may be NULL): block_fold_partials(B) partials of |P x|^2
+// sq_part (forward only, may be NULL): block_fold_partials(B) partials of |P x|^2.
+// A block range [blk0, blk0 + nblk) (nblk < 0: all 2^d): forward writes those
+// blocks only (y holds nblk nb elements); inverse reads them (the rest count
+// as 0) and writes their contribution to every element of the grid vector
 void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, double* sq_part,
-                hipStream_t s);
+                hipStream_t s, int64_t blk0 = 0, int64_t nblk = -1);
 int64_t block_fold_partials(const BlockOp* B);
+// x, y: the vectors of blocks [blk0, blk0 + nblk) (nblk < 0: all)
 void block_apply(const BlockOp* B, const double* x, double* y, double shift, double* work,
                  double* dot_partials, const int* skip, hipStream_t stream, int64_t* n_partials,
-                 const MpFuse* cg, int cgp, hipEvent_t* ev);
+                 const MpFuse* cg, int cgp, hipEvent_t* ev, int64_t blk0 = 0,
+                 int64_t nblk = -1);
 int64_t block_prologue_blocks(const BlockOp* B);
 int64_t block_partials_needed(const BlockOp* B);
 int64_t block_side_half(int64_t n);

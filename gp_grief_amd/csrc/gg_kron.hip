@@ -1517,6 +1517,30 @@ int gg_kron_block_fold(const gg_kron* K, int inverse, const double* x_dev, doubl
   });
 }
 
+int gg_kron_block_fold_range(const gg_kron* K, int inverse, const double* x_dev, double* y_dev,
+                             int64_t blk0, int64_t nblk, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(K->blk != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    GG_REQUIRE(x_dev != y_dev, GG_ERR_VALUE, "x and y must not alias");
+    GG_REQUIRE(nblk >= 1, GG_ERR_VALUE, "empty block range");
+    gg::block_fold(K->blk, inverse != 0, x_dev, y_dev, nullptr, gg::as_stream(stream), blk0,
+                   nblk);
+  });
+}
+
+int gg_kron_block_matvec_range(const gg_kron* K, const double* x_dev, double* y_dev,
+                               double shift, double* work_dev, int64_t blk0, int64_t nblk,
+                               gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(K != nullptr && x_dev && y_dev, GG_ERR_VALUE, "NULL argument");
+    GG_REQUIRE(K->blk != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    GG_REQUIRE(nblk >= 1, GG_ERR_VALUE, "empty block range");
+    gg::block_apply(K->blk, x_dev, y_dev, shift, work_dev, nullptr, nullptr,
+                    gg::as_stream(stream), nullptr, nullptr, 0, nullptr, blk0, nblk);
+  });
+}
+
 int gg_kron_block_matvec(const gg_kron* K, const double* x_dev, double* y_dev, double shift,
                          double* work_dev, gg_stream stream) {
   return gg::guard([&] {

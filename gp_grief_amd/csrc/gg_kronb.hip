@@ -67,8 +67,11 @@ struct BlockOp {
   int pTF = 0;   // pair axes: h = 16 pTF + 4
   int cus = 256;
   int pair_abl = 0;   // diag ablation of the pair kernel's memory streams (GG_BLK_PAIR_ABL)
-  // blk_pair_lds_kernel (TF 2 and 6; GG_BLK_PAIR_LDS=0: blk_pair_kernel)
+  // blk_pair_lds_kernel (TF 2 and 6; GG_BLK_PAIR_LDS=0: blk_pair_kernel) with
+  // pair_spw slabs per workgroup (2 when a block holds an even slab count;
+  // GG_BLK_PAIR_SPW=1 forces 1)
   bool pair_lds = false;
+  int pair_spw = 1;
   bool fast = true;   // blk_mode_fast_kernel where instantiated (GG_BLK_MODE_FAST=0: off)
 };
 
@@ -78,10 +81,15 @@ struct BlockOp {
 // transform over the d parity bits, scaled by 2^{-d/2} (orthogonal; its own
 // inverse).  Consecutive threads take consecutive i'_{d-1}: the corner reads
 // are ascending or descending runs, the block writes ascending runs.
+// A block range [blk0, blk0 + nblk) (a rank of the sharded CG): the forward
+// fold writes only those blocks (y holds them contiguously); the inverse reads
+// only those (the others count as 0) and writes this range's contribution to
+// every grid element (summed over the ranks by the caller).
 struct FoldGeom {
   int d;
   int64_t m[kBlkMaxD], h[kBlkMaxD], stride[kBlkMaxD];
   int64_t nb;
+  int64_t blk0, nblk;
 };
 
 template <int D>
@@ -114,7 +122,10 @@ __global__ __launch_bounds__(256) void blk_fold_kernel(const double* __restrict_
       }
     } else {
 #pragma unroll
-      for (int c = 0; c < C; ++c) v[c] = x[(int64_t)c * g.nb + t];
+      for (int c = 0; c < C; ++c) {
+        const int64_t lb = (int64_t)c - g.blk0;   // wave-uniform
+        v[c] = (lb >= 0 && lb < g.nblk) ? x[lb * g.nb + t] : 0.0;
+      }
     }
 #pragma unroll
     for (int b = 1; b < C; b <<= 1)
@@ -128,8 +139,10 @@ __global__ __launch_bounds__(256) void blk_fold_kernel(const double* __restrict_
     if (!inverse) {
 #pragma unroll
       for (int c = 0; c < C; ++c) {
+        const int64_t lb = (int64_t)c - g.blk0;
+        if (lb < 0 || lb >= g.nblk) continue;
         const double w = v[c] * scale;
-        y[(int64_t)c * g.nb + t] = w;
+        y[lb * g.nb + t] = w;
         acc = fma(w, w, acc);
       }
     } else {
@@ -237,6 +250,7 @@ struct ModeArgs {
   int64_t per_wg;   // groups per workgroup (contiguous ranges)
   int64_t nb;       // block size
   int bitpos;       // parity bit of the axis in the block index
+  int64_t blk0;     // global index of the vector's first block (sharded CG)
   const int* skip;
   // CG prologue (KIND 1)
   double* r;
@@ -354,9 +368,10 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
   // fragments are staged once per segment, the k-step pipeline runs inside
   int64_t sg0 = g0;
   while (sg0 < g1) {
-    const int64_t B0 = sg0 / a.gpb;
+    const int64_t B0 = sg0 / a.gpb + a.blk0;   // global block index
     const int par = (int)((B0 >> a.bitpos) & 1);
-    const int64_t Bend = ((B0 >> a.bitpos) + 1) << a.bitpos;   // first block of the next parity run
+    // first (local) block of the next parity run
+    const int64_t Bend = (((B0 >> a.bitpos) + 1) << a.bitpos) - a.blk0;
     const int64_t sg1 = min(g1, Bend * a.gpb);
     // stage the factor (every wave done with the previous one)
     __syncthreads();
@@ -652,9 +667,9 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
 
   int64_t sg0 = g0;
   while (sg0 < g1) {
-    const int64_t B0 = sg0 / a.gpb;
+    const int64_t B0 = sg0 / a.gpb + a.blk0;   // global block index
     const int par = (int)((B0 >> a.bitpos) & 1);
-    const int64_t Bend = ((B0 >> a.bitpos) + 1) << a.bitpos;
+    const int64_t Bend = (((B0 >> a.bitpos) + 1) << a.bitpos) - a.blk0;
     const int64_t sg1 = min(g1, Bend * a.gpb);
     __syncthreads();
     {
@@ -819,14 +834,16 @@ struct PairArgs {
   const double* f3T;
   const double* f2S;   // F_{d-2} fragments [KS][TF+1][64]
   const double* f2T;
-  int64_t nslab;       // 2^d * slabs per block
+  int64_t nslab;       // slabs of the vector (its blocks x slabs per block)
   int64_t spb;         // slabs per block
+  int64_t blk0;        // global index of the vector's first block (parity bits)
   const double* P;     // epilogue: q = Z + shift * P, partials (nullptr: plain)
   double shift;
   double* partials;    // [grid] p.q, [pstride + grid] r.q (0), [2 pstride + grid] q.q
   int64_t pstride;
   const int* skip;
   int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
+                       // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -908,6 +925,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
+      if (A.abl & 4) break;   // diag: GEMM 2 without its k-loop
       const double f = fr[s % kPF];
       if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
 #pragma unroll
@@ -977,7 +995,7 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
   uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
   asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f), "+v"(o_z), "+v"(o_zt));
-  const int64_t blk = slab / A.spb;
+  const int64_t blk = slab / A.spb + A.blk0;
   const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
   const double* f3 = par3 ? A.f3T : A.f3S;
   const double* f2 = par2 ? A.f2T : A.f2S;
@@ -1116,11 +1134,11 @@ __global__ __launch_bounds__(64 * kBlkPairWaves, 2) void blk_pair_kernel(PairArg
 
 // ------------------------------------------- pair kernel, LDS-staged X ring
 // The same slab product with GEMM 1's operands moving global -> LDS by
-// LDS-DMA (global_load_lds_dwordx4) through a ring of kPairNS stages shared by
+// LDS-DMA (global_load_lds_dwordx4) through a ring of NS stages shared by
 // the two waves of a slab, instead of straight into registers: there
 // (blk_pair_kernel) the register prefetch is one k-step deep -- W holds 164
 // of the 256 registers -- and HBM latency stays exposed (MFMA busy ~0.60).
-// Here kPairNS - 1 k-steps stay in flight without registers, each X byte
+// Here NS - 1 k-steps stay in flight without registers, each X byte
 // crosses L2 -> CU once per slab (both waves read the LDS copy), and the ring
 // runs straight across slab boundaries (the next slab's first stages land
 // while GEMM 2 of this one runs).
@@ -1138,13 +1156,18 @@ __global__ __launch_bounds__(64 * kBlkPairWaves, 2) void blk_pair_kernel(PairArg
 // are the counted ones: a wait on an ordinary load while an LDS-DMA younger
 // than it is in flight is compiled as vmcnt(0) (the pending events are mixed),
 // which is why the fragments ride in the ring too.  Per stage: s_waitcnt
-// vmcnt((kPairNS - 2) DPW) (this wave's DMAs of the stage landed), s_barrier
+// vmcnt((NS - 2) DPW) (this wave's DMAs of the stage landed), s_barrier
 // (the partner's have, and both finished reading the previous stage), then
-// the DMAs of stage + kPairNS - 1 into the freed slot.  Past the workgroup's
+// the DMAs of stage + NS - 1 into the freed slot.  Past the workgroup's
 // last slab the DMAs re-read its last stage, so the count holds everywhere.
 // GEMM 2 keeps its ordinary loads (F_{d-2} fragments, p): its first wait
 // drains the next slab's DMAs once per slab.
-constexpr int kPairNS = 4;
+// ring stages: 4 (one slab per workgroup, 4 workgroups per CU) or 6 (two
+// slabs of one block per workgroup sharing the fragment image, 2 per CU)
+template <int SPW>
+constexpr int pair_ns() {
+  return SPW == 2 ? 6 : 4;
+}
 
 template <int N>
 __device__ __forceinline__ void blk_wait_vm() {
@@ -1152,18 +1175,23 @@ __device__ __forceinline__ void blk_wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int TF>
+template <int TF, int SPW>
 struct PairRing {
   static constexpr int H = 16 * TF + 4;
   static constexpr int KS = 4 * TF + 1;     // stages per slab (k-steps)
   static constexpr int JT = TF + 1;         // fragments per k-step
   static constexpr int XG = ((TF + 1) + 1) / 2 * 2;   // row groups, even
-  static constexpr int XI = XG / 2;         // X DMAs per stage (1 KiB: 2 groups)
+  static constexpr int XI = XG / 2;         // X DMAs per slab and stage (1 KiB: 2 groups)
   static constexpr int FI = (JT + 1) / 2;   // fragment DMAs (1 KiB: 2 fragments)
-  static constexpr int DPW = (XI + FI) / 2; // DMAs per wave per stage
-  static constexpr int XD = XG * 64;        // doubles of the X image
-  static constexpr int STAGE = XD + 2 * FI * 64;   // doubles per stage
-  static_assert((XI + FI) % 2 == 0, "equal DMA counts per wave");
+  static constexpr int NW = 2 * SPW;        // waves per workgroup
+  // DMAs per stage, padded to a multiple of the wave count (the pads re-read
+  // the last fragment pair into its own place)
+  static constexpr int TOT = (SPW * XI + FI + NW - 1) / NW * NW;
+  static constexpr int DPW = TOT / NW;      // DMAs per wave per stage
+  static constexpr int XD = XG * 64;        // doubles of one slab's X image
+  static constexpr int FD = SPW * XD;       // the fragment image's offset
+  static constexpr int STAGE = FD + 2 * FI * 64;   // doubles per stage
+  static constexpr int NS = pair_ns<SPW>();
 };
 
 // where a slab's operands live: X byte offset, F_{d-1} fragments (parity)
@@ -1172,15 +1200,14 @@ struct PairSlabSrc {
   const double* f3;
 };
 
-template <int TF, int J0, int NJ, bool TJ, typename Issue>
-__device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, int cslot,
+template <int TF, int SPW, int J0, int NJ, bool TJ, typename Issue>
+__device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, int sl, int cslot,
                                               bool early, PairSlabSrc cur, PairSlabSrc nxt,
                                               bool nxt_valid, const double* ring, Issue&& issue,
                                               double& pq, double& qq) {
-  typedef PairRing<TF> R;
+  typedef PairRing<TF, SPW> R;
   constexpr int KS = R::KS;
-  constexpr int NS = kPairNS;
-  static_assert((NS & (NS - 1)) == 0, "ring slots: a power of two");
+  constexpr int NS = R::NS;
   constexpr int NJB = NJ + (TJ ? 1 : 0);
   constexpr int Y = (NS - 2) * R::DPW;
   static_assert(Y <= 63, "ring too deep for the counted wait");
@@ -1188,11 +1215,11 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
   const int n16 = lane & 15, kq = lane >> 4;
   // LDS byte offsets within a stage: X rows 16 t + n16 (piece kq >> 1, half
   // kq & 1), the tail rows 16 TF + (n16 & 3), the role's fragments
-  uint32_t o_x = (uint32_t)((((kq >> 1) * 16 + n16) * 2 + (kq & 1)) * 8);
-  uint32_t o_xt = (uint32_t)((((kq >> 1) * 16 + (n16 & 3)) * 2 + (kq & 1)) * 8);
-  uint32_t o_f = (uint32_t)((R::XD + lane) * 8);
+  uint32_t o_x = (uint32_t)((sl * R::XD + ((kq >> 1) * 16 + n16) * 2 + (kq & 1)) * 8);
+  uint32_t o_xt = (uint32_t)((sl * R::XD + ((kq >> 1) * 16 + (n16 & 3)) * 2 + (kq & 1)) * 8);
+  uint32_t o_f = (uint32_t)((R::FD + lane) * 8);
   asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f));
-  const int64_t blk = slab / A.spb;
+  const int64_t blk = slab / A.spb + A.blk0;
   const double* f2 = ((blk >> 1) & 1) ? A.f2T : A.f2S;
   const int64_t sbyte = slab * (int64_t)R::H * R::H * 8;
 
@@ -1226,7 +1253,7 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
       const bool in_next = sn >= KS;
       const PairSlabSrc src = in_next && nxt_valid ? nxt : cur;
       const int st = in_next ? (nxt_valid ? sn - KS : KS - 1) : sn;
-      issue(src, st, (slot + NS - 1) & (NS - 1));
+      issue(src, st, slot == 0 ? NS - 1 : slot - 1);
     }
     const char* sb = rb + slot * (R::STAGE * 8);
     double xa[TF + 1], fb[NJB];
@@ -1236,6 +1263,10 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
 #pragma unroll
     for (int u = 0; u < NJ; ++u) fb[u] = *reinterpret_cast<const double*>(sb + o_f + (J0 + u) * 512);
     if (TJ) fb[NJ] = *reinterpret_cast<const double*>(sb + o_f + TF * 512);
+    if (A.abl & 8) {   // diag: GEMM 1 without its MFMAs
+      slot = (slot + 1) & (NS - 1);
+      continue;
+    }
 #pragma unroll
     for (int t = 0; t < TF; ++t)
 #pragma unroll
@@ -1250,49 +1281,61 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
         Wj[t] = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[t], fb[NJ], Wj[t], 0, 0, 0);
       Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
     }
-    slot = (slot + 1) & (NS - 1);
+    slot = slot + 1 == NS ? 0 : slot + 1;
   }
   pair_gemm2<TF, J0, NJ, TJ>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
 }
 
-template <int TF, int JA>
-__global__ __launch_bounds__(128, 2) void blk_pair_lds_kernel(PairArgs A) {
-  typedef PairRing<TF> R;
-  constexpr int NS = kPairNS;
+// SPW slabs per workgroup (2 waves each; SPW = 2: slabs 2 u, 2 u + 1 of one
+// block, so one fragment image serves both -- the host requires an even
+// slab count per block)
+template <int TF, int JA, int SPW>
+__global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) {
+  typedef PairRing<TF, SPW> R;
+  constexpr int NS = R::NS;
   constexpr int H = R::H;
   constexpr int64_t FSK = (int64_t)R::JT * 64 * 8;   // fragment bytes per k-step
+  constexpr int64_t SB = (int64_t)H * H * 8;          // bytes per slab
   __shared__ __attribute__((aligned(16))) double ring[NS * R::STAGE];
   if (A.skip != nullptr && *A.skip) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int sl = wave >> 1;   // this wave's slab of the workgroup's SPW
   const int64_t G = gridDim.x;
-  // slabs of this workgroup: blockIdx.x + it G, it < nmine (grid <= nslab)
+  // units (SPW consecutive slabs) of this workgroup: blockIdx.x + it G
+  const int64_t nunit = A.nslab / SPW;
   const int nmine = __builtin_amdgcn_readfirstlane(
-      (int)((A.nslab - (int64_t)blockIdx.x + G - 1) / G));
-  // this wave's DMAs: global index i = wave DPW + j; i < XI: X pieces of row
-  // groups 2 i, 2 i + 1 (lane -> group 2 i + (lane >> 5), column pair
-  // (lane >> 4) & 1, row r16 = lane & 15); else fragments 2 (i - XI), +1
+      (int)((nunit - (int64_t)blockIdx.x + G - 1) / G));
+  // this wave's DMAs: global index i = wave DPW + j; i < SPW XI: X pieces of
+  // slab i / XI, row groups 2 (i % XI), +1 (lane -> group + (lane >> 5),
+  // column pair (lane >> 4) & 1, row lane & 15); else fragments 2 f, 2 f + 1,
+  // f = min(i - SPW XI, FI - 1)
   uint32_t dlane[R::DPW];
+  uint32_t dlds[R::DPW];
 #pragma unroll
   for (int j = 0; j < R::DPW; ++j) {
     const int i = wave * R::DPW + j;
-    if (i < R::XI) {
-      const int t = 2 * i + (lane >> 5);
+    if (i < SPW * R::XI) {
+      const int xs = i / R::XI, xi = i % R::XI;
+      const int t = 2 * xi + (lane >> 5);
       const int row = min(16 * t + (lane & 15), H - 1);
-      dlane[j] = (uint32_t)((row * H + 2 * ((lane >> 4) & 1)) * 8);
+      dlane[j] = (uint32_t)(xs * SB + (row * H + 2 * ((lane >> 4) & 1)) * 8);
+      dlds[j] = (uint32_t)(xs * R::XD + xi * 128);
     } else {
-      dlane[j] = (uint32_t)((2 * (i - R::XI) * 64 + 2 * lane) * 8);
+      const int f = min(i - SPW * R::XI, R::FI - 1);
+      dlane[j] = (uint32_t)((2 * f * 64 + 2 * lane) * 8);
+      dlds[j] = (uint32_t)(R::FD + f * 128);
     }
   }
   auto src_at = [&](int it) {
-    const int64_t slab = (int64_t)blockIdx.x + (int64_t)it * G;
+    const int64_t slab = ((int64_t)blockIdx.x + (int64_t)it * G) * SPW;
     PairSlabSrc p;
-    p.xoff = uni64(slab * (int64_t)H * H * 8);
-    const int par = __builtin_amdgcn_readfirstlane((int)((slab / A.spb) & 1));
+    p.xoff = uni64(slab * SB);
+    const int par = __builtin_amdgcn_readfirstlane((int)((slab / A.spb + A.blk0) & 1));
     p.f3 = par ? A.f3T : A.f3S;
     return p;
   };
-  // k-step st of a slab into ring slot `slot`
+  // k-step st of a unit into ring slot `slot`
   auto issue = [&](const PairSlabSrc& p, int st, int slot) {
     const char* xb = ubase(A.X, p.xoff + (int64_t)st * 32);
     const char* fbs = ubase(p.f3, (int64_t)st * FSK);
@@ -1300,32 +1343,33 @@ __global__ __launch_bounds__(128, 2) void blk_pair_lds_kernel(PairArgs A) {
 #pragma unroll
     for (int j = 0; j < R::DPW; ++j) {
       const int i = wave * R::DPW + j;   // wave-uniform
-      const char* src = i < R::XI ? xb : fbs;
+      const char* src = i < SPW * R::XI ? xb : fbs;
       __builtin_amdgcn_global_load_lds(
           reinterpret_cast<const __attribute__((address_space(1))) void*>(
               reinterpret_cast<uintptr_t>(src + dlane[j])),
-          (__attribute__((address_space(3))) void*)(dst + i * 128), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(dst + dlds[j]), 16, 0, 0);
     }
   };
   PairSlabSrc cur = src_at(0);
 #pragma unroll
   for (int j = 0; j + 1 < NS; ++j) issue(cur, min(j, R::KS - 1), j);   // stages 0 .. NS - 2
   double pq = 0.0, qq = 0.0;
-  int cslot = 0;   // slot of the current slab's k-step 0
+  int cslot = 0;   // slot of the current unit's k-step 0
   for (int it = 0; it < nmine; ++it) {
-    const int64_t slab = (int64_t)blockIdx.x + (int64_t)it * G;
+    const int64_t slab = ((int64_t)blockIdx.x + (int64_t)it * G) * SPW + sl;
     const bool nv = it + 1 < nmine;
     const PairSlabSrc nxt = nv ? src_at(it + 1) : cur;
     const int role = (wave + it) & 1;
     if (role == 0)
-      pair_slab_lds<TF, 0, JA, true>(A, slab, cslot, it == 0, cur, nxt, nv, ring, issue, pq, qq);
+      pair_slab_lds<TF, SPW, 0, JA, true>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring, issue,
+                                          pq, qq);
     else
-      pair_slab_lds<TF, JA, TF - JA, false>(A, slab, cslot, it == 0, cur, nxt, nv, ring, issue,
-                                            pq, qq);
-    cslot = (cslot + R::KS) & (NS - 1);
+      pair_slab_lds<TF, SPW, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
+                                                 issue, pq, qq);
+    cslot = (cslot + R::KS) % NS;
     cur = nxt;
   }
-  blk_wait_vm<0>();   // the DMAs past the last slab land before the wave ends
+  blk_wait_vm<0>();   // the DMAs past the last unit land before the wave ends
   if (A.partials != nullptr) {
     // the reduction reuses the ring (one LDS object in this kernel: a second
     // one gets alias scopes, and the compiler then waits vmcnt(0) between
@@ -1339,13 +1383,18 @@ __global__ __launch_bounds__(128, 2) void blk_pair_lds_kernel(PairArgs A) {
     }
     if (lane == 0) {
       red[wave] = pq;
-      red[2 + wave] = qq;
+      red[R::NW + wave] = qq;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      A.partials[blockIdx.x] = red[0] + red[1];
+      double s0 = 0.0, s1 = 0.0;
+      for (int w = 0; w < R::NW; ++w) {
+        s0 += red[w];
+        s1 += red[R::NW + w];
+      }
+      A.partials[blockIdx.x] = s0;
       A.partials[A.pstride + blockIdx.x] = 0.0;
-      A.partials[2 * A.pstride + blockIdx.x] = red[2] + red[3];
+      A.partials[2 * A.pstride + blockIdx.x] = s1;
     }
   }
 }
@@ -1394,11 +1443,11 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
 }
 
 // pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
-static blk_pair_fn select_pair(int TF, bool lds = false) {
+static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1) {
   if (lds) {
     switch (TF) {
-      case 2: return blk_pair_lds_kernel<2, 1>;
-      case 6: return blk_pair_lds_kernel<6, 3>;
+      case 2: return spw == 2 ? blk_pair_lds_kernel<2, 1, 2> : blk_pair_lds_kernel<2, 1, 1>;
+      case 6: return spw == 2 ? blk_pair_lds_kernel<6, 3, 2> : blk_pair_lds_kernel<6, 3, 1>;
       default: return nullptr;
     }
   }
@@ -1475,6 +1524,12 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     B->pair_abl = pe ? atoi(pe) : 0;
     const char* le = getenv("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
     B->pair_lds = select_pair(TF, true) != nullptr && !(le && atoi(le) == 0);
+    {
+      int64_t spb = 1;
+      for (int k = 0; k + 2 < d; ++k) spb *= rows[k] / 2;
+      const char* se = getenv("GG_BLK_PAIR_SPW");   // A/B knob, read at creation only
+      B->pair_spw = (spb % 2 == 0 && !(se && atoi(se) == 1)) ? 2 : 1;
+    }
     for (int k = 0; k < d; ++k) {
       const int64_t m = B->m[k], h = B->h[k];
       const double* F = factors[k];
@@ -1544,11 +1599,21 @@ static int fold_grid(const BlockOp* B) {
 }
 int64_t block_fold_partials(const BlockOp* B) { return fold_grid(B); }
 
+int64_t block_nb(const BlockOp* B) { return B->nb; }
+
 void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, double* sq_part,
-                hipStream_t s) {
+                hipStream_t s, int64_t blk0, int64_t nblk) {
+  if (nblk < 0) {
+    blk0 = 0;
+    nblk = (int64_t)1 << B->d;
+  }
+  GG_REQUIRE(blk0 >= 0 && nblk >= 1 && blk0 + nblk <= ((int64_t)1 << B->d), GG_ERR_VALUE,
+             "block range outside the 2^d blocks");
   FoldGeom g{};
   g.d = B->d;
   g.nb = B->nb;
+  g.blk0 = blk0;
+  g.nblk = nblk;
   int64_t st = 1;
   for (int k = B->d - 1; k >= 0; --k) {
     g.m[k] = B->m[k];
@@ -1587,7 +1652,8 @@ static int mode_waves(int kind, const BlockOp* B, int k) {
   return kind == 0 ? fast_waves<0>() : kind == 1 ? fast_waves<1>() : fast_waves<2>();
 }
 
-static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* grid_out) {
+static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* grid_out,
+                             int64_t nblk = -1) {
   const int d = B->d;
   int64_t inner = 1, outer = 1;
   for (int i = k + 1; i < d; ++i) inner *= B->h[i];
@@ -1598,7 +1664,7 @@ static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* g
   a.inner = inner;
   a.spb = outer * (inner / 16);
   a.gpb = ceil_div(a.spb, (int64_t)W);
-  a.ngroups = a.gpb << d;
+  a.ngroups = a.gpb * (nblk < 0 ? ((int64_t)1 << d) : nblk);
   const int64_t grid = std::min<int64_t>(a.ngroups, (int64_t)B->cus);
   a.per_wg = ceil_div(a.ngroups, grid);
   a.nb = B->nb;
@@ -1621,9 +1687,11 @@ int64_t block_prologue_blocks(const BlockOp* B) {
 // workgroups of the pair launch: blk_pair_kernel 2 slabs each, 2 per CU;
 // blk_pair_lds_kernel one slab each, 4 per CU (28 KiB of LDS ring apiece at
 // h = 100), persistent
-static int pair_grid(const BlockOp* B) {
-  int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) << B->d;
-  if (B->pair_lds) return (int)std::min<int64_t>(nslab, (int64_t)B->cus * 4);
+static int pair_grid(const BlockOp* B, int64_t nblk = -1) {
+  const int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) *
+                        (nblk < 0 ? ((int64_t)1 << B->d) : nblk);
+  if (B->pair_lds)
+    return (int)std::min<int64_t>(nslab / B->pair_spw, (int64_t)B->cus * 4 / B->pair_spw);
   return (int)std::min<int64_t>(ceil_div(nslab, kBlkPairWaves / 2), (int64_t)B->cus * 2);
 }
 int64_t block_partials_needed(const BlockOp* B) { return pair_grid(B); }
@@ -1639,8 +1707,14 @@ int64_t block_partials_needed(const BlockOp* B) { return pair_grid(B); }
 // its input while storing) with the p.q / q.q partials.
 void block_apply(const BlockOp* B, const double* x, double* y, double shift, double* work,
                  double* dot_partials, const int* skip, hipStream_t stream, int64_t* n_partials,
-                 const MpFuse* cg, int cgp, hipEvent_t* ev) {
+                 const MpFuse* cg, int cgp, hipEvent_t* ev, int64_t blk0, int64_t nblk) {
   const int d = B->d;
+  if (nblk < 0) {
+    blk0 = 0;
+    nblk = (int64_t)1 << d;
+  }
+  GG_REQUIRE(blk0 >= 0 && nblk >= 1 && blk0 + nblk <= ((int64_t)1 << d), GG_ERR_VALUE,
+             "block range outside the 2^d blocks");
   if (cg == nullptr) cgp = 0;
   GG_REQUIRE(cgp == 0 || cgp == 2, GG_ERR_VALUE, "block basis: plain or fused CG only");
   GG_REQUIRE(cgp == 0 || d >= 3, GG_ERR_VALUE, "block basis CG: d >= 3");
@@ -1665,7 +1739,8 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     else if (cgp == 2 && k == 1 && cg->sx != nullptr && cg->xdefer == 2)
       kind = 2;
     const int W = mode_waves(kind, B, k);
-    mode_geometry(B, k, W, a, &grid);
+    mode_geometry(B, k, W, a, &grid, nblk);
+    a.blk0 = blk0;
     a.X = src;
     a.Y = chain;
     a.skip = skip;
@@ -1712,10 +1787,11 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   p.f2S = B->frag[k2][0];
   p.f2T = B->frag[k2][1];
   p.spb = B->nb / (B->h[k3] * B->h[k2]);
-  p.nslab = p.spb << d;
+  p.nslab = p.spb * nblk;
+  p.blk0 = blk0;
   p.skip = skip;
   p.abl = B->pair_abl;
-  const int grid = pair_grid(B);
+  const int grid = pair_grid(B, nblk);
   if (cgp == 2) {
     p.P = cg->p_out;
     p.shift = shift;
@@ -1725,8 +1801,8 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     p.P = x;
     p.shift = shift;
   }
-  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds), dim3(grid),
-                     dim3(B->pair_lds ? 128 : 64 * kBlkPairWaves), 0, stream, p);
+  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw), dim3(grid),
+                     dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0, stream, p);
   GG_LAUNCH_CHECK();
   if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
   if (n_partials) *n_partials = (cgp == 2) ? grid : 0;

@@ -706,6 +706,10 @@ struct gg_cg {
   bool block = false;
   double* xb = nullptr;
   double* q2 = nullptr;
+  // a rank of the block-sharded CG (gg_cg_create_blocks): the handle's
+  // vectors are blocks [rblk0, rblk0 + rnblk) of the block layout (rnblk > 0);
+  // only the _partial / _finish entry points drive it
+  int64_t rblk0 = 0, rnblk = -1;
   int launches() const { return block ? gg::block_launches(blk) : gg::kron_d(K); }
 };
 
@@ -839,6 +843,67 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   });
 }
 
+int gg_cg_work_elems_blocks(const gg_kron* K, int64_t nblk, int64_t* elems) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
+    const gg::BlockOp* B = gg::kron_block(K);
+    GG_REQUIRE(B != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    GG_REQUIRE(nblk >= 1 && nblk <= ((int64_t)1 << gg::block_d(B)), GG_ERR_VALUE,
+               "block count outside 1..2^d");
+    // r, p, q, p2, p3, p4 and q2 (the pair launch's q)
+    *elems = kCgAlignSlack + 7 * cg_vec_stride(nblk * gg::block_nb(B));
+  });
+}
+
+int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shift,
+                        double* work_dev, gg_cg** out) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && work_dev && out, GG_ERR_VALUE, "NULL argument");
+    const gg::BlockOp* B = gg::kron_block(K);
+    GG_REQUIRE(B != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
+    GG_REQUIRE(gg::block_d(B) >= 3, GG_ERR_VALUE, "the block-sharded CG needs d >= 3");
+    GG_REQUIRE(blk0 >= 0 && nblk >= 1 && blk0 + nblk <= ((int64_t)1 << gg::block_d(B)),
+               GG_ERR_VALUE, "block range outside the 2^d blocks");
+    GG_REQUIRE((reinterpret_cast<uintptr_t>(work_dev) & 15) == 0, GG_ERR_VALUE,
+               "the CG workspace must be 16-byte aligned");
+    const int64_t n = nblk * gg::block_nb(B);
+    gg_cg* cg = new gg_cg();
+    try {
+      cg->K = K;
+      cg->shift = shift;
+      cg->n = n;
+      const int64_t vs = cg_vec_stride(n);
+      work_dev = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(work_dev) + 255) &
+                                           ~static_cast<uintptr_t>(255));
+      cg->r = work_dev;
+      cg->p = work_dev + vs;
+      cg->q = work_dev + 2 * vs;
+      cg->p2 = work_dev + 3 * vs;
+      cg->p3 = work_dev + 4 * vs;
+      cg->p4 = work_dev + 5 * vs;
+      cg->q2 = work_dev + 6 * vs;
+      cg->blk = B;
+      cg->basis = 1;
+      cg->rblk0 = blk0;
+      cg->rnblk = nblk;
+      cg->fused = true;   // layout 0, x_defer 2, rq 1: the block path's only form
+      cg->mv_partials = gg::block_partials_needed(B);
+      GG_HIP(hipMalloc(&cg->partials,
+                       std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials) * sizeof(double)));
+      cg->rr_count = gg::block_prologue_blocks(B);
+      GG_HIP(hipMalloc(&cg->rr_part, 2 * cg->rr_count * sizeof(double)));
+      GG_HIP(hipMemset(cg->rr_part, 0, 2 * cg->rr_count * sizeof(double)));
+      GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
+      GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
+      GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
+    } catch (...) {
+      gg_cg_destroy(cg);
+      throw;
+    }
+    *out = cg;
+  });
+}
+
 int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) {
   return gg::guard([&] {
     GG_REQUIRE(K && work_dev && out, GG_ERR_VALUE, "NULL argument");
@@ -964,6 +1029,8 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
     GG_REQUIRE(cg && b_dev && x_dev, GG_ERR_VALUE, "NULL argument");
     GG_REQUIRE(rtol >= 0 && atol >= 0, GG_ERR_VALUE,
                "tolerances must be real, non-negative numbers");
+    GG_REQUIRE(cg->rnblk < 0, GG_ERR_VALUE,
+               "a block-range handle (gg_cg_create_blocks) runs through gg_cg_start_partial");
     hipStream_t s = gg::as_stream(stream);
     cg->b = b_dev;
     cg->x = x_dev;
@@ -1283,7 +1350,9 @@ int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* r
     hipStream_t s = gg::as_stream(stream);
     cg->b = b_dev;
     cg->x = x_dev;
-    cg->block = false;   // the sharded rank: the handle's own operator layout
+    // the sharded rank: the handle's own operator layout, or its blocks of
+    // the block layout (gg_cg_create_blocks; b and x in that layout)
+    cg->block = cg->rnblk > 0;
     cg->await_finish = false;
     const int64_t n = cg->n;
     GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
@@ -1352,10 +1421,18 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     fz.er = rq_ident ? nullptr : cg->r;
     fz.pqo_stride = rq_ident ? cg->rr_count : 0;
     fz.pstride = cg->mv_partials;
-    gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
-                   &cg->sc->done, s, &nparts, &fz, 2, ev);
+    if (cg->block) {
+      // the rank's blocks: d - 1 launches, q2 <- (K + s I) p_new
+      fz.blk_q_out = cg->q2;
+      gg::block_apply(cg->blk, cg->p, cg->q, cg->shift, nullptr, cg->partials, &cg->sc->done, s,
+                      &nparts, &fz, 2, ev, cg->rblk0, cg->rnblk);
+    } else {
+      gg::kron_apply(cg->K, false, cg->p, cg->q, cg->shift, cg->mv_work, cg->partials,
+                     &cg->sc->done, s, &nparts, &fz, 2, ev);
+    }
     GG_REQUIRE(pro_blocks > 0 && pro_blocks <= cg->rr_count, GG_ERR_RUNTIME,
                "fused CG: no prologue launch recorded");
+    if (cg->block) std::swap(cg->q, cg->q2);
     hipLaunchKernelGGL(gg::cg_local_red_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
                        pro_blocks, cg->rr_count, cg->partials, nparts, cg->mv_partials,
                        rq_ident ? 1 : 0, red_dev);
@@ -1404,7 +1481,8 @@ int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream) {
     const int nb = gg::vec_blocks(n);
     if (cg->xdefer == 2) {
       hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
-                         gg::kron_side_half(cg->K, n), cg->sc);
+                         cg->block ? gg::block_side_half(n) : gg::kron_side_half(cg->K, n),
+                         cg->sc);
       GG_LAUNCH_CHECK();
     } else if (cg->xdefer == 1) {
       hipLaunchKernelGGL(gg::cg_x_flush_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,

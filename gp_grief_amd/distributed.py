@@ -109,6 +109,12 @@ class TorchExchange(object):
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
 
+    def size(self):
+        return self.dist.get_world_size(self.group)
+
+    def rank(self):
+        return self.dist.get_rank(self.group)
+
 
 class HipEngine(object):
     """This rank's share of the sharded operator and CG scalars on its GPU."""
@@ -707,15 +713,17 @@ class ParityShardCG(object):
         self.n_local = self.e.n_local
         self.x = None
         self._prof = None
-        self.mode = "parity"
+        self.mode = getattr(self.e, "mode", "parity")
         self.recurrence = "fused"
 
-    # per-phase timing on the compute stream (as DistKronCG.profile)
+    # per-phase timing on the compute stream (as DistKronCG.profile); host
+    # timestamps when there is no GPU (the CPU rehearsal's test engines)
     def profile(self, enable, iterations=64):
+        import torch
         self._prof = [] if enable else None
+        self._host_timer = not torch.cuda.is_available()
         self.e.profile(enable)
-        if enable:
-            import torch
+        if enable and not self._host_timer:
             pool = getattr(self, "_ev_pool", [])
             while len(pool) < 4 * max(1, int(iterations)) + 1:
                 pool.append(torch.cuda.Event(enable_timing=True))
@@ -723,6 +731,10 @@ class ParityShardCG(object):
 
     def _mark(self, name):
         if self._prof is not None:
+            if self._host_timer:
+                import time
+                self._prof.append((name, time.perf_counter()))
+                return
             import torch
             k = len(self._prof)
             if k < len(self._ev_pool):
@@ -734,14 +746,16 @@ class ParityShardCG(object):
             self._prof.append((name, e))
 
     def profile_read(self):
-        import torch
-        torch.cuda.synchronize()
         out = {}
         ev = self._prof or []
+        if not getattr(self, "_host_timer", False):
+            import torch
+            torch.cuda.synchronize()
         for (_, e0), (n1, e1) in zip(ev[:-1], ev[1:]):
             if n1 == "start":
                 continue
-            out[n1] = out.get(n1, 0.0) + e0.elapsed_time(e1)
+            dt = 1e3 * (e1 - e0) if self._host_timer else e0.elapsed_time(e1)
+            out[n1] = out.get(n1, 0.0) + dt
         return out
 
     def apply(self, x, y):
@@ -788,3 +802,207 @@ class ParityShardCG(object):
                 break
         it, conv, res, tol = self.status()
         return self.x, (0 if conv else it)
+
+
+# ---------------------------------------------------------------- block sharding
+# The operator in its parity-block basis (gg_kronb.hip)
+# is block diagonal over the 2^d parity patterns beta (block index B =
+# sum_k beta_k 2^{d-1-k}, factor 0 the most significant bit).  With G = 2^K
+# ranks, rank g owns blocks [g 2^d / G, (g + 1) 2^d / G) -- the blocks whose
+# top K bits are g, i.e. the parity sharding of factors 0..K-1 above -- and
+# runs the single-GPU block kernels on them (gg_cg_create_blocks: d - 1
+# launches per iteration, no exchange, one all-reduce of five doubles).  The
+# right-hand side is folded on the device straight from the grid vector into
+# the rank's blocks (gg_kron_block_fold_range); the solution's unfold writes
+# each rank's contribution to the grid vector, summed by one all-reduce.
+
+def block_range(d, world, rank):
+    """(first block, block count) of rank `rank` of `world` = 2^K <= 2^d."""
+    nb = (1 << int(d)) // int(world)
+    return int(rank) * nb, nb
+
+
+def block_shard_ok(K, world):
+    """world = 2^K <= 2^d and K (a KronMatrix) has a device parity-block
+    basis with d >= 3 (every factor square, even-order, centrosymmetric; the
+    last two of equal order h in {20, 36, 100})."""
+    world = int(world)
+    if world < 1 or world & (world - 1):
+        return False
+    d = len(K.K)
+    if d < 3 or world > (1 << d):
+        return False
+    try:
+        return bool(K._device().block_info()[0])
+    except Exception:  # noqa: BLE001 -- no device library / no GPU
+        return False
+
+
+class BlockHipEngine(object):
+    """Rank `rank`'s blocks of the operator's parity-block basis as a resident
+    fused CG driven through gg_cg_*_partial / _finish (the engine interface
+    of ParityHipEngine); vectors are the rank's blocks, C order inside each."""
+
+    mode = "block"
+
+    def __init__(self, K, world, rank, shift):
+        if not block_shard_ok(K, world):
+            raise ValueError("block sharding needs 2^K <= 2^d ranks and a parity-block basis")
+        self.K = K
+        self.dk = K._device()
+        self.d = len(K.K)
+        self.blk0, self.nblk = block_range(self.d, world, rank)
+        L = native.lib()
+        we = ctypes.c_int64()
+        native.check(L.gg_cg_work_elems_blocks(self.dk.h, self.nblk, ctypes.byref(we)),
+                     "gg_cg_work_elems_blocks")
+        self.work = dev.empty(we.value)
+        h = ctypes.c_void_p()
+        native.check(L.gg_cg_create_blocks(self.dk.h, self.blk0, self.nblk, float(shift),
+                                           native.dptr(self.work), ctypes.byref(h)),
+                     "gg_cg_create_blocks")
+        self.h = h
+        self.shift = float(shift)
+        _, n, self.launches = self.dk.block_info()
+        self.n = n
+        self.n_local = n // (1 << self.d) * self.nblk
+        self.local_factors = None
+        self.red5 = dev.zeros(5)
+        self.red1 = dev.zeros(1)
+
+    def empty(self):
+        return dev.empty(self.n_local)
+
+    def zeros(self):
+        return dev.zeros(self.n_local)
+
+    def fold(self, b_grid, out=None):
+        """This rank's blocks of P b (b: the grid vector, on the device)."""
+        return self.dk.block_fold_range(b_grid, self.blk0, self.nblk, out=out)
+
+    def unfold(self, x_local, out=None):
+        """This rank's contribution to P^T x (a grid vector; the sum over
+        the ranks is the solution)."""
+        return self.dk.block_fold_range(x_local, self.blk0, self.nblk, inverse=True, out=out)
+
+    def apply(self, x, y):
+        self.dk.block_matvec_range(x, self.blk0, self.nblk, out=y)
+
+    def _c(self, name, *args):
+        native.check(getattr(native.lib(), name)(self.h, *args, native.stream_ptr()), name)
+
+    def start_partial(self, b, x):
+        self._c("gg_cg_start_partial", native.dptr(b), native.dptr(x), native.dptr(self.red1))
+        return self.red1
+
+    def start_finish(self, rtol, atol):
+        self._c("gg_cg_start_finish", native.dptr(self.red1), float(rtol), float(atol))
+
+    def iterate_partial(self):
+        self._c("gg_cg_iterate_partial", native.dptr(self.red5))
+        return self.red5
+
+    def iterate_finish(self):
+        self._c("gg_cg_iterate_finish", native.dptr(self.red5))
+
+    def close_partial(self):
+        self._c("gg_cg_close_partial", native.dptr(self.red1))
+        return self.red1
+
+    def close_finish(self):
+        self._c("gg_cg_close_finish", native.dptr(self.red1))
+
+    def status(self):
+        it, conv = ctypes.c_int(), ctypes.c_int()
+        res, tol = ctypes.c_double(), ctypes.c_double()
+        native.check(native.lib().gg_cg_status(self.h, ctypes.byref(it), ctypes.byref(conv),
+                                               ctypes.byref(res), ctypes.byref(tol),
+                                               native.stream_ptr()))
+        return it.value, bool(conv.value), res.value, tol.value
+
+    def profile(self, enable):
+        native.check(native.lib().gg_cg_profile(self.h, int(bool(enable))), "gg_cg_profile")
+
+    def profile_read(self):
+        """(profiled iterations, [summed ms per launch position])."""
+        nm = ctypes.c_int()
+        buf = (ctypes.c_double * 16)()
+        native.check(native.lib().gg_cg_profile_read(self.h, ctypes.byref(nm), buf, 16),
+                     "gg_cg_profile_read")
+        return nm.value, [buf[k] for k in range(self.launches)]
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None) is not None and self.h.value:
+                native.load().gg_cg_destroy(self.h)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def comm_exchange(comm):
+    """(exchange, world, rank) of a `comm` argument: an exchange object
+    (TorchExchange, or the tests' virtual-rank exchange) with size() / rank();
+    a torch.distributed process group; or True / "world" for the default
+    group."""
+    if hasattr(comm, "all_reduce") and hasattr(comm, "size"):
+        return comm, int(comm.size()), int(comm.rank())
+    ex = TorchExchange(None if comm is True or comm == "world" else comm)
+    return ex, ex.size(), ex.rank()
+
+
+def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_every=20,
+          decomposition="auto", engine=None):
+    """CG on (K + shift I) x = b across the ranks of `comm` (every rank passes
+    the same K and b, numpy or a device tensor; every rank gets the whole x
+    back, as a device tensor).  decomposition: "block" (the parity-block
+    basis, blocks over 2^K ranks, no exchange), "parity" (factors 0..K-1 in
+    the even / odd basis, host-folded blocks), "transpose" (factor 0 sharded,
+    two exchanges per matvec) or "auto" (the first that applies, in that
+    order).  Returns (x, info, iterations, decomposition).  engine (tests):
+    a factory (K, world, rank, shift) -> engine for the block decomposition
+    in place of BlockHipEngine (its fold / unfold take host arrays)."""
+    import torch
+    ex, world, rank = comm_exchange(comm)
+    F = [np.asarray(f, dtype=np.float64) for f in K.K]
+    m = [f.shape[0] for f in F]
+    n = int(np.prod(m))
+    maxiter = 10 * n if maxiter is None else int(maxiter)
+    if decomposition == "auto":
+        decomposition = ("block" if engine is not None or block_shard_ok(K, world) else
+                         "parity" if parity_ok(F, world) else "transpose")
+    if decomposition == "block":
+        if engine is not None:
+            eng = engine(K, world, rank, shift)
+            bg = b
+        else:
+            eng = BlockHipEngine(K, world, rank, shift)
+            bg = dev.to_device(b).reshape(-1)
+        cg = ParityShardCG(F, world, rank, ex, shift, engine=eng)
+        xl, info = cg.solve(eng.fold(bg), rtol, atol, maxiter, check_every)
+        x = eng.unfold(xl)
+        ex.all_reduce(x)
+        it = cg.status()[0]
+    elif decomposition == "parity":
+        bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
+                        dtype=np.float64).reshape(-1)
+        cg = ParityShardCG(F, world, rank, ex, shift)
+        bl = dev.to_device(parity_fold(bh, m, world)[rank])
+        xl, info = cg.solve(bl, rtol, atol, maxiter, check_every)
+        parts = ex.all_gather_object(dev.to_host(xl))
+        x = dev.to_device(parity_unfold(parts, m))
+        it = cg.status()[0]
+    elif decomposition == "transpose":
+        bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
+                        dtype=np.float64).reshape(-1)
+        eng = HipEngine(F, world, rank)
+        cg = DistKronCG(eng, ex, shift)
+        xl, info = cg.solve(dev.to_device(scatter_global(bh, m, world, rank)), rtol, atol,
+                            maxiter, check_every)
+        parts = ex.all_gather_object(dev.to_host(xl))
+        x = dev.to_device(gather_global(parts, m))
+        it = cg.status()[0]
+    else:
+        raise ValueError("decomposition must be 'auto', 'block', 'parity' or 'transpose'")
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    return x, info, it, decomposition

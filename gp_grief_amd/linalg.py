@@ -237,7 +237,7 @@ class KronCG(object):
 
 
 def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, callback=None,
-       recurrence="fused", fusion=None, basis=None):
+       recurrence="fused", fusion=None, basis=None, comm=None, decomposition="auto"):
     """Solve (K + shift I) x = b with CG on the device (x0 = 0).
 
     Same stopping rule and iterates as scipy.sparse.linalg.cg (recurrence:
@@ -247,6 +247,13 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
     solve, with no arguments beyond the counter protocol (the iterates stay on
     the device).  Returns (x, info) like scipy: info = 0 converged, else the
     number of iterations run.
+
+    comm (multi-GPU, one process per GPU): a torch.distributed process group,
+    True for the default group, or an exchange object -- every rank calls cg
+    with the same K and b and gets the whole x; the solve is sharded by
+    distributed.solve (decomposition "auto": the parity-block basis's blocks
+    over 2^K ranks where it exists, else the even / odd parity blocks, else
+    factor 0 sharded).
     """
     from . import device as dev
     n = int(K.shape[0])
@@ -258,6 +265,18 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         maxiter = n * 10
     if check_every is None:
         check_every = 10 if n >= 1 << 20 else 50
+    if comm is not None:
+        from . import distributed
+        x, info, it, how = distributed.solve(K, bd, shift, comm, rtol, atol, maxiter,
+                                             check_every, decomposition)
+        if callback is not None:
+            for _ in range(it):
+                callback()
+        out = (x.reshape(tuple(b.shape)) if b.numel() == n else x) if was_dev else \
+            dev.to_host(x).reshape(np.shape(b))
+        cg.last = CGResult(out, info, it, None, None)
+        cg.last.decomposition = how
+        return out, info
     solver = KronCG(K, shift, recurrence, fusion=fusion, basis=basis)
     solver.start(bd, rtol, atol)
     # one call: the library polls the device's done flag every check_every

@@ -49,6 +49,10 @@ SIGNATURES = {
                            ctypes.POINTER(ctypes.c_int)],
     "gg_kron_block_fold": [_vp, ctypes.c_int, _c_dp, _c_dp, _vp],
     "gg_kron_block_matvec": [_vp, _c_dp, _c_dp, ctypes.c_double, _c_dp, _vp],
+    "gg_kron_block_fold_range": [_vp, ctypes.c_int, _c_dp, _c_dp, ctypes.c_int64, ctypes.c_int64,
+                                 _vp],
+    "gg_kron_block_matvec_range": [_vp, _c_dp, _c_dp, ctypes.c_double, _c_dp, ctypes.c_int64,
+                                   ctypes.c_int64, _vp],
     "gg_kron_block_matvec_timed": [_vp, _c_dp, _c_dp, ctypes.c_double, _c_dp, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double), _vp],
@@ -62,6 +66,9 @@ SIGNATURES = {
     "gg_diag_divide": [_c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
     "gg_cg_work_elems": [_vp, _c_i64p],
     "gg_cg_create": [_vp, ctypes.c_double, _c_dp, ctypes.POINTER(ctypes.c_void_p)],
+    "gg_cg_work_elems_blocks": [_vp, ctypes.c_int64, _c_i64p],
+    "gg_cg_create_blocks": [_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, _c_dp,
+                            ctypes.POINTER(ctypes.c_void_p)],
     "gg_cg_destroy": [_vp],
     "gg_cg_start": [_vp, _c_dp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
     "gg_cg_iterate": [_vp, ctypes.c_int, ctypes.c_int, _vp],

@@ -85,6 +85,28 @@ class _DeviceKron(object):
                                                      native.stream_ptr()), "gg_kron_block_fold")
         return y
 
+    def block_fold_range(self, xd, blk0, nblk, inverse=False, out=None):
+        """Blocks [blk0, blk0 + nblk) of P x from the grid vector x; inverse:
+        their contribution P^T (those blocks) to the grid vector
+        (gg_kron_block_fold_range; summed over a sharded CG's ranks)."""
+        _, n, _ = self.block_info()
+        nl = n // (1 << len(self._keep)) * int(nblk)
+        y = dev.empty(n if inverse else nl) if out is None else out
+        native.check(native.lib().gg_kron_block_fold_range(
+            self.h, int(bool(inverse)), native.dptr(xd), native.dptr(y), int(blk0), int(nblk),
+            native.stream_ptr()), "gg_kron_block_fold_range")
+        return y
+
+    def block_matvec_range(self, xd, blk0, nblk, shift=0.0, out=None):
+        """(P K P^T + shift I) on blocks [blk0, blk0 + nblk) of the block
+        layout (gg_kron_block_matvec_range)."""
+        y = dev.empty(xd.numel()) if out is None else out
+        native.check(native.lib().gg_kron_block_matvec_range(
+            self.h, native.dptr(xd), native.dptr(y), float(shift),
+            native.dptr(self._block_work()), int(blk0), int(nblk), native.stream_ptr()),
+            "gg_kron_block_matvec_range")
+        return y
+
     def _block_work(self):
         if "block" not in self._work:
             self._work["block"] = dev.empty(self.n_rows)

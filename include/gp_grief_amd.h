@@ -100,6 +100,18 @@ int gg_kron_block_fold(const gg_kron* K, int inverse, const double* x_dev, doubl
  * The operator of kron_matrix.py:52-97 in the parity-block basis.           */
 int gg_kron_block_matvec(const gg_kron* K, const double* x_dev, double* y_dev, double shift,
                          double* work_dev, gg_stream stream);
+/* A block range [blk0, blk0 + nblk) of the block layout (a rank of the
+ * block-sharded CG: rank g of G = 2^K ranks owns blocks g 2^d / G ..): the
+ * forward fold writes those blocks only (y: nblk * n / 2^d doubles, x the full
+ * grid vector); the inverse reads them (y's other blocks count as 0) and
+ * writes their contribution to every element of the grid vector y -- summed
+ * over the ranks, P^T of the whole block vector.                           */
+int gg_kron_block_fold_range(const gg_kron* K, int inverse, const double* x_dev, double* y_dev,
+                             int64_t blk0, int64_t nblk, gg_stream stream);
+/* y = (P K P^T + shift I) x on blocks [blk0, blk0 + nblk) (x, y hold them). */
+int gg_kron_block_matvec_range(const gg_kron* K, const double* x_dev, double* y_dev,
+                               double shift, double* work_dev, int64_t blk0, int64_t nblk,
+                               gg_stream stream);
 /* reps of gg_kron_block_matvec with HIP events around each of its d - 1
  * launches (synchronising; as gg_kron_matvec_timed).                       */
 int gg_kron_block_matvec_timed(const gg_kron* K, const double* x_dev, double* y_dev,
@@ -214,6 +226,15 @@ int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, doub
  * operator (e); no reference counterpart for sharding. */
 int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* rr_dev,
                         gg_stream stream);
+/* A sharded-CG rank over blocks [blk0, blk0 + nblk) of the operator's
+ * parity-block layout (d >= 3): the rank's part of the operator is exactly
+ * those diagonal blocks, so the _partial / _finish steps above run the block
+ * kernels on them (gg_kron_block_matvec_range) with no exchange.  b and x are
+ * the rank's blocks (gg_kron_block_fold_range).  work_dev: 16-byte aligned,
+ * gg_cg_work_elems_blocks doubles.  gg_cg_start refuses such a handle.      */
+int gg_cg_work_elems_blocks(const gg_kron* K, int64_t nblk, int64_t* elems);
+int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shift,
+                        double* work_dev, gg_cg** out);
 int gg_cg_start_finish(gg_cg* cg, const double* rr_dev, double rtol, double atol,
                        gg_stream stream);
 int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream);

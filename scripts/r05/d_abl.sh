@@ -4,9 +4,9 @@
 set -o pipefail
 O=gpurun_out/r05_d
 mkdir -p $O
-for a in 0 1 3; do
+for a in 0 4 8 12; do
   GG_BLK_PAIR_ABL=$a timeout -k 10 120 python3 tools/block_bench.py --no-cg --no-grid --reps 5 > $O/abl$a.json 2> $O/abl$a.err || exit 1
   echo "abl=$a $(cat $O/abl$a.json)"
 done
-timeout -k 10 240 python3 tools/block_bench.py --reps 5 > $O/bench.json 2> $O/bench.err || exit 1
-cat $O/bench.json
+
+

@@ -216,6 +216,12 @@ class ThreadExchange(object):
 
     in_process = True  # peers' device buffers are plain pointers
 
+    def size(self):
+        return self.G
+
+    def rank(self):
+        return self.local.rank
+
     def barrier(self):
         torch.cuda.synchronize()
         self.bar.wait()
@@ -385,3 +391,68 @@ class ParityNumpyEngine(object):
 
     def profile(self, enable):
         pass
+
+
+class BlockNumpyEngine(ParityNumpyEngine):
+    """distributed.BlockHipEngine restated with NumPy on torch CPU tensors:
+    rank g's blocks [g 2^d / G, (g + 1) 2^d / G) of the operator in its
+    parity-block basis (oracle.kron.block_factors per block, kron_matvec
+    inside each), with ParityNumpyEngine's fused recurrence; fold / unfold
+    through oracle.kron.block_fold (the unfold is this rank's contribution,
+    the rest of the block vector zero)."""
+
+    mode = "block"
+
+    def __init__(self, K, world, rank, shift):
+        from gp_grief_amd.distributed import block_range
+        F = [np.asarray(f, dtype=np.float64) for f in K.K]
+        self.ms = [f.shape[0] for f in F]
+        self.d = len(F)
+        self.blk0, self.nblk = block_range(self.d, world, rank)
+        st = [oracle.kron.block_factors(f) for f in F]
+        self.nb = int(np.prod([m // 2 for m in self.ms]))
+        self.blocks = [[st[k][(b >> (self.d - 1 - k)) & 1] for k in range(self.d)]
+                       for b in range(self.blk0, self.blk0 + self.nblk)]
+        self.shift = float(shift)
+        self.n_local = self.nb * self.nblk
+        self.red5 = torch.zeros(5, dtype=torch.float64)
+        self.red1 = torch.zeros(1, dtype=torch.float64)
+        self.sc = {}
+
+    def profile(self, enable):
+        self._prof_on = bool(enable)
+        self._prof_n, self._prof_s = 0, 0.0
+
+    def profile_read(self):
+        """(iterations, [ms per launch position]): the host time of the
+        block products split evenly over the d - 1 launch positions."""
+        L = self.d - 1
+        return self._prof_n, [1e3 * self._prof_s / L] * L
+
+    def _A(self, v):
+        import time
+        t0 = time.perf_counter()
+        out = self._Kb(v) + self.shift * v
+        if getattr(self, "_prof_on", False):
+            self._prof_n += 1
+            self._prof_s += time.perf_counter() - t0
+        return out
+
+    def _Kb(self, v):
+        out = np.empty_like(v)
+        for j, fs in enumerate(self.blocks):
+            out[j * self.nb:(j + 1) * self.nb] = oracle.kron_matvec(
+                fs, v[j * self.nb:(j + 1) * self.nb])
+        return out
+
+    def apply(self, x, y):
+        y.numpy()[:] = self._Kb(x.numpy())
+
+    def fold(self, b):
+        bb = oracle.kron.block_fold(np.asarray(b, dtype=np.float64).reshape(-1), self.ms)
+        return torch.from_numpy(bb[self.blk0 * self.nb:(self.blk0 + self.nblk) * self.nb].copy())
+
+    def unfold(self, xl):
+        full = np.zeros(self.nb << self.d)
+        full[self.blk0 * self.nb:(self.blk0 + self.nblk) * self.nb] = np.asarray(xl)
+        return torch.from_numpy(oracle.kron.block_fold(full, self.ms, inverse=True))

@@ -149,26 +149,31 @@ def test_block_fast_kernels_match_generic(gg, monkeypatch, ms):
 
 @pytest.mark.parametrize("ms", [(40, 8, 72, 72), (10, 200, 200), (6, 14, 40, 40)])
 def test_block_pair_lds_kernel_matches_register_kernel(gg, monkeypatch, ms):
-    """blk_pair_lds_kernel (GEMM 1's operands through the LDS-DMA ring) and
-    blk_pair_kernel run the same MFMA chains in the same k order: the block
-    matvec is bitwise equal (pair orders 72 and 200; order 40 has no LDS
-    variant and must fall back); a fused CG agrees to 1e-12 (the p.q / q.q
-    partials group over different workgroups)."""
+    """blk_pair_lds_kernel (GEMM 1's operands through the LDS-DMA ring; one
+    or two slabs per workgroup) and blk_pair_kernel run the same MFMA chains
+    in the same k order: the block matvec is bitwise equal (pair orders 72
+    and 200; order 40 has no LDS variant and must fall back; (10, 200, 200)
+    has an odd slab count per block, so SPW 2 falls back to 1); a fused CG
+    agrees to 1e-12 (the p.q / q.q partials group over different
+    workgroups)."""
     F = factors(ms)
     n = int(np.prod(ms))
     x = np.random.default_rng(9).standard_normal(n)
     out = []
-    for lds in ("1", "0"):
+    for lds, spw in (("1", "2"), ("1", "1"), ("0", "2")):
         monkeypatch.setenv("GG_BLK_PAIR_LDS", lds)
+        monkeypatch.setenv("GG_BLK_PAIR_SPW", spw)
         K = gg.tensors.KronMatrix(F, sym=True)
         y = host(gg, K._device().block_matvec(dev(gg, x), shift=0.02))
         s = gg.linalg.KronCG(K, 0.02)
         s.start(dev(gg, x), rtol=1e-14)
         s.iterate(7)
         out.append((y, host(gg, s.x), s.status()))
-    assert np.array_equal(out[0][0], out[1][0])
-    assert rel(out[0][1], out[1][1]) < 1e-12
-    assert out[0][2][0] == out[1][2][0] == 7
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert rel(out[0][1], o[1]) < 1e-12
+        assert o[2][0] == 7
+    assert out[0][2][0] == 7
 
 
 def test_block_matvec_repeatable(gg):

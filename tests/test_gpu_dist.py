@@ -285,3 +285,136 @@ def test_parity_sharded_cg_processes(gpu, tmp_path, world, m, d):
     assert len({int(r["iters"]) for r in res}) == 1
     assert abs(int(res[0]["iters"]) - it) <= max(2, 0.02 * it)
     assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+
+
+# ---------------------------------------------------------------- block sharding
+@pytest.mark.parametrize("ms,blk0,nblk", [((6, 12, 40, 40), 4, 4), ((8, 72, 72), 2, 2),
+                                          ((40, 40, 40, 40), 15, 1), ((6, 12, 40, 40), 0, 16)])
+def test_block_fold_and_matvec_range_vs_oracle(gpu, ms, blk0, nblk):
+    """gg_kron_block_fold_range / gg_kron_block_matvec_range: a rank's blocks
+    of P b, of (P K P^T + s I) x_b, and its contribution to P^T x_b, against
+    oracle.kron.block_fold / block_matvec (kron_matrix.py:52-97 restated)."""
+    import gp_grief_amd as gg
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    dk = K._device()
+    n = int(np.prod(ms))
+    nb = n >> len(ms)
+    b = np.random.default_rng(21).standard_normal(n)
+    full = oracle.kron.block_fold(b, ms)
+    loc = gg.device.to_host(dk.block_fold_range(gg.device.to_device(b), blk0, nblk))
+    want = full[blk0 * nb:(blk0 + nblk) * nb]
+    assert np.linalg.norm(loc - want) <= 1e-15 * np.linalg.norm(want) + 1e-300
+    y = gg.device.to_host(dk.block_matvec_range(gg.device.to_device(want), blk0, nblk,
+                                                shift=0.05))
+    ref = (oracle.kron.block_matvec(F, full) + 0.05 * full)[blk0 * nb:(blk0 + nblk) * nb]
+    assert np.linalg.norm(y - ref) / np.linalg.norm(ref) < 1e-13
+    part = np.zeros(n)
+    part[blk0 * nb:(blk0 + nblk) * nb] = want
+    back = gg.device.to_host(dk.block_fold_range(gg.device.to_device(want), blk0, nblk,
+                                                 inverse=True))
+    ref = oracle.kron.block_fold(part, ms, inverse=True)
+    assert np.linalg.norm(back - ref) <= 1e-15 * np.linalg.norm(ref) + 1e-300
+
+
+def reference_factors_ms(ms):
+    g = [np.linspace(0, 1, m) for m in ms]
+    return [oracle.cov_1d("RBF", x, x, 1.0, 0.15 * (1 + 0.1 * k)) + 1e-12 * np.eye(len(x))
+            for k, x in enumerate(g)]
+
+
+@pytest.mark.parametrize("world,ms,shift", [(2, (6, 12, 40, 40), 0.05), (4, (6, 12, 40, 40), 0.05),
+                                            (8, (40, 40, 40, 40), 0.5), (16, (6, 12, 40, 40), 0.05),
+                                            (4, (8, 72, 72), 0.2), (2, (40, 8, 72, 72), 0.1)])
+def test_block_sharded_cg_virtual_ranks(gpu, world, ms, shift):
+    """distributed.solve, block decomposition: each virtual rank (a thread)
+    runs the block kernels on its 2^d / G blocks (gg_cg_create_blocks,
+    gg_cg_*_partial / _finish), folds b on the device and contributes its
+    unfold to the all-reduced x.  Every rank's x equals the oracle CG's (1e-8),
+    the iteration count the oracle's within 2 % and the single-GPU block
+    CG's exactly or within 2 (the restart vs repair of a cancelled beta)."""
+    import gp_grief_amd as gg
+    from gp_grief_amd.distributed import solve
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(22).standard_normal(n)
+    ex = ThreadExchange(world)
+
+    def body(g):
+        ex.bind(g)
+        x, info, it, how = solve(K, b, shift, ex, rtol=1e-10, maxiter=20000, check_every=9)
+        return gg.device.to_host(x), info, it, how
+
+    res = run_threads(world, body)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b,
+                                   rtol=1e-10)
+    assert all(r[3] == "block" and r[1] == 0 for r in res)
+    assert len({r[2] for r in res}) == 1
+    assert abs(res[0][2] - it) <= max(2, 0.02 * it)
+    for r in res:
+        assert np.linalg.norm(r[0] - xs) / np.linalg.norm(xs) < 1e-8
+    x1, i1 = gg.linalg.cg(K, b[:, None], shift=shift, rtol=1e-10, maxiter=20000)
+    assert abs(gg.linalg.cg.last.iters - res[0][2]) <= 2
+
+
+def test_cg_comm_api_virtual_ranks(gpu):
+    """The drop-in entry point: linalg.cg(K, y, comm=...) on every rank
+    returns the whole solution (host in, host out), sharded underneath."""
+    import gp_grief_amd as gg
+    ms, shift, world = (6, 12, 40, 40), 0.05, 4
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    y = np.random.default_rng(23).standard_normal((int(np.prod(ms)), 1))
+    ex = ThreadExchange(world)
+
+    def body(g):
+        ex.bind(g)
+        x, info = gg.linalg.cg(K, y, shift=shift, rtol=1e-10, comm=ex)
+        return x, info, gg.linalg.cg.last.decomposition
+
+    res = run_threads(world, body)
+    xs, _, _ = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, y[:, 0],
+                               rtol=1e-10)
+    for x, info, how in res:
+        assert info == 0 and how == "block" and x.shape == y.shape
+        assert np.linalg.norm(x[:, 0] - xs) / np.linalg.norm(xs) < 1e-8
+
+
+def _block_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from dist_helpers import bind_device
+    bind_device(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gp_grief_amd as gg
+    ms = (6, 12, 40, 40)
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    y = np.random.default_rng(24).standard_normal(int(np.prod(ms)))
+    x, info = gg.linalg.cg(K, y, shift=0.05, rtol=1e-10, comm=True)
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), x=x, info=info,
+             iters=gg.linalg.cg.last.iters, how=gg.linalg.cg.last.decomposition)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_block_sharded_cg_processes(gpu, tmp_path):
+    """Two processes (rank g on device g % count), linalg.cg(comm=True) over
+    the default process group (gloo here; RCCL on a multi-GPU node)."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.start_processes(_block_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(2)]
+    ms = (6, 12, 40, 40)
+    F = reference_factors_ms(ms)
+    y = np.random.default_rng(24).standard_normal(int(np.prod(ms)))
+    xs, _, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + 0.05 * v, y, rtol=1e-10)
+    for r in res:
+        assert str(r["how"]) == "block" and int(r["info"]) == 0
+        assert abs(int(r["iters"]) - it) <= max(2, 0.02 * it)
+        assert np.linalg.norm(r["x"] - xs) / np.linalg.norm(xs) < 1e-8
