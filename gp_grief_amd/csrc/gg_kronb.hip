@@ -858,7 +858,7 @@ __device__ __forceinline__ double bcast_group(double v) {
 
 // GEMM 2 and the epilogue of one slab (both pair kernels): Z = F2 W from the
 // role's W accumulators, q = Z (+ shift p, the p.q / q.q partials) stored.
-template <int TF, int J0, int NJ, bool TJ>
+template <int TF, int J0, int NJ, bool TJ, int EPI = -1, int PF = 4>
 __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, const double* f2,
                                            const bd4 (&W)[TF][NJ > 0 ? NJ : 1],
                                            const double (&Wta)[NJ > 0 ? NJ : 1],
@@ -874,7 +874,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
   uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
   asm volatile("" : "+v"(o_f), "+v"(o_z), "+v"(o_zt));
   // one 16-row strip t_i at a time
-  const bool epi = A.P != nullptr;
+  const bool epi = EPI < 0 ? A.P != nullptr : EPI != 0;
   const double sh = A.shift;
   // k-step s: B operands from the accumulators
   auto bfull = [&](int s, int u) -> double {
@@ -919,7 +919,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     const int64_t fti = (int64_t)ti * 512;
     // A fragments kPF k-steps ahead; the scheduling barriers keep each step's
     // loads / MFMAs in place
-    constexpr int kPF = 4;
+    constexpr int kPF = PF;
     double fr[kPF];
 #pragma unroll
     for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
@@ -952,7 +952,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int u = 0; u < NJ; ++u) Z4[u] = 0.0;
     const int64_t zrow = sbyte + (int64_t)16 * TF * H * 8;
     const int64_t fti = (int64_t)TF * 512;
-    constexpr int kPF = 4;
+    constexpr int kPF = PF;
     double fr[kPF];
 #pragma unroll
     for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
@@ -1183,7 +1183,7 @@ struct PairRing {
   static constexpr int XG = ((TF + 1) + 1) / 2 * 2;   // row groups, even
   static constexpr int XI = XG / 2;         // X DMAs per slab and stage (1 KiB: 2 groups)
   static constexpr int FI = (JT + 1) / 2;   // fragment DMAs (1 KiB: 2 fragments)
-  static constexpr int NW = 2 * SPW;        // waves per workgroup
+  static constexpr int NW = 2 * SPW;        // waves per workgroup (two roles per slab)
   // DMAs per stage, padded to a multiple of the wave count (the pads re-read
   // the last fragment pair into its own place)
   static constexpr int TOT = (SPW * XI + FI + NW - 1) / NW * NW;
@@ -1200,7 +1200,7 @@ struct PairSlabSrc {
   const double* f3;
 };
 
-template <int TF, int SPW, int J0, int NJ, bool TJ, typename Issue>
+template <int TF, int SPW, int EPI, int J0, int NJ, bool TJ, typename Issue>
 __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, int sl, int cslot,
                                               bool early, PairSlabSrc cur, PairSlabSrc nxt,
                                               bool nxt_valid, const double* ring, Issue&& issue,
@@ -1283,13 +1283,17 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
     }
     slot = slot + 1 == NS ? 0 : slot + 1;
   }
-  pair_gemm2<TF, J0, NJ, TJ>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
+  pair_gemm2<TF, J0, NJ, TJ, EPI>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
 }
 
 // SPW slabs per workgroup (2 waves each; SPW = 2: slabs 2 u, 2 u + 1 of one
 // block, so one fragment image serves both -- the host requires an even
-// slab count per block)
-template <int TF, int JA, int SPW>
+// slab count per block).  EPI: the fused CG's epilogue (q = Z + shift p with
+// the p.q / q.q partials) compiled in or out.  Three roles per slab (W in 114
+// registers, 3 waves per SIMD) measured slower: 15.4 against 11.4 ms at 200^4
+// -- every role streams all of F_{d-2}'s fragments in GEMM 2, half the MFMAs
+// per fragment load (profiles/r05/i_*).
+template <int TF, int JA, int SPW, int EPI>
 __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) {
   typedef PairRing<TF, SPW> R;
   constexpr int NS = R::NS;
@@ -1359,13 +1363,13 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     const int64_t slab = ((int64_t)blockIdx.x + (int64_t)it * G) * SPW + sl;
     const bool nv = it + 1 < nmine;
     const PairSlabSrc nxt = nv ? src_at(it + 1) : cur;
-    const int role = (wave + it) & 1;
+    const int role = (wave + it) & 1;   // roles alternate per unit
     if (role == 0)
-      pair_slab_lds<TF, SPW, 0, JA, true>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring, issue,
-                                          pq, qq);
+      pair_slab_lds<TF, SPW, EPI, 0, JA, true>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
+                                               issue, pq, qq);
     else
-      pair_slab_lds<TF, SPW, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
-                                                 issue, pq, qq);
+      pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
+                                                      ring, issue, pq, qq);
     cslot = (cslot + R::KS) % NS;
     cur = nxt;
   }
@@ -1443,14 +1447,17 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
 }
 
 // pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
-static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1) {
-  if (lds) {
-    switch (TF) {
-      case 2: return spw == 2 ? blk_pair_lds_kernel<2, 1, 2> : blk_pair_lds_kernel<2, 1, 1>;
-      case 6: return spw == 2 ? blk_pair_lds_kernel<6, 3, 2> : blk_pair_lds_kernel<6, 3, 1>;
-      default: return nullptr;
-    }
+template <int EPI>
+static blk_pair_fn select_pair_lds(int TF, int spw) {
+  switch (TF) {
+    case 2: return spw == 2 ? blk_pair_lds_kernel<2, 1, 2, EPI> : blk_pair_lds_kernel<2, 1, 1, EPI>;
+    case 6: return spw == 2 ? blk_pair_lds_kernel<6, 3, 2, EPI> : blk_pair_lds_kernel<6, 3, 1, EPI>;
+    default: return nullptr;
   }
+}
+
+static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false) {
+  if (lds) return epi ? select_pair_lds<1>(TF, spw) : select_pair_lds<0>(TF, spw);
   switch (TF) {
     case 1: return blk_pair_kernel<1, 1>;
     case 2: return blk_pair_kernel<2, 1>;
@@ -1690,7 +1697,7 @@ int64_t block_prologue_blocks(const BlockOp* B) {
 static int pair_grid(const BlockOp* B, int64_t nblk = -1) {
   const int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) *
                         (nblk < 0 ? ((int64_t)1 << B->d) : nblk);
-  if (B->pair_lds)
+  if (B->pair_lds)   // 4 slabs in flight per CU (the LDS ring's budget)
     return (int)std::min<int64_t>(nslab / B->pair_spw, (int64_t)B->cus * 4 / B->pair_spw);
   return (int)std::min<int64_t>(ceil_div(nslab, kBlkPairWaves / 2), (int64_t)B->cus * 2);
 }
@@ -1801,7 +1808,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     p.P = x;
     p.shift = shift;
   }
-  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw), dim3(grid),
+  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr), dim3(grid),
                      dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0, stream, p);
   GG_LAUNCH_CHECK();
   if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
