@@ -514,10 +514,7 @@ __global__ void splitk_reduce_kernel(int M, int N, int S, const double* __restri
   }
 }
 
-// Dynamic LDS the next TN launches of this host thread reserve at least
-// (0: the kernel's own need; gg_potrf's GG_POTRF_WIDE_LDS A/B knob).
-static thread_local size_t g_tn_min_lds = 0;
-constexpr size_t kTnMaxLds = 64 * 1024;
+
 
 template <int BK, int NS, int MW>
 static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alpha, const double* A,
@@ -527,10 +524,10 @@ static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alph
   const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_kernel<BK, NS, MW>);
   if (!attr) {
     GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)std::max(tn_glds_lds<BK, NS>(), kTnMaxLds)));
+                               (int)tn_glds_lds<BK, NS>()));
     attr = true;
   }
-  const size_t lds = std::max(tn_glds_lds<BK, NS>(), std::min(g_tn_min_lds, kTnMaxLds));
+  const size_t lds = tn_glds_lds<BK, NS>();
   hipLaunchKernelGGL((gemm_tn_glds_kernel<BK, NS, MW>), grid, dim3(kGemmThreads), lds, s, M, N,
                      K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
 }
@@ -622,7 +619,7 @@ static void launch_tn_wide(dim3 grid, hipStream_t s, int M, int N, int K, double
 // profiles/r03/n/gram_xcd_ab.jsonl); 3 was 53.0 TF on the C5 Gram against
 // 46.9 TF for the register-staged kernel (profiles/r02_g_gram_tn_variants.jsonl)
 static int gemm_tn_variant() {
-  const char* e = getenv("GG_GEMM_TN");
+  const char* e = gg::knob("GG_GEMM_TN");
   return e ? atoi(e) : 14;
 }
 
@@ -656,7 +653,7 @@ static int tn_splitk(int M, int N, int K, int uplo) {
   (void)uplo;
   if (K < 4096) return 1;
   const int64_t cap_k = std::max<int64_t>(1, K / (64 * kBK));
-  const char* e = getenv("GG_GEMM_SPLITK");
+  const char* e = gg::knob("GG_GEMM_SPLITK");
   if (e != nullptr) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), cap_k));
   const int64_t cap_mem = std::max<int64_t>(1, (int64_t)1e9 / ((int64_t)M * N));
   // the XCD-slab grid wants whole groups of 8 slabs; small Grams (few tiles)
@@ -812,8 +809,9 @@ constexpr int kNB = 64;
 // Streams of the calling device for gg_potrf's look-ahead (created once per
 // device, never destroyed: they live as long as the process).  which 0: the
 // factorisation chain (the critical path) at the highest priority; 1: the
-// wide trailing updates at the lowest; 2: the in-panel updates beside the
-// chain (highest).
+// wide trailing updates at the lowest.  (A CU-masked wide stream -- R of
+// every 32 CUs left to the chain -- measured slower than the priorities,
+// rounds 3-4: removed.)
 hipStream_t aux_stream(int which) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, hipStream_t> streams;
@@ -825,19 +823,7 @@ hipStream_t aux_stream(int which) {
   int least = 0, greatest = 0;
   GG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
   hipStream_t st;
-  if (which >= 16) {
-    // which = 16 + R: a CU-masked stream without the CUs whose bit index i
-    // has i % 32 < R (R of every 32 -- R per XCD whether the mask's words or
-    // its bits modulo 8 follow the XCDs)
-    int cus = 0;
-    GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    std::vector<uint32_t> mask((size_t)ceil_div(cus, 32), 0u);
-    for (int i = 0; i < cus; ++i)
-      if (i % 32 >= which - 16) mask[(size_t)(i / 32)] |= 1u << (i % 32);
-    GG_HIP(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
-  } else {
-    GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 1 ? least : greatest));
-  }
+  GG_HIP(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, which == 1 ? least : greatest));
   streams[{dev, which}] = st;
   return st;
 }
@@ -861,181 +847,6 @@ __device__ __forceinline__ double quad_sum(double v) {
   const int lo2 = __builtin_amdgcn_mov_dpp((int)b2, 0x4E, 0xF, 0xF, false);
   const int hi2 = __builtin_amdgcn_mov_dpp((int)(b2 >> 32), 0x4E, 0xF, 0xF, false);
   return v + __longlong_as_double(((long long)hi2 << 32) | (unsigned int)lo2);
-}
-
-// Fused diagonal-block factor + panel TRSM of one 64-column block (k0, nb):
-//   L_bb = chol(A[k0:k0+nb, k0:k0+nb])              (every workgroup, in LDS)
-//   L[rows, k0:k0+nb] = A[rows, k0:k0+nb] L_bb^-T    (workgroup b: 64 rows
-//                                                     k0 + nb + 64 b ...)
-// The last workgroup to arrive also stores L_bb (W = L_bb^-1 for gg_potrs is
-// formed after the factorisation, potrf_winv_kernel).  The 64 x 64 factor is cheap enough to repeat in every workgroup,
-// so a block step is ONE launch with no dependency between its workgroups.
-// Thread t owns row i = t / 4 and the columns j = (t & 3) + 4 u, u < 16, of
-// the block in registers (factor: D; TRSM: its row of the panel).  Every loop
-// is unrolled, so "is column j past k" is a compile-time fact except inside
-// one group of four columns, handled by a select: the code has no divergent
-// branches.  Factor: right-looking, two barriers per column k (pivot, then
-// column k in LDS).  TRSM: right-looking over the columns; x_j is broadcast
-// among the four threads of a row (one quad) by DPP.  Entries above the
-// diagonal take harmless updates and are never stored.
-// Padding rows / columns >= nb form an identity block (no effect on < nb).
-__global__ __launch_bounds__(256) void potrf_ftrsm_kernel(double* __restrict__ A, int64_t lda,
-                                                           int n, int k0, int nb, int P0,
-                                                           int* __restrict__ status,
-                                                           int* __restrict__ arrived,
-                                                           long long* __restrict__ stamps) {
-  // optional phase timing (GG_POTRF_PROF): wave 0 of every workgroup writes
-  // the 100 MHz clock at the phase boundaries (lane-varying slots keep these
-  // vector stores)
-  auto stamp = [&](int k) {
-    if (stamps != nullptr && threadIdx.x < 64)
-      stamps[(((int64_t)(k0 / kNB) * 160 + blockIdx.x) * 4 + k) * 64 + threadIdx.x] =
-          __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
-  __shared__ double Lf[kNB][kNB + 1];
-  __shared__ double Lb[kNB][kNB + 1];   // panel rows of the block / its update
-  __shared__ double Lr[kNB][kNB + 1];   // panel rows of this workgroup's rows / their update
-  __shared__ double colk[kNB + 256];   // column k, then one dummy slot per thread
-  __shared__ double invd[kNB];
-  __shared__ double piv;
-  __shared__ int last;
-  const int tid = threadIdx.x;
-  const int i = tid >> 2, q = tid & 3;
-  const int lane = tid & 63, wave = tid >> 6;
-  double* Abb = A + (int64_t)k0 * lda + k0;
-  const int64_t rbase = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB;   // this WG's rows
-  // ---- left-looking update by the panel's earlier columns [P0, k0) (the
-  // in-panel update, MFMA): D -= L_b L_b^T, R -= L_r L_b^T with L_b =
-  // L[k0:k0+64, P0:k0], L_r = L[rows, P0:k0], 64 columns per LDS chunk.  Wave
-  // w owns output rows 16w .. 16w+15 (4 column tiles of each product).
-  const bool upd = k0 > P0;
-  d4 dacc[4], racc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    dacc[t] = d4{0.0, 0.0, 0.0, 0.0};
-    racc[t] = d4{0.0, 0.0, 0.0, 0.0};
-  }
-  for (int c0 = P0; c0 < k0; c0 += kNB) {
-    for (int e = tid; e < kNB * kNB; e += 256) {
-      const int r = e >> 6, c = e & 63;
-      Lb[r][c] = r < nb ? A[(int64_t)(k0 + r) * lda + c0 + c] : 0.0;
-      Lr[r][c] = (rbase + r < n) ? A[(rbase + r) * lda + c0 + c] : 0.0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < kNB / 4; ++ks) {
-      const int kk = 4 * ks + (lane >> 4);
-      const double ad = Lb[16 * wave + (lane & 15)][kk];
-      const double ar = Lr[16 * wave + (lane & 15)][kk];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const double bv = Lb[16 * t + (lane & 15)][kk];
-        dacc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ad, bv, dacc[t], 0, 0, 0);
-        racc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ar, bv, racc[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  if (upd) {
-    // MFMA result layout: row 4 r + (lane >> 4), column lane & 15 of tile t
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        Lb[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = dacc[t][r];
-        Lr[16 * wave + 4 * r + (lane >> 4)][16 * t + (lane & 15)] = racc[t][r];
-      }
-    __syncthreads();
-  }
-  stamp(1);
-  double d[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = q + 4 * u;
-    d[u] = (i < nb && j <= i) ? Abb[(int64_t)i * lda + j] - (upd ? Lb[i][j] : 0.0)
-                              : (i == j ? 1.0 : 0.0);
-  }
-  bool bad = false;
-#pragma unroll
-  for (int k = 0; k < kNB; ++k) {
-    const int ku = k >> 2, kq = k & 3;
-    if (tid == 4 * k + kq) piv = d[ku];
-    __syncthreads();
-    const double dkk = piv;
-    if (k < nb && (!(dkk > 0.0) || !isfinite(dkk))) bad = true;
-    const double lkk = sqrt(fmax(dkk, 0.0));
-    const double il = 1.0 / lkk;
-    const bool own = q == kq && i >= k;
-    const double lv = (i == k) ? lkk : d[ku] * il;
-    d[ku] = own ? lv : d[ku];
-    colk[own ? i : kNB + tid] = lv;
-    __syncthreads();
-    const double li = colk[i];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      if (4 * u + 3 <= k) continue;             // columns j <= k: final
-      const double upd = fma(-li, colk[q + 4 * u], d[u]);
-      d[u] = (4 * u > k) ? upd : (q > kq ? upd : d[u]);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = q + 4 * u;
-    Lf[i][j] = (j <= i) ? d[u] : 0.0;
-  }
-  __syncthreads();
-  if (tid < kNB) invd[tid] = 1.0 / Lf[tid][tid];
-  stamp(2);
-  // The block is factored in place: the LAST workgroup to have read it (every
-  // workgroup holds the same L_bb) stores L_bb and W, so no workgroup can
-  // read a half-written block.  No waiting: the counter only picks the writer.
-  if (tid == 0) last = atomicAdd(arrived, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (last) {
-    if (bad && tid == 0) *status = 1;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int j = q + 4 * u;
-      if (i < nb && j <= i) Abb[(int64_t)i * lda + j] = d[u];
-    }
-  }
-  // ---- TRSM for this workgroup's 64 rows below the block
-  const int64_t row = (int64_t)k0 + nb + (int64_t)blockIdx.x * kNB + i;
-  if (row >= n) return;
-  double* Ar = A + row * lda + k0;
-  double x[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = q + 4 * u;
-    x[u] = j < nb ? Ar[j] - (upd ? Lr[i][j] : 0.0) : 0.0;
-  }
-#define GG_TRSM_STEP(J, jq_)                                                         \
-  do {                                                                               \
-    const int ju_ = (J) >> 2;                                                        \
-    const double own_ = x[ju_] * invd[J];                                            \
-    x[ju_] = q == jq_ ? own_ : x[ju_];                                               \
-    const double xj_ = quad_bcast<jq_>(own_);                                        \
-    _Pragma("unroll") for (int u = 0; u < 16; ++u) {                                 \
-      if (4 * u + 3 <= (J)) continue;                                                \
-      const double upd_ = fma(-xj_, Lf[q + 4 * u][J], x[u]);                         \
-      x[u] = (4 * u > (J)) ? upd_ : (q > jq_ ? upd_ : x[u]);                         \
-    }                                                                                \
-  } while (0)
-#pragma unroll
-  for (int j = 0; j < kNB; j += 4) {
-    GG_TRSM_STEP(j, 0);
-    GG_TRSM_STEP(j + 1, 1);
-    GG_TRSM_STEP(j + 2, 2);
-    GG_TRSM_STEP(j + 3, 3);
-  }
-#undef GG_TRSM_STEP
-#pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int j = q + 4 * u;
-    if (j < nb) Ar[j] = x[u];
-  }
-  stamp(3);
 }
 
 // ---- Cholesky block step, round 3 (potrf_fac_kernel + potrf_upd_kernel).
@@ -1600,24 +1411,6 @@ __global__ __launch_bounds__(256) void trsv_chain_kernel(int n, const double* __
   }
 }
 
-// dst[c][r] = src[r][c] (rows x cols -> cols x rows), 32 x 32 LDS tiles
-__global__ __launch_bounds__(256) void transpose_kernel(const double* __restrict__ src,
-                                                        int64_t lds, int rows, int cols,
-                                                        double* __restrict__ dst, int64_t ldd) {
-  __shared__ double tile[32][33];
-  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int k = ty; k < 32; k += 8) {
-    const int r = r0 + k, c = c0 + tx;
-    tile[k][tx] = (r < rows && c < cols) ? src[(int64_t)r * lds + c] : 0.0;
-  }
-  __syncthreads();
-  for (int k = ty; k < 32; k += 8) {
-    const int c = c0 + k, r = r0 + tx;
-    if (c < cols && r < rows) dst[(int64_t)c * ldd + r] = tile[tx][k];
-  }
-}
-
 // Triangular solve with many right-hand sides as one chained launch per
 // direction: workgroup (b, j) computes the 64 x 64 block X[b, j] (block row b
 // of the solution, column chunk j of the right-hand sides).  Linear ids run
@@ -1950,20 +1743,14 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     // 12.9 ms, p = 5000 4.09 -> 3.95), else 256 (p = 1000: 0.74 vs 0.89 ms;
     // profiles/r03/w_potrf_ab.jsonl).  GG_POTRF_PANEL=<columns> (multiple of
     // 64) for A/B.
-    const char* pe = getenv("GG_POTRF_PANEL");
+    const char* pe = gg::knob("GG_POTRF_PANEL");
     const int kPanel = pe ? std::max(gg::kNB, (atoi(pe) / gg::kNB) * gg::kNB)
                           : (n >= 4096 ? 8 : 4) * gg::kNB;
     // GG_POTRF_LOOKAHEAD=0: everything on s (A/B and debugging)
-    const char* la = getenv("GG_POTRF_LOOKAHEAD");
+    const char* la = gg::knob("GG_POTRF_LOOKAHEAD");
     const bool lookahead = !(la != nullptr && atoi(la) == 0);
     hipStream_t cs = lookahead ? gg::aux_stream(0) : s;   // factor chain, high priority
-    // GG_POTRF_CUMASK=R (1..31, A/B): the wide updates on a CU-masked stream
-    // that leaves R CUs of every 32 to the chain, instead of the low-priority
-    // stream (whose workgroups hold every CU until they drain)
-    const char* cm = getenv("GG_POTRF_CUMASK");
-    const int cu_res = cm ? std::max(0, std::min(31, atoi(cm))) : 0;
-    hipStream_t ws = lookahead ? gg::aux_stream(cu_res > 0 ? 16 + cu_res : 1) : s;
-    hipStream_t us = lookahead ? gg::aux_stream(2) : s;   // in-panel updates, high priority
+    hipStream_t ws = lookahead ? gg::aux_stream(1) : s;   // wide updates, low priority
     std::vector<hipEvent_t> evs;
     auto new_event = [&]() {
       hipEvent_t e;
@@ -1977,7 +1764,6 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       GG_HIP(hipEventRecord(e0, s));
       GG_HIP(hipStreamWaitEvent(cs, e0, 0));
       GG_HIP(hipStreamWaitEvent(ws, e0, 0));
-      GG_HIP(hipStreamWaitEvent(us, e0, 0));
     }
     // two transposed-panel buffers (kPanel x ldt each), stream-ordered
     const int64_t ldt = (n + 1) & ~1;   // even: 16-byte aligned rows for the DMA
@@ -1991,7 +1777,7 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
     }
     // GG_POTRF_PROF=<file>: per-block-launch phase stamps of every workgroup
     // (raw int64: nblk, 160, 4, then [nblk][160][4] 100 MHz ticks; 0 = absent)
-    const char* prof = getenv("GG_POTRF_PROF");
+    const char* prof = gg::knob("GG_POTRF_PROF");
     long long* pstamps = nullptr;
     const size_t nstamp = (size_t)nblk * 160 * 4 * 64;
     if (prof != nullptr && nblk <= 160) {
@@ -2003,56 +1789,29 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         GG_HIP(hipStreamWaitEvent(cs, ep, 0));
       }
     }
-    // GG_POTRF_V1=1: the round-2 block step (left-looking in-panel update and
-    // column-at-a-time factor inside the block launch, transpose + MFMA GEMM
-    // narrow update) for A/B
-    const char* v1e = getenv("GG_POTRF_V1");
-    const bool v1 = v1e != nullptr && atoi(v1e) != 0;
-    const char* fue = getenv("GG_POTRF_FUSE");
-    const bool fuse = fue != nullptr && atoi(fue) != 0;
-    // GG_POTRF_WIDE_LDS=<bytes>: pad the wide update's workgroups (A/B: at 56 KB
-    // two share a CU and a block step fits beside them; measured no faster,
-    // the block steps slow down beside FP64 MFMA waves -- unpadded by default)
-    const char* wl = getenv("GG_POTRF_WIDE_LDS");
-    const size_t wide_lds = (lookahead && wl) ? (size_t)atol(wl) : 0;
-    for (int P0 = 0; P0 < n && !v1; P0 += kPanel) {
+    // (Measured slower and removed, rounds 2-4: the round-2 left-looking block
+    // step; F(k) applying block k - 1's term itself with the in-panel update
+    // on a side stream; padding the wide update's workgroups so a block step
+    // fits beside them; a CU-masked wide stream.)
+    for (int P0 = 0; P0 < n; P0 += kPanel) {
       const int pend = std::min(n, P0 + kPanel);
       double* LT = (lt_buf && pend < n) ? lt_buf + (int64_t)((P0 / kPanel) & 1) * kPanel * ldt
                                         : nullptr;
       // Block step k: F(k) factors column block k and solves the rows below
       // it; U(k) gives the panel's later column blocks the term of block k.
-      // GG_POTRF_FUSE=1 (A/B): F(k) applies the newest term (block k - 1) to its
-      // own column block itself and U(k) covers blocks k + 2.. on the side
-      // stream us, beside F(k + 1) (F(k + 2) waits for it) -- measured slower:
-      // the fused MFMA term costs the block step ~8 us, about the U launch it
-      // replaces (profiles/r03/v_potrf_fused.txt).
-      std::vector<hipEvent_t> ev_u((size_t)gg::ceil_div(pend - P0, gg::kNB), nullptr);
       for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
-        const int b = k0 / gg::kNB, bi = (k0 - P0) / gg::kNB;
+        const int b = k0 / gg::kNB;
         const int nb = std::min(gg::kNB, n - k0);
         const int grid = std::max(1, (int)gg::ceil_div(n - k0 - nb, gg::kNB));
-        if (fuse && bi >= 2 && ev_u[bi - 2] != nullptr)
-          GG_HIP(hipStreamWaitEvent(cs, ev_u[bi - 2], 0));
         hipLaunchKernelGGL(gg::potrf_fac_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n, k0,
-                           nb, P0, pend, (fuse && bi >= 1) ? k0 - gg::kNB : -1, LT, ldt, status,
-                           arrived + b, pstamps);
+                           nb, P0, pend, -1, LT, ldt, status, arrived + b, pstamps);
         GG_LAUNCH_CHECK();
-        const int c0 = k0 + (fuse ? 2 : 1) * gg::kNB;
+        const int c0 = k0 + gg::kNB;
         if (c0 < pend) {
-          hipStream_t u = fuse ? us : cs;
-          if (u != cs) {
-            hipEvent_t ef = new_event();
-            GG_HIP(hipEventRecord(ef, cs));
-            GG_HIP(hipStreamWaitEvent(u, ef, 0));
-          }
           dim3 ug((unsigned)gg::ceil_div(n - c0, gg::kNB), (unsigned)gg::ceil_div(pend - c0, gg::kNB));
-          hipLaunchKernelGGL(gg::potrf_upd_kernel<false>, ug, dim3(256), 0, u, A_dev, lda, n, k0,
+          hipLaunchKernelGGL(gg::potrf_upd_kernel<false>, ug, dim3(256), 0, cs, A_dev, lda, n, k0,
                              k0 + gg::kNB, c0, pend);
           GG_LAUNCH_CHECK();
-          if (u != cs) {
-            ev_u[bi] = new_event();
-            GG_HIP(hipEventRecord(ev_u[bi], u));
-          }
         }
       }
       if (pend >= n) break;
@@ -2078,58 +1837,6 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
         if (lookahead) GG_HIP(hipStreamWaitEvent(ws, ef, 0));
         const int pw = pend - P0;
         const double* Lw = LT + (nend - pend);
-        gg::g_tn_min_lds = wide_lds;
-        gg::gemm(true, false, n - nend, n - nend, pw, -1.0, Lw, ldt, Lw, ldt, 1.0,
-                 A_dev + (int64_t)nend * lda + nend, lda, 1, ws);
-        gg::g_tn_min_lds = 0;
-        if (lookahead) {
-          ev_wide = new_event();
-          GG_HIP(hipEventRecord(ev_wide, ws));
-        }
-      } else {
-        ev_wide = nullptr;
-      }
-    }
-    for (int P0 = 0; P0 < n && v1; P0 += kPanel) {
-      const int pend = std::min(n, P0 + kPanel);
-      for (int k0 = P0; k0 < pend; k0 += gg::kNB) {
-        const int b = k0 / gg::kNB;
-        const int nb = std::min(gg::kNB, n - k0);
-        const int rest = n - k0 - nb;
-        const int grid = std::max(1, (int)gg::ceil_div(rest, gg::kNB));
-        // the block's update by the panel's earlier blocks is left-looking,
-        // inside the same launch (no in-panel GEMM)
-        hipLaunchKernelGGL(gg::potrf_ftrsm_kernel, dim3(grid), dim3(256), 0, cs, A_dev, lda, n,
-                           k0, nb, P0, status, arrived + b, pstamps);
-        GG_LAUNCH_CHECK();
-        (void)rest;
-      }
-      if (pend >= n) break;
-      const int nend = std::min(n, pend + kPanel);
-      const int pw = pend - P0;
-      // the panel's rows below it, transposed (k-major, pw x (n - pend)) into
-      // one of two buffers (panel P reuses the buffer of P - 2, whose wide
-      // update cs already waited for), so both updates below are TN products
-      // on the LDS-DMA Gram kernel instead of NT register-staged GEMMs
-      double* LT = lt_buf + (int64_t)((P0 / kPanel) & 1) * kPanel * ldt;
-      {
-        dim3 tg((unsigned)gg::ceil_div(pw, 32), (unsigned)gg::ceil_div(n - pend, 32));
-        hipLaunchKernelGGL(gg::transpose_kernel, tg, dim3(256), 0, cs,
-                           A_dev + (int64_t)pend * lda + P0, lda, n - pend, pw, LT, ldt);
-        GG_LAUNCH_CHECK();
-      }
-      // narrow: A[pend:, pend:nend] -= L[pend:, P] L[pend:nend, P]^T (lower)
-      if (ev_wide) GG_HIP(hipStreamWaitEvent(cs, ev_wide, 0));
-      gg::gemm(true, false, n - pend, nend - pend, pw, -1.0, LT, ldt, LT, ldt, 1.0,
-               A_dev + (int64_t)pend * lda + pend, lda, 1, cs);
-      if (nend < n) {
-        // wide: A[nend:, nend:] -= L[nend:, P] L[nend:, P]^T (lower), on ws
-        if (lookahead) {
-          hipEvent_t ef = new_event();
-          GG_HIP(hipEventRecord(ef, cs));
-          GG_HIP(hipStreamWaitEvent(ws, ef, 0));
-        }
-        const double* Lw = LT + (nend - pend);
         gg::gemm(true, false, n - nend, n - nend, pw, -1.0, Lw, ldt, Lw, ldt, 1.0,
                  A_dev + (int64_t)nend * lda + nend, lda, 1, ws);
         if (lookahead) {
@@ -2141,14 +1848,12 @@ int gg_potrf(int n, double* A_dev, int64_t lda, double* winv_dev, double* logdet
       }
     }
     if (lookahead) {
-      // join: s waits for everything issued on cs, ws and us
-      hipEvent_t ec = new_event(), ew = new_event(), eu = new_event();
+      // join: s waits for everything issued on cs and ws
+      hipEvent_t ec = new_event(), ew = new_event();
       GG_HIP(hipEventRecord(ec, cs));
       GG_HIP(hipEventRecord(ew, ws));
-      GG_HIP(hipEventRecord(eu, us));
       GG_HIP(hipStreamWaitEvent(s, ec, 0));
       GG_HIP(hipStreamWaitEvent(s, ew, 0));
-      GG_HIP(hipStreamWaitEvent(s, eu, 0));
     }
     if (lt_buf) GG_HIP(hipFreeAsync(lt_buf, s));
     hipLaunchKernelGGL(gg::potrf_winv_kernel, dim3(nblk), dim3(256), 0, s, A_dev, lda, n,
@@ -2201,7 +1906,7 @@ int gg_potrs(int n, int r, const double* L_dev, int64_t lda, const double* winv_
     const bool tri = (which & 4) != 0;
     // one right-hand side: each direction is ONE chained launch
     // (trsv_chain_kernel) instead of a GEMM pair per block row
-    const char* ch = getenv("GG_TRSV_CHAIN");
+    const char* ch = gg::knob("GG_TRSV_CHAIN");
     if (r == 1 && !tri && ldb == 1 && !(ch != nullptr && atoi(ch) == 0)) {
       // [forward flags | backward flags | status | two tickets]
       int* flags = nullptr;

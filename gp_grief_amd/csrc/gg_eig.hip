@@ -1029,10 +1029,10 @@ int gg_sym_eig_batched(int count, const int64_t* m, const double* A_dev, double*
     const bool lds_a = mmax <= gg::kLdsMaxM;
     // tridiagonalisation + implicit QL (default), or the round-robin Jacobi
     // (GG_EIG=jacobi: reference implementation kept for A/B)
-    const char* ev = getenv("GG_EIG");
+    const char* ev = gg::knob("GG_EIG");
     const bool jacobi = ev != nullptr && std::string(ev) == "jacobi";
     long long* dstamps = nullptr;
-    const bool prof = getenv("GG_EIG_PROF") != nullptr;
+    const bool prof = gg::knob("GG_EIG_PROF") != nullptr;
     if (!jacobi && prof) {
       GG_HIP(hipMallocAsync(&dstamps, 8 * 64 * sizeof(long long) * count, s));
       GG_HIP(hipMemsetAsync(dstamps, 0, 8 * 64 * sizeof(long long) * count, s));

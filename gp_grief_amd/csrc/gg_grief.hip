@@ -262,7 +262,7 @@ static bool launch_tables_mfma(int nf, const int* kinds, const double* variances
                                const int* ms, const double* const* qsels, const int* us,
                                double* ltab, double* stab, int U, const int* col0s,
                                hipStream_t s) {
-  const char* tv = getenv("GG_GRIEF_TABLES");   // 0: the lane-quad kernel (A/B)
+  const char* tv = gg::knob("GG_GRIEF_TABLES");   // 0: the lane-quad kernel (A/B)
   if (tv && atoi(tv) == 0) return false;
   if (nf < 1 || nf > kTabMaxF) return false;
   TabBatch B;
@@ -421,7 +421,7 @@ static void launch_phi_pair(dim3 grid, size_t lds, hipStream_t s, const double* 
 static bool launch_phi_pair_d(hipStream_t s, const double* L, const double* S, int U, int64_t n,
                               const int* cidx, int d, const double* ll, int p, double* phi) {
   static const bool on = [] {
-    const char* e = getenv("GG_PHI_PAIR");   // A/B knob: 0 = the 256-column kernel
+    const char* e = gg::knob("GG_PHI_PAIR");   // A/B knob: 0 = the 256-column kernel
     return !(e != nullptr && atoi(e) == 0);
   }();
   if (!on || d > 8 || (p & 1) || (reinterpret_cast<uintptr_t>(phi) & 15)) return false;

@@ -200,6 +200,12 @@ void launch_reduce_to(const double* partials, int64_t count, double* out, hipStr
 // streaming kernel sized to sit beside the ring mode products (gg_vec.hip)
 void launch_x_half(double* x, int64_t n, int64_t H, const CgScalars* sc, hipStream_t s);
 
+// ---- environment switches (gg_knobs.hip): the process snapshot of every
+// GG_* variable, taken at the first lookup and re-taken at gg_kron_create /
+// gg_cg_create / gg_knobs_reload (never getenv on a launch path)
+const char* knob(const char* name);
+void knobs_reload();
+
 // ---- the Kronecker operator in its parity-block basis (gg_kronb.hip) ----
 struct BlockOp;
 // nullptr when the operator has no block form (a factor not square, of odd

@@ -793,7 +793,7 @@ static ModeConfig cfg_glds() {
 // five strided vector passes (tools/hbm_stream_bench.hip: 3R2W in the A
 // pattern at 4.18 / 4.43 / 4.66 TB/s for 4 / 8 / 12 waves in lockstep).
 static int pro_variant() {
-  const char* e = getenv("GG_MP_PRO");
+  const char* e = gg::knob("GG_MP_PRO");
   return e ? atoi(e) : 0;
 }
 
@@ -854,7 +854,7 @@ static ModeConfig config_for(int variant, int cgp) {
 constexpr int kNumVariants = 14;
 
 static int mode_variant() {
-  const char* e = getenv("GG_MP_VARIANT");  // tuning knob, re-read per call
+  const char* e = gg::knob("GG_MP_VARIANT");  // tuning knob, re-read per call
   return e ? atoi(e) : 0;
 }
 
@@ -934,7 +934,7 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
       }
   GG_HIP(hipMalloc(&f.frag, h.size() * sizeof(double)));
   GG_HIP(hipMemcpy(f.frag, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (t4_supported(f.JT) && f.p - 16 * (int64_t)(f.JT - 1) <= 8 && getenv("GG_MP_NO_T4") == nullptr) {
+  if (t4_supported(f.JT) && f.p - 16 * (int64_t)(f.JT - 1) <= 8 && gg::knob("GG_MP_NO_T4") == nullptr) {
     const int JF = f.JT + 1;
     std::vector<double> h4(((size_t)f.KS + 8) * JF * 64, 0.0);
     for (int ks = 0; ks < f.KS; ++ks)
@@ -955,18 +955,18 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
 
 // the centrosymmetric split (mode_product_fold_kernel) for square factors
 static int fold_min_size() {
-  const char* e = getenv("GG_KRON_FOLD_MIN");
+  const char* e = gg::knob("GG_KRON_FOLD_MIN");
   const int v = e ? atoi(e) : 48;
   return v < 8 ? 8 : v;   // h >= 4: the kernel's unclamped row walk stays in bounds
 }
 static bool fold_enabled() {
-  const char* e = getenv("GG_KRON_FOLD");
+  const char* e = gg::knob("GG_KRON_FOLD");
   return !(e && atoi(e) == 0);
 }
 // tail fragments of a half of hS columns in JT tiles (even m, JT >= 4 only:
 // the instantiated shapes)
 static int fold_tail(int64_t m, int JT) {
-  if (m % 2 != 0 || JT < 4 || getenv("GG_MP_NO_T4") != nullptr) return 0;
+  if (m % 2 != 0 || JT < 4 || gg::knob("GG_MP_NO_T4") != nullptr) return 0;
   const int64_t r = (m - m / 2) - 16 * (int64_t)(JT - 1);
   return r <= 4 ? 1 : r <= 8 ? 2 : 0;
 }
@@ -1050,7 +1050,7 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
 // GG_FOLD_RING_SIDE=1: the CG side-job launch on the ring kernel (opt-in:
 // 8.6 vs 8.2 ms per side launch at 200^4, profiles/r04/j_side_ab.txt)
 static bool ring_side_env() {
-  const char* e = getenv("GG_FOLD_RING_SIDE");
+  const char* e = gg::knob("GG_FOLD_RING_SIDE");
   return e && atoi(e) == 1;
 }
 
@@ -1379,6 +1379,7 @@ int gg_kron_create(int d, const int64_t* rows, const int64_t* cols,
   return gg::guard([&] {
     GG_REQUIRE(out != nullptr, GG_ERR_VALUE, "out is NULL");
     GG_REQUIRE(d >= 1, GG_ERR_VALUE, "need at least one factor");
+    gg::knobs_reload();   // the handle's switches are the environment's now
     gg::set_lds_limits();
     gg_kron* K = new gg_kron();
     try {

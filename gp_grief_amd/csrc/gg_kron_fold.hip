@@ -710,7 +710,7 @@ static FoldConfig cfg_fold() {
 // GG_FOLD_LEAN=0 disables them; GG_FOLD_LEAN_PRO=1 / 2 (A/B only) takes a
 // lean fused-CG prologue with 1 / 2 k-steps per chunk -- 0.2-0.3 ms slower.
 static int env_int(const char* name, int dflt = 0) {
-  const char* e = getenv(name);
+  const char* e = gg::knob(name);
   return e ? atoi(e) : dflt;
 }
 
@@ -788,7 +788,7 @@ static FoldConfig cfg_fold_var() {
 }
 
 static int fold_variant() {
-  const char* e = getenv("GG_FOLD_VARIANT");
+  const char* e = gg::knob("GG_FOLD_VARIANT");
   return e ? atoi(e) : 0;
 }
 
@@ -832,7 +832,7 @@ static FoldConfig fold_staged_by_kind(int kind, bool lean_ok) {
 }
 
 bool fold_staged_available(int JT, int TT, int kind) {
-  const char* e = getenv("GG_FOLD_STAGE");   // A/B knob: 0 = direct stores
+  const char* e = gg::knob("GG_FOLD_STAGE");   // A/B knob: 0 = direct stores
   if (e && atoi(e) == 0) return false;
   return (kind == 0 || kind == 3 || kind == 6) && JT >= 1 && JT <= 8 &&
          (TT == 0 || JT >= 4);
@@ -894,7 +894,7 @@ static FoldConfig fold_by_kind(int kind, bool lean_ok) {
           default: return wide_cfg(2);
         }
       }
-      const char* e = getenv("GG_FOLD_PRO_KC");
+      const char* e = gg::knob("GG_FOLD_PRO_KC");
       if (e && atoi(e) == 1) return fold_pro_kc1();
     }
     if (kind == 7) {

@@ -542,7 +542,7 @@ static const int kRingVariants[] = {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 17,
                                     21, 25, 26, 27, 28, 31, 32, 41, 42, 43};
 
 int ring_variant_env() {
-  const char* e = getenv("GG_FOLD_RING");   // unset: the default (42); 0: off
+  const char* e = gg::knob("GG_FOLD_RING");   // unset: the default (42); 0: off
   return e ? atoi(e) : 42;
 }
 

@@ -842,8 +842,15 @@ struct PairArgs {
   double* partials;    // [grid] p.q, [pstride + grid] r.q (0), [2 pstride + grid] q.q
   int64_t pstride;
   const int* skip;
+  // the fused CG's balanced x side job (blk_pair_lds_kernel, SIDE): x += c0 p0
+  // + c1 p1 over half sc->xh of x -- [soff, soff + sn) or [soff_h1, soff_h1 +
+  // sn_h1); each wave slot (unit * waves + wave) takes sstep elements
+  const CgScalars* sc;
+  double* sx;
+  int64_t soff, sn, soff_h1, sn_h1, sstep;
   int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
-                       // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs
+                       // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs;
+                       // 32 the x side job back in the second launch (A/B)
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -1293,7 +1300,11 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
 // registers, 3 waves per SIMD) measured slower: 15.4 against 11.4 ms at 200^4
 // -- every role streams all of F_{d-2}'s fragments in GEMM 2, half the MFMAs
 // per fragment load (profiles/r05/i_*).
-template <int TF, int JA, int SPW, int EPI>
+// SIDE: after each unit's GEMM 2 (W dead, the registers free) the wave applies
+// its slice of the fused CG's x side job with ordinary 16-byte loads and
+// stores -- streaming work the memory-bound second launch carried before,
+// here beside the MFMA-bound slab products.
+template <int TF, int JA, int SPW, int EPI, int SIDE>
 __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) {
   typedef PairRing<TF, SPW> R;
   constexpr int NS = R::NS;
@@ -1354,6 +1365,53 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
           (__attribute__((address_space(3))) void*)(dst + dlds[j]), 16, 0, 0);
     }
   };
+  // the side job's half for this iteration (sc->xh, fixed during the launch)
+  double sc0 = 0.0, sc1 = 0.0;
+  const double* sp0 = nullptr;
+  const double* sp1 = nullptr;
+  double* sxo = nullptr;
+  int64_t slen = 0;
+  if (SIDE) {
+    const int xh = A.sc->xh;
+    if (xh < 2 && !A.sc->done) {
+      const int64_t off = xh ? A.soff_h1 : A.soff;
+      slen = xh ? A.sn_h1 : A.sn;
+      sc0 = A.sc->xc[0];
+      sc1 = A.sc->xc[1];
+      sp0 = A.sc->xp[0] + off;
+      sp1 = A.sc->xp[1] + off;
+      sxo = A.sx + off;
+    }
+  }
+  // this wave's slice [q0, q1) of the half: 16 bytes per lane, kSB batches
+  // of loads in flight (the expression of mp_side_job / cg_x_half_kernel)
+  auto side_chunk = [&](int64_t slot) {
+    const int64_t q0 = slot * A.sstep;
+    const int64_t q1 = min(slen, q0 + A.sstep);
+    constexpr int kSB = 8;
+    for (int64_t e0 = q0 + 2 * lane; e0 < q1; e0 += kSB * 128) {
+      double2 xv[kSB], a[kSB], b[kSB];
+#pragma unroll
+      for (int u = 0; u < kSB; ++u) {
+        const int64_t e = e0 + (int64_t)u * 128;
+        if (e + 1 < q1) {
+          xv[u] = ld2g(sxo + e);
+          a[u] = ld2g(sp0 + e);
+          b[u] = ld2g(sp1 + e);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kSB; ++u) {
+        const int64_t e = e0 + (int64_t)u * 128;
+        if (e + 1 < q1) {
+          double2 o;
+          o.x = xv[u].x + (sc0 * a[u].x + sc1 * b[u].x);
+          o.y = xv[u].y + (sc0 * a[u].y + sc1 * b[u].y);
+          st2g(sxo + e, o);
+        }
+      }
+    }
+  };
   PairSlabSrc cur = src_at(0);
 #pragma unroll
   for (int j = 0; j + 1 < NS; ++j) issue(cur, min(j, R::KS - 1), j);   // stages 0 .. NS - 2
@@ -1370,6 +1428,7 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     else
       pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
                                                       ring, issue, pq, qq);
+    if (SIDE && slen > 0) side_chunk(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
     cslot = (cslot + R::KS) % NS;
     cur = nxt;
   }
@@ -1447,17 +1506,27 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
 }
 
 // pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
-template <int EPI>
+template <int EPI, int SIDE>
 static blk_pair_fn select_pair_lds(int TF, int spw) {
   switch (TF) {
-    case 2: return spw == 2 ? blk_pair_lds_kernel<2, 1, 2, EPI> : blk_pair_lds_kernel<2, 1, 1, EPI>;
-    case 6: return spw == 2 ? blk_pair_lds_kernel<6, 3, 2, EPI> : blk_pair_lds_kernel<6, 3, 1, EPI>;
+    case 2:
+      return spw == 2 ? blk_pair_lds_kernel<2, 1, 2, EPI, SIDE>
+                      : blk_pair_lds_kernel<2, 1, 1, EPI, SIDE>;
+    case 6:
+      return spw == 2 ? blk_pair_lds_kernel<6, 3, 2, EPI, SIDE>
+                      : blk_pair_lds_kernel<6, 3, 1, EPI, SIDE>;
     default: return nullptr;
   }
 }
 
-static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false) {
-  if (lds) return epi ? select_pair_lds<1>(TF, spw) : select_pair_lds<0>(TF, spw);
+// epi: the fused CG's epilogue; side: its x side job rides in the launch
+// (LDS kernel only; the CG epilogue always comes with it there)
+static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false,
+                               bool side = false) {
+  if (lds) {
+    if (side) return select_pair_lds<1, 1>(TF, spw);
+    return epi ? select_pair_lds<1, 0>(TF, spw) : select_pair_lds<0, 0>(TF, spw);
+  }
   switch (TF) {
     case 1: return blk_pair_kernel<1, 1>;
     case 2: return blk_pair_kernel<2, 1>;
@@ -1491,7 +1560,7 @@ static void blk_set_lds_limits(const BlockOp* B) {
 BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
                       const double* const* factors) {
   if (d < 2 || d > kBlkMaxD) return nullptr;
-  const char* env = getenv("GG_KRON_BLOCK");   // read once, at handle creation
+  const char* env = gg::knob("GG_KRON_BLOCK");   // read once, at handle creation
   if (env && atoi(env) == 0) return nullptr;
   for (int k = 0; k < d; ++k) {
     if (rows[k] != cols[k] || rows[k] % 2 != 0 || rows[k] < 2) return nullptr;
@@ -1525,16 +1594,16 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     B->n = B->nb << d;
     B->pTF = TF;
     B->cus = blk_cus();
-    const char* fe = getenv("GG_BLK_MODE_FAST");   // A/B knob, read at creation only
+    const char* fe = gg::knob("GG_BLK_MODE_FAST");   // A/B knob, read at creation only
     B->fast = !(fe && atoi(fe) == 0);
-    const char* pe = getenv("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
+    const char* pe = gg::knob("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
     B->pair_abl = pe ? atoi(pe) : 0;
-    const char* le = getenv("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
+    const char* le = gg::knob("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
     B->pair_lds = select_pair(TF, true) != nullptr && !(le && atoi(le) == 0);
     {
       int64_t spb = 1;
       for (int k = 0; k + 2 < d; ++k) spb *= rows[k] / 2;
-      const char* se = getenv("GG_BLK_PAIR_SPW");   // A/B knob, read at creation only
+      const char* se = gg::knob("GG_BLK_PAIR_SPW");   // A/B knob, read at creation only
       B->pair_spw = (spb % 2 == 0 && !(se && atoi(se) == 1)) ? 2 : 1;
     }
     for (int k = 0; k < d; ++k) {
@@ -1737,13 +1806,18 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   const double* src = x;
   double* chain = cgp == 2 ? y : work;
   int pos = 0;
+  // the fused CG's x side job: in the pair launch where the LDS pair kernel
+  // runs (beside its MFMA-bound slab products), else in the second launch (a
+  // streaming kernel after the first when d = 3)
+  const bool side = cgp == 2 && cg->sx != nullptr && cg->xdefer == 2;
+  const bool pair_side = side && B->pair_lds && !(B->pair_abl & 32);
   for (int k = 0; k + 2 < d; ++k) {
     ModeArgs a{};
     int grid = 0;
     int kind = 0;
     if (cgp == 2 && k == 0)
       kind = 1;
-    else if (cgp == 2 && k == 1 && cg->sx != nullptr && cg->xdefer == 2)
+    else if (k == 1 && side && !pair_side)
       kind = 2;
     const int W = mode_waves(kind, B, k);
     mode_geometry(B, k, W, a, &grid, nblk);
@@ -1778,7 +1852,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     const size_t lds = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * W), lds, stream, a);
     GG_LAUNCH_CHECK();
-    if (cgp == 2 && k == 0 && d == 3 && cg->sx != nullptr && cg->xdefer == 2)
+    if (k == 0 && d == 3 && side && !pair_side)
       // no second launch to carry the x side job: its half as a streaming kernel
       launch_x_half(cg->sx, cg->sn, block_side_half(cg->sn), cg->sc, stream);
     if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
@@ -1808,8 +1882,22 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     p.P = x;
     p.shift = shift;
   }
-  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr), dim3(grid),
-                     dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0, stream, p);
+  if (pair_side) {
+    p.sc = cg->sc;
+    p.sx = cg->sx;
+    const int64_t sn = cg->sn;
+    const int64_t H = block_side_half(sn);
+    p.soff = 0;
+    p.sn = std::min(H, sn);
+    p.soff_h1 = p.sn;
+    p.sn_h1 = sn - p.sn;
+    // wave slots: every unit's waves (units = slabs / pair_spw, 2 pair_spw waves)
+    const int64_t slots = p.nslab / B->pair_spw * 2 * B->pair_spw;
+    p.sstep = 2 * ceil_div(std::max<int64_t>(std::max(p.sn, p.sn_h1), 1), 2 * slots);
+  }
+  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr, pair_side),
+                     dim3(grid), dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0,
+                     stream, p);
   GG_LAUNCH_CHECK();
   if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
   if (n_partials) *n_partials = (cgp == 2) ? grid : 0;

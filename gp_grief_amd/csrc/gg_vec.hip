@@ -821,9 +821,10 @@ int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream 
 // 200^4 -- the "slow level" of rounds 3-4, reproduced by the diagnostic knob
 // GG_CG_VEC_PAD (elements, even; added to the stride: pad 2 = every vector
 // 16 bytes further off the line than the previous; tools/prologue_levels.py,
-// profiles/r04/n_levels.jsonl).
+// profiles/r04/n_levels.jsonl).  Read from the snapshot gg_cg_work_elems
+// takes, which gg_cg_create lays the workspace out by.
 static int64_t cg_vec_pad() {
-  const char* e = getenv("GG_CG_VEC_PAD");
+  const char* e = gg::knob("GG_CG_VEC_PAD");
   const int64_t v = e ? atoll(e) : 0;
   return v > 0 ? 2 * (v / 2) : 0;
 }
@@ -833,6 +834,7 @@ constexpr int64_t kCgAlignSlack = 32;   // doubles: room to round the base up to
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
+    gg::knobs_reload();   // the CG handle made next latches this snapshot
     const int64_t n = gg::kron_n(K);
     // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
     // product's own output for an odd number of factors, MpFuse::first_dst);
@@ -907,6 +909,8 @@ int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shi
 int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) {
   return gg::guard([&] {
     GG_REQUIRE(K && work_dev && out, GG_ERR_VALUE, "NULL argument");
+    // the switches (GG_CG_*) come from the snapshot gg_cg_work_elems took, so
+    // the vector stride (GG_CG_VEC_PAD) is the one the workspace was sized for
     int64_t nr = 0, nc = 0, we = 0;
     gg_kron_shape(K, 0, &nr, &nc, &we);
     GG_REQUIRE(nr == nc, GG_ERR_VALUE, "CG needs a square operator");
@@ -932,14 +936,14 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       if (cg->blk != nullptr) {
         cg->xb = work_dev + 6 * vs;
         cg->q2 = work_dev + 7 * vs;
-        const char* be = getenv("GG_CG_BASIS");   // read once per handle
+        const char* be = gg::knob("GG_CG_BASIS");   // read once per handle
         if (be) cg->basis = atoi(be) != 0 ? 1 : 0;
       } else {
         cg->basis = 0;
       }
-      const char* xd = getenv("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
+      const char* xd = gg::knob("GG_CG_XDEFER");   // A/B knob: 0, 1 or 2
       if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
-      const char* rqe = getenv("GG_CG_RQ");       // A/B knob: 0 (epilogue reads r) or 1
+      const char* rqe = gg::knob("GG_CG_RQ");       // A/B knob: 0 (epilogue reads r) or 1
       if (rqe) cg->rq = std::min(2, std::max(0, atoi(rqe)));   // 2: diagnostic
       cg->mv_partials = gg::kron_partials_needed(K, false);
       if (cg->blk) cg->mv_partials = std::max(cg->mv_partials, gg::block_partials_needed(cg->blk));
@@ -965,7 +969,7 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       // 232 of 512 VGPRs per SIMD), so it holds CUs the ring needs: mode
       // products 1-2 7.7 -> 11.0-11.5 ms, the iteration 38.8 -> 46-47.5 ms
       // (profiles/r04/w_side_async)
-      const char* sa = getenv("GG_CG_SIDE_ASYNC");
+      const char* sa = gg::knob("GG_CG_SIDE_ASYNC");
       if (cg->fused && sa && atoi(sa) == 1) {
         GG_HIP(hipStreamCreateWithFlags(&cg->side_stream, hipStreamNonBlocking));
         for (hipEvent_t& e : cg->side_ev) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1649,7 +1653,7 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
     // prologue (CGP 3: the MFMA operand is w itself, written over u_prev)
     // when the chain's first step writes its scratch, not y (an even number
     // of factors); otherwise it is its own streaming pass.
-    const bool fuse = gg::kron_d(K) % 2 == 0 && getenv("GG_LANCZOS_UNFUSED") == nullptr;
+    const bool fuse = gg::kron_d(K) % 2 == 0 && gg::knob("GG_LANCZOS_UNFUSED") == nullptr;
     for (int j = 0; j < steps; ++j) {
       int64_t np = 0;
       if (j == 0 || !fuse) {

@@ -65,6 +65,7 @@ SIGNATURES = {
     "gg_scale_rows": [_c_dp, ctypes.c_int64, ctypes.c_int64, _c_dp, ctypes.c_int, _vp],
     "gg_diag_divide": [_c_dp, ctypes.c_double, _c_dp, _c_dp, ctypes.c_int64, _vp],
     "gg_cg_work_elems": [_vp, _c_i64p],
+    "gg_knobs_reload": [],
     "gg_cg_create": [_vp, ctypes.c_double, _c_dp, ctypes.POINTER(ctypes.c_void_p)],
     "gg_cg_work_elems_blocks": [_vp, ctypes.c_int64, _c_i64p],
     "gg_cg_create_blocks": [_vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_double, _c_dp,
@@ -255,6 +256,13 @@ def lib():
         check(L.gg_set_device(torch.cuda.current_device()), "gg_set_device")
         _ready = True
     return L
+
+
+def knobs_reload():
+    """Re-read the library's GG_* environment switches (gg_knobs_reload): the
+    handle-free entry points (dense, GRIEF, eigen) see the environment as of
+    this call; Kronecker / CG handles latch it when they are made."""
+    check(lib().gg_knobs_reload(), "gg_knobs_reload")
 
 
 def stream_ptr():

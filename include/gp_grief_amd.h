@@ -42,6 +42,13 @@ typedef struct gg_cg gg_cg;
 /* ------------------------------------------------------------------ runtime */
 int gg_abi_version(void);
 int gg_last_error(char* buf, size_t len);
+/* The library's GG_* environment switches (kernel-variant A/B knobs and
+ * diagnostics) are read from a process snapshot, never on a launch path: taken
+ * at the first use and again at every gg_kron_create and gg_cg_work_elems (so
+ * a handle latches the environment it was made in); gg_knobs_reload re-takes
+ * it for the handle-free entry points (dense / GRIEF / eigen).  No reference
+ * counterpart (the reference has no native code).                           */
+int gg_knobs_reload(void);
 int gg_set_device(int device);
 int gg_device_synchronize(void);
 

@@ -97,6 +97,17 @@ def test_gemm_tn_splitk(gg, monkeypatch, S, uplo):
     import torch
     from gp_grief_amd import dense, native
     monkeypatch.setenv("GG_GEMM_SPLITK", S)
+    native.knobs_reload()
+    try:
+        _splitk_case(native, dense, S, uplo)
+    finally:
+        monkeypatch.delenv("GG_GEMM_SPLITK")
+        native.knobs_reload()
+
+
+def _splitk_case(native, dense, S, uplo):
+    import ctypes
+    import torch
     rng = np.random.default_rng(int(S) + 10 * uplo)
     K, M = 20000, 258
     R = rng.standard_normal((K, M))
@@ -181,21 +192,26 @@ def test_cholesky_solve_logdet(gg, n):
     assert np.all(np.triu(Xi, 1) == 0)
 
 
-@pytest.mark.parametrize("reserve", ["2", "8"])
-def test_cholesky_cu_masked_wide_updates(gg, monkeypatch, reserve):
-    """GG_POTRF_CUMASK=R (opt-in A/B): the wide trailing updates on a
-    CU-masked stream give the same factor as the default look-ahead streams
-    (the same kernels on the same operands: bitwise)."""
+def test_cholesky_lookahead_streams_bitwise(gg, monkeypatch):
+    """The look-ahead schedule (factor chain and wide trailing updates on two
+    priority streams) gives the factor of the serial schedule
+    (GG_POTRF_LOOKAHEAD=0, every launch on the caller's stream): the same
+    kernels on the same operands in a dependency-equivalent order, bitwise."""
     import torch
     from gp_grief_amd import dense
     n = 4500   # 512-column panels: several wide updates
     rng = np.random.default_rng(7)
     G = rng.standard_normal((n, n + 10))
     P = torch.from_numpy(G.dot(G.T) / n + 0.1 * np.eye(n)).cuda()
-    monkeypatch.delenv("GG_POTRF_CUMASK", raising=False)
+    monkeypatch.delenv("GG_POTRF_LOOKAHEAD", raising=False)
     ref = dense.Cholesky(P.clone())
-    monkeypatch.setenv("GG_POTRF_CUMASK", reserve)
-    ch = dense.Cholesky(P.clone())
+    monkeypatch.setenv("GG_POTRF_LOOKAHEAD", "0")
+    gg.native.knobs_reload()
+    try:
+        ch = dense.Cholesky(P.clone())
+    finally:
+        monkeypatch.delenv("GG_POTRF_LOOKAHEAD", raising=False)
+        gg.native.knobs_reload()
     assert torch.equal(torch.tril(ch.L), torch.tril(ref.L))
     assert ch.logdet == ref.logdet
 

@@ -14,6 +14,7 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from gp_grief_amd import dense
+    import gp_grief_amd as gg
     sizes = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else
                               "300,1000,2500,5000,7500,10000").split(",")]
     print(json.dumps({"stream_priority_range": list(torch.cuda.Stream.priority_range())}),
@@ -28,6 +29,7 @@ def main():
         Lv = torch.linalg.cholesky(P)
         for la in ("0", "1"):
             os.environ["GG_POTRF_LOOKAHEAD"] = la
+            gg.native.knobs_reload()
             rec = {"p": p, "lookahead": int(la)}
             try:
                 ch = dense.Cholesky(P.clone())

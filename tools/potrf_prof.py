@@ -54,7 +54,7 @@ def main():
     a = ap.parse_args()
     os.environ["GG_POTRF_LOOKAHEAD"] = a.lookahead
     import torch
-    from gp_grief_amd import dense
+    from gp_grief_amd import dense, native
     gen = torch.Generator(device="cuda")
     gen.manual_seed(0)
     for p in [int(v) for v in a.sizes.split(",")]:
@@ -75,9 +75,11 @@ def main():
         fd, path = tempfile.mkstemp(suffix=".bin")
         os.close(fd)
         os.environ["GG_POTRF_PROF"] = path
+        native.knobs_reload()
         ch = dense.Cholesky(P.clone())
         torch.cuda.synchronize()
         del os.environ["GG_POTRF_PROF"]
+        native.knobs_reload()
         res = analyse(path)
         os.unlink(path)
         L = torch.tril(ch.L)
