@@ -1700,6 +1700,7 @@ int gg_kron_dist_create(int d, const int64_t* m, const double* const* factors_ho
     GG_REQUIRE(world >= 1 && rank >= 0 && rank < world, GG_ERR_VALUE, "bad rank / world");
     GG_REQUIRE(m[0] % world == 0, GG_ERR_VALUE, "world size must divide the factor-0 size");
     GG_REQUIRE(m[1] % world == 0, GG_ERR_VALUE, "world size must divide the factor-1 size");
+    gg::knobs_reload();   // the handle's switches are the environment's now
     gg::set_lds_limits();
     gg_kron_dist* D = new gg_kron_dist();
     try {

@@ -1945,6 +1945,7 @@ extern "C" {
 
 int gg_cgs_create(gg_cgs** out) {
   return gg::guard([&] {
+    gg::knobs_reload();   // the handle's switches are the environment's now
     GG_REQUIRE(out, GG_ERR_VALUE, "NULL argument");
     gg_cgs* c = new gg_cgs();
     try {
