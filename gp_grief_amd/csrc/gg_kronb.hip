@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
   auto side_chunk = [&](int64_t slot) {
     const int64_t q0 = slot * A.sstep;
     const int64_t q1 = min(slen, q0 + A.sstep);
-    constexpr int kSB = 8;
+    constexpr int kSB = 16;
     for (int64_t e0 = q0 + 2 * lane; e0 < q1; e0 += kSB * 128) {
       double2 xv[kSB], a[kSB], b[kSB];
 #pragma unroll
