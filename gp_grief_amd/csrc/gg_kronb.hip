@@ -568,7 +568,7 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
   constexpr int W = fast_waves<KIND>();
   constexpr int JT = TF + 1;
   constexpr int KS = 4 * TF + 1;
-  constexpr int kD = (KS % 5 == 0) ? 5 : (KS % 3 == 0) ? 3 : KS;   // ring depth, divides KS
+  constexpr int kD = KIND == 0 ? KS : (KS % 5 == 0) ? 5 : (KS % 3 == 0) ? 3 : KS;   // ring depth, divides KS
   extern __shared__ __attribute__((aligned(16))) double lds[];
   if (a.skip != nullptr && *a.skip) return;
 
