@@ -676,24 +676,20 @@ def block_launch_passes(d):
     """Passes over N of each launch of the fused CG iteration in the
     parity-block basis (gg_kronb.hip block_apply; d - 1 launches): the first
     (axis 0, in place) carries the prologue -- p_old (its MFMA operand), r and
-    q_old read, r, p_new and the output written; the second (d >= 4) the
-    balanced x side job (half of x per iteration: x, p_{j-2}, p_{j-1} read, x
-    written = 2 passes); the last (the pair of innermost axes) reads its input
-    and p_new, writes q."""
+    q_old read, r, p_new and the output written; the last (the pair of
+    innermost axes, blk_pair_lds_kernel) reads its input and p_new, writes q,
+    and carries the balanced x side job (half of x per iteration: x,
+    p_{j-2}, p_{j-1} read, x written = 2 passes); the ones between are plain."""
     passes = [2.0] * (d - 1)
     passes[0] += 4.0
-    if d >= 4:
-        passes[1] += 2.0
-    passes[-1] += 1.0
+    passes[-1] += 1.0 + 2.0
     return passes
 
 
 def block_launch_kernels(d):
     kinds = ["plain"] * (d - 1)
     kinds[0] = "prologue"
-    if d >= 4:
-        kinds[1] = "side"
-    kinds[-1] = "pair-epilogue"
+    kinds[-1] = "pair-epilogue-side"
     return kinds
 
 
@@ -812,10 +808,12 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
 
 
 PMC_JSON = os.path.join("profiles", "r04", "pmc_mode_product.json")
-# the sources that decide the CG mode products' HBM traffic
+PMC_JSON_BLOCK = os.path.join("profiles", "r05", "pmc_block.json")
+# the sources that decide the CG launches' HBM traffic
 KERNEL_SOURCES = ["gp_grief_amd/csrc/gg_kron.hip", "gp_grief_amd/csrc/gg_kron_fold.hip",
                   "gp_grief_amd/csrc/gg_mp.h", "gp_grief_amd/csrc/gg_internal.h",
-                  "gp_grief_amd/csrc/gg_vec.hip", "gp_grief_amd/csrc/gg_kron_ring.hip"]
+                  "gp_grief_amd/csrc/gg_vec.hip", "gp_grief_amd/csrc/gg_kron_ring.hip",
+                  "gp_grief_amd/csrc/gg_kronb.hip"]
 
 
 def kernel_source_hash():
@@ -835,7 +833,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
     state, by kernels built from the same sources (sha256 of KERNEL_SOURCES
     recorded in the JSON), and every launch matched its algorithmic bytes;
     else (None, reason)."""
-    path = os.path.join(ROOT, PMC_JSON)
+    path = os.path.join(ROOT, PMC_JSON_BLOCK if block else PMC_JSON)
     if (m, d) != (200, 4):
         return None, "no PMC passes for this workload"
     if not os.path.exists(path):
