@@ -94,6 +94,10 @@ struct CgScalars {
   int xs;
   double xsc;
   const double* xsp;
+  int cancels;      // fused CG: cancelled betas so far (repaired, or restarted by
+                    // a sharded rank / GG_CG_RESTART)
+  double cancel_tol;  // the cancellation test's threshold (0: 1e-6; set once per
+                      // handle from GG_CG_CANCEL_TOL, a test switch)
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is

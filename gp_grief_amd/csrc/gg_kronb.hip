@@ -18,7 +18,13 @@
 // rounding; the fold x -> P x and the unfold run once per solve.
 //
 // Layout in HBM ("block layout"): block beta (index B = sum_k beta_k 2^{d-1-k},
-// slowest) of n_b = prod h_k elements, C order over (i'_0, ..., i'_{d-1}).
+// slowest) of n_b = prod h_k elements, C order over the slab index (i'_0, ...,
+// i'_{d-3}); a slab (the two innermost axes, h x h, h = h_{d-2} = h_{d-1} =
+// 16 TF + 4) k-step tiled: element (i, a) at (a >> 2) 4 h + 4 i + (a & 3), so
+// the h x 4 columns one k-step of the pair kernel's GEMM 1 contracts are one
+// contiguous 32 h-byte run (whole 128-B lines; row-major they were 32 bytes
+// of every row, each line touched by four k-steps apart in time).  Every other
+// kernel treats a slab as a flat run of h^2 columns.
 //
 // Why: the fold makes each factor's h x h matrix an ordinary dense GEMM (no
 // mirrored rows inside the kernels), and it makes the two innermost axes of a
@@ -102,13 +108,24 @@ __global__ __launch_bounds__(256) void blk_fold_kernel(const double* __restrict_
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < g.nb;
        t += (int64_t)gridDim.x * blockDim.x) {
     int64_t lo = 0, span[D];
-    int64_t rem = t;
+    // t is the position in the block layout: the slab (outer axes, C order)
+    // and, inside it, the k-step tiled (i, a) of the two innermost axes
+    const int64_t hs = g.h[D - 1];
+    const int64_t q = t % (hs * hs);
+    int64_t rem = t / (hs * hs);
+    {
+      const int64_t a4 = q / (4 * hs), r4 = q - a4 * 4 * hs;
+      const int64_t i = r4 >> 2, a = 4 * a4 + (r4 & 3);
+      lo = i * g.stride[D - 2] + a * g.stride[D - 1];
+      span[D - 2] = (g.m[D - 2] - 1 - 2 * i) * g.stride[D - 2];   // low -> mirrored corner
+      span[D - 1] = (g.m[D - 1] - 1 - 2 * a) * g.stride[D - 1];
+    }
 #pragma unroll
-    for (int k = D - 1; k >= 0; --k) {
+    for (int k = D - 3; k >= 0; --k) {
       const int64_t i = rem % g.h[k];
       rem /= g.h[k];
       lo += i * g.stride[k];
-      span[k] = (g.m[k] - 1 - 2 * i) * g.stride[k];   // low -> mirrored corner
+      span[k] = (g.m[k] - 1 - 2 * i) * g.stride[k];
     }
     double v[C];
     if (!inverse) {
@@ -211,7 +228,6 @@ __device__ __forceinline__ double2 ld2g(const double* p) {
 __device__ __forceinline__ void st2g(double* p, double2 v) {
   *reinterpret_cast<gd2*>(reinterpret_cast<uintptr_t>(p)) = gd2v{v.x, v.y};
 }
-
 // ------------------------------------------------- in-place mode product
 // Axis k <= d-3 of every block, in place: Y[o][j][c] = sum_i F[j][i] X[o][i][c]
 // (F = S_k or T_k by the block's parity bit for axis k; X may equal Y).
@@ -877,9 +893,16 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
   const int lane = threadIdx.x & 63;
   const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
   uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
-  uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
-  uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
+  // Z in the k-step tiled slab (element (i, a) at (a >> 2) 4 H + 4 i + (a & 3)):
+  // zb(i0, a0) the byte offset of the 4-row, 16-column (or 16-row, 4-column)
+  // group at row i0, column a0 (multiples of 4); lanes add
+  //   o_z:  row + kq, column + n16 (the full tiles, the tail rows' 4x4 blocks)
+  //   o_zt: row + 4 b4 + kq, column + l3 (the tail columns, the corner)
+  // -- every wave store / load covers whole 128-B lines
+  uint32_t o_z = (uint32_t)(((n16 >> 2) * 4 * H + 4 * kq + (n16 & 3)) * 8);
+  uint32_t o_zt = (uint32_t)((16 * b4 + 4 * kq + l3) * 8);
   asm volatile("" : "+v"(o_f), "+v"(o_z), "+v"(o_zt));
+  auto zb = [&](int i0, int a0) -> int64_t { return sbyte + ((int64_t)a0 * H + 4 * i0) * 8; };
   // one 16-row strip t_i at a time
   const bool epi = EPI < 0 ? A.P != nullptr : EPI != 0;
   const double sh = A.shift;
@@ -912,7 +935,6 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     double Zt = 0.0;
 #pragma unroll
     for (int u = 0; u < NJ; ++u) Z[u] = bd4{0.0, 0.0, 0.0, 0.0};
-    const int64_t zrow = sbyte + (int64_t)16 * ti * H * 8;   // row 16 ti
     // epilogue operands issued now, consumed after the k-loop
     double pv[NJ > 0 ? NJ : 1][4], pvt = 0.0;
     if (epi) {
@@ -920,8 +942,8 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
       for (int u = 0; u < NJ; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          pv[u][r] = ldu(A.P, zrow + (int64_t)(4 * r * H + 16 * (J0 + u)) * 8, o_z);
-      if (TJ) pvt = ldu(A.P, zrow + (int64_t)16 * TF * 8, o_zt);
+          pv[u][r] = ldu(A.P, zb(16 * ti + 4 * r, 16 * (J0 + u)), o_z);
+      if (TJ) pvt = ldu(A.P, zb(16 * ti, 16 * TF), o_zt);
     }
     const int64_t fti = (int64_t)ti * 512;
     // A fragments kPF k-steps ahead; the scheduling barriers keep each step's
@@ -947,8 +969,8 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int u = 0; u < NJ; ++u)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        put(zrow + (int64_t)(4 * r * H + 16 * (J0 + u)) * 8, o_z, Z[u][r], epi ? pv[u][r] : 0.0);
-    if (TJ) put(zrow + (int64_t)16 * TF * 8, o_zt, Zt, pvt);
+        put(zb(16 * ti + 4 * r, 16 * (J0 + u)), o_z, Z[u][r], epi ? pv[u][r] : 0.0);
+    if (TJ) put(zb(16 * ti, 16 * TF), o_zt, Zt, pvt);
   }
   // tail rows i = 16 TF + r: A = F2's replicated tail fragment; the outputs of
   // v_mfma_f64_4x4x4_4b_f64: lane 16 r + 4 b + c -> row 16 TF + r, column
@@ -957,7 +979,6 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     double Z4[NJ > 0 ? NJ : 1], Z4t = 0.0;
 #pragma unroll
     for (int u = 0; u < NJ; ++u) Z4[u] = 0.0;
-    const int64_t zrow = sbyte + (int64_t)16 * TF * H * 8;
     const int64_t fti = (int64_t)TF * 512;
     constexpr int kPF = PF;
     double fr[kPF];
@@ -975,12 +996,12 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     }
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
-      const int64_t ub = zrow + (int64_t)16 * (J0 + u) * 8;
+      const int64_t ub = zb(16 * TF, 16 * (J0 + u));
       put(ub, o_z, Z4[u], epi ? ldu(A.P, ub, o_z) : 0.0);
     }
     if (TJ && b4 == 0) {
       // lane 16 r + c (b = 0): row 16 TF + r, column 16 TF + c
-      const int64_t ub = zrow + (int64_t)16 * TF * 8;
+      const int64_t ub = zb(16 * TF, 16 * TF);
       put(ub, o_zt, Z4t, epi ? ldu(A.P, ub, o_zt) : 0.0);
     }
   }
@@ -996,8 +1017,8 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   const int lane = threadIdx.x & 63;
   const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
   // lane byte offsets (opaque: recomputed per slab, never hoisted as a set)
-  uint32_t o_x = (uint32_t)((n16 * H + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
-  uint32_t o_xt = (uint32_t)((l3 * H + kq) * 8);        // X tail rows 16 TF + l3
+  uint32_t o_x = (uint32_t)((n16 * 4 + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
+  uint32_t o_xt = (uint32_t)((l3 * 4 + kq) * 8);        // X tail rows 16 TF + l3
   uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
   uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
   uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
@@ -1024,10 +1045,10 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   for (int u = 0; u < NJ; ++u) Wta[u] = 0.0;
 
   auto ld1 = [&](int s, double (&xa)[TF + 1], double (&fb)[NJB > 0 ? NJB : 1]) {
-    const int64_t xs = xbyte + (int64_t)s * 32;
+    const int64_t xs = xbyte + (int64_t)s * H * 32;   // the k-step's h x 4 run
 #pragma unroll
-    for (int t = 0; t < TF; ++t) xa[t] = ldu(A.X, xs + (int64_t)t * 16 * H * 8, o_x);
-    xa[TF] = ldu(A.X, xs + (int64_t)TF * 16 * H * 8, o_xt);
+    for (int t = 0; t < TF; ++t) xa[t] = ldu(A.X, xs + (int64_t)t * 512, o_x);
+    xa[TF] = ldu(A.X, xs + (int64_t)TF * 512, o_xt);
     const int64_t fs = (int64_t)s * FS;
 #pragma unroll
     for (int u = 0; u < NJ; ++u) fb[u] = ldu(f3, fs + (int64_t)(J0 + u) * 512, o_f);
@@ -1049,20 +1070,18 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
       Wc = __builtin_amdgcn_mfma_f64_4x4x4f64(xa[TF], fb[NJ], Wc, 0, 0, 0);
     }
   };
-  // L2 prefetch of X: k-step s reads columns 4 s .. 4 s + 3 of every row, so
-  // a row's 128-B line is first touched every fourth k-step -- one k-step of
-  // register prefetch does not cover that HBM miss.  Every pair of k-steps
-  // touches the lines two line columns ahead (4-byte loads, rows lane and
-  // 64 + lane); a touch's value is folded into a junk sum two pairs later,
-  // so it never makes a k-step wait (the sum is stored once per kernel)
+  // L2 prefetch of X: one k-step of register prefetch does not cover an HBM
+  // miss.  Every pair of k-steps touches the runs of k-steps s + 8 and s + 9
+  // (one 4-byte load per 128-B line: KS lines per k-step); a touch's value is
+  // folded into a junk sum two pairs later, so it never makes a k-step wait
+  // (the sum is stored once per kernel)
   auto touch = [&](int s, float& t0, float& t1) {
-    int cb = (s >> 2) + 2;
-    cb = cb < (H + 15) / 16 ? cb : (H + 15) / 16 - 1;
-    const int r1 = 64 + lane < H ? 64 + lane : H - 1;
+    const int s0 = s + 8 < KS ? s + 8 : KS - 1, s1 = s + 9 < KS ? s + 9 : KS - 1;
+    const int ln = lane < KS ? lane : KS - 1;
     t0 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
-        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)lane * H + 16 * cb) * 8);
+        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)s0 * H * 4 + 16 * ln) * 8);
     t1 = *reinterpret_cast<const __attribute__((address_space(1))) float*>(
-        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)r1 * H + 16 * cb) * 8);
+        reinterpret_cast<uintptr_t>(A.X) + xbyte + ((int64_t)s1 * H * 4 + 16 * ln) * 8);
   };
   {
     double xa0[TF + 1], fb0[NJB > 0 ? NJB : 1], xa1[TF + 1], fb1[NJB > 0 ? NJB : 1];
@@ -1334,7 +1353,7 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
       const int xs = i / R::XI, xi = i % R::XI;
       const int t = 2 * xi + (lane >> 5);
       const int row = min(16 * t + (lane & 15), H - 1);
-      dlane[j] = (uint32_t)(xs * SB + (row * H + 2 * ((lane >> 4) & 1)) * 8);
+      dlane[j] = (uint32_t)(xs * SB + (row * 4 + 2 * ((lane >> 4) & 1)) * 8);
       dlds[j] = (uint32_t)(xs * R::XD + xi * 128);
     } else {
       const int f = min(i - SPW * R::XI, R::FI - 1);
@@ -1352,7 +1371,7 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
   };
   // k-step st of a unit into ring slot `slot`
   auto issue = [&](const PairSlabSrc& p, int st, int slot) {
-    const char* xb = ubase(A.X, p.xoff + (int64_t)st * 32);
+    const char* xb = ubase(A.X, p.xoff + (int64_t)st * H * 32);   // the k-step's h x 4 run
     const char* fbs = ubase(p.f3, (int64_t)st * FSK);
     double* dst = ring + slot * R::STAGE;
 #pragma unroll

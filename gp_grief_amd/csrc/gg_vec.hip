@@ -361,7 +361,8 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     // |r_{j+1}|^2 from three terms of size ~rho: when it is below 1e-6 rho
     // the expansion has lost too many digits for beta -- apply the update
     // and take the true r.r instead (repair kernels before the next matvec)
-    sc->repair = rt < 1e-6 * rho ? 1 : 0;
+    sc->repair = rt < (sc->cancel_tol > 0.0 ? sc->cancel_tol : 1e-6) * rho ? 1 : 0;
+    sc->cancels += sc->repair;
     sc->beta = sc->repair ? 0.0 : rt / rho;
     sc->first = 0;
     sc->pending = 1;
@@ -451,6 +452,7 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->pending = 0;
     sc->alpha = sc->beta = sc->pq = sc->rq = sc->qq = 0.0;
     sc->repair = 0;
+    sc->cancels = 0;
     sc->xpend = 0;
     sc->xh = 2;
     sc->xs = 0;
@@ -663,6 +665,19 @@ static KronDiag make_diag(int d, const int64_t* m, int64_t* n_out) {
 }  // namespace gg
 
 // ------------------------------------------------------------------- CG state
+namespace gg {
+// a handle's scalar block: zeroed, with the cancellation threshold of the
+// knob snapshot (GG_CG_CANCEL_TOL, tests: forces the repair / restart paths)
+static void scalars_clear(CgScalars* sc) {
+  GG_HIP(hipMemset(sc, 0, sizeof(CgScalars)));
+  const char* e = knob("GG_CG_CANCEL_TOL");
+  if (e) {
+    const double t = atof(e);
+    GG_HIP(hipMemcpy(&sc->cancel_tol, &t, sizeof(double), hipMemcpyHostToDevice));
+  }
+}
+}  // namespace gg
+
 struct gg_cg {
   const gg_kron* K = nullptr;
   double shift = 0.0;
@@ -710,6 +725,10 @@ struct gg_cg {
   // vectors are blocks [rblk0, rblk0 + rnblk) of the block layout (rnblk > 0);
   // only the _partial / _finish entry points drive it
   int64_t rblk0 = 0, rnblk = -1;
+  // A/B (GG_CG_RESTART=1, latched at create): gg_cg_iterate restarts a
+  // cancelled beta (p = r) as a sharded rank does instead of repairing it --
+  // the restart penalty measured on one GPU with everything else equal
+  bool restart = false;
   int launches() const { return block ? gg::block_launches(blk) : gg::kron_d(K); }
 };
 
@@ -852,6 +871,7 @@ int gg_cg_work_elems_blocks(const gg_kron* K, int64_t nblk, int64_t* elems) {
     GG_REQUIRE(B != nullptr, GG_ERR_VALUE, "the operator has no parity-block basis");
     GG_REQUIRE(nblk >= 1 && nblk <= ((int64_t)1 << gg::block_d(B)), GG_ERR_VALUE,
                "block count outside 1..2^d");
+    gg::knobs_reload();   // the CG handle made next latches this snapshot
     // r, p, q, p2, p3, p4 and q2 (the pair launch's q)
     *elems = kCgAlignSlack + 7 * cg_vec_stride(nblk * gg::block_nb(B));
   });
@@ -897,7 +917,7 @@ int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shi
       GG_HIP(hipMemset(cg->rr_part, 0, 2 * cg->rr_count * sizeof(double)));
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
-      GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
+      gg::scalars_clear(cg->sc);
     } catch (...) {
       gg_cg_destroy(cg);
       throw;
@@ -945,6 +965,8 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       if (xd) cg->xdefer = std::min(2, std::max(0, atoi(xd)));
       const char* rqe = gg::knob("GG_CG_RQ");       // A/B knob: 0 (epilogue reads r) or 1
       if (rqe) cg->rq = std::min(2, std::max(0, atoi(rqe)));   // 2: diagnostic
+      const char* rse = gg::knob("GG_CG_RESTART");  // A/B: restart instead of repair
+      cg->restart = rse && atoi(rse) == 1;
       cg->mv_partials = gg::kron_partials_needed(K, false);
       if (cg->blk) cg->mv_partials = std::max(cg->mv_partials, gg::block_partials_needed(cg->blk));
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
@@ -963,7 +985,7 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       }
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
-      GG_HIP(hipMemset(cg->sc, 0, sizeof(gg::CgScalars)));
+      gg::scalars_clear(cg->sc);
       // the concurrent x side job (GG_CG_SIDE_ASYNC=1, opt-in): at 200^4 the
       // streaming kernel (50 VGPRs) cannot sit beside a ring workgroup (2 x
       // 232 of 512 VGPRs per SIMD), so it holds CUs the ring needs: mode
@@ -1205,13 +1227,15 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         // repair (no-op unless the last beta cancelled): x += alpha p,
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
         // pending update (x_defer: r only, x keeps its deferred steps)
-        hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                           xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
-                           cg->partials, 2);
-        GG_LAUNCH_CHECK();
-        hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
-                           (int64_t)nb, cg->sc, 2);
-        GG_LAUNCH_CHECK();
+        if (!cg->restart) {
+          hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                             xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                             cg->partials, 2);
+          GG_LAUNCH_CHECK();
+          hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
+                             (int64_t)nb, cg->sc, 2);
+          GG_LAUNCH_CHECK();
+        }
         gg::MpFuse fz;
         fz.r = cg->r;
         fz.q_old = cg->q;
@@ -1516,6 +1540,17 @@ int gg_cg_close_finish(gg_cg* cg, const double* rr_dev, gg_stream stream) {
   });
 }
 
+int gg_cg_cancels(gg_cg* cg, int* cancels, gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && cancels, GG_ERR_VALUE, "NULL argument");
+    hipStream_t s = gg::as_stream(stream);
+    GG_HIP(hipMemcpyAsync(cg->sc_host, cg->sc, sizeof(gg::CgScalars), hipMemcpyDeviceToHost,
+                          s));
+    GG_HIP(hipStreamSynchronize(s));
+    *cancels = cg->sc_host->cancels;
+  });
+}
+
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream) {
   return gg::guard([&] {
@@ -1788,6 +1823,7 @@ __global__ void cgs_init_kernel(CgScalars* sc, const double* rr, double rtol, do
   // the fused recurrence's state (unused by the textbook one)
   sc->rq = sc->qq = 0.0;
   sc->repair = 0;
+  sc->cancels = 0;
   sc->xpend = 0;
   sc->xh = 2;
   sc->xs = 0;
@@ -1950,7 +1986,7 @@ int gg_cgs_create(gg_cgs** out) {
     gg_cgs* c = new gg_cgs();
     try {
       GG_HIP(hipMalloc(&c->sc, sizeof(gg::CgScalars)));
-      GG_HIP(hipMemset(c->sc, 0, sizeof(gg::CgScalars)));
+      gg::scalars_clear(c->sc);
       GG_HIP(hipHostMalloc(&c->host, sizeof(gg::CgScalars), hipHostMallocDefault));
       GG_HIP(hipMalloc(&c->partials, 2 * gg::kVecBlocks * sizeof(double)));
     } catch (...) {

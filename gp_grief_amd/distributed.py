@@ -687,6 +687,9 @@ class ParityHipEngine(object):
     def status(self):
         return self.cg.status()
 
+    def cancels(self):
+        return self.cg.cancels()
+
     def profile(self, enable):
         self.cg.profile(enable)
 
@@ -788,6 +791,11 @@ class ParityShardCG(object):
     def status(self):
         """(iterations, converged, residual norm, tolerance) -- gg_cg_status."""
         return self.e.status()
+
+    def cancels(self):
+        """Cancelled betas this solve (each restarted the recurrence; the
+        engine's gg_cg_cancels, or 0 for an engine without the count)."""
+        return self.e.cancels() if hasattr(self.e, "cancels") else 0
 
     def solve(self, b, rtol=1e-5, atol=0.0, maxiter=None, check_every=20):
         self.start(b, rtol, atol)
@@ -920,6 +928,11 @@ class BlockHipEngine(object):
                                                native.stream_ptr()))
         return it.value, bool(conv.value), res.value, tol.value
 
+    def cancels(self):
+        v = ctypes.c_int()
+        self._c("gg_cg_cancels", ctypes.byref(v))
+        return v.value
+
     def profile(self, enable):
         native.check(native.lib().gg_cg_profile(self.h, int(bool(enable))), "gg_cg_profile")
 
@@ -960,7 +973,9 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
     two exchanges per matvec) or "auto" (the first that applies, in that
     order).  Returns (x, info, iterations, decomposition).  engine (tests):
     a factory (K, world, rank, shift) -> engine for the block decomposition
-    in place of BlockHipEngine (its fold / unfold take host arrays)."""
+    in place of BlockHipEngine (its fold / unfold take host arrays).
+    solve.last_cancels: the calling rank's cancelled-beta restarts (block /
+    parity; the transpose decomposition's CG has no cancellation test)."""
     import torch
     ex, world, rank = comm_exchange(comm)
     F = [np.asarray(f, dtype=np.float64) for f in K.K]
@@ -982,12 +997,14 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
         x = eng.unfold(xl)
         ex.all_reduce(x)
         it = cg.status()[0]
+        solve.last_cancels = cg.cancels()
     elif decomposition == "parity":
         bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
                         dtype=np.float64).reshape(-1)
         cg = ParityShardCG(F, world, rank, ex, shift)
         bl = dev.to_device(parity_fold(bh, m, world)[rank])
         xl, info = cg.solve(bl, rtol, atol, maxiter, check_every)
+        solve.last_cancels = cg.cancels()
         parts = ex.all_gather_object(dev.to_host(xl))
         x = dev.to_device(parity_unfold(parts, m))
         it = cg.status()[0]
@@ -1001,6 +1018,7 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
         parts = ex.all_gather_object(dev.to_host(xl))
         x = dev.to_device(gather_global(parts, m))
         it = cg.status()[0]
+        solve.last_cancels = None
     else:
         raise ValueError("decomposition must be 'auto', 'block', 'parity' or 'transpose'")
     if torch.cuda.is_available():

@@ -205,6 +205,14 @@ class KronCG(object):
                                                native.stream_ptr()))
         return it.value, bool(conv.value), res.value, tol.value
 
+    def cancels(self):
+        """Cancelled betas since start (gg_cg_cancels; synchronising)."""
+        from . import native
+        v = ctypes.c_int()
+        native.check(native.lib().gg_cg_cancels(self.h, ctypes.byref(v), native.stream_ptr()),
+                     "gg_cg_cancels")
+        return v.value
+
     def profile(self, enable=True):
         """Record HIP events around every mode product of later iterations."""
         from . import native

@@ -92,6 +92,7 @@ SIGNATURES = {
     "gg_cg_iterate_finish": [_vp, _c_dp, _vp],
     "gg_cg_close_partial": [_vp, _c_dp, _vp],
     "gg_cg_close_finish": [_vp, _c_dp, _vp],
+    "gg_cg_cancels": [_vp, ctypes.POINTER(ctypes.c_int), _vp],
     "gg_cg_status": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), _vp],
     "gg_cg_profile": [_vp, ctypes.c_int],

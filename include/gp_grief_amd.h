@@ -216,6 +216,13 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
 int gg_cg_close(gg_cg* cg, gg_stream stream);
 int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, double* tol,
                  gg_stream stream); /* synchronising */
+/* Cancelled betas of the fused recurrence since start (|r_{j+1}|^2 from the
+ * three-term expansion below 1e-6 rho_j): repaired by gg_cg_iterate with a
+ * true r.r, restarted (p = r) by a sharded rank's _finish, and by
+ * gg_cg_iterate too when GG_CG_RESTART=1 at gg_cg_create (the A/B that
+ * measures the restart penalty on one GPU).  Synchronising.  No reference
+ * counterpart (scipy's textbook CG has no cancellation test).              */
+int gg_cg_cancels(gg_cg* cg, int* cancels, gg_stream stream);
 /* A rank of a sharded CG whose operator is block-diagonal across ranks (the
  * parity sharding of gp_grief_amd/distributed.py: this handle's operator is
  * the rank's block, (K + shift I) restricted to it), every dot product

@@ -281,11 +281,37 @@ def rowcol_kr_expand(R, K, C, logged=False):
 # device fold / block operator can be checked against the dense product of
 # kron_matvec (kron_matrix.py:52-97), which itself is reference-pinned.
 
+def _slab_perm(hr, hc):
+    """pos[i hc + a] = (a // 4) 4 hr + w i + a % 4, w = min(4, hc - 4 (a // 4))
+    (the last column group narrower when hc % 4 != 0: host-only shapes)."""
+    i, a = np.meshgrid(np.arange(hr), np.arange(hc), indexing="ij")
+    q = a // 4
+    w = np.minimum(4, hc - 4 * q)
+    return (q * 4 * hr + w * i + a % 4).reshape(-1)
+
+
+def slab_tile(xb, hs, inverse=False):
+    """The block layout's k-step tiling of each slab (gg_kronb.hip header): the
+    two innermost axes (hr x hc) of every block, C-order element (i, a) at
+    position (a // 4) 4 hr + 4 i + a % 4 (whole 4-column groups; the device
+    block basis has hc = 16 TF + 4).  inverse=True undoes it."""
+    hr, hc = int(hs[-2]), int(hs[-1])
+    pos = _slab_perm(hr, hc)
+    t = np.asarray(xb, dtype=np.float64).reshape(-1, hr * hc)
+    out = np.empty_like(t)
+    if inverse:
+        out[:, :] = t[:, pos]
+    else:
+        out[:, pos] = t
+    return out.reshape(-1)
+
+
 def block_fold(x, ms, inverse=False):
     """P x for the orthogonal per-axis butterfly u_i = (x_i + x_{m-1-i}) / sqrt 2,
     v_i = (x_i - x_{m-1-i}) / sqrt 2 (i < m/2) on every axis (C order, factor 0
     slowest).  Block layout: parity pattern beta (bit d-1-k for axis k) slowest,
-    then (i'_0 .. i'_{d-1}) C order.  inverse=True applies P^T (block -> grid).
+    then (i'_0 .. i'_{d-3}) C order, each slab (i'_{d-2}, i'_{d-1}) k-step tiled
+    (slab_tile).  inverse=True applies P^T (block -> grid).
     """
     ms = [int(m) for m in ms]
     d = len(ms)
@@ -304,9 +330,9 @@ def block_fold(x, ms, inverse=False):
                 nxt.append((lo + hi) * s)
                 nxt.append((lo - hi) * s)
             parts = nxt
-        return np.concatenate([p.reshape(-1) for p in parts])
+        return slab_tile(np.concatenate([p.reshape(-1) for p in parts]), hs)
     nb = int(np.prod(hs))
-    y = np.asarray(x, dtype=np.float64).reshape(-1)
+    y = slab_tile(x, hs, inverse=True)
     parts = [y[b * nb:(b + 1) * nb].reshape(hs) for b in range(2 ** d)]
     for k in reversed(range(d)):
         nxt = []
@@ -334,10 +360,11 @@ def block_matvec(factors, xb):
     S_k (beta_k = 0) / T_k (beta_k = 1) (kron_matvec on each block)."""
     d = len(factors)
     st = [block_factors(F) for F in factors]
-    nb = int(np.prod([np.shape(F)[0] // 2 for F in factors]))
-    xb = np.asarray(xb, dtype=np.float64).reshape(-1)
+    hs = [np.shape(F)[0] // 2 for F in factors]
+    nb = int(np.prod(hs))
+    xb = slab_tile(xb, hs, inverse=True)
     out = np.empty_like(xb)
     for b in range(2 ** d):
         fs = [st[k][(b >> (d - 1 - k)) & 1] for k in range(d)]
         out[b * nb:(b + 1) * nb] = kron_matvec(fs, xb[b * nb:(b + 1) * nb])
-    return out
+    return slab_tile(out, hs)

@@ -439,11 +439,13 @@ class BlockNumpyEngine(ParityNumpyEngine):
         return out
 
     def _Kb(self, v):
+        hs = [m // 2 for m in self.ms]
+        v = oracle.kron.slab_tile(v, hs, inverse=True)   # the block layout's slab tiling
         out = np.empty_like(v)
         for j, fs in enumerate(self.blocks):
             out[j * self.nb:(j + 1) * self.nb] = oracle.kron_matvec(
                 fs, v[j * self.nb:(j + 1) * self.nb])
-        return out
+        return oracle.kron.slab_tile(out, hs)
 
     def apply(self, x, y):
         y.numpy()[:] = self._Kb(x.numpy())

@@ -331,8 +331,9 @@ def test_block_sharded_cg_virtual_ranks(gpu, world, ms, shift):
     runs the block kernels on its 2^d / G blocks (gg_cg_create_blocks,
     gg_cg_*_partial / _finish), folds b on the device and contributes its
     unfold to the all-reduced x.  Every rank's x equals the oracle CG's (1e-8),
-    the iteration count the oracle's within 2 % and the single-GPU block
-    CG's within 1 % (the restart vs repair of a cancelled beta)."""
+    the iteration count the oracle's and the single-GPU block CG's within 2 %
+    (the restart vs repair of a cancelled beta, and the summation order:
+    test_restart_penalty_single_gpu separates the two)."""
     import gp_grief_amd as gg
     from gp_grief_amd.distributed import solve
     F = reference_factors_ms(ms)
@@ -356,9 +357,130 @@ def test_block_sharded_cg_virtual_ranks(gpu, world, ms, shift):
         assert np.linalg.norm(r[0] - xs) / np.linalg.norm(xs) < 1e-8
     # against the single-GPU block CG: the sharded recurrence restarts a
     # cancelled beta (p = r) where the single-GPU one repairs it with a true
-    # r.r -- (6, 12, 40, 40) at 0.05: 1732 vs 1725 iterations (0.4 %)
+    # r.r, and its dot products sum in another order -- (6, 12, 40, 40) at
+    # 0.05: 1732 vs 1725 iterations with row-major slabs, 1737 vs 1716 with
+    # k-step tiled ones (the same arithmetic, other rounding)
     x1, i1 = gg.linalg.cg(K, b[:, None], shift=shift, rtol=1e-10, maxiter=20000)
-    assert abs(gg.linalg.cg.last.iters - res[0][2]) <= max(2, 0.01 * res[0][2])
+    assert abs(gg.linalg.cg.last.iters - res[0][2]) <= max(2, 0.02 * res[0][2])
+
+
+@pytest.mark.parametrize("ms,shift", [((6, 12, 40, 40), 0.05), ((40, 8, 72, 72), 0.02),
+                                      ((8, 8, 200, 200), 0.01)])
+def test_restart_penalty_single_gpu(gpu, monkeypatch, ms, shift):
+    """The restart penalty by itself: gg_cg_iterate repairs a cancelled beta
+    with a true r.r (a second pass over r); a sharded rank restarts (p = r)
+    to keep one all-reduce per iteration.  GG_CG_RESTART=1 makes the
+    single-GPU CG restart too, everything else equal (same layout, same
+    kernels, same summation order).  Both solutions equal the oracle's (1e-8);
+    the restart's iteration count stays within 2 % of the repair's.  The
+    counts are printed (DESIGN.md section 6 quotes them)."""
+    import gp_grief_amd as gg
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(23).standard_normal(n)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b,
+                                   rtol=1e-10) if n <= 2_000_000 else (None, 0, None)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GG_CG_RESTART", flag)
+        cg = gg.linalg.KronCG(K, shift)
+        cg.start(gg.device.to_device(b), rtol=1e-10)
+        while True:
+            cg.iterate(50)
+            k, conv, res, tol = cg.status()
+            if conv or k >= 20000:
+                break
+        assert conv
+        out[flag] = (k, cg.cancels(), gg.device.to_host(cg.x))
+    for flag, (k, c, x) in out.items():
+        if xs is not None:
+            assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8
+    (k0, c0, x0), (k1, c1, x1) = out["0"], out["1"]
+    print("restart penalty %s shift %g: repair %d iterations (%d cancelled), restart %d (%d)"
+          % (ms, shift, k0, c0, k1, c1))
+    assert np.linalg.norm(x1 - x0) / np.linalg.norm(x0) < 1e-7
+    if c0 == 0:
+        assert k1 == k0
+    assert abs(k1 - k0) <= max(2, 0.02 * k0)
+
+
+def test_forced_cancellations_restart_vs_repair(gpu, monkeypatch):
+    """Both branches of a cancelled beta, made frequent: GG_CG_CANCEL_TOL=0.1
+    counts every step whose |r_{j+1}|^2 expansion is below 0.1 rho_j as
+    cancelled.  The single-GPU CG repairs (true r.r, textbook beta), the
+    single-GPU CG with GG_CG_RESTART=1 and a block-sharded solve over two
+    virtual ranks restart (p = r).  All three converge to the oracle's x
+    (1e-8) with cancellations counted; the iteration counts are the restart
+    penalty at that rate (printed)."""
+    import gp_grief_amd as gg
+    from gp_grief_amd.distributed import solve
+    ms, shift = (6, 12, 40, 40), 0.05
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    b = np.random.default_rng(25).standard_normal(int(np.prod(ms)))
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b,
+                                   rtol=1e-10)
+    monkeypatch.setenv("GG_CG_CANCEL_TOL", "0.1")
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("GG_CG_RESTART", flag)
+        cg = gg.linalg.KronCG(K, shift)
+        cg.start(gg.device.to_device(b), rtol=1e-10)
+        while True:
+            cg.iterate(50)
+            k, conv, res, tol = cg.status()
+            if conv or k >= 20000:
+                break
+        assert conv
+        out["restart" if flag == "1" else "repair"] = (k, cg.cancels(), gg.device.to_host(cg.x))
+    monkeypatch.setenv("GG_CG_RESTART", "0")
+    ex = ThreadExchange(2)
+
+    def body(g):
+        ex.bind(g)
+        x, info, k, how = solve(K, b, shift, ex, rtol=1e-10, maxiter=20000, check_every=10,
+                                decomposition="block")
+        assert info == 0 and how == "block"
+        return k, solve.last_cancels, gg.device.to_host(x)
+
+    out["sharded"] = run_threads(2, body)[0]
+    print("forced cancellations (tol 0.1), oracle %d iterations: %s"
+          % (it, ", ".join("%s %d (%d cancelled)" % (n, v[0], v[1]) for n, v in out.items())))
+    for n, (k, c, x) in out.items():
+        assert c > 0, n
+        assert np.linalg.norm(x - xs) / np.linalg.norm(xs) < 1e-8, n
+        assert k <= 2 * it, n
+
+
+@pytest.mark.parametrize("how", ["block", "parity", "transpose"])
+def test_ill_conditioned_decompositions_virtual_ranks(gpu, how):
+    """(6, 12, 40, 40) at shift 0.05 (cond ~ 1e3, about 1700 iterations to
+    1e-10) over 2 virtual ranks in each decomposition: x equals the oracle
+    CG's (1e-8) and the iteration count is within 2 % of the oracle's."""
+    import gp_grief_amd as gg
+    from gp_grief_amd.distributed import solve
+    ms, shift, world = (6, 12, 40, 40), 0.05, 2
+    F = reference_factors_ms(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    b = np.random.default_rng(24).standard_normal(int(np.prod(ms)))
+    ex = ThreadExchange(world)
+
+    def body(g):
+        ex.bind(g)
+        x, info, it, got = solve(K, b, shift, ex, rtol=1e-10, maxiter=20000, check_every=11,
+                                 decomposition=how)
+        return gg.device.to_host(x), info, it, got, solve.last_cancels
+
+    res = run_threads(world, body)
+    xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b,
+                                   rtol=1e-10)
+    assert all(r[3] == how and r[1] == 0 for r in res)
+    assert len({r[2] for r in res}) == 1
+    print("%s: %d iterations (oracle %d), cancelled betas %s" % (how, res[0][2], it, res[0][4]))
+    assert abs(res[0][2] - it) <= max(2, 0.02 * it)
+    for r in res:
+        assert np.linalg.norm(r[0] - xs) / np.linalg.norm(xs) < 1e-8
 
 
 def test_cg_comm_api_virtual_ranks(gpu):
