@@ -140,13 +140,6 @@ struct MpFuse {
   int xdefer = 0;
   int64_t soff = 0;
   int64_t soff_h1 = 0, sn_h1 = 0;
-  // x_defer 2 with a side stream (gg_cg): the x update runs as its own
-  // streaming kernel on side_stream, concurrently with the plain mode
-  // products 1..d-2 (which then carry no side job and take the ring kernel);
-  // side_ev[0] orders it after the prologue, side_ev[1] the caller's scalars
-  // after it
-  hipStream_t side_stream = nullptr;
-  hipEvent_t side_ev[2] = {nullptr, nullptr};
   // output of the first mode product when the ping-pong would put it in y
   // (odd d): the fused prologue still reads q_old == y in other workgroups
   double* first_dst = nullptr;

@@ -573,192 +573,19 @@ __global__ __launch_bounds__(kWaves * 64, kMinW) void mode_product_kernel(
       pqo_acc);
 }
 
-// All-LDS-DMA pipeline (plain / side-job / fused-epilogue roles, CGP = 0):
-// both operands go global -> LDS with global_load_lds (16 B per lane), kNS
-// stages in flight, one raw s_barrier per chunk preceded by a counted
-// s_waitcnt vmcnt(N) that retires only the oldest stage -- so the HBM stream
-// of X runs kNS - 1 chunks ahead of the MFMAs instead of being drained at
-// every barrier (an ordinary global load or __syncthreads() while an LDS DMA
-// is in flight makes hipcc wait vmcnt(0); cdna_hip_programming.md
-// "Pipelining across barriers").  Stage layout (doubles):
-//   B: [k-step][tile][lane]  kKC * JT * 64       (factor fragments, as packed)
-//   A: [wave][row][16]       4 * kKC * 4 * 16    (X rows of the wave's strip)
-// The A operand of lane l at k-step s is A[wave][4 s + (l >> 4)][l & 15]: one
-// conflict-free ds_read_b64 of 512 contiguous bytes.  Needs M even and X
-// 16-byte aligned (16-byte row segments); kron_apply checks.
-//
-// A launch grid smaller than the strip count makes it persistent: workgroup b
-// runs strips b, b + grid, ... as one flat chunk sequence.
-template <int JT, int kKC, int kNS, int kMinW, int kEpi>
-__global__ __launch_bounds__(256, kMinW) void mode_product_glds_kernel(
-    const double* X, double* __restrict__ Y, const double* __restrict__ Bf,
-    int64_t M, int q, int p, int KS, int jt_total, int jt0,
-    const double* __restrict__ xs, double shift, double* __restrict__ dot_partials,
-    const int* __restrict__ skip, OutMap om, MpFuse fz) {
-  constexpr int kWaves = 4;
-  constexpr int kThreads = 256;
-  constexpr int kBChunk2 = kKC * JT * 32;                  // double2 of B per stage
-  constexpr int kPerT = (kBChunk2 + kThreads - 1) / kThreads;
-  constexpr int kARows = kKC * 4;                          // X rows per wave per stage
-  static_assert(kARows % 8 == 0, "whole 1 KiB A instructions per wave");
-  constexpr int kAInstr = kARows / 8;
-  constexpr int kBD = kKC * JT * 64;                       // B doubles per stage
-  constexpr int kStage = kBD + kWaves * kARows * 16;       // doubles per stage
-  // B instructions the last wave issues per stage (the fewest of any wave);
-  // vmcnt(N) with the minimum only ever waits a little longer in other waves
-  constexpr int kBLast = (kBChunk2 - 3 * 64 + kThreads - 1) / kThreads;
-  constexpr int kN = kBLast + kAInstr;
-  constexpr int kWaitN = (kN & 15) | (((kN >> 4) & 3) << 14) | (7 << 4) | (15 << 8);
-  constexpr int kWait0 = (7 << 4) | (15 << 8);
-  if (skip != nullptr && *skip) return;
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // kNS * kStage + red
-  double* red = lds + kNS * kStage;                             // 4 * kWaves doubles
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int krow = lane >> 4;
-  const int nchunks = (KS + kKC - 1) / kKC;
-  // persistent: this workgroup runs strips blockIdx.x + i * gridDim.x (64 rows
-  // of Y each) as one flat chunk sequence, so the stage ring never drains
-  // between strips and no workgroup is ever relaunched
-  const int64_t nstrips = (M + kWaves * 16 - 1) / (kWaves * 16);
-  if ((int64_t)blockIdx.x >= nstrips) return;
-  const int64_t my_strips = (nstrips - 1 - blockIdx.x) / gridDim.x + 1;
-  const int64_t G = my_strips * nchunks;
-
-  // B staging addresses (lane-linear in LDS), recomputed per issue (cheap
-  // integer work; keeping them live across the strip epilogue would spill)
-  const double* __restrict__ bbase = Bf + (int64_t)jt0 * 64;
-  const int64_t bchunk = (int64_t)kKC * jt_total * 64;
-  // A staging: instruction j of this wave loads rows 8 j + (lane >> 3),
-  // columns b0 + 2 (lane & 7) .. +1 of the chunk; rows past q clamp to q - 1,
-  // columns past M to M - 2 (those output rows are never stored)
-  const int arow = lane >> 3;
-  const int acol = 2 * (lane & 7);
-
-  // the next chunk to issue: strip ii (its first row b0i), chunk ic, stage is
-  int64_t b0i = ((int64_t)blockIdx.x * kWaves + wave) * 16;
-  const int64_t b0step = (int64_t)gridDim.x * kWaves * 16;
-  int ic = 0, is = 0;
-  auto issue = [&]() {
-    const int c = ic;
-    double* st = lds + is * kStage;
-    const double* cb = bbase + (int64_t)c * bchunk;
-#pragma unroll
-    for (int u = 0; u < kPerT; ++u) {
-      const int bi = threadIdx.x + u * kThreads;
-      const int s_ = bi / (JT * 32);
-      if (bi < kBChunk2)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(cb + s_ * jt_total * 64 +
-                                                            2 * (bi - s_ * (JT * 32))),
-            (__attribute__((address_space(3))) void*)(st + (u * kThreads + wave * 64) * 2), 16,
-            0, 0);
-    }
-    double* sa = st + kBD + wave * kARows * 16;
-    const int64_t col = min(b0i + acol, M - 2);
-#pragma unroll
-    for (int j = 0; j < kAInstr; ++j) {
-      const int k = min(c * kARows + 8 * j + arow, q - 1);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(X + (int64_t)k * M + col),
-          (__attribute__((address_space(3))) void*)(sa + j * 128), 16, 0, 0);
-    }
-    is = is + 1 == kNS ? 0 : is + 1;
-    if (++ic == nchunks) {
-      ic = 0;
-      b0i += b0step;
-    }
-  };
-
-  d4 acc[JT];
-#pragma unroll
-  for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-
-#pragma unroll
-  for (int g = 0; g < kNS - 1; ++g)
-    if (g < G) issue();
-
-  int c = 0, sc = 0;  // chunk of the current strip, its stage
-  int64_t i = 0;
-  for (int64_t g = 0; g < G; ++g) {
-    // retire chunk g (chunks g+1 .. g+kNS-2 may stay in flight)
-    if (kNS == 3 && g + 1 < G)
-      __builtin_amdgcn_s_waitcnt(kWaitN);
-    else if (kNS == 4 && g + 2 < G)
-      __builtin_amdgcn_s_waitcnt((((2 * kN) & 15) | ((((2 * kN) >> 4) & 3) << 14)) | (7 << 4) |
-                                 (15 << 8));
-    else if (kNS == 4 && g + 1 < G)
-      __builtin_amdgcn_s_waitcnt(kWaitN);
-    else
-      __builtin_amdgcn_s_waitcnt(kWait0);
-    __builtin_amdgcn_s_barrier();
-    if (g + kNS - 1 < G) issue();
-    const double* st = lds + sc * kStage;
-    sc = sc + 1 == kNS ? 0 : sc + 1;
-    const double* sa = st + kBD + wave * kARows * 16 + krow * 16 + (lane & 15);
-    const int kcn = min(kKC, KS - c * kKC);
-    const bool tail = c == nchunks - 1;
-#pragma unroll
-    for (int s = 0; s < kKC; ++s) {
-      if (s < kcn) {
-        double a = sa[s * 64];
-        if (tail && (c * kARows + 4 * s + krow) >= q) a = 0.0;
-#pragma unroll
-        for (int t = 0; t < JT; ++t) {
-          const double b = st[(s * JT + t) * 64 + lane];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-        }
-      }
-    }
-    if (tail) {
-      const int64_t blk = (int64_t)blockIdx.x + i * gridDim.x;
-      const int64_t b0 = (blk * kWaves + wave) * 16;
-      if (kEpi == 0) {
-        // plain role (no shift / dots: kron_apply never sends xs here)
-        const int col = lane & 15;
-#pragma unroll
-        for (int t = 0; t < JT; ++t) {
-          const int j = (jt0 + t) * 16 + col;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t row = b0 + krow + 4 * r;
-            if (row < M && j < p) Y[row * p + j] = acc[t][r];
-          }
-        }
-      } else {
-        mp_finish<JT, kWaves, 1, true, kEpi, 0, true, 1>(acc, Y, M, p, jt0, xs, shift,
-                                                         dot_partials, om, fz, 0.0, b0, 0, red,
-                                                         blk);
-      }
-#pragma unroll
-      for (int t = 0; t < JT; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-      c = 0;
-      ++i;
-    } else {
-      ++c;
-    }
-  }
-}
-
-template <int JT, int KC, int NS>
-static constexpr size_t glds_lds_bytes() {
-  return ((size_t)NS * (KC * JT * 64 + 4 * KC * 4 * 16) + 16) * sizeof(double);
-}
-
 // Launch configuration of one mode product: waves per workgroup, k-steps per
 // LDS chunk.  The default -- 4-wave workgroups (one wave per SIMD), 3 k-steps
 // per chunk, three independent workgroups per CU, factor chunks staged by
 // global_load_lds -- was chosen by A/B on MI355X (profiles/r01_*_mode_variants):
 // three workgroups drift apart, so one's barrier or epilogue overlaps the
-// others' MFMAs.  GG_MP_VARIANT selects another for tuning runs (plain mode
-// products only; the CG-fused ones always use the default).
+// others' MFMAs.  The other shapes of that A/B (12 / 8 / 2-wave workgroups,
+// 2 / 4 k-steps, register-staged chunks, the all-LDS-DMA and persistent
+// kernels, paired stores, s_setprio, and the wider fused-CG prologues) were
+// measured slower and live in the history (round 4).
 struct ModeConfig {
   mode_kernel_t fn;
   int waves, kc, split, jtl;  // jtl: tiles staged per launch
   size_t lds;                 // dynamic LDS bytes
-  bool glds;                  // all-LDS-DMA kernel: needs M even, X 16-B aligned
-  int pers;                   // > 0: persistent, at most pers workgroups per CU
   bool t4 = false;            // reads Factor::frag4 (JT + 1 fragments per k-step)
 };
 
@@ -767,36 +594,19 @@ template <int JT, int W, int KC, int CGP, int MINW, int SPLIT, int OPT, int EPI 
 static ModeConfig cfg() {
   constexpr int JW = (JT + SPLIT - 1) / SPLIT;
   return ModeConfig{mode_product_kernel<JW, W, KC, CGP, MINW, true, SPLIT, OPT, EPI>, W, KC,
-                    SPLIT, JW * SPLIT, 2 * (size_t)KC * JW * SPLIT * 64 * sizeof(double), false,
-                    0};
+                    SPLIT, JW * SPLIT, 2 * (size_t)KC * JW * SPLIT * 64 * sizeof(double)};
 }
 
 template <int JT, int W, int KC, int CGP, int MINW, int OPT, int EPI = 0>
 static ModeConfig cfg_t4() {
   return ModeConfig{mode_product_kernel<JT, W, KC, CGP, MINW, true, 1, OPT, EPI, true>, W, KC, 1,
-                    JT + 1, 2 * (size_t)KC * (JT + 1) * 64 * sizeof(double), false, 0, true};
+                    JT + 1, 2 * (size_t)KC * (JT + 1) * 64 * sizeof(double), true};
 }
 
-template <int JT, int KC, int NS, int MINW, int EPI = 0, int PERS = 0>
-static ModeConfig cfg_glds() {
-  return ModeConfig{mode_product_glds_kernel<JT, KC, NS, MINW, EPI>, 4, KC, 1, JT,
-                    glds_lds_bytes<JT, KC, NS>(), true, PERS};
-}
 
-// variant 0 is the default; the others are kept for A/B runs (tools/tune_mode.py)
 // cgp: 0 plain, 1 textbook CG prologue, 2 fused CG prologue, 3 fused CG
 // epilogue (+ side job when d = 2), 4 fused CG side job, 5 / 6 fusion layouts
 // 2 / 1 epilogues, 7 Lanczos prologue
-// GG_MP_PRO selects the fused-CG prologue launch's shape (A/B; p = 200 only):
-// 1 / 3: 12-wave workgroups (one per CU) with 3 / 4 k-steps per chunk,
-// 2: 8-wave workgroups -- wider row segments per workgroup for the prologue's
-// five strided vector passes (tools/hbm_stream_bench.hip: 3R2W in the A
-// pattern at 4.18 / 4.43 / 4.66 TB/s for 4 / 8 / 12 waves in lockstep).
-static int pro_variant() {
-  const char* e = gg::knob("GG_MP_PRO");
-  return e ? atoi(e) : 0;
-}
-
 // the default shapes with the 4x4x4 tail (kT4), for factors with frag4
 template <int JT>
 static ModeConfig config_t4(int cgp) {
@@ -816,66 +626,37 @@ static ModeConfig config_t4(int cgp) {
 }
 
 template <int JT>
-static ModeConfig config_for(int variant, int cgp) {
-  if (cgp == 1) return cfg<JT, 4, 3, 1, 3, 1, 2>();
-  if (cgp == 7) return cfg<JT, 4, 3, 3, 3, 1, 2>();   // Lanczos prologue (CGP 3)
-  if constexpr (JT == 13) {
-    if (cgp == 2) {
-      switch (pro_variant()) {
-        case 1: return cfg<JT, 12, 3, 2, 1, 1, 2>();
-        case 2: return cfg<JT, 8, 3, 2, 1, 1, 2>();
-        case 3: return cfg<JT, 12, 4, 2, 1, 1, 2>();
-        default: break;
-      }
-    }
-  }
-  if (cgp == 2) return cfg<JT, 4, 3, 2, 3, 1, 2>();
-  if (cgp == 3) return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
-  if (cgp == 4) return cfg<JT, 4, 3, 0, 3, 1, 2, 1>();
-  if (cgp == 5) return cfg<JT, 4, 3, 0, 3, 1, 2, 3>();
-  if (cgp == 6) return cfg<JT, 4, 3, 0, 3, 1, 2, 4>();
-  switch (variant) {
-    case 1: return cfg<JT, 12, 4, 0, 3, 1, 2>();
-    case 2: return cfg<JT, 12, 4, 0, 3, 1, 0>();  // register-staged factor chunks
-    case 3: return cfg<JT, 4, 4, 0, 3, 1, 2>();
-    case 4: return cfg<JT, 4, 2, 0, 3, 1, 2>();
-    case 5: return cfg<JT, 2, 2, 0, 3, 1, 2>();
-    case 6: return cfg<JT, 8, 4, 0, 4, 2, 2>();   // columns split over two waves
-    case 7: return cfg<JT, 12, 4, 0, 3, 1, 3>();  // + sched_barrier around the prefetch
-    case 8: return cfg_glds<JT, 2, 3, 3>();        // all-LDS-DMA, 3 stages
-    case 9: return cfg_glds<JT, 2, 4, 2>();        // all-LDS-DMA, 4 stages
-    case 10: return cfg_glds<JT, 2, 3, 3, 0, 3>();   // persistent, 3 workgroups / CU
-    case 11: return cfg<JT, 4, 3, 0, 3, 1, 2 | 4>();   // 16-byte paired stores
-    case 12: return cfg<JT, 4, 3, 0, 3, 1, 2 | 8>();   // s_setprio around the MFMAs
-    case 13: return cfg<JT, 4, 3, 0, 3, 1, 2 | 4 | 8>();
+static ModeConfig config_for(int cgp) {
+  switch (cgp) {
+    case 1: return cfg<JT, 4, 3, 1, 3, 1, 2>();
+    case 2: return cfg<JT, 4, 3, 2, 3, 1, 2>();
+    case 3: return cfg<JT, 4, 3, 0, 3, 1, 2, 2>();
+    case 4: return cfg<JT, 4, 3, 0, 3, 1, 2, 1>();
+    case 5: return cfg<JT, 4, 3, 0, 3, 1, 2, 3>();
+    case 6: return cfg<JT, 4, 3, 0, 3, 1, 2, 4>();
+    case 7: return cfg<JT, 4, 3, 3, 3, 1, 2>();   // Lanczos prologue (CGP 3)
     default: return cfg<JT, 4, 3, 0, 3, 1, 2>();
   }
 }
-constexpr int kNumVariants = 14;
 
-static int mode_variant() {
-  const char* e = gg::knob("GG_MP_VARIANT");  // tuning knob, re-read per call
-  return e ? atoi(e) : 0;
-}
-
-static ModeConfig select_kernel(int jt, int variant, int cgp) {
+static ModeConfig select_kernel(int jt, int cgp) {
   switch (jt) {
-    case 1: return config_for<1>(variant, cgp);
-    case 2: return config_for<2>(variant, cgp);
-    case 3: return config_for<3>(variant, cgp);
-    case 4: return config_for<4>(variant, cgp);
-    case 5: return config_for<5>(variant, cgp);
-    case 6: return config_for<6>(variant, cgp);
-    case 7: return config_for<7>(variant, cgp);
-    case 8: return config_for<8>(variant, cgp);
-    case 9: return config_for<9>(variant, cgp);
-    case 10: return config_for<10>(variant, cgp);
-    case 11: return config_for<11>(variant, cgp);
-    case 12: return config_for<12>(variant, cgp);
-    case 13: return config_for<13>(variant, cgp);
-    case 14: return config_for<14>(variant, cgp);
-    case 15: return config_for<15>(variant, cgp);
-    case 16: return config_for<16>(variant, cgp);
+    case 1: return config_for<1>(cgp);
+    case 2: return config_for<2>(cgp);
+    case 3: return config_for<3>(cgp);
+    case 4: return config_for<4>(cgp);
+    case 5: return config_for<5>(cgp);
+    case 6: return config_for<6>(cgp);
+    case 7: return config_for<7>(cgp);
+    case 8: return config_for<8>(cgp);
+    case 9: return config_for<9>(cgp);
+    case 10: return config_for<10>(cgp);
+    case 11: return config_for<11>(cgp);
+    case 12: return config_for<12>(cgp);
+    case 13: return config_for<13>(cgp);
+    case 14: return config_for<14>(cgp);
+    case 15: return config_for<15>(cgp);
+    case 16: return config_for<16>(cgp);
     default: throw Error(GG_ERR_VALUE, "bad tile count");
   }
 }
@@ -934,7 +715,7 @@ static void pack_fragments(const double* K, int64_t rows, int64_t cols, bool tra
       }
   GG_HIP(hipMalloc(&f.frag, h.size() * sizeof(double)));
   GG_HIP(hipMemcpy(f.frag, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (t4_supported(f.JT) && f.p - 16 * (int64_t)(f.JT - 1) <= 8 && gg::knob("GG_MP_NO_T4") == nullptr) {
+  if (t4_supported(f.JT) && f.p - 16 * (int64_t)(f.JT - 1) <= 8) {
     const int JF = f.JT + 1;
     std::vector<double> h4(((size_t)f.KS + 8) * JF * 64, 0.0);
     for (int ks = 0; ks < f.KS; ++ks)
@@ -966,7 +747,7 @@ static bool fold_enabled() {
 // tail fragments of a half of hS columns in JT tiles (even m, JT >= 4 only:
 // the instantiated shapes)
 static int fold_tail(int64_t m, int JT) {
-  if (m % 2 != 0 || JT < 4 || gg::knob("GG_MP_NO_T4") != nullptr) return 0;
+  if (m % 2 != 0 || JT < 4) return 0;
   const int64_t r = (m - m / 2) - 16 * (int64_t)(JT - 1);
   return r <= 4 ? 1 : r <= 8 ? 2 : 0;
 }
@@ -1047,13 +828,6 @@ static void plan_sizes(const std::vector<Factor>& fs, int64_t n_in, int64_t& max
   }
 }
 
-// GG_FOLD_RING_SIDE=1: the CG side-job launch on the ring kernel (opt-in:
-// 8.6 vs 8.2 ms per side launch at 200^4, profiles/r04/j_side_ab.txt)
-static bool ring_side_env() {
-  const char* e = gg::knob("GG_FOLD_RING_SIDE");
-  return e && atoi(e) == 1;
-}
-
 int64_t kron_side_half(const gg_kron* K, int64_t n);
 
 void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, double shift,
@@ -1085,10 +859,6 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
   int64_t size = n_in;
   const double* src = x;
   int64_t np_total = 0;
-  // the x side job as a concurrent kernel on the CG's side stream (balanced
-  // x_defer, d >= 3): mode products 1..d-2 run plain (the ring kernel)
-  const bool side_async = cgp == 2 && cg->side_stream != nullptr && cg->sx != nullptr &&
-                          cg->xdefer == 2 && d >= 3 && cg->sc != nullptr;
   if (ev) GG_HIP(hipEventRecord(ev[0], stream));
   for (int k = 0; k < d; ++k) {
     const Factor& f = fs[k];
@@ -1110,7 +880,6 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
       dst = cg->first_dst;
     }
     const bool last = (k == d - 1);
-    const int variant = mode_variant();
     if (M > 0) {
       const double* step_src = src;
       for (int jt0 = 0; jt0 < f.JT; jt0 += kMaxJT) {
@@ -1124,37 +893,29 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
         // the x side job rides on the second mode product; with d >= 4 the
         // third (also a plain, MFMA-bound one) takes the second half of x
         const bool split_side = cgp == 2 && d >= 4 && cg->sx != nullptr;
-        const bool side = !side_async && cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
+        const bool side = cgp == 2 && jt0 == 0 && cg->sx != nullptr &&
                           (k == 1 || (split_side && k == 2));
         const int epi_kind = !epi ? 0 : cg->ep_out == nullptr ? 3 : cg->ex != nullptr ? 5 : 6;
         const int kind = epi ? epi_kind : side ? 4 : pro;
-        ModeConfig mc = select_kernel(jt, variant, kind);
-        const bool with_xs = last && (shift != 0.0 || dot_partials != nullptr);
-        if (mc.glds && (M % 2 != 0 || M < 2 || (reinterpret_cast<uintptr_t>(step_src) & 15) ||
-                        with_xs))
-          mc = select_kernel(jt, 0, kind);
+        ModeConfig mc = select_kernel(jt, kind);
         // the default shapes take the 4x4x4 tail when the factor has frag4
-        if (f.frag4 != nullptr && jt0 == 0 && jt == f.JT && variant == 0 &&
-            !(kind == 2 && pro_variant() != 0) && jt == 13)
-          mc = config_t4<13>(kind);
+        if (f.frag4 != nullptr && jt0 == 0 && jt == f.JT && jt == 13) mc = config_t4<13>(kind);
         // centrosymmetric factors: the even/odd split (half the MFMA work)
-        const bool fold = f.ffrag != nullptr && jt0 == 0 && variant == 0 && fold_kind(kind) &&
-                          !(pro && last) && !(kind == 2 && pro_variant() != 0);
-        bool ring_side = false;
+        const bool fold =
+            f.ffrag != nullptr && jt0 == 0 && fold_kind(kind) && !(pro && last);
         if (fold) {
           const double* xs_ = last && (shift != 0.0 || dot_partials != nullptr)
                                   ? (((cgp == 2 && cg->ep_out == nullptr) || cgp == 3) ? cg->p_out
                                                                                       : x)
                                   : nullptr;
           // the persistent LDS-DMA ring kernel (gg_kron_ring.hip) for the plain
-          // launch (GG_FOLD_RING=<variant>)
-          const int rv = ring_variant_env();
+          // launch (GG_FOLD_RING=0: the chunked kernel, A/B)
           const bool ring_ok =
-              rv > 0 && xs_ == nullptr && f.rfrag != nullptr && M % 2 == 0 && M >= 2 &&
+              ring_variant_env() != 0 && xs_ == nullptr && f.rfrag != nullptr && M % 2 == 0 && M >= 2 &&
               ((reinterpret_cast<uintptr_t>(step_src) | reinterpret_cast<uintptr_t>(dst)) & 15) ==
                   0;
-          if (ring_ok && kind == 0 && (skip == nullptr || side_async)) {
-            const RingConfig rc = select_ring(f.fJT, f.fTT, rv);
+          if (ring_ok && kind == 0 && skip == nullptr) {
+            const RingConfig rc = select_ring(f.fJT, f.fTT);
             const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
             const int grid = ring_grid(rc, cu_count(), nb);
             hipLaunchKernelGGL(rc.fn, dim3((unsigned)grid), dim3(64 * rc.waves), rc.lds, stream,
@@ -1162,11 +923,6 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             GG_LAUNCH_CHECK();
             continue;
           }
-          // the CG side-job launch (balanced x_defer) on the ring: the side
-          // chunks ride in its stages (GG_FOLD_RING_SIDE=0 keeps the chunked
-          // kernel)
-          // (decided here, launched below once the side-job fields of fz are set)
-          ring_side = ring_ok && kind == 4 && side && cg->xdefer == 2 && ring_side_env();
           const bool aligned =
               f.p % 2 == 0 &&
               ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(xs_) |
@@ -1188,7 +944,7 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
             GG_REQUIRE(4 * nch * fc.kc <= (int64_t)f.q && 32 * M < ((int64_t)1 << 32),
                        GG_ERR_VALUE, "lean folded kernel outside its row / offset range");
           }
-          mc = ModeConfig{fc.fn, fc.waves, fc.kc, 1, fc.jf, fc.lds, false, 0, false};
+          mc = ModeConfig{fc.fn, fc.waves, fc.kc, 1, fc.jf, fc.lds, false};
         }
         const int64_t nblk = ceil_div(M, (int64_t)(mc.waves / mc.split) * 16);
         GG_REQUIRE(nblk < (int64_t)1 << 31, GG_ERR_VALUE, "vector too long for one launch");
@@ -1266,20 +1022,6 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
           }
         }
         int64_t grid = nblk;
-        if (mc.pers > 0) grid = std::min<int64_t>(nblk, (int64_t)cu_count() * mc.pers);
-        if (ring_side) {
-          const RingConfig rc = select_ring_side(f.fJT, f.fTT);
-          const int64_t nb = ceil_div(M, (int64_t)16 * rc.waves);
-          if (fz.sc != nullptr && fz.sx != nullptr && fz.xdefer == 2 &&
-              ring_side_capacity(nb, f.fKS) >= std::max(fz.sn, fz.sn_h1) &&
-              ((reinterpret_cast<uintptr_t>(fz.sx) & 15) | ((fz.soff | fz.soff_h1) & 1)) == 0) {
-            const int rgrid = ring_grid(rc, cu_count(), nb);
-            hipLaunchKernelGGL(rc.fn, dim3((unsigned)rgrid), dim3(64 * rc.waves), rc.lds, stream,
-                               step_src, dst, f.rfrag, M, (int)f.q, f.fKS, nb, skip, fz);
-            GG_LAUNCH_CHECK();
-            continue;
-          }
-        }
         hipLaunchKernelGGL(mc.fn, dim3((unsigned)grid), dim3(mc.waves * 64),
                            mode_lds_bytes(mc), stream, step_src, dst,
                            fold ? f.ffrag : mc.t4 ? f.frag4 : f.frag, M, (int)f.q, (int)f.p,
@@ -1294,15 +1036,6 @@ void kron_apply(const gg_kron* K, bool transpose, const double* x, double* y, do
       }
     }
     (void)out_size;
-    if (side_async && k == 0) {
-      // after the prologue (which read the x_defer state the previous scalars
-      // wrote): half sc->xh of the active pair, beside mode products 1..d-2
-      GG_HIP(hipEventRecord(cg->side_ev[0], stream));
-      GG_HIP(hipStreamWaitEvent(cg->side_stream, cg->side_ev[0], 0));
-      launch_x_half(cg->sx, cg->sn, kron_side_half(K, cg->sn), cg->sc, cg->side_stream);
-      GG_HIP(hipEventRecord(cg->side_ev[1], cg->side_stream));
-    }
-    if (side_async && k == d - 1) GG_HIP(hipStreamWaitEvent(stream, cg->side_ev[1], 0));
     if (ev) GG_HIP(hipEventRecord(ev[k + 1], stream));
     size = out_size;
     src = dst;
@@ -1352,14 +1085,13 @@ int64_t kron_side_half(const gg_kron* K, int64_t n) {
 static void set_lds_limits() {
   static bool done = false;
   if (done) return;
-  for (int v = 0; v < kNumVariants; ++v)
-    for (int jt = 1; jt <= kMaxJT; ++jt)
-      for (int cgp = 0; cgp < 8; ++cgp) {
-        const ModeConfig mc = select_kernel(jt, v, cgp);
-        GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)mode_lds_bytes(mc)));
-      }
+  for (int jt = 1; jt <= kMaxJT; ++jt)
+    for (int cgp = 0; cgp < 8; ++cgp) {
+      const ModeConfig mc = select_kernel(jt, cgp);
+      GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)mode_lds_bytes(mc)));
+    }
   for (int cgp = 0; cgp < 8; ++cgp) {
     const ModeConfig mc = config_t4<13>(cgp);
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mc.fn),

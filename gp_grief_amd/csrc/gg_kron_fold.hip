@@ -707,8 +707,14 @@ static FoldConfig cfg_fold() {
 // in their range (lean_ok); fused CG at 200^4, interleaved processes:
 // 41.25 -> 40.98 ms per iteration (side launches 8.05 -> 7.95 ms, the side
 // kernel's 3 spilled VGPRs gone; profiles/r03/ak_lean_cg_ab.jsonl).
-// GG_FOLD_LEAN=0 disables them; GG_FOLD_LEAN_PRO=1 / 2 (A/B only) takes a
-// lean fused-CG prologue with 1 / 2 k-steps per chunk -- 0.2-0.3 ms slower.
+// GG_FOLD_LEAN=0 disables them (the clamped kernels every other shape takes).
+// Non-temporal masks (round 4, profiles/r04/u_nt, t_pro_nt, zf_lz): the CG
+// epilogue's p loads and q stores (8.66-8.76 -> 8.59-8.64 ms), the side
+// launches' operand and x-stream accesses (7.89-7.96 -> 7.84-7.89), the
+// prologue's operand / r / q_old loads and p_new / r stores (13.90 -> 13.63),
+// the Lanczos epilogue's streams (8.54-8.64 -> 8.38-8.47); the other masks,
+// an epilogue that prefetches its next p batch, 1 / 2 k-step lean prologues
+// and 12-wave side launches measured slower and live in the history.
 static int env_int(const char* name, int dflt = 0) {
   const char* e = gg::knob(name);
   return e ? atoi(e) : dflt;
@@ -722,98 +728,28 @@ static FoldConfig lean_cfg(int kind, bool staged) {
   constexpr int JT = 7, TT = 1;
   if (staged) {
     switch (kind) {
-      case 3:
-        // GG_FOLD_EPI_NT: non-temporal streams of the CG epilogue (default 6:
-        // the p operand loads and the q stores; epilogue 8.66-8.76 -> 8.59-8.64
-        // ms at 200^4, interleaved, profiles/r04/u_nt)
-        if (env_int("GG_FOLD_EPI_PRE") == 1) return cfg_fold<JT, TT, 3, true, 4 | 192 | 256>();
-        switch (env_int("GG_FOLD_EPI_NT", 6)) {
-          case 1: return cfg_fold<JT, TT, 3, true, 4 | 32>();
-          case 2: return cfg_fold<JT, TT, 3, true, 4 | 64>();
-          case 4: return cfg_fold<JT, TT, 3, true, 4 | 128>();
-          case 6: return cfg_fold<JT, TT, 3, true, 4 | 192>();
-          case 7: return cfg_fold<JT, TT, 3, true, 4 | 224>();
-          default: return cfg_fold<JT, TT, 3, true, 4>();
-        }
+      case 3: return cfg_fold<JT, TT, 3, true, 4 | 192>();   // p loads, q stores nt
       case 6: return cfg_fold<JT, TT, 6, true, 4>();
-      default:
-        // the shift / dot epilogue of a plain launch (the fused Lanczos
-        // step's last mode product): non-temporal operand loads and output
-        // stores (default; GG_FOLD_LZE=0 restores normal ones) -- 200^4
-        // Lanczos epilogue 8.54-8.64 -> 8.38-8.47 ms (profiles/r04/zf_lz)
-        if (env_int("GG_FOLD_LZE", 1) == 1) return cfg_fold<JT, TT, 0, true, 4 | 192>();
-        return cfg_fold<JT, TT, 0, true, 4>();
+      default: return cfg_fold<JT, TT, 0, true, 4 | 192>();   // shift / dot epilogue nt
     }
   }
   switch (kind) {
     case 3: return cfg_fold<JT, TT, 3, false, 4>();
-    case 4:
-      // GG_FOLD_SIDE_NT: non-temporal streams of the side-job launches
-      // (default 3: A-operand loads and the x side job's loads / stores;
-      // 7.89-7.96 -> 7.84-7.89 ms per launch, profiles/r04/u_nt)
-      switch (env_int("GG_FOLD_SIDE_NT", 3)) {
-        case 1: return cfg_fold<JT, TT, 4, false, 4 | 32>();
-        case 2: return cfg_fold<JT, TT, 4, false, 4 | 64>();
-        case 3: return cfg_fold<JT, TT, 4, false, 4 | 96>();
-        default: return cfg_fold<JT, TT, 4, false, 4>();
-      }
+    case 4: return cfg_fold<JT, TT, 4, false, 4 | 96>();   // operand, x stream nt
     case 6: return cfg_fold<JT, TT, 6, false, 4>();
     default: return cfg_fold<JT, TT, 0, false, 4>();
   }
-}
-
-static FoldConfig lean_pro_cfg(int mode) {
-  return mode == 2 ? cfg_fold<7, 1, 2, false, 4, 2>() : cfg_fold<7, 1, 2, false, 4, 1>();
 }
 
 // 12-wave workgroups (one per CU, the B chunks staged once for 192 rows b,
 // 1.5 KB row segments): default for the fused-CG prologue of the m = 200
 // shape (GG_FOLD_PRO_W=4 restores 4 waves) -- 200^4, interleaved processes:
 // prologue 13.58-13.66 -> 13.18-13.21 ms, iteration 40.19-40.42 -> 39.93-39.95
-// ms (profiles/r03/an_wide_cg_ab.jsonl); the side-job launches lose 0.7 ms
-// each with them (GG_FOLD_SIDE_W=12, A/B only).  The prologue's r.r partials
-// array is sized for 4-wave blocks and zeroed at allocation (gg_cg_create).
-static FoldConfig wide_cfg(int kind) {
-  return kind == 2 ? cfg_fold<7, 1, 2, false, 0, 0, 12>() : cfg_fold<7, 1, 4, false, 4, 0, 12>();
-}
-
-// plain-launch A/B variants (GG_FOLD_VARIANT, m = 200 shape only); WV waves
-// per workgroup
-template <int KC, int MINW, int OPT, int WV = 4>
-static FoldConfig cfg_fold_var() {
-  constexpr int JT = 7, TT = 1;
-  constexpr int JF = 2 * (JT - 1 + TT);
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, KC, 0, MINW, 0, false, OPT, false, WV>,
-                    KC, JF, 2 * (size_t)KC * JF * 64 * sizeof(double), (OPT & 4) != 0, WV};
-}
-
-static int fold_variant() {
-  const char* e = gg::knob("GG_FOLD_VARIANT");
-  return e ? atoi(e) : 0;
-}
-
-static FoldConfig fold_variant_cfg(int v) {
-  switch (v) {
-    case 1: return cfg_fold_var<2, 3, 0>();
-    case 2: return cfg_fold_var<4, 3, 0>();
-    case 3: return cfg_fold_var<3, 2, 0>();
-    case 4: return cfg_fold_var<6, 2, 0>();
-    case 5: return cfg_fold_var<3, 3, 1>();
-    case 6: return cfg_fold_var<3, 3, 2>();
-    case 7: return cfg_fold_var<1, 3, 0>();
-    case 8: return cfg_fold_var<3, 3, 4>();
-    case 9: return cfg_fold_var<3, 3, 8>();
-    case 10: return cfg_fold_var<3, 3, 12>();
-    case 11: return cfg_fold_var<3, 2, 12>();
-    case 12: return cfg_fold_var<6, 2, 12>();
-    case 13: return cfg_fold_var<3, 3, 20>();
-    case 14: return cfg_fold_var<3, 3, 4, 6>();
-    case 15: return cfg_fold_var<3, 3, 4, 12>();
-    case 16: return cfg_fold_var<6, 3, 4, 12>();
-    case 17: return cfg_fold_var<6, 3, 4, 6>();
-    default: return cfg_fold_var<3, 3, 0>();
-  }
-}
+// ms (profiles/r03/an_wide_cg_ab.jsonl), with its operand / r / q_old loads and
+// p_new / r stores non-temporal (Y, read by the next launch, a normal store).
+// The prologue's r.r partials array is sized for 4-wave blocks and zeroed at
+// allocation (gg_cg_create).
+static FoldConfig wide_pro_cfg() { return cfg_fold<7, 1, 2, false, 96, 0, 12>(); }
 
 // the staged epilogue (kStg) for the launches whose epilogue reads the fused
 // operands (kinds 0 with a shift / dot operand, 3 and 6): measured at 200^4
@@ -832,8 +768,6 @@ static FoldConfig fold_staged_by_kind(int kind, bool lean_ok) {
 }
 
 bool fold_staged_available(int JT, int TT, int kind) {
-  const char* e = gg::knob("GG_FOLD_STAGE");   // A/B knob: 0 = direct stores
-  if (e && atoi(e) == 0) return false;
   return (kind == 0 || kind == 3 || kind == 6) && JT >= 1 && JT <= 8 &&
          (TT == 0 || JT >= 4);
 }
@@ -864,53 +798,16 @@ FoldConfig select_fold_staged(int JT, int TT, int kind, bool lean_ok) {
   throw Error(GG_ERR_VALUE, "no staged folded kernel for this factor shape");
 }
 
-// fused-CG prologue with one k-step per chunk (A/B: GG_FOLD_PRO_KC=1)
-static FoldConfig fold_pro_kc1() {
-  constexpr int JT = 7, TT = 1;
-  constexpr int JF = 2 * (JT - 1 + TT);
-  return FoldConfig{mode_product_fold_kernel<JT, JT, TT, TT, 1, 2, 3, 0, false, 0, false>, 1, JF,
-                    2 * (size_t)1 * JF * 64 * sizeof(double)};
-}
-
 template <int JT, int TT>
 static FoldConfig fold_by_kind(int kind, bool lean_ok) {
   if constexpr (JT == 7 && TT == 1) {
-    if (kind == 0 && fold_variant() != 0 && lean_ok) return fold_variant_cfg(fold_variant());
-    if (kind == 2) {
-      const int lp = env_int("GG_FOLD_LEAN_PRO");
-      if (lean_ok && (lp == 1 || lp == 2)) return lean_pro_cfg(lp);
-      if (env_int("GG_FOLD_PRO_W", 12) == 12) {
-        // non-temporal prologue streams (default mask 3: the operand / r /
-        // q_old loads and the p_new / r stores; Y, read by the next launch,
-        // stays a normal store) -- 200^4, interleaved processes on two boxes:
-        // prologue 13.90 -> 13.63 ms, iteration 40.62 -> 40.36 ms (mask 7,
-        // Y too: mixed, the side launches +0.1 ms; profiles/r04/t_pro_nt*)
-        switch (env_int("GG_FOLD_PRO_NT", 3)) {
-          case 1: return cfg_fold<7, 1, 2, false, 32, 0, 12>();
-          case 2: return cfg_fold<7, 1, 2, false, 64, 0, 12>();
-          case 3: return cfg_fold<7, 1, 2, false, 96, 0, 12>();
-          case 6: return cfg_fold<7, 1, 2, false, 192, 0, 12>();
-          case 7: return cfg_fold<7, 1, 2, false, 224, 0, 12>();
-          default: return wide_cfg(2);
-        }
-      }
-      const char* e = gg::knob("GG_FOLD_PRO_KC");
-      if (e && atoi(e) == 1) return fold_pro_kc1();
-    }
-    if (kind == 7) {
-      // the fused Lanczos prologue: 12-wave workgroups with non-temporal
-      // streams, as the CG prologue (default 2) -- 200^4 Lanczos step 34.1-35.1
-      // -> 33.47-33.50 ms, prologue 11.9-12.5 -> 11.3 ms, tridiagonal
-      // bitwise unchanged (profiles/r04/zf_lz).  GG_FOLD_LZ: 0 = 4-wave plain,
-      // 1 = 12-wave, 3 = 4-wave non-temporal (A/B)
-      switch (env_int("GG_FOLD_LZ", 2)) {
-        case 1: return cfg_fold<7, 1, 7, false, 0, 0, 12>();
-        case 2: return cfg_fold<7, 1, 7, false, 96, 0, 12>();
-        case 3: return cfg_fold<7, 1, 7, false, 96>();
-        default: break;
-      }
-    }
-    if (lean_ok && kind == 4 && env_int("GG_FOLD_SIDE_W") == 12) return wide_cfg(4);
+    // the fused CG prologue on 12-wave workgroups (GG_FOLD_PRO_W=4: 4 waves)
+    if (kind == 2 && env_int("GG_FOLD_PRO_W", 12) == 12) return wide_pro_cfg();
+    // the fused Lanczos prologue: 12-wave workgroups with non-temporal
+    // streams, as the CG prologue -- 200^4 Lanczos step 34.1-35.1 -> 33.47-33.50
+    // ms, prologue 11.9-12.5 -> 11.3 ms, tridiagonal bitwise unchanged
+    // (profiles/r04/zf_lz)
+    if (kind == 7) return cfg_fold<7, 1, 7, false, 96, 0, 12>();
     if (lean_ok && env_int("GG_FOLD_LEAN", 1) == 1 && lean_kind(kind, false))
       return lean_cfg(kind, false);
   }
@@ -954,11 +851,6 @@ FoldConfig select_fold(int JT, int TT, int kind, bool lean_ok) {
 }
 
 void set_fold_lds_limits() {
-  {
-    const FoldConfig fc = fold_pro_kc1();
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
-  }
   for (int jt = 1; jt <= 8; ++jt)
     for (int tt = 0; tt <= 2; ++tt) {
       if (tt > 0 && jt < 4) continue;
@@ -975,18 +867,8 @@ void set_fold_lds_limits() {
       GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
     }
-  for (int kind : {2, 4}) {
-    const FoldConfig fc = wide_cfg(kind);
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
-  }
-  for (int lp : {1, 2}) {
-    const FoldConfig fc = lean_pro_cfg(lp);
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
-  }
-  for (int v = 1; v <= 17; ++v) {
-    const FoldConfig fc = fold_variant_cfg(v);
+  {
+    const FoldConfig fc = wide_pro_cfg();
     GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(fc.fn),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)fc.lds));
   }

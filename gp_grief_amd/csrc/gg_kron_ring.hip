@@ -80,33 +80,26 @@ __device__ __forceinline__ double swap_adjacent(double v) {
 // that slot; read stage c + 1's operands into the second register set; the
 // step's MFMAs on the first.  So the MFMAs never wait on LDS latency, and
 // NS - 1 stages are in flight across every barrier.
-template <int JS, int TS, int W, int NS, int MINW, int ABL = 0, int KC = 1, bool SIDE = false>
+template <int JS, int TS, int W, int NS, int MINW, int KC>
 __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     const double* __restrict__ X, double* __restrict__ Y, const double* __restrict__ Bf,
     int64_t M, int m, int KS, int64_t nblk, const int* __restrict__ skip, MpFuse fz) {
   constexpr int RB = 16 * W;           // rows b per block
   constexpr int kA = 8 * RB;           // A image doubles per k-step
   constexpr int kB = 16 * 64;          // B image doubles per k-step (16 fragments)
-  // SIDE: the fused CG's x side job rides in the ring -- per k-step a chunk
-  // of kSC elements of x, p_{j-2}, p_{j-1} (+ one junk KiB so that every wave
-  // issues one side DMA), and every wave stores its 32 updated x elements
-  constexpr int kSC = 256;
-  constexpr int kSide = SIDE ? 4 * kSC : 0;
-  constexpr int kStep = kA + kB + kSide;
+  constexpr int kStep = kA + kB;
   constexpr int kStage = KC * kStep;   // a stage: KC k-steps
   constexpr int kBw = 8 / W;           // B DMAs per wave per k-step
-  constexpr int LW = KC * (1 + kBw + (SIDE ? 1 : 0));   // DMAs per wave per stage
+  constexpr int LW = KC * (1 + kBw);   // DMAs per wave per stage
   constexpr int kE = 4 * JS;           // epilogue stores per wave per block
-  // younger ops at a stage's wait: the DMAs of NS - 3 stages, and (SIDE) the
-  // side stores of the NS - 2 steps since its own DMAs
-  constexpr int Y0 = (NS - 3) * LW + (SIDE ? NS - 2 : 0);
+  // younger ops at a stage's wait: the DMAs of NS - 3 stages
+  constexpr int Y0 = (NS - 3) * LW;
   constexpr int YE = Y0 + kE;          // ... with an epilogue since its DMAs
   constexpr int FS = JS - (TS > 0 ? 1 : 0) + TS;
   constexpr int NF = 2 * FS;
   static_assert(W == 4 || W == 8, "one A DMA per wave: W KiB of A per k-step");
   static_assert(NF <= 16, "16 fragment slots per k-step");
   static_assert(KC == 1 || KC == 2, "one or two k-steps per stage");
-  static_assert(!SIDE || (W == 8 && KC == 1), "side job: 8 waves, one k-step per stage");
   static_assert(NS >= 4 && YE <= 63 && (NS - 2) * LW <= 63,
                 "ring depth outside the counted-vmcnt range");
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -156,55 +149,15 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     a_loff = drow + (acol <= room ? acol : room) * 8;
   };
   block_start();
-  // side job (mp_side_job, balanced x_defer): this launch applies half
-  // sc->xh of the pending pair x += c0 p0 + c1 p1 over [soff, soff + sn) (or
-  // the h1 range); xh >= 2: nothing pending -- the DMAs and stores still
-  // issue (stores to g_ring_trash), so the counted waits hold either way
-  double sc0 = 0.0, sc1 = 0.0;
-  const double* sx_src = nullptr;
-  const double* sp0 = nullptr;
-  const double* sp1 = nullptr;
-  double* sx_dst = nullptr;
-  int64_t slen = 0;
-  if (SIDE) {
-    const int xh = fz.sc->xh;
-    const int64_t len = xh >= 2 ? 0 : (xh ? fz.sn_h1 : fz.sn);
-    if (len >= 2) {
-      const int64_t off = xh ? fz.soff_h1 : fz.soff;
-      slen = len;
-      sc0 = fz.sc->xc[0];
-      sc1 = fz.sc->xc[1];
-      sx_dst = fz.sx + off;
-      sx_src = fz.sx + off;
-      sp0 = fz.sc->xp[0] + off;
-      sp1 = fz.sc->xp[1] + off;
-    } else {
-      // nothing to apply: the DMAs re-read x[0], x[1] (always valid)
-      sx_dst = fz.sx;
-      sx_src = sp0 = sp1 = fz.sx;
-    }
-  }
-  const int s_arr = wave >> 1;   // side DMA of this wave: x, p0, p1, junk
-  const double* s_base = s_arr == 1 ? sp0 : s_arr == 2 ? sp1 : sx_src;
-  const int64_t s_lane = (int64_t)(wave & 1) * 128 + 2 * lane;   // element in the chunk
-
   // the next stage's DMA sources, prepared (with the cursor's branches)
   // outside the MFMA region so that the DMAs issue branch-free inside it
-  int64_t na_off[KC], nb_off[KC], na_loff[KC], ns_el[KC];
+  int64_t na_off[KC], nb_off[KC], na_loff[KC];
   auto prep_stage = [&] {
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
       na_off[k] = a_off;
       na_loff[k] = a_loff;
       nb_off[k] = (int64_t)i_s * kB * 8;
-      if (SIDE) {
-        // chunk q = global block * KS + step; clamped to a valid pair
-        const int64_t it = i_it < nmine ? i_it : nmine - 1;
-        const int64_t q = ((int64_t)blockIdx.x + it * G) * KS + i_s;
-        int64_t e = q * kSC + s_lane;
-        if (e > slen - 2) e = slen >= 2 ? slen - 2 : 0;   // slen < 2: e = 0
-        ns_el[k] = e;
-      }
       if (++i_s == KS) {
         i_s = 0;
         ++i_it;
@@ -215,7 +168,6 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
     }
   };
   auto issue_prepped = [&](int slot) {
-    if (ABL & 16) return;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
       double* st = lds + slot * kStage + k * kStep;
@@ -230,10 +182,6 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
                 sbase(Bf, nb_off[k] + (int64_t)p * 128 * 8) + b_loff),
             (__attribute__((address_space(3))) void*)(st + kA + p * 128), 16, 0, 0);
       }
-      if (SIDE)
-        __builtin_amdgcn_global_load_lds(
-            (const __attribute__((address_space(1))) void*)(s_base + ns_el[k]),
-            (__attribute__((address_space(3))) void*)(st + kA + kB + wave * 128), 16, 0, 0);
     }
   };
 
@@ -344,12 +292,7 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
             const double2 o = pair(t, hf, rp);
             const char* yb = rp ? y2 : y0;
             const uint32_t off = hf ? off1 - 128 * t : off0 + 128 * t;
-            if ((t < JS - 1 || 16 * t + ce < h) && !(ABL & 8)) {
-              if (ABL & 64)   // diagnostic: keep the arithmetic, drop the store
-                asm volatile("" ::"v"(o.x), "v"(o.y), "v"(yb + off));
-              else
-                gstore2(const_cast<char*>(yb) + off, o);
-            }
+            if (t < JS - 1 || 16 * t + ce < h) gstore2(const_cast<char*>(yb) + off, o);
             // one pair at a time: the accumulators die as they are stored
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -370,17 +313,11 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
           const int64_t row = b0 + 4 * (rp + (odd ? 1 : 0)) + krow;
           const int64_t col = hf ? (int64_t)(m - 2 - j) : (int64_t)j;
           double* dst = (j < h && row < M) ? Y + row * m + col : g_ring_trash + 2 * lane;
-          if (!(ABL & 8)) gstore2(dst, o);
+          gstore2(dst, o);
           __builtin_amdgcn_sched_barrier(0);
         }
   };
 
-  if (ABL & 32) {
-    // desynchronise the workgroups' block epilogues (their store bursts):
-    // workgroup g starts (g * 7 mod 16) sixteenths of a block late
-    const int q = (int)((blockIdx.x * 7) & 15);
-    for (int i = 0; i < q; ++i) __builtin_amdgcn_s_sleep(60);
-  }
 #pragma unroll
   for (int q = 0; q < NS - 1; ++q) {
     prep_stage();
@@ -408,70 +345,26 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
       // stage j + 1 landed (stages j + 2 .. j + NS - 2 stay in flight, plus an
       // epilogue's stores if one ran after stage j + 1's DMAs were issued) and
       // this wave's reads are back in registers
-      if (!(ABL & 1)) {
-        const bool ep = last_ep >= j - NS + 2;
-        if (SIDE && c < NS - 2) {
-          // warm-up: stage j + 1 came from the prologue, so only the c side
-          // stores issued so far are younger -- count none of them (a wait
-          // for at least stage j + 1)
-          if (ep)
-            wait_vm<(NS - 3) * LW + kE>();
-          else
-            wait_vm<(NS - 3) * LW>();
-        } else if (ep) {
-          wait_vm<YE>();
-        } else {
-          wait_vm<Y0>();
-        }
-      }
+      if (last_ep >= j - NS + 2)
+        wait_vm<YE>();
+      else
+        wait_vm<Y0>();
       __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0) only (vmcnt 63, expcnt 7)
-      if (!(ABL & 2)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       // nobody reads stage j - 1 any more: its slot takes stage j + NS - 1
       issue_prepped((j + NS - 1) % NS);
-      // the side store below must issue after these DMAs (the counted waits
-      // take it as younger than them)
-      if (SIDE) __builtin_amdgcn_sched_barrier(0);
-    }
-    if (SIDE) {
-      // this step's chunk (landed: stage c was retired one step ago):
-      // lanes 0..15 of wave w update elements w * 32 + 2 l, 2 l + 1
-      const double* st = lds + ((c / KC) % NS) * kStage + (c % KC) * kStep + kA + kB;
-      const int el = wave * 32 + 2 * lane;
-      const int64_t q = ((int64_t)blockIdx.x + c_it * G) * KS + c_s;
-      const int64_t e = q * kSC + el;
-      if (lane < 16) {
-        // inline-asm LDS reads: hipcc would otherwise drain every DMA in
-        // flight (vmcnt(0)) before a ds_read it cannot tell apart from them
-        double2 xv, a0, a1;
-        const uint32_t la = (uint32_t)reinterpret_cast<uintptr_t>(st + el);
-        asm volatile(
-            "ds_read_b128 %0, %3\n\t"
-            "ds_read_b128 %1, %3 offset:2048\n\t"
-            "ds_read_b128 %2, %3 offset:4096\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(xv), "=&v"(a0), "=&v"(a1)   // early clobber: la is read after the first load issues
-            : "v"(la)
-            : "memory");
-        double2 o;
-        o.x = xv.x + (sc0 * a0.x + sc1 * a1.x);   // mp_side_job's expression
-        o.y = xv.y + (sc0 * a0.y + sc1 * a1.y);
-        double* dst = e + 1 < slen ? sx_dst + e : g_ring_trash + 2 * lane;
-        if (!(ABL & 8)) gstore2(dst, o);
-      }
     }
     // past the last step this reads a landed slot's stale operands (unused)
     read_step(c + 1, nxt);
-    if (!(ABL & 4)) mma(cur);
-    if (ABL & 128) {   // interleave (the default variant)
-      // interleave: after the u / v adds, one MFMA then up to two other
-      // instructions (LDS reads, DMAs, scalar / vector address work)
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+    mma(cur);
+    // interleave: after the u / v adds, one MFMA then up to two other
+    // instructions (LDS reads, DMAs, scalar / vector address work)
+    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
 #pragma unroll
-      for (int i = 0; i < 2 * FS; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100 | 0x020 | 0x004 | 0x002, 2, 0);
-      }
+    for (int i = 0; i < 2 * FS; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100 | 0x020 | 0x004 | 0x002, 2, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (first) prep_stage();
@@ -493,75 +386,33 @@ __global__ __launch_bounds__(64 * W, MINW) void mode_product_ring_kernel(
   wait_vm<0>();
 }
 
-template <int JS, int TS, int W, int NS, int MINW, int ABL = 0, int KC = 1, bool SIDE = false>
-static RingConfig cfg_ring() {
-  return RingConfig{mode_product_ring_kernel<JS, TS, W, NS, MINW, ABL, KC, SIDE>, W, NS, KC,
-                    (size_t)NS * KC * (8 * 16 * W + 16 * 64 + (SIDE ? 1024 : 0)) *
-                        sizeof(double)};
+// The configuration (A/B in profiles/r04/h_ring_ab.jsonl, 200^4 plain
+// launch interleaved in one process: chunked kernel 6.69-6.83 ms, 8 waves x 9
+// one-k-step stages 6.60-6.68, 4 two-k-step stages 6.45-6.50, the same with
+// the DMAs and LDS reads interleaved between the MFMAs 6.36-6.42): 8 waves,
+// 4 stages of two k-steps, interleaved.  The other shapes of that table (4
+// waves, 5-9 stages, no interleave), the timing-only ablations of
+// profiles/r04/f_ring_ablate.jsonl and the side-job carrier (8.6 vs 8.2 ms
+// per side launch, profiles/r04/j_side_ab.txt) were measured slower and live
+// in the history (round 4).
+static RingConfig ring_config() {
+  constexpr int JS = 7, TS = 1, W = 8, NS = 4, MINW = 2, KC = 2;
+  return RingConfig{mode_product_ring_kernel<JS, TS, W, NS, MINW, KC>, W, NS, KC,
+                    (size_t)NS * KC * (8 * 16 * W + 16 * 64) * sizeof(double)};
 }
-
-// variants (GG_FOLD_RING=<v>; A/B in profiles/r04/, the default 42):
-//   1 = 8 waves, 9 one-k-step stages (144 KiB), 2 = 6 stages, 4 = 7, 5 = 5;
-//   3 = 4 waves, 6 stages (two workgroups per CU); 31 / 32 = 8 waves, 5 / 4
-//   two-k-step stages; 41 / 42 / 43 = 1 / 32 / 31 with the DMAs and LDS reads
-//   interleaved between the MFMAs (sched_group_barrier).  200^4 plain launch,
-//   interleaved in one process: chunked kernel 6.69-6.83 ms, 1: 6.60-6.68,
-//   32: 6.45-6.50, 42: 6.36-6.42 (profiles/r04/h_ring_ab.jsonl).
-//   Diagnostic ablations of 1 (WRONG results, timing only): 11 no vmcnt
-//   wait, 12 no barrier, 13 neither, 14 no MFMA, 15 no epilogue stores, 16 no
-//   DMA (and no wait), 17 no wait / barrier / MFMA, 21 / 25 workgroup start
-//   staggered, 26 = 16 + 21, 27 epilogue arithmetic without its stores, 28 =
-//   27 + 16 (profiles/r04/f_ring_ablate.jsonl).
-static RingConfig ring_variant(int v) {
-  switch (v) {
-    case 1: return cfg_ring<7, 1, 8, 9, 2>();
-    case 2: return cfg_ring<7, 1, 8, 6, 2>();
-    case 3: return cfg_ring<7, 1, 4, 6, 2>();
-    case 4: return cfg_ring<7, 1, 8, 7, 2>();
-    case 5: return cfg_ring<7, 1, 8, 5, 2>();
-    case 11: return cfg_ring<7, 1, 8, 9, 2, 1>();
-    case 12: return cfg_ring<7, 1, 8, 9, 2, 2>();
-    case 13: return cfg_ring<7, 1, 8, 9, 2, 3>();
-    case 14: return cfg_ring<7, 1, 8, 9, 2, 4>();
-    case 15: return cfg_ring<7, 1, 8, 9, 2, 8>();
-    case 16: return cfg_ring<7, 1, 8, 9, 2, 17>();
-    case 17: return cfg_ring<7, 1, 8, 9, 2, 7>();
-    case 21: return cfg_ring<7, 1, 8, 9, 2, 32>();
-    case 25: return cfg_ring<7, 1, 8, 5, 2, 32>();
-    case 26: return cfg_ring<7, 1, 8, 9, 2, 49>();
-    case 27: return cfg_ring<7, 1, 8, 9, 2, 64>();
-    case 28: return cfg_ring<7, 1, 8, 9, 2, 64 + 17>();
-    case 31: return cfg_ring<7, 1, 8, 5, 2, 0, 2>();
-    case 32: return cfg_ring<7, 1, 8, 4, 2, 0, 2>();
-    case 41: return cfg_ring<7, 1, 8, 9, 2, 128>();
-    case 43: return cfg_ring<7, 1, 8, 5, 2, 128, 2>();
-    default: return cfg_ring<7, 1, 8, 4, 2, 128, 2>();   // 42
-  }
-}
-static const int kRingVariants[] = {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16, 17,
-                                    21, 25, 26, 27, 28, 31, 32, 41, 42, 43};
 
 int ring_variant_env() {
-  const char* e = gg::knob("GG_FOLD_RING");   // unset: the default (42); 0: off
-  return e ? atoi(e) : 42;
+  const char* e = gg::knob("GG_FOLD_RING");   // unset / nonzero: the ring; 0: off (A/B)
+  return e ? atoi(e) : 1;
 }
-
-// the side-job variant (launch kind 4 with balanced x_defer): 8 waves, 6
-// one-k-step stages of 24 KiB (A, B, side chunk), interleaved
-RingConfig select_ring_side(int JT, int TT) {
-  GG_REQUIRE(JT == 7 && TT == 1, GG_ERR_VALUE, "no ring kernel for this factor shape");
-  return cfg_ring<7, 1, 8, 6, 2, 128, 1, true>();
-}
-
-int64_t ring_side_capacity(int64_t nblk, int KS) { return nblk * KS * 256; }
 
 bool ring_available(int JT, int TT, int64_t m) {
   return JT == 7 && TT == 1 && m % 8 == 0 && m / 2 == 100;
 }
 
-RingConfig select_ring(int JT, int TT, int variant) {
+RingConfig select_ring(int JT, int TT) {
   GG_REQUIRE(JT == 7 && TT == 1, GG_ERR_VALUE, "no ring kernel for this factor shape");
-  return ring_variant(variant);
+  return ring_config();
 }
 
 int ring_grid(const RingConfig& rc, int cus, int64_t nblk) {
@@ -574,16 +425,9 @@ int ring_grid(const RingConfig& rc, int cus, int64_t nblk) {
 }
 
 void set_ring_lds_limits() {
-  {
-    const RingConfig rc = select_ring_side(7, 1);
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rc.fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)rc.lds));
-  }
-  for (int v : kRingVariants) {
-    const RingConfig rc = ring_variant(v);
-    GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rc.fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)rc.lds));
-  }
+  const RingConfig rc = ring_config();
+  GG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(rc.fn),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)rc.lds));
 }
 
 }  // namespace gg

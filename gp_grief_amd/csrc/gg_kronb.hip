@@ -866,7 +866,8 @@ struct PairArgs {
   int64_t soff, sn, soff_h1, sn_h1, sstep;
   int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
                        // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs;
-                       // 32 the x side job back in the second launch (A/B)
+                       // 32 the x side job back in the second launch (A/B); 64 GEMM 2
+                       // without fragment loads, 128 no side job (timing only)
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -956,7 +957,8 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int s = 0; s < KS; ++s) {
       if (A.abl & 4) break;   // diag: GEMM 2 without its k-loop
       const double f = fr[s % kPF];
-      if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
+      // diag 64: GEMM 2 without its fragment loads (the first kPF reused)
+      if (s + kPF < KS && !(A.abl & 64)) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
 #pragma unroll
       for (int u = 0; u < NJ; ++u)
         Z[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, bfull(s, u), Z[u], 0, 0, 0);
@@ -1447,7 +1449,9 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     else
       pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
                                                       ring, issue, pq, qq);
-    if (SIDE && slen > 0) side_chunk(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
+    // diag 128: the side job skipped (timing only)
+    if (SIDE && slen > 0 && !(A.abl & 128))
+      side_chunk(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
     cslot = (cslot + R::KS) % NS;
     cur = nxt;
   }

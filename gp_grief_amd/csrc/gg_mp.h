@@ -202,13 +202,9 @@ struct RingConfig {
   int waves, ns, kc;   // waves per workgroup, ring stages, k-steps per stage
   size_t lds;          // dynamic LDS bytes
 };
-int ring_variant_env();   // GG_FOLD_RING: 0 = off, else the variant
+int ring_variant_env();   // GG_FOLD_RING: 0 = off (the chunked kernel), else on
 bool ring_available(int JT, int TT, int64_t m);
-RingConfig select_ring(int JT, int TT, int variant);
-// the CG side-job launch (kind 4, balanced x_defer): side slices up to
-// ring_side_capacity(nblk, KS) elements (256 per k-step of every block)
-RingConfig select_ring_side(int JT, int TT);
-int64_t ring_side_capacity(int64_t nblk, int KS);
+RingConfig select_ring(int JT, int TT);
 // persistent grid: resident workgroups per CU x CUs, at most nblk
 int ring_grid(const RingConfig& rc, int cus, int64_t nblk);
 void set_ring_lds_limits();

@@ -703,9 +703,6 @@ struct gg_cg {
   // rank of a sharded CG (gg_cg_*_partial / _finish): an iteration's local
   // sums await the caller's all-reduce (the p_new of that iteration)
   bool await_finish = false;
-  // the x side job's own stream and its two ordering events (MpFuse)
-  hipStream_t side_stream = nullptr;
-  hipEvent_t side_ev[2] = {nullptr, nullptr};
   // live timing of the mode products (gg_cg_profile): d + 1 events per
   // profiled iteration, recorded on the CG stream, read back on demand
   bool profiling = false;
@@ -986,16 +983,6 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       GG_HIP(hipMalloc(&cg->sc, sizeof(gg::CgScalars)));
       GG_HIP(hipHostMalloc(&cg->sc_host, sizeof(gg::CgScalars), hipHostMallocDefault));
       gg::scalars_clear(cg->sc);
-      // the concurrent x side job (GG_CG_SIDE_ASYNC=1, opt-in): at 200^4 the
-      // streaming kernel (50 VGPRs) cannot sit beside a ring workgroup (2 x
-      // 232 of 512 VGPRs per SIMD), so it holds CUs the ring needs: mode
-      // products 1-2 7.7 -> 11.0-11.5 ms, the iteration 38.8 -> 46-47.5 ms
-      // (profiles/r04/w_side_async)
-      const char* sa = gg::knob("GG_CG_SIDE_ASYNC");
-      if (cg->fused && sa && atoi(sa) == 1) {
-        GG_HIP(hipStreamCreateWithFlags(&cg->side_stream, hipStreamNonBlocking));
-        for (hipEvent_t& e : cg->side_ev) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      }
     } catch (...) {
       gg_cg_destroy(cg);
       throw;
@@ -1012,9 +999,6 @@ int gg_cg_destroy(gg_cg* cg) {
     if (cg->sc) (void)hipFree(cg->sc);
     if (cg->sc_host) (void)hipHostFree(cg->sc_host);
     for (hipEvent_t e : cg->events) (void)hipEventDestroy(e);
-    for (hipEvent_t e : cg->side_ev)
-      if (e) (void)hipEventDestroy(e);
-    if (cg->side_stream) (void)hipStreamDestroy(cg->side_stream);
     delete cg;
   });
 }
@@ -1252,11 +1236,6 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         fz.sn = n;
         fz.xdefer = xmode;
         fz.first_dst = cg->first_dst;
-        if (xmode == 2) {
-          fz.side_stream = cg->side_stream;
-          fz.side_ev[0] = cg->side_ev[0];
-          fz.side_ev[1] = cg->side_ev[1];
-        }
         // r.q: conjugacy identity (layout 0: the prologue adds p_new.q_old
         // partials, the epilogue skips its pass over r) or read in the epilogue
         const bool rq_ident = cg->rq != 0 && cg->fusion == 0;
@@ -1440,11 +1419,6 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     fz.sn = n;
     fz.xdefer = xmode;
     fz.first_dst = cg->first_dst;
-    if (xmode == 2) {
-      fz.side_stream = cg->side_stream;
-      fz.side_ev[0] = cg->side_ev[0];
-      fz.side_ev[1] = cg->side_ev[1];
-    }
     const bool rq_ident = cg->rq != 0;
     fz.er = rq_ident ? nullptr : cg->r;
     fz.pqo_stride = rq_ident ? cg->rr_count : 0;
@@ -1688,7 +1662,7 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
     // prologue (CGP 3: the MFMA operand is w itself, written over u_prev)
     // when the chain's first step writes its scratch, not y (an even number
     // of factors); otherwise it is its own streaming pass.
-    const bool fuse = gg::kron_d(K) % 2 == 0 && gg::knob("GG_LANCZOS_UNFUSED") == nullptr;
+    const bool fuse = gg::kron_d(K) % 2 == 0;
     for (int j = 0; j < steps; ++j) {
       int64_t np = 0;
       if (j == 0 || !fuse) {

@@ -92,7 +92,10 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
  * x_{m-1-i}) / sqrt 2) makes the operator block diagonal over the 2^d parity
  * patterns, each block a Kronecker product of h_k x h_k matrices
  * S = F[j][i] + F[j][m-1-i], T = F[j][i] - F[j][m-1-i].  Block layout: block
- * B = sum_k beta_k 2^{d-1-k} (slowest) of prod h_k elements, C order inside.
+ * B = sum_k beta_k 2^{d-1-k} (slowest) of prod h_k elements, C order over the
+ * slab index (i_0 .. i_{d-3}) inside; a slab (the innermost two axes, h x h)
+ * k-step tiled: element (i, a) at (a / 4) 4 h + 4 i + a % 4 (round 5: each
+ * 4-column group contiguous, the unit the pair launch's GEMM 1 contracts).
  * A matvec there is d - 1 launches (the last two axes of a block share one
  * launch): the CG (gg_cg_*) runs in this basis by default when it exists
  * (gg_cg_set_basis), folding b at start and unfolding x at every close.

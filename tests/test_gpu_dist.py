@@ -406,9 +406,10 @@ def test_restart_penalty_single_gpu(gpu, monkeypatch, ms, shift):
 
 
 def test_forced_cancellations_restart_vs_repair(gpu, monkeypatch):
-    """Both branches of a cancelled beta, made frequent: GG_CG_CANCEL_TOL=0.1
-    counts every step whose |r_{j+1}|^2 expansion is below 0.1 rho_j as
-    cancelled.  The single-GPU CG repairs (true r.r, textbook beta), the
+    """Both branches of a cancelled beta, made frequent: GG_CG_CANCEL_TOL=0.3
+    counts every step whose |r_{j+1}|^2 expansion is below 0.3 rho_j as
+    cancelled (24 of the ~1714 steps of this solve have beta < 0.3; none is
+    below the production threshold 1e-6).  The single-GPU CG repairs (true r.r, textbook beta), the
     single-GPU CG with GG_CG_RESTART=1 and a block-sharded solve over two
     virtual ranks restart (p = r).  All three converge to the oracle's x
     (1e-8) with cancellations counted; the iteration counts are the restart
@@ -421,7 +422,7 @@ def test_forced_cancellations_restart_vs_repair(gpu, monkeypatch):
     b = np.random.default_rng(25).standard_normal(int(np.prod(ms)))
     xs, info, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + shift * v, b,
                                    rtol=1e-10)
-    monkeypatch.setenv("GG_CG_CANCEL_TOL", "0.1")
+    monkeypatch.setenv("GG_CG_CANCEL_TOL", "0.3")
     out = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("GG_CG_RESTART", flag)
@@ -445,7 +446,7 @@ def test_forced_cancellations_restart_vs_repair(gpu, monkeypatch):
         return k, solve.last_cancels, gg.device.to_host(x)
 
     out["sharded"] = run_threads(2, body)[0]
-    print("forced cancellations (tol 0.1), oracle %d iterations: %s"
+    print("forced cancellations (tol 0.3), oracle %d iterations: %s"
           % (it, ", ".join("%s %d (%d cancelled)" % (n, v[0], v[1]) for n, v in out.items())))
     for n, (k, c, x) in out.items():
         assert c > 0, n

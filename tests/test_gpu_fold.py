@@ -110,51 +110,6 @@ def test_fold_lean_matches_clamped(gg, monkeypatch, m0):
     assert rel(out["1"][0], oracle.kron_matvec(F, x[:, 0])) < 1e-13
 
 
-def test_fold_nontemporal_variants_bitwise(gg, monkeypatch):
-    """Non-temporal loads / stores in the CG launches (GG_FOLD_PRO_NT,
-    GG_FOLD_EPI_NT, GG_FOLD_SIDE_NT masks) run the same arithmetic: a fused
-    CG at 200^3 agrees bitwise with every mask off."""
-    F = [grid_factor(200, 0.1), grid_factor(200, 0.13), grid_factor(200, 0.2, "Matern52")]
-    x = np.random.default_rng(5).standard_normal((200 ** 3, 1))
-    knobs = ["GG_FOLD_PRO_NT", "GG_FOLD_EPI_NT", "GG_FOLD_SIDE_NT", "GG_FOLD_EPI_PRE"]
-    cases = [{"GG_FOLD_PRO_NT": "0", "GG_FOLD_EPI_NT": "0", "GG_FOLD_SIDE_NT": "0"}] + \
-        [{"GG_FOLD_PRO_NT": v} for v in ("1", "2", "3", "6", "7")] + \
-        [{"GG_FOLD_EPI_NT": v} for v in ("1", "2", "4", "6", "7")] + \
-        [{"GG_FOLD_SIDE_NT": v} for v in ("1", "2", "3")] + [{}, {"GG_FOLD_EPI_PRE": "1"}]
-    out = []
-    for case in cases:
-        for k in knobs:
-            monkeypatch.delenv(k, raising=False)
-        for k, v in case.items():
-            monkeypatch.setenv(k, v)
-        K = kron(gg, F)
-        xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=6, recurrence="fused")
-        out.append(np.asarray(xs))
-    for o in out[1:]:
-        assert np.array_equal(out[0], o)
-
-
-@pytest.mark.parametrize("d", [3, 4])
-def test_cg_side_job_stream_matches_inline(gg, monkeypatch, d):
-    """The x side job as a concurrent kernel on the CG's side stream (opt-in,
-    beside ring mode products) and inside the mode products
-    (GG_CG_SIDE_ASYNC=0): the same iterates (r and p do not depend on x) and x
-    to rounding."""
-    m = 200 if d == 3 else 40
-    F = [grid_factor(m, 0.1 + 0.02 * k) for k in range(d)]
-    x = np.random.default_rng(6).standard_normal((m ** d, 1))
-    out = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("GG_CG_SIDE_ASYNC", flag)   # 1: opt-in stream
-        K = kron(gg, F)
-        for maxiter in (7, 8):
-            xs, info = gg.linalg.cg(K, x, shift=0.05, rtol=0.0, maxiter=maxiter,
-                                    recurrence="fused")
-            out[(flag, maxiter)] = np.asarray(xs)
-    for maxiter in (7, 8):
-        assert rel(out[("1", maxiter)], out[("0", maxiter)]) < 1e-14
-
-
 def test_cg_open_iterations_chain_bitwise(gg):
     """iterate(close=False) calls continue one open fused recurrence: open(5)
     + open(7) + close() is the same launch sequence as iterate(12), bitwise;
@@ -173,26 +128,6 @@ def test_cg_open_iterations_chain_bitwise(gg):
         out.append((cg.x.cpu().numpy().copy(), cg.status()))
     assert np.array_equal(out[0][0], out[1][0])
     assert out[0][1][0] == out[1][1][0] == 12 and out[0][1][2] == out[1][1][2]
-
-
-def test_lanczos_launch_variants(gg, monkeypatch):
-    """The fused Lanczos step's prologue shapes (GG_FOLD_LZ: 4- / 12-wave,
-    non-temporal) and its epilogue's non-temporal streams (GG_FOLD_LZE): the
-    non-temporal variants of one shape give the same tridiagonal bitwise; the
-    two shapes sum |w|^2 over different workgroups, equal to 1e-12."""
-    F = [grid_factor(200, 0.1), grid_factor(16, 0.3), grid_factor(16, 0.25),
-         grid_factor(200, 0.2, "Matern52")]
-    K = kron(gg, F)
-    assert fold_mask(K) & 0b1001 == 0b1001
-    out = {}
-    for lz, lze in (("0", "0"), ("3", "1"), ("1", "0"), ("2", "1")):
-        monkeypatch.setenv("GG_FOLD_LZ", lz)
-        monkeypatch.setenv("GG_FOLD_LZE", lze)
-        a, b = gg.linalg.lanczos_tridiag(K, 0.01, 12, seed=3, probe=1)
-        out[lz] = (np.asarray(a), np.asarray(b))
-    for x, y in (("0", "3"), ("1", "2")):   # the same shape, non-temporal or not
-        assert np.array_equal(out[x][0], out[y][0]) and np.array_equal(out[x][1], out[y][1])
-    assert rel(out["2"][0], out["0"][0]) < 1e-12 and rel(out["2"][1], out["0"][1]) < 1e-12
 
 
 def test_fold_centrosymmetric_nonsymmetric_and_transpose(gg, fold_small):

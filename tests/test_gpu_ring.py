@@ -16,7 +16,7 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["1", "3", "5", "31", "32", "41", "42", "43"]
+VARIANTS = ["1"]   # the ring (one configuration since round 5); "0" is the chunked kernel
 
 
 def rel(a, b):
@@ -113,25 +113,3 @@ def test_ring_lanczos_unchanged(gg, monkeypatch):
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize("dims", [(200, 200, 200, 4), (6, 200, 200, 5)])
-def test_ring_side_job_cg(gg, monkeypatch, dims):
-    """The fused CG's side-job launches (x += c0 p_{j-2} + c1 p_{j-1} riding
-    on mode products 2 and 3) on the ring kernel (default) against the chunked
-    kernel (GG_FOLD_RING_SIDE=0): the same iterate and residual after 9
-    iterations (partial and whole side slices, the x flush at exit)."""
-    import torch
-    F = [grid_factor(m, 0.1 + 0.03 * k) for k, m in enumerate(dims)]
-    n = int(np.prod(dims))
-    b = torch.from_numpy(np.random.default_rng(7).standard_normal(n)).cuda()
-    out = {}
-    for side in ("0", "1"):
-        monkeypatch.setenv("GG_FOLD_RING_SIDE", side)
-        K = gg.tensors.KronMatrix(F, sym=True)
-        cg = gg.linalg.KronCG(K, 0.05)
-        cg.start(b, rtol=0.0)
-        cg.iterate(9)
-        it, _, res, _ = cg.status()
-        out[side] = (it, res, cg.x.cpu().numpy())
-    assert out["0"][0] == out["1"][0] == 9
-    assert abs(out["0"][1] - out["1"][1]) <= 1e-12 * out["0"][1]
-    assert rel(out["1"][2], out["0"][2]) < 1e-13

@@ -37,8 +37,7 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
     print(json.dumps({"grid": a.grid, "dims": a.dims, "n": n, "ms_per_matvec": ms,
-                      "fold_mask": dk.fold_mask(), "reps": a.reps,
-                      "variant": os.environ.get("GG_FOLD_VARIANT", "0")}), flush=True)
+                      "fold_mask": dk.fold_mask(), "reps": a.reps}), flush=True)
 
 
 if __name__ == "__main__":
