@@ -866,8 +866,8 @@ struct PairArgs {
   int64_t soff, sn, soff_h1, sn_h1, sstep;
   int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
                        // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs;
-                       // 32 the x side job back in the second launch (A/B); 64 GEMM 2
-                       // without fragment loads, 128 no side job (timing only)
+                       // 32 the x side job back in the second launch (A/B); 128 no
+                       // side job (timing only)
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -957,8 +957,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int s = 0; s < KS; ++s) {
       if (A.abl & 4) break;   // diag: GEMM 2 without its k-loop
       const double f = fr[s % kPF];
-      // diag 64: GEMM 2 without its fragment loads (the first kPF reused)
-      if (s + kPF < KS && !(A.abl & 64)) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
+      if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
 #pragma unroll
       for (int u = 0; u < NJ; ++u)
         Z[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(f, bfull(s, u), Z[u], 0, 0, 0);
