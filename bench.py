@@ -1186,8 +1186,9 @@ def main():
     block = solver.basis == "block"
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
                                   solver.fusion, fold_mask, solver.xdefer, solver.rq, block)
+    # the block basis has no per-factor fold state (tools/pmc_block.py records 0)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
-                               fold_mask, solver.xdefer, solver.rq, block)
+                               0 if block else fold_mask, solver.xdefer, solver.rq, block)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,

@@ -79,6 +79,11 @@ struct BlockOp {
   bool pair_lds = false;
   int pair_spw = 1;
   bool fast = true;   // blk_mode_fast_kernel where instantiated (GG_BLK_MODE_FAST=0: off)
+  // the CG prologue's r / q_old / p_old loads and r / p_new stores non-temporal
+  // (default; GG_BLK_PRO_NT=0 off): 200^4 prologue 13.84-14.02 -> 13.52-13.58
+  // ms, interleaved processes (profiles/r05/y_pro_nt)
+  bool pro_nt = true;
+  bool epi_nt = false;   // the pair launch's p loads / q stores non-temporal (GG_BLK_EPI_NT, A/B)
 };
 
 // ------------------------------------------------------------------ fold
@@ -217,6 +222,22 @@ __device__ __forceinline__ double ldu(const void* p, int64_t uoff, uint32_t voff
 __device__ __forceinline__ void stu(void* p, int64_t uoff, uint32_t voff, double v) {
   gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
   *reinterpret_cast<gdouble*>(b + voff) = v;
+}
+// the same, non-temporal (streams touched once per iteration)
+template <bool NT>
+__device__ __forceinline__ double lduq(const void* p, int64_t uoff, uint32_t voff) {
+  if constexpr (!NT) return ldu(p, uoff, voff);
+  gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
+  return __builtin_nontemporal_load(reinterpret_cast<const gdouble*>(b + voff));
+}
+template <bool NT>
+__device__ __forceinline__ void stuq(void* p, int64_t uoff, uint32_t voff, double v) {
+  if constexpr (!NT) {
+    stu(p, uoff, voff, v);
+  } else {
+    gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
+    __builtin_nontemporal_store(v, reinterpret_cast<gdouble*>(b + voff));
+  }
 }
 // 16-byte global accesses (per-lane addresses)
 typedef double gd2v __attribute__((ext_vector_type(2)));
@@ -574,13 +595,17 @@ __device__ __attribute__((aligned(16))) double g_blk_trash[6 * 64];
 
 // waves per workgroup of the fast kernel: 12 (3 per SIMD) for the plain
 // launch, 8 (2 per SIMD, 256 registers) for the fused ones
+// (KIND 3: the prologue, KIND 1, with its r / q_old / p_old loads and r /
+// p_new stores non-temporal -- Y, read by the next launch, stays normal)
 template <int KIND>
 constexpr int fast_waves() {
   return KIND == 0 ? 12 : 8;
 }
 
-template <int TF, int KIND>
-__global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kernel(ModeArgs a) {
+template <int TF, int KIND_>
+__global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_kernel(ModeArgs a) {
+  constexpr bool NT = KIND_ == 3;
+  constexpr int KIND = KIND_ == 3 ? 1 : KIND_;
   constexpr int W = fast_waves<KIND>();
   constexpr int JT = TF + 1;
   constexpr int KS = 4 * TF + 1;
@@ -604,6 +629,10 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
   auto stq = [&](bool valid, void* p, int64_t uoff, uint32_t voff, double v) {
     void* bp = valid ? p : static_cast<void*>(g_blk_trash);
     stu(bp, valid ? uoff : 0, valid ? voff : o_t, v);
+  };
+  auto stq_nt = [&](bool valid, void* p, int64_t uoff, uint32_t voff, double v) {
+    void* bp = valid ? p : static_cast<void*>(g_blk_trash);
+    stuq<NT>(bp, valid ? uoff : 0, valid ? voff : o_t, v);
   };
 
   struct Cur {
@@ -705,10 +734,10 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
     auto issue = [&](int slot, int s) {
       // k-step s of the load cursor's strip (s compile-time)
       const int64_t ub = l_base * 8 + (int64_t)s * rstep;
-      ring[slot][0] = ldu(a.X, ub, o_e);
+      ring[slot][0] = lduq<NT>(a.X, ub, o_e);
       if (KIND == 1) {
-        ring[slot][1] = ldu(a.r, ub, o_e);
-        ring[slot][2] = ldu(a.q_old, ub, o_e);
+        ring[slot][1] = lduq<NT>(a.r, ub, o_e);
+        ring[slot][2] = lduq<NT>(a.q_old, ub, o_e);
       }
       if (KIND == 2) {
         bool own;
@@ -760,8 +789,8 @@ __global__ __launch_bounds__(64 * fast_waves<KIND>(), 1) void blk_mode_fast_kern
             if (pqo_on) pqo_acc = pqo;
           }
           // stores unconditional: a spare strip's go to the trash slot
-          stq(cvalid, a.r, ub, o_e, r);
-          stq(cvalid, a.p_out, ub, o_e, xb);
+          stq_nt(cvalid, a.r, ub, o_e, r);
+          stq_nt(cvalid, a.p_out, ub, o_e, xb);
         }
         const double* fs = reinterpret_cast<const double*>(lb + (s * JT) * 512);
 #pragma unroll
@@ -882,7 +911,7 @@ __device__ __forceinline__ double bcast_group(double v) {
 
 // GEMM 2 and the epilogue of one slab (both pair kernels): Z = F2 W from the
 // role's W accumulators, q = Z (+ shift p, the p.q / q.q partials) stored.
-template <int TF, int J0, int NJ, bool TJ, int EPI = -1, int PF = 4>
+template <int TF, int J0, int NJ, bool TJ, int EPI = -1, int PF = 4, bool NT = false>
 __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, const double* f2,
                                            const bd4 (&W)[TF][NJ > 0 ? NJ : 1],
                                            const double (&Wta)[NJ > 0 ? NJ : 1],
@@ -928,7 +957,7 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
       pq = fma(p, q, pq);
       qq = fma(q, q, qq);
     }
-    stu(A.Y, ub, vo, q);
+    stuq<NT>(A.Y, ub, vo, q);
   };
 #pragma unroll 1
   for (int ti = 0; ti < TF; ++ti) {
@@ -943,8 +972,8 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
       for (int u = 0; u < NJ; ++u)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          pv[u][r] = ldu(A.P, zb(16 * ti + 4 * r, 16 * (J0 + u)), o_z);
-      if (TJ) pvt = ldu(A.P, zb(16 * ti, 16 * TF), o_zt);
+          pv[u][r] = lduq<NT>(A.P, zb(16 * ti + 4 * r, 16 * (J0 + u)), o_z);
+      if (TJ) pvt = lduq<NT>(A.P, zb(16 * ti, 16 * TF), o_zt);
     }
     const int64_t fti = (int64_t)ti * 512;
     // A fragments kPF k-steps ahead; the scheduling barriers keep each step's
@@ -998,12 +1027,12 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
       const int64_t ub = zb(16 * TF, 16 * (J0 + u));
-      put(ub, o_z, Z4[u], epi ? ldu(A.P, ub, o_z) : 0.0);
+      put(ub, o_z, Z4[u], epi ? lduq<NT>(A.P, ub, o_z) : 0.0);
     }
     if (TJ && b4 == 0) {
       // lane 16 r + c (b = 0): row 16 TF + r, column 16 TF + c
       const int64_t ub = zb(16 * TF, 16 * TF);
-      put(ub, o_zt, Z4t, epi ? ldu(A.P, ub, o_zt) : 0.0);
+      put(ub, o_zt, Z4t, epi ? lduq<NT>(A.P, ub, o_zt) : 0.0);
     }
   }
 }
@@ -1227,7 +1256,7 @@ struct PairSlabSrc {
   const double* f3;
 };
 
-template <int TF, int SPW, int EPI, int J0, int NJ, bool TJ, typename Issue>
+template <int TF, int SPW, int EPI, int J0, int NJ, bool TJ, bool NT, typename Issue>
 __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, int sl, int cslot,
                                               bool early, PairSlabSrc cur, PairSlabSrc nxt,
                                               bool nxt_valid, const double* ring, Issue&& issue,
@@ -1310,7 +1339,7 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
     }
     slot = slot + 1 == NS ? 0 : slot + 1;
   }
-  pair_gemm2<TF, J0, NJ, TJ, EPI>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
+  pair_gemm2<TF, J0, NJ, TJ, EPI, 4, NT>(A, sbyte, f2, W, Wta, Wj, Wc, pq, qq);
 }
 
 // SPW slabs per workgroup (2 waves each; SPW = 2: slabs 2 u, 2 u + 1 of one
@@ -1443,10 +1472,10 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     const PairSlabSrc nxt = nv ? src_at(it + 1) : cur;
     const int role = (wave + it) & 1;   // roles alternate per unit
     if (role == 0)
-      pair_slab_lds<TF, SPW, EPI, 0, JA, true>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
+      pair_slab_lds<TF, SPW, EPI, 0, JA, true, SIDE == 2>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
                                                issue, pq, qq);
     else
-      pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
+      pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false, SIDE == 2>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
                                                       ring, issue, pq, qq);
     // diag 128: the side job skipped (timing only)
     if (SIDE && slen > 0 && !(A.abl & 128))
@@ -1520,11 +1549,16 @@ static blk_mode_fn mode_fast_fn(int JT) {
 // h = 16 (JT - 1) + 4 exactly (KS = 4 JT - 3)
 static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast = false) {
   if (T4 && h == 16 * (JT - 1) + 4 && fast) {
-    const blk_mode_fn f = kind == 1 ? mode_fast_fn<1>(JT)
-                                    : kind == 2 ? mode_fast_fn<2>(JT) : mode_fast_fn<0>(JT);
+    const blk_mode_fn f = kind == 3   ? mode_fast_fn<3>(JT)
+                          : kind == 1 ? mode_fast_fn<1>(JT)
+                          : kind == 2 ? mode_fast_fn<2>(JT)
+                                      : mode_fast_fn<0>(JT);
     if (f != nullptr) return f;
   }
-  return kind == 1 ? mode_fn<1>(JT, T4) : kind == 2 ? mode_fn<2>(JT, T4) : mode_fn<0>(JT, T4);
+  // kind 3 (the non-temporal prologue) exists on the fast kernel only
+  return (kind == 1 || kind == 3) ? mode_fn<1>(JT, T4)
+         : kind == 2              ? mode_fn<2>(JT, T4)
+                                  : mode_fn<0>(JT, T4);
 }
 
 // pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
@@ -1542,11 +1576,12 @@ static blk_pair_fn select_pair_lds(int TF, int spw) {
 }
 
 // epi: the fused CG's epilogue; side: its x side job rides in the launch
-// (LDS kernel only; the CG epilogue always comes with it there)
+// (LDS kernel only; the CG epilogue always comes with it there); nt: that
+// launch's p loads and q stores non-temporal (SIDE = 2)
 static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false,
-                               bool side = false) {
+                               bool side = false, bool nt = false) {
   if (lds) {
-    if (side) return select_pair_lds<1, 1>(TF, spw);
+    if (side) return nt ? select_pair_lds<1, 2>(TF, spw) : select_pair_lds<1, 1>(TF, spw);
     return epi ? select_pair_lds<1, 0>(TF, spw) : select_pair_lds<0, 0>(TF, spw);
   }
   switch (TF) {
@@ -1571,7 +1606,7 @@ static int blk_cus() {
 static void blk_set_lds_limits(const BlockOp* B) {
   for (int k = 0; k + 2 < B->d; ++k) {
     const size_t bytes = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
-    for (int kind = 0; kind < 3; ++kind)
+    for (int kind = 0; kind < 4; ++kind)
       GG_HIP(hipFuncSetAttribute(
           reinterpret_cast<const void*>(
               select_mode(kind, B->JT[k], B->T4[k], (int)B->h[k], B->fast)),
@@ -1618,6 +1653,10 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     B->cus = blk_cus();
     const char* fe = gg::knob("GG_BLK_MODE_FAST");   // A/B knob, read at creation only
     B->fast = !(fe && atoi(fe) == 0);
+    const char* ne = gg::knob("GG_BLK_PRO_NT");      // A/B knob, read at creation only
+    B->pro_nt = !(ne && atoi(ne) == 0);
+    const char* ee = gg::knob("GG_BLK_EPI_NT");      // A/B knob, read at creation only
+    B->epi_nt = ee && atoi(ee) == 1;
     const char* pe = gg::knob("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
     B->pair_abl = pe ? atoi(pe) : 0;
     const char* le = gg::knob("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
@@ -1744,10 +1783,12 @@ void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, doub
 static int mode_waves(int kind, const BlockOp* B, int k) {
   const int JT = B->JT[k];
   const bool fast = B->T4[k] && B->h[k] == 16 * (JT - 1) + 4 && B->fast &&
-                    (kind == 1 ? mode_fast_fn<1>(JT) : kind == 2 ? mode_fast_fn<2>(JT)
-                                                                : mode_fast_fn<0>(JT)) != nullptr;
+                    (kind == 3   ? mode_fast_fn<3>(JT)
+                     : kind == 1 ? mode_fast_fn<1>(JT)
+                     : kind == 2 ? mode_fast_fn<2>(JT)
+                                 : mode_fast_fn<0>(JT)) != nullptr;
   if (!fast) return kBlkModeWaves;
-  return kind == 0 ? fast_waves<0>() : kind == 1 ? fast_waves<1>() : fast_waves<2>();
+  return kind == 0 ? fast_waves<0>() : kind == 2 ? fast_waves<2>() : fast_waves<1>();
 }
 
 static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* grid_out,
@@ -1838,7 +1879,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     int grid = 0;
     int kind = 0;
     if (cgp == 2 && k == 0)
-      kind = 1;
+      kind = B->pro_nt ? 3 : 1;
     else if (k == 1 && side && !pair_side)
       kind = 2;
     const int W = mode_waves(kind, B, k);
@@ -1847,7 +1888,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     a.X = src;
     a.Y = chain;
     a.skip = skip;
-    if (kind == 1) {
+    if (kind == 1 || kind == 3) {
       a.r = cg->r;
       a.q_old = cg->q_old;
       a.p_out = cg->p_out;
@@ -1917,7 +1958,8 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     const int64_t slots = p.nslab / B->pair_spw * 2 * B->pair_spw;
     p.sstep = 2 * ceil_div(std::max<int64_t>(std::max(p.sn, p.sn_h1), 1), 2 * slots);
   }
-  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr, pair_side),
+  hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr, pair_side,
+                                 B->epi_nt),
                      dim3(grid), dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0,
                      stream, p);
   GG_LAUNCH_CHECK();

@@ -176,6 +176,27 @@ def test_block_pair_lds_kernel_matches_register_kernel(gg, monkeypatch, ms):
     assert out[0][2][0] == 7
 
 
+@pytest.mark.parametrize("ms", [(40, 40, 40, 40), (8, 200, 200)])
+def test_block_prologue_nontemporal_bitwise(gg, monkeypatch, ms):
+    """The CG prologue with non-temporal streams (GG_BLK_PRO_NT, fast kernel
+    KIND 3, the default) and the pair launch's non-temporal p loads / q stores
+    (GG_BLK_EPI_NT) run the same arithmetic: a fused CG agrees bitwise."""
+    F = factors(ms)
+    x = np.random.default_rng(10).standard_normal(int(np.prod(ms)))
+    out = []
+    for pro, epi in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("GG_BLK_PRO_NT", pro)
+        monkeypatch.setenv("GG_BLK_EPI_NT", epi)
+        K = gg.tensors.KronMatrix(F, sym=True)
+        s = gg.linalg.KronCG(K, 0.03)
+        s.start(dev(gg, x), rtol=1e-14)
+        s.iterate(8)
+        out.append((host(gg, s.x), s.status()))
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0])
+        assert out[0][1] == o[1]
+
+
 def test_block_matvec_repeatable(gg):
     """Bitwise repeatable (no atomics; fixed slab / strip assignment)."""
     ms = (12, 72, 72)
