@@ -83,7 +83,11 @@ struct BlockOp {
   // (default; GG_BLK_PRO_NT=0 off): 200^4 prologue 13.84-14.02 -> 13.52-13.58
   // ms, interleaved processes (profiles/r05/y_pro_nt)
   bool pro_nt = true;
-  bool epi_nt = false;   // the pair launch's p loads / q stores non-temporal (GG_BLK_EPI_NT, A/B)
+  // the fused CG pair launch's p loads and q stores non-temporal (default;
+  // GG_BLK_EPI_NT=0 off): iteration 35.87-36.00 -> 35.41-35.54 ms on one box,
+  // interleaved (the pair launch -0.2 ms, the next prologue -0.25;
+  // profiles/r05/z_epi_nt)
+  bool epi_nt = true;
 };
 
 // ------------------------------------------------------------------ fold
@@ -223,7 +227,7 @@ __device__ __forceinline__ void stu(void* p, int64_t uoff, uint32_t voff, double
   gchar* b = reinterpret_cast<gchar*>(reinterpret_cast<uintptr_t>(ubase(p, uoff)));
   *reinterpret_cast<gdouble*>(b + voff) = v;
 }
-// the same, non-temporal (streams touched once per iteration)
+// the same, non-temporal when NT (CG streams touched once per iteration)
 template <bool NT>
 __device__ __forceinline__ double lduq(const void* p, int64_t uoff, uint32_t voff) {
   if constexpr (!NT) return ldu(p, uoff, voff);
@@ -1408,6 +1412,8 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     for (int j = 0; j < R::DPW; ++j) {
       const int i = wave * R::DPW + j;   // wave-uniform
       const char* src = i < SPW * R::XI ? xb : fbs;
+      // (non-temporal X DMAs: no gain with tiled slabs, +1.5 ms with
+      // row-major ones -- profiles/r05/z_epi_nt, r_nt)
       __builtin_amdgcn_global_load_lds(
           reinterpret_cast<const __attribute__((address_space(1))) void*>(
               reinterpret_cast<uintptr_t>(src + dlane[j])),
@@ -1420,7 +1426,7 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
   const double* sp1 = nullptr;
   double* sxo = nullptr;
   int64_t slen = 0;
-  if (SIDE) {
+  if (SIDE & 1) {
     const int xh = A.sc->xh;
     if (xh < 2 && !A.sc->done) {
       const int64_t off = xh ? A.soff_h1 : A.soff;
@@ -1472,13 +1478,13 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     const PairSlabSrc nxt = nv ? src_at(it + 1) : cur;
     const int role = (wave + it) & 1;   // roles alternate per unit
     if (role == 0)
-      pair_slab_lds<TF, SPW, EPI, 0, JA, true, SIDE == 2>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
+      pair_slab_lds<TF, SPW, EPI, 0, JA, true, (SIDE & 2) != 0>(A, slab, sl, cslot, it == 0, cur, nxt, nv, ring,
                                                issue, pq, qq);
     else
-      pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false, SIDE == 2>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
+      pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false, (SIDE & 2) != 0>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
                                                       ring, issue, pq, qq);
     // diag 128: the side job skipped (timing only)
-    if (SIDE && slen > 0 && !(A.abl & 128))
+    if ((SIDE & 1) && slen > 0 && !(A.abl & 128))
       side_chunk(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
     cslot = (cslot + R::KS) % NS;
     cur = nxt;
@@ -1577,11 +1583,11 @@ static blk_pair_fn select_pair_lds(int TF, int spw) {
 
 // epi: the fused CG's epilogue; side: its x side job rides in the launch
 // (LDS kernel only; the CG epilogue always comes with it there); nt: that
-// launch's p loads and q stores non-temporal (SIDE = 2)
+// launch's p loads and q stores non-temporal (SIDE bit 2)
 static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false,
                                bool side = false, bool nt = false) {
   if (lds) {
-    if (side) return nt ? select_pair_lds<1, 2>(TF, spw) : select_pair_lds<1, 1>(TF, spw);
+    if (side) return nt ? select_pair_lds<1, 3>(TF, spw) : select_pair_lds<1, 1>(TF, spw);
     return epi ? select_pair_lds<1, 0>(TF, spw) : select_pair_lds<0, 0>(TF, spw);
   }
   switch (TF) {
@@ -1656,7 +1662,7 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     const char* ne = gg::knob("GG_BLK_PRO_NT");      // A/B knob, read at creation only
     B->pro_nt = !(ne && atoi(ne) == 0);
     const char* ee = gg::knob("GG_BLK_EPI_NT");      // A/B knob, read at creation only
-    B->epi_nt = ee && atoi(ee) == 1;
+    B->epi_nt = !(ee && atoi(ee) == 0);
     const char* pe = gg::knob("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
     B->pair_abl = pe ? atoi(pe) : 0;
     const char* le = gg::knob("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
@@ -1874,6 +1880,9 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   // streaming kernel after the first when d = 3)
   const bool side = cgp == 2 && cg->sx != nullptr && cg->xdefer == 2;
   const bool pair_side = side && B->pair_lds && !(B->pair_abl & 32);
+  // (a share of each x half on a concurrent stream beside the plain launch
+  // measured slower: 20 % of it made the plain launch +0.76 ms and the pair
+  // launch -0.55 ms, profiles/r05/za_conc)
   for (int k = 0; k + 2 < d; ++k) {
     ModeArgs a{};
     int grid = 0;

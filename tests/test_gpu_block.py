@@ -179,12 +179,13 @@ def test_block_pair_lds_kernel_matches_register_kernel(gg, monkeypatch, ms):
 @pytest.mark.parametrize("ms", [(40, 40, 40, 40), (8, 200, 200)])
 def test_block_prologue_nontemporal_bitwise(gg, monkeypatch, ms):
     """The CG prologue with non-temporal streams (GG_BLK_PRO_NT, fast kernel
-    KIND 3, the default) and the pair launch's non-temporal p loads / q stores
-    (GG_BLK_EPI_NT) run the same arithmetic: a fused CG agrees bitwise."""
+    KIND 3) and the pair launch's non-temporal p loads / q stores
+    (GG_BLK_EPI_NT), both the default, run the same arithmetic: a fused CG
+    agrees bitwise with either off."""
     F = factors(ms)
     x = np.random.default_rng(10).standard_normal(int(np.prod(ms)))
     out = []
-    for pro, epi in (("0", "0"), ("1", "0"), ("1", "1")):
+    for pro, epi in (("0", "0"), ("1", "0"), ("1", "1"), ("0", "1")):
         monkeypatch.setenv("GG_BLK_PRO_NT", pro)
         monkeypatch.setenv("GG_BLK_EPI_NT", epi)
         K = gg.tensors.KronMatrix(F, sym=True)
