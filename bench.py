@@ -856,7 +856,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
     per = {pp["position"]: pp["traffic_bytes"] for pp in rec.get("per_position", [])}
     if not all(i in per for i in positions):
         return None, "PMC passes miss a launch position"
-    return float(np.mean([per[i] for i in positions])), PMC_JSON
+    return float(np.mean([per[i] for i in positions])), PMC_JSON_BLOCK if block else PMC_JSON
 
 
 # ---------------------------------------------------------------- CPU leg
