@@ -969,7 +969,9 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     double Zt = 0.0;
 #pragma unroll
     for (int u = 0; u < NJ; ++u) Z[u] = bd4{0.0, 0.0, 0.0, 0.0};
-    // epilogue operands issued now, consumed after the k-loop
+    // epilogue operands issued now, consumed after the k-loop (issuing them
+    // behind the first kPF fragments, so the first k-steps' waits do not
+    // cover them, measured slower: +0.3 ms per pair launch, profiles/r05/zc_pv_order)
     double pv[NJ > 0 ? NJ : 1][4], pvt = 0.0;
     if (epi) {
 #pragma unroll
@@ -1049,14 +1051,13 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   constexpr int NJB = NJ + (TJ ? 1 : 0);   // B fragments per k-step
   constexpr int64_t FS = (int64_t)(TF + 1) * 64 * 8;   // bytes per fragment k-step
   const int lane = threadIdx.x & 63;
-  const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3, b4 = (lane >> 2) & 3;
-  // lane byte offsets (opaque: recomputed per slab, never hoisted as a set)
+  const int n16 = lane & 15, kq = lane >> 4, l3 = lane & 3;
+  // lane byte offsets (opaque: recomputed per slab, never hoisted as a set;
+  // GEMM 2's own in pair_gemm2)
   uint32_t o_x = (uint32_t)((n16 * 4 + kq) * 8);        // X rows 16 t + n16, column 4 s + kq
   uint32_t o_xt = (uint32_t)((l3 * 4 + kq) * 8);        // X tail rows 16 TF + l3
   uint32_t o_f = (uint32_t)(lane * 8);                  // fragments
-  uint32_t o_z = (uint32_t)((kq * H + n16) * 8);        // Z rows 4 r + kq, column n16
-  uint32_t o_zt = (uint32_t)(((4 * b4 + kq) * H + l3) * 8);   // Z tail columns
-  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f), "+v"(o_z), "+v"(o_zt));
+  asm volatile("" : "+v"(o_x), "+v"(o_xt), "+v"(o_f));
   const int64_t blk = slab / A.spb + A.blk0;
   const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
   const double* f3 = par3 ? A.f3T : A.f3S;
