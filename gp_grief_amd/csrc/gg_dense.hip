@@ -278,140 +278,6 @@ __device__ __forceinline__ void gemm_tn_glds_tile(
       }
 }
 
-// 128 x 256 tile variant (4 waves of 64 x 128, one workgroup per CU): half
-// the B-fragment reads per MFMA of the 128 x 128 tile.  Its 4 x 8 x 4 f64
-// accumulators fill the 256 AGPRs, which hipcc does not keep there across the
-// stage loop when they come from the MFMA builtin (it round-trips them through
-// VGPRs every stage): here every definition and use is an inline-asm MFMA
-// with an "a" operand.  Hazards the asm must carry itself (the compiler pads
-// none inside a statement): s_nop 1 before each MFMA (a VALU-written operand,
-// only the zero init has one) and >= 18 wait states between the last MFMA and
-// the first accumulator read (s_nop ahead of the epilogue); the accumulate
-// chain (D -> the next MFMA's C, 32 MFMAs apart) needs none.  Fragments of
-// k-step s + 1 are read into the second register set before k-step s's MFMAs.
-__device__ __forceinline__ void mfma_f64_acc(d4& acc, double a, double b) {
-  asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-
-template <int kBKg, int kNSg>
-__global__ __launch_bounds__(kGemmThreads, 1) void gemm_tn_wide_kernel(
-    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
-    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
-    int kchunk, double* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) double gl[];
-  constexpr int kJT = 8;                         // 16-column accumulator tiles per wave
-  constexpr int kLdB = 256 + kPad;               // B k-row stride in LDS (doubles)
-  constexpr int kStageD = kBKg * (kLdT + kLdB);  // doubles per stage (A then B)
-  constexpr int kPerWave = kBKg / 4;             // k-rows of A (and of B) per wave
-  constexpr int kInstr = 3 * kPerWave;           // DMA instructions per wave per stage
-  constexpr int kSteps = kBKg / 4;
-  static_assert(kBKg % 4 == 0 && kGemmThreads == 256, "four waves share a stage's k-rows");
-  const int m0 = blockIdx.y * kBM, n0 = blockIdx.x * 256, kz = blockIdx.z;
-  if (uplo == 1 && n0 > m0 + kBM - 1) return;
-  if (uplo == 2 && m0 > n0 + 255) return;
-  const int kbeg = kz * kchunk;
-  const int kend = min(K, kbeg + kchunk);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 128;
-  const int nst = (kend - kbeg + kBKg - 1) / kBKg;
-  const int acol = min(m0 + 2 * lane, M - 2);
-  const int bcol0 = min(n0 + 2 * lane, N - 2), bcol1 = min(n0 + 128 + 2 * lane, N - 2);
-
-  auto issue = [&](int g) {
-    double* st = gl + (g % kNSg) * kStageD;
-    const int k0 = kbeg + g * kBKg;
-#pragma unroll
-    for (int j = 0; j < kPerWave; ++j) {
-      const int r = wave * kPerWave + j;
-      const int k = min(k0 + r, kend - 1);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(A + (int64_t)k * lda + acol),
-          (__attribute__((address_space(3))) void*)(st + r * kLdT), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(B + (int64_t)k * ldb + bcol0),
-          (__attribute__((address_space(3))) void*)(st + kBKg * kLdT + r * kLdB), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(B + (int64_t)k * ldb + bcol1),
-          (__attribute__((address_space(3))) void*)(st + kBKg * kLdT + r * kLdB + 128), 16, 0,
-          0);
-    }
-  };
-
-  d4 acc[4][kJT];
-  const double zero = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < kJT; ++j)
-      asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(zero));
-
-#pragma unroll
-  for (int g = 0; g < kNSg - 1; ++g)
-    if (g < nst) issue(g);
-  for (int g = 0; g < nst; ++g) {
-    const int younger = min(kNSg - 2, nst - 1 - g);
-    if (younger >= 2)
-      __builtin_amdgcn_s_waitcnt(((2 * kInstr) & 15) | ((((2 * kInstr) >> 4) & 3) << 14) |
-                                 (7 << 4) | (15 << 8));
-    else if (younger == 1)
-      __builtin_amdgcn_s_waitcnt((kInstr & 15) | (((kInstr >> 4) & 3) << 14) | (7 << 4) |
-                                 (15 << 8));
-    else
-      __builtin_amdgcn_s_waitcnt((7 << 4) | (15 << 8));
-    __builtin_amdgcn_s_barrier();
-    if (g + kNSg - 1 < nst) issue(g + kNSg - 1);
-    const double* a_s = gl + (g % kNSg) * kStageD;
-    const double* b_s = a_s + kBKg * kLdT;
-    const int krem = kend - (kbeg + g * kBKg);
-    const bool full = krem >= kBKg;
-    double af[2][4], bf[2][kJT];
-    auto frag = [&](int s_, double (&a)[4], double (&b)[kJT]) {
-      const int kk = 4 * s_ + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        a[i] = a_s[kk * kLdT + (lane & 15) + wm + 16 * i];
-        if (!full && kk >= krem) a[i] = 0.0;
-      }
-#pragma unroll
-      for (int j = 0; j < kJT; ++j) b[j] = b_s[kk * kLdB + (lane & 15) + wn + 16 * j];
-    };
-    frag(0, af[0], bf[0]);
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-      if (s + 1 < kSteps) frag(s + 1, af[(s + 1) & 1], bf[(s + 1) & 1]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < kJT; ++j) mfma_f64_acc(acc[i][j], af[s & 1][i], bf[s & 1][j]);
-    }
-  }
-  // the last MFMA's D -> the accumulator reads below
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < kJT; ++j) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+a"(acc[i][j]));
-  double* P = partial ? partial + (int64_t)kz * M * N : nullptr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < kJT; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm + 16 * i + (lane >> 4) + 4 * r;
-        const int col = n0 + wn + 16 * j + (lane & 15);
-        if (row >= M || col >= N) continue;
-        if (uplo == 1 && col > row) continue;
-        if (uplo == 2 && row > col) continue;
-        const double v = acc[i][j][r];
-        if (P) {
-          P[(int64_t)row * N + col] = v;
-        } else {
-          double* c = C + (int64_t)row * ldc + col;
-          *c = (beta == 0.0) ? alpha * v : fma(alpha, v, beta * *c);
-        }
-      }
-}
-
 template <int kBKg, int kNSg, int kMinWg>
 __global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_kernel(
     int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
@@ -466,33 +332,6 @@ static void launch_tn_xcd(dim3 grid, hipStream_t s, int M, int N, int K, double 
                      uplo, kchunk, part, gn, gm, S);
 }
 
-// Persistent, XCD-grouped variant: the grid is the resident slot count (a
-// multiple of 8); workgroup g works on XCD g % 8 (round-robin dispatch), and
-// in round r the XCD's slots take the contiguous range [r G + x S, r G +
-// (x + 1) S) of a host-built tile order (compact supertiles of the valid
-// tiles).  All slots run the same k-loop length, so the workgroups resident
-// on an XCD stream the few A / B panels of their supertile in near lockstep
-// and share them in that XCD's L2 (the launch-order grid streams ~one panel
-// per workgroup: 13 % L2 hits on the C5 Gram).
-template <int kBKg, int kNSg, int kMinWg>
-__global__ __launch_bounds__(kGemmThreads, kMinWg) void gemm_tn_glds_pers_kernel(
-    int M, int N, int K, double alpha, const double* __restrict__ A, int64_t lda,
-    const double* __restrict__ B, int64_t ldb, double beta, double* C, int64_t ldc, int uplo,
-    int kchunk, double* __restrict__ partial, const int* __restrict__ tiles, int ntiles) {
-  extern __shared__ __attribute__((aligned(16))) double gl[];
-  const int G = gridDim.x, S = G / 8;
-  const int g = blockIdx.x, x = g & 7, slot = g >> 3;
-  for (int base = 0; base < ntiles; base += G) {
-    const int t = base + x * S + slot;
-    if (t < ntiles) {
-      const int mb = tiles[2 * t], nb = tiles[2 * t + 1];
-      gemm_tn_glds_tile<kBKg, kNSg>(M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo,
-                                    kchunk, partial, mb * kBM, nb * kBN, blockIdx.z, gl);
-    }
-    __syncthreads();   // LDS stages are reused by the next tile
-  }
-}
-
 template <int kBKg, int kNSg>
 constexpr size_t tn_glds_lds() {
   return (size_t)kNSg * 2 * kBKg * kLdT * sizeof(double);
@@ -532,92 +371,15 @@ static void launch_tn(dim3 grid, hipStream_t s, int M, int N, int K, double alph
                      K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
 }
 
-// Tile order for gemm_tn_glds_pers_kernel (device int pairs (mb, nb)):
-// supertiles of 8 m-blocks x 12 n-blocks, row-major, the valid tiles of each
-// row-major inside it.  Built once per (device, grid shape, uplo) and kept.
-static const int* tn_tile_order(int gm, int gn, int uplo, int* ntiles, hipStream_t s) {
-  static std::mutex mu;
-  static std::map<std::tuple<int, int, int, int>, std::pair<int*, int>> cache;
-  int dev = 0;
-  GG_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_tuple(dev, gm, gn, uplo);
-  auto it = cache.find(key);
-  if (it != cache.end()) {
-    *ntiles = it->second.second;
-    return it->second.first;
-  }
-  constexpr int SM = 8, SN = 12;
-  std::vector<int> order;
-  for (int sm = 0; sm < gm; sm += SM)
-    for (int sn = 0; sn < gn; sn += SN)
-      for (int mb = sm; mb < std::min(gm, sm + SM); ++mb)
-        for (int nb = sn; nb < std::min(gn, sn + SN); ++nb) {
-          const int m0 = mb * kBM, n0 = nb * kBN;
-          if (uplo == 1 && n0 > m0 + kBM - 1) continue;
-          if (uplo == 2 && m0 > n0 + kBN - 1) continue;
-          order.push_back(mb);
-          order.push_back(nb);
-        }
-  int* d = nullptr;
-  GG_HIP(hipMalloc(&d, std::max<size_t>(order.size(), 2) * sizeof(int)));
-  GG_HIP(hipMemcpyAsync(d, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice, s));
-  GG_HIP(hipStreamSynchronize(s));
-  const int nt = (int)(order.size() / 2);
-  cache[key] = {d, nt};
-  *ntiles = nt;
-  return d;
-}
-
-template <int BK, int NS, int MW>
-static void launch_tn_pers(dim3 grid, hipStream_t s, int M, int N, int K, double alpha,
-                           const double* A, int64_t lda, const double* B, int64_t ldb,
-                           double beta, double* C, int64_t ldc, int uplo, int kchunk,
-                           double* part) {
-  static bool attr = false;
-  const void* fn = reinterpret_cast<const void*>(&gemm_tn_glds_pers_kernel<BK, NS, MW>);
-  if (!attr) {
-    GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)tn_glds_lds<BK, NS>()));
-    attr = true;
-  }
-  int ntiles = 0;
-  const int* tiles = tn_tile_order((int)grid.y, (int)grid.x, uplo, &ntiles, s);
-  int cus = 0, dev = 0;
-  GG_HIP(hipGetDevice(&dev));
-  GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  int G = std::min(ntiles, cus * MW);
-  G = std::max(8, G - G % 8);
-  const size_t lds = tn_glds_lds<BK, NS>();
-  hipLaunchKernelGGL((gemm_tn_glds_pers_kernel<BK, NS, MW>), dim3(G, 1, grid.z),
-                     dim3(kGemmThreads), lds, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
-                     uplo, kchunk, part, tiles, ntiles);
-}
-
-template <int BK, int NS>
-static void launch_tn_wide(dim3 grid, hipStream_t s, int M, int N, int K, double alpha,
-                           const double* A, int64_t lda, const double* B, int64_t ldb,
-                           double beta, double* C, int64_t ldc, int uplo, int kchunk,
-                           double* part) {
-  static bool attr = false;
-  const void* fn = reinterpret_cast<const void*>(&gemm_tn_wide_kernel<BK, NS>);
-  constexpr size_t lds = (size_t)NS * BK * (kLdT + 256 + kPad) * sizeof(double);
-  if (!attr) {
-    GG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    attr = true;
-  }
-  const dim3 g2((unsigned)ceil_div(N, 256), grid.y, grid.z);
-  hipLaunchKernelGGL((gemm_tn_wide_kernel<BK, NS>), g2, dim3(kGemmThreads), lds, s, M, N, K,
-                     alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
-}
-
-// TN-GEMM variant (A/B knob, read per call): GG_GEMM_TN=0 register-staged
-// gemm_kernel, 1..5 the LDS-DMA kernel's stage shapes, 14 the same tile with
-// the XCD-slab split-K grid.  Default 14 (BK 8, 2 stages, 3 waves/SIMD, each
-// K-slab's tiles on one XCD): n = 1e5, p = 1000 3.37 -> 2.60 ms (29.7 -> 38.5
-// TF), p = 5000 47.0 -> 43.8 ms against 3 (the same tile, launch-order grid;
-// profiles/r03/n/gram_xcd_ab.jsonl); 3 was 53.0 TF on the C5 Gram against
-// 46.9 TF for the register-staged kernel (profiles/r02_g_gram_tn_variants.jsonl)
+// TN-GEMM variant (A/B knob, from the handle-free snapshot): GG_GEMM_TN=0 the
+// register-staged gemm_kernel, else the LDS-DMA kernel with the XCD-slab
+// split-K grid (BK 8, 2 stages, 3 waves/SIMD, each K-slab's tiles on one
+// XCD): n = 1e5, p = 1000 3.37 -> 2.60 ms (29.7 -> 38.5 TF), p = 5000 47.0 ->
+// 43.8 ms against the same tile on the launch-order grid
+// (profiles/r03/n/gram_xcd_ab.jsonl; 53.0 against 46.9 TF for the
+// register-staged kernel on the C5 Gram, profiles/r02_g_gram_tn_variants.jsonl).
+// The other stage shapes, the persistent supertile grid and the 128 x 256
+// AGPR tile of those A/Bs measured slower and live in the history (round 4).
 static int gemm_tn_variant() {
   const char* e = gg::knob("GG_GEMM_TN");
   return e ? atoi(e) : 14;
@@ -684,30 +446,14 @@ void gemm(bool ta, bool tb, int M, int N, int K, double alpha, const double* A, 
   double* part = (S > 1) ? splitk_buf : nullptr;
   // TN with even shapes and 16-byte aligned operands: the LDS-DMA kernel
   // (GG_GEMM_TN selects its stage shape for A/B; 0 = the register-staged one)
-  const int tnv = gemm_tn_variant();
   if (tri == 0 && tn_dma_shape(ta, tb, M, N) &&
       (lda % 2) == 0 && (ldb % 2) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0) &&
       ((reinterpret_cast<uintptr_t>(B) & 15) == 0)) {
-    switch (tnv) {
-      case 1: launch_tn<16, 2, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 2: launch_tn<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 3: launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 4: launch_tn<16, 3, 1>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 6: launch_tn_pers<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 8: launch_tn<4, 4, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 9: launch_tn<4, 3, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 10: launch_tn_pers<4, 4, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 11: launch_tn_wide<16, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 12: launch_tn_wide<8, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 13: launch_tn_wide<8, 4>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 7: launch_tn_pers<8, 3, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-      case 14:
-        // unsplit products keep the launch-order grid (one slab: nothing to group)
-        if (grid.z > 1) launch_tn_xcd<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
-        else launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
-        break;
-      default: launch_tn<8, 4, 2>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part); break;
-    }
+    // unsplit products keep the launch-order grid (one slab: nothing to group)
+    if (grid.z > 1)
+      launch_tn_xcd<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
+    else
+      launch_tn<8, 2, 3>(grid, s, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, uplo, kchunk, part);
     GG_LAUNCH_CHECK();
     if (part) {
       const int64_t total = (int64_t)M * N;
