@@ -73,7 +73,7 @@ struct BlockOp {
   int pTF = 0;   // pair axes: h = 16 pTF + 4
   int cus = 256;
   int pair_abl = 0;   // diag ablation of the pair kernel's memory streams (GG_BLK_PAIR_ABL)
-  // blk_pair_lds_kernel (TF 2 and 6; GG_BLK_PAIR_LDS=0: blk_pair_kernel) with
+  // blk_pair_lds_kernel (TF 2..6; GG_BLK_PAIR_LDS=0: blk_pair_kernel) with
   // pair_spw slabs per workgroup (2 when a block holds an even slab count;
   // GG_BLK_PAIR_SPW=1 forces 1)
   bool pair_lds = false;
@@ -1545,9 +1545,16 @@ static blk_mode_fn mode_fn(int JT, bool T4) {
 }
 template <int KIND>
 static blk_mode_fn mode_fast_fn(int JT) {
+  // the fused kinds ring kD k-steps of three operands, kD | KS: KS = 13 / 17
+  // (JT 4 / 5) are prime, the whole strip in flight spills -- the generic
+  // kernel there (JT 5: KIND 1 / 3 52 B of scratch, KIND 2 404 B; JT 4 KIND 2 88 B)
+  if (KIND != 0 && (JT == 5 || (KIND == 2 && JT == 4))) return nullptr;
   switch (JT) {
     case 2: return blk_mode_fast_kernel<1, KIND>;
     case 3: return blk_mode_fast_kernel<2, KIND>;
+    case 4: return blk_mode_fast_kernel<3, KIND>;
+    case 5: return blk_mode_fast_kernel<4, KIND>;
+    case 6: return blk_mode_fast_kernel<5, KIND>;
     case 7: return blk_mode_fast_kernel<6, KIND>;
     default: return nullptr;
   }
@@ -1568,13 +1575,23 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
                                   : mode_fn<0>(JT, T4);
 }
 
-// pair kernel shapes: h = 16 TF + 4 for TF in {1, 2, 6} (m = 40, 72, 200)
+// pair kernel shapes: h = 16 TF + 4 for TF in 1..6 (m = 40, 72, 104, 136, 168,
+// 200); JA = TF / 2 full column tiles (+ the 4-column tail) for role 0
 template <int EPI, int SIDE>
 static blk_pair_fn select_pair_lds(int TF, int spw) {
   switch (TF) {
     case 2:
       return spw == 2 ? blk_pair_lds_kernel<2, 1, 2, EPI, SIDE>
                       : blk_pair_lds_kernel<2, 1, 1, EPI, SIDE>;
+    case 3:
+      return spw == 2 ? blk_pair_lds_kernel<3, 1, 2, EPI, SIDE>
+                      : blk_pair_lds_kernel<3, 1, 1, EPI, SIDE>;
+    case 4:
+      return spw == 2 ? blk_pair_lds_kernel<4, 2, 2, EPI, SIDE>
+                      : blk_pair_lds_kernel<4, 2, 1, EPI, SIDE>;
+    case 5:
+      return spw == 2 ? blk_pair_lds_kernel<5, 2, 2, EPI, SIDE>
+                      : blk_pair_lds_kernel<5, 2, 1, EPI, SIDE>;
     case 6:
       return spw == 2 ? blk_pair_lds_kernel<6, 3, 2, EPI, SIDE>
                       : blk_pair_lds_kernel<6, 3, 1, EPI, SIDE>;
@@ -1594,6 +1611,9 @@ static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi =
   switch (TF) {
     case 1: return blk_pair_kernel<1, 1>;
     case 2: return blk_pair_kernel<2, 1>;
+    case 3: return blk_pair_kernel<3, 1>;
+    case 4: return blk_pair_kernel<4, 2>;
+    case 5: return blk_pair_kernel<5, 2>;
     case 6: return blk_pair_kernel<6, 3>;
     default: return nullptr;
   }

@@ -99,7 +99,8 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
  * A matvec there is d - 1 launches (the last two axes of a block share one
  * launch): the CG (gg_cg_*) runs in this basis by default when it exists
  * (gg_cg_set_basis), folding b at start and unfolding x at every close.
- * Existence: 2 <= d <= 6, h_{d-2} = h_{d-1} in {20, 36, 100}, every h <= 112
+ * Existence: 2 <= d <= 6, h_{d-2} = h_{d-1} = 16 TF + 4, TF in 1..6 (m = 40,
+ * 72, 104, 136, 168, 200), every h <= 112
  * (GG_KRON_BLOCK=0 at gg_kron_create disables it).  No reference counterpart:
  * an execution detail of kron_matrix.py:52-97.                              */
 int gg_kron_block_info(const gg_kron* K, int* available, int64_t* n, int* launches);

@@ -64,6 +64,10 @@ SHAPES = [
     (40, 8, 72, 72),
     (4, 6, 8, 40, 40),
     (200, 6, 40, 40),
+    (6, 104, 104),        # pair TF 3 .. 5 (h = 52, 68, 84: round 5)
+    (4, 136, 136),
+    (2, 168, 168),
+    (104, 8, 136, 136),   # a fast mode kernel of order 104 (axis 0): JT 4
 ]
 
 
@@ -123,7 +127,8 @@ def test_block_matvec_vs_oracle(gg, ms, shift):
 
 
 @pytest.mark.parametrize("ms", [(40, 40, 40, 40), (200, 6, 40, 40), (40, 8, 72, 72),
-                                (72, 36, 72, 72)])
+                                (72, 36, 72, 72), (104, 8, 72, 72), (136, 4, 40, 40),
+                                (168, 4, 40, 40)])
 def test_block_fast_kernels_match_generic(gg, monkeypatch, ms):
     """The fixed-count mode kernels (h = 16 TF + 4: blk_mode_fast_kernel) and
     the generic ones compute the same k-step sums in the same order: the block
@@ -147,7 +152,8 @@ def test_block_fast_kernels_match_generic(gg, monkeypatch, ms):
     assert out[0][2][0] == out[1][2][0] == 9
 
 
-@pytest.mark.parametrize("ms", [(40, 8, 72, 72), (10, 200, 200), (6, 14, 40, 40)])
+@pytest.mark.parametrize("ms", [(40, 8, 72, 72), (10, 200, 200), (6, 14, 40, 40),
+                                (6, 104, 104), (4, 136, 136), (2, 168, 168)])
 def test_block_pair_lds_kernel_matches_register_kernel(gg, monkeypatch, ms):
     """blk_pair_lds_kernel (GEMM 1's operands through the LDS-DMA ring; one
     or two slabs per workgroup) and blk_pair_kernel run the same MFMA chains
@@ -216,7 +222,9 @@ def oracle_cg(F, b, shift, rtol, maxiter):
 
 @pytest.mark.parametrize("ms,shift", [((10, 40, 40), 0.05), ((6, 12, 40, 40), 0.05),
                                       ((4, 8, 72, 72), 0.2), ((8, 6, 8, 40, 40), 0.1),
-                                      ((40, 40, 40, 40), 0.5), ((40, 72, 72), 0.2)])
+                                      ((40, 40, 40, 40), 0.5), ((40, 72, 72), 0.2),
+                                      ((6, 104, 104), 0.1), ((4, 6, 136, 136), 0.1),
+                                      ((8, 6, 168, 168), 0.2)])
 def test_block_cg_vs_oracle(gg, ms, shift):
     F = factors(ms)
     K = gg.tensors.KronMatrix(F, sym=True)
