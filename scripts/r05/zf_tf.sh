@@ -3,7 +3,7 @@
 # d = 4): block vs grid K*x and fused CG per iteration
 set -o pipefail
 export PYTHONUNBUFFERED=1
-O=gpurun_out/r05_zf
+O=gpurun_out/r05_zg
 mkdir -p $O
 for m in 104 136 168; do
   timeout -k 10 300 python -u tools/block_bench.py --m $m --d 4 --iters 20 --reps 4 --grid-cg > $O/m$m.json 2> $O/m$m.err || { tail -5 $O/m$m.err; exit 1; }
