@@ -565,6 +565,7 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
                    "cg_recurrence": "fused",
                    "cg_basis": "block",
                    "blocks_per_rank": (1 << d) // world,
+                   "cg_x_window": int(getattr(eng, "xwin", 0)),
                    "n_per_rank": nl,
                    "launches_per_iteration": d - 1,
                    "timed_region": "exactly `steps` fused CG iterations continuing the "
@@ -593,7 +594,8 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
         res_["local_launch_ms"] = per_pos
         # the dominant kernel of a rank (its blocks are whole blocks: the
         # single-GPU block roofline with n -> N / G)
-        roof, extra = roofline_report(per_pos, nl, m, d, "fused", ms_per_step, block=True)
+        roof, extra = roofline_report(per_pos, nl, m, d, "fused", ms_per_step, block=True,
+                                      xwin=int(getattr(eng, "xwin", 0)))
         roof["scope"] = "per rank: the rank's dominant launch on its N / G elements " \
                         "(max over ranks of the per-launch %s means)" \
                         % ("HIP-event" if on_gpu else "host-timer (CPU rehearsal engine)")
@@ -672,17 +674,19 @@ def launch_passes(d, recurrence, fusion=0, xdefer=False, rq=False):
     return passes
 
 
-def block_launch_passes(d):
+def block_launch_passes(d, xwin=0):
     """Passes over N of each launch of the fused CG iteration in the
     parity-block basis (gg_kronb.hip block_apply; d - 1 launches): the first
     (axis 0, in place) carries the prologue -- p_old (its MFMA operand), r and
     q_old read, r, p_new and the output written; the last (the pair of
     innermost axes, blk_pair_lds_kernel) reads its input and p_new, writes q,
-    and carries the balanced x side job (half of x per iteration: x,
-    p_{j-2}, p_{j-1} read, x written = 2 passes); the ones between are plain."""
+    and carries the x side job: xwin = 0, mode 2's balanced pairs (half of x
+    per iteration: x, p_{j-2}, p_{j-1} read, x written = 2 passes); xwin = K,
+    mode 3's window (one of K regions of x read and written, its K pending
+    directions read = (K + 2) / K passes); the ones between are plain."""
     passes = [2.0] * (d - 1)
     passes[0] += 4.0
-    passes[-1] += 1.0 + 2.0
+    passes[-1] += 1.0 + ((xwin + 2.0) / xwin if xwin >= 2 else 2.0)
     return passes
 
 
@@ -727,14 +731,14 @@ def dominant_group(per_pos, kinds):
 
 
 def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0,
-                    xdefer=False, rq=False, block=False):
+                    xdefer=False, rq=False, block=False, xwin=0):
     """fold_mask bit k: mode product k runs on the centrosymmetric split
     (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
     the roofline prices the work the kernel actually does.  block: the CG runs
     in the parity-block basis (d - 1 launches)."""
     if block:
         flops = block_launch_flops(n, m, d)
-        passes = block_launch_passes(d)
+        passes = block_launch_passes(d, xwin)
         kinds = block_launch_kernels(d)
     else:
         flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
@@ -826,7 +830,7 @@ def kernel_source_hash():
 
 
 def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True, rq=False,
-                block=False):
+                block=False, xwin=0):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
     positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
     when they were taken on this workload, recurrence, fusion layout and fold
@@ -845,7 +849,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
         return None, "PMC passes taken with another recurrence / fusion layout"
     if rec.get("fold_mask", 0) != fold_mask:
         return None, "PMC passes taken with another fold state"
-    if int(rec.get("x_deferred", 0)) != int(xdefer):
+    if int(rec.get("x_deferred", 0)) != int(xdefer) or int(rec.get("x_window", 0)) != int(xwin):
         return None, "PMC passes taken with another x-update schedule"
     if int(rec.get("rq_identity", 0)) != int(rq):
         return None, "PMC passes taken with another r.q source"
@@ -977,15 +981,17 @@ def grief_leg(names, torch, cpu, dist=None, world=1, rank=0):
     return out
 
 
-def lanczos_passes(d):
-    """8-byte passes over N per fused Lanczos step by mode-product position
-    (gg_vec.hip gg_lanczos_probe, even d): the first mode product's prologue
-    reads the previous output Y (its MFMA operand), u and u_prev and writes
-    w = cy Y + cu u + cp u_prev over u_prev (+3 beyond the plain 2); the last
-    epilogue reads w for shift * w and w.(K w + shift w) (+1)."""
-    passes = [2.0] * d
+def lanczos_passes(d, block=False):
+    """8-byte passes over N per fused Lanczos step by launch position
+    (gg_vec.hip gg_lanczos_probe; grid basis: d mode products, even d; block
+    basis: d - 1 launches, round 6): the first launch's prologue reads the
+    previous output Y, u and u_prev and writes w = cy Y + cu u + cp u_prev
+    over u_prev (+3 beyond the plain 2); the last (the epilogue / the pair
+    launch) reads w for shift * w and w.(K w + shift w) (+1)."""
+    L = d - 1 if block else d
+    passes = [2.0] * L
     passes[0] += 3.0
-    passes[d - 1] += 1.0
+    passes[L - 1] += 1.0
     return passes
 
 
@@ -1017,18 +1023,21 @@ def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
     st = step_ms[:k]
     ms = float(np.mean(st))
     steady = float(np.mean(st[1:])) if k > 1 else ms
-    passes = lanczos_passes(d) if d % 2 == 0 else None
+    block, L = linalg.lanczos_info(K)
+    passes = lanczos_passes(d, block) if (block or d % 2 == 0) else None
     out = {"steps": k, "ms_per_step": ms, "steps_per_s": 1e3 / ms,
            "steady_ms_per_step": steady, "first_step_ms": st[0],
            "step_ms_min": float(np.min(st)), "step_ms_max": float(np.max(st)),
            "ms_source": "mean of per-step HIP events the library records on its stream "
                         "(gg_lanczos_probe_timed); workspace allocated before timing",
-           "mode_product_ms_by_position": [t / steps for t in launch_ms],
+           "basis": "block" if block else "grid", "launches_per_step": L,
+           "mode_product_ms_by_position": [t / steps for t in launch_ms[:L]],
            "bracket_ms": bracket, "bracket_ms_per_step": bracket / max(k, 1),
            "workspace_alloc_s": alloc_s}
     if passes is not None and k > 1:
         byts = 8.0 * n * sum(passes)
-        flop = sum((1.0 if (fold_mask >> i) & 1 else 2.0) * n * m for i in range(d))
+        flop = (sum(block_launch_flops(n, m, d)) if block else
+                sum((1.0 if (fold_mask >> i) & 1 else 2.0) * n * m for i in range(d)))
         out["roofline"] = {
             "passes_per_step": sum(passes), "passes_by_position": passes,
             "algorithmic_bytes_per_step": byts, "flop_per_step": flop,
@@ -1037,7 +1046,9 @@ def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
             "achieved_tflops": flop / (steady * 1e-3) / 1e12,
             "frac_mfma": flop / (steady * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
             "basis": "steady steps (2..k): the fused step with the update pass as the "
-                     "first mode product's prologue"}
+                     "first launch's prologue" + (" (parity-block basis: the probe folded "
+                                                  "once, d - 1 launches per step)" if block
+                                                  else "")}
     return out
 
 
@@ -1103,6 +1114,94 @@ def time_block_matvec(K, n, m, d, torch, dev, reps=5):
             "launch_frac_hbm": [16.0 * n / (t * 1e-3) / 1e9 / HBM_PEAK_GBS for t in pos]}
 
 
+# ---------------------------------------------------------------- the box
+class ClockSampler(object):
+    """GPU 0's clocks, temperatures and power sampled by amdsmi every
+    `period` s on a background thread (the timed CG region; VERDICT r05 item 2:
+    every bench line explains its box).  Reports min / mean / max per field
+    and the board's identity; {"error": ...} where amdsmi is unavailable."""
+
+    def __init__(self, period=0.05):
+        import threading
+        self.period = period
+        self.samples = []
+        self.error = None
+        self.ident = {}
+        self._stop = threading.Event()
+        self._thr = None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self.smi = amdsmi
+            self.h = amdsmi.amdsmi_get_processor_handles()[0]
+            try:
+                self.ident["bdf"] = amdsmi.amdsmi_get_gpu_device_bdf(self.h)
+            except Exception:  # noqa: BLE001
+                pass
+            try:
+                self.ident["serial"] = amdsmi.amdsmi_get_gpu_board_info(self.h).get(
+                    "product_serial")
+            except Exception:  # noqa: BLE001
+                pass
+        except Exception as e:  # noqa: BLE001
+            self.smi = None
+            self.error = "%s: %s" % (type(e).__name__, e)
+
+    def sample(self):
+        smi, h = self.smi, self.h
+        rec = {}
+        for key, typ in (("gfx_mhz", "GFX"), ("mem_mhz", "MEM"), ("fclk_mhz", "DF")):
+            try:
+                rec[key] = float(smi.amdsmi_get_clock_info(h, getattr(smi.AmdSmiClkType, typ))
+                                 ["clk"])
+            except Exception:  # noqa: BLE001
+                pass
+        for key, typ in (("temp_hotspot_c", "HOTSPOT"), ("temp_mem_c", "VRAM")):
+            try:
+                rec[key] = float(smi.amdsmi_get_temp_metric(
+                    h, getattr(smi.AmdSmiTemperatureType, typ),
+                    smi.AmdSmiTemperatureMetric.CURRENT))
+            except Exception:  # noqa: BLE001
+                pass
+        try:
+            p = smi.amdsmi_get_power_info(h)
+            v = p.get("socket_power", p.get("current_socket_power"))
+            if v not in (None, "N/A"):
+                rec["power_w"] = float(v)
+        except Exception:  # noqa: BLE001
+            pass
+        return rec
+
+    def _run(self):
+        while not self._stop.is_set():
+            self.samples.append(self.sample())
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self.smi is not None:
+            import threading
+            self._thr = threading.Thread(target=self._run, daemon=True)
+            self._thr.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self._thr is not None:
+            self._stop.set()
+            self._thr.join()
+        return False
+
+    def report(self):
+        if self.smi is None:
+            return {"error": self.error}
+        out = {"samples": len(self.samples), "period_s": self.period, "gpu": self.ident,
+               "source": "amdsmi on GPU 0 during the timed CG iterations"}
+        keys = sorted({k for s in self.samples for k in s})
+        for k in keys:
+            v = [s[k] for s in self.samples if k in s]
+            out[k] = {"min": min(v), "mean": float(np.mean(v)), "max": max(v)}
+        return out
+
+
 # ---------------------------------------------------------------- main
 def main():
     a = parse()
@@ -1150,6 +1249,9 @@ def main():
                               fusion=a.fusion if a.recurrence == "fused" else None)
     solver.start(y, rtol=0.0, atol=0.0)   # never "converges": exactly the steps asked for
     torch.cuda.synchronize()
+    # this box's memory floor for the prologue launch: its six streams alone
+    # over the same buffers (gg_cg_calibrate), before any iteration
+    cal_ms, cal_off = solver.calibrate(5)
 
     # ---- CG: warmup, then exactly `steps` iterations bracketed by sync.  The
     # recurrence stays open across the two calls (steady state, as inside a
@@ -1163,10 +1265,12 @@ def main():
     # iterations, recorded by the library on the stream the kernels run on
     solver.profile(True)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    solver.iterate(a.steps, check_every=0, close=False)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    clocks = ClockSampler()
+    with clocks:
+        t0 = time.perf_counter()
+        solver.iterate(a.steps, check_every=0, close=False)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
     n_mv, mode_ms = solver.profile_read()
     solver.profile(False)
     assert n_mv == a.steps, (n_mv, a.steps)
@@ -1185,10 +1289,12 @@ def main():
     fold_mask = K._device().fold_mask()
     block = solver.basis == "block"
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
-                                  solver.fusion, fold_mask, solver.xdefer, solver.rq, block)
+                                  solver.fusion, fold_mask, solver.xdefer, solver.rq, block,
+                                  solver.xwin)
     # the block basis has no per-factor fold state (tools/pmc_block.py records 0)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
-                               0 if block else fold_mask, solver.xdefer, solver.rq, block)
+                               0 if block else fold_mask, solver.xdefer, solver.rq, block,
+                               solver.xwin)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -1209,6 +1315,7 @@ def main():
                    "cg_recurrence": solver.recurrence,
                    "cg_fusion_layout": solver.fusion,
                    "cg_x_deferred": solver.xdefer,
+                   "cg_x_window": solver.xwin,
                    "cg_rq_identity": solver.rq,
                    "cg_basis": solver.basis,
                    "launches_per_iteration": solver.launches(),
@@ -1221,6 +1328,19 @@ def main():
         "closing_ms": closing_ms,
     }
     result.update(extra)
+    # the box: the prologue's streams alone on these
+    # buffers -- the launch's memory floor here -- beside the launch itself
+    cal_bytes = 6.0 * 8.0 * n
+    result["prologue_calibration_gbs"] = cal_bytes / (cal_ms * 1e-3) / 1e9
+    result["prologue_calibration"] = {
+        "ms": cal_ms, "bytes": cal_bytes,
+        "pattern": "read p_old, r, q; write r, p_new, q (the fused prologue's six streams, "
+                   "its non-temporal mask, no MFMA work; gg_cg_calibrate, 5 passes)",
+        "buffer_offsets_mod_2MiB": dict(zip(["r", "p_old", "p_new", "q"], cal_off)),
+        "buffers_256B_aligned": all(v % 256 == 0 for v in cal_off),
+        "prologue_launch_ms": per_pos[0],
+        "prologue_launch_vs_streams": per_pos[0] / cal_ms}
+    result["box"] = clocks.report()
     del solver, y
     torch.cuda.empty_cache()
     if a.matvec > 0:

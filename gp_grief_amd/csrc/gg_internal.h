@@ -65,6 +65,8 @@ constexpr int kWave = 64;
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ---- device scalar block shared by the Krylov drivers (CG / Lanczos) ----
+constexpr int kXWinMax = 8;       // x_defer mode 3: the largest window
+constexpr int kXWinDefault = 8;   // and the default (GG_CG_XWIN; profiles/r06/b_win)
 struct CgScalars {
   double rho;       // r.r of the current residual
   double rho_prev;  // r.r of the previous residual
@@ -98,6 +100,23 @@ struct CgScalars {
                     // a sharded rank / GG_CG_RESTART)
   double cancel_tol;  // the cancellation test's threshold (0: 1e-6; set once per
                       // handle from GG_CG_CANCEL_TOL, a test switch)
+  // x_defer mode 3 (window, block-basis CG): x is cut into wk regions; every
+  // iteration's side job brings ONE region up to date with the steps it has
+  // not seen (at most wk: region r is visited every wk iterations), so an
+  // iteration moves x once per wk iterations and every direction once --
+  // (wk + 2) / wk passes instead of 2.  Step i (alpha_i, p_i) sits in ring slot
+  // i % (wk + 1) of (wc, wp); the host keeps wk + 1 direction buffers.
+  int wk;           // window (0: off)
+  int wn;           // steps with a known alpha
+  int wnext;        // next region to arm (round robin)
+  int warm;         // a side job is armed for the next pair launch
+  int wa[kXWinMax];            // steps applied per region
+  double wc[kXWinMax + 1];
+  const double* wp[kXWinMax + 1];
+  // the armed side job: region sreg, x += sum_{t < scnt} scoef[t] sdir[t]
+  int sreg, scnt;
+  double scoef[kXWinMax];
+  const double* sdir[kXWinMax];
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
@@ -137,7 +156,10 @@ struct MpFuse {
   // the slice) when sc->xpend == 2, instead of alpha p_side when pending.
   // xdefer 2: the slice is [soff, soff + sn) of x for half sc->xh == 0 and
   // [soff_h1, soff_h1 + sn_h1) for half 1 (sx / sp are then x / p at offset 0)
+  // xdefer 3 (window, block basis, pair launch only): the side job the scalars
+  // armed in sc (sreg, scnt, scoef, sdir) over region sreg of xwin regions
   int xdefer = 0;
+  int xwin = 0;
   int64_t soff = 0;
   int64_t soff_h1 = 0, sn_h1 = 0;
   // output of the first mode product when the ping-pong would put it in y
@@ -231,5 +253,12 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
 int64_t block_prologue_blocks(const BlockOp* B);
 int64_t block_partials_needed(const BlockOp* B);
 int64_t block_side_half(int64_t n);
+// x_defer mode 3: the length of each of the K regions (even; the last may be
+// shorter) and whether the operator's pair launch can carry that side job
+int64_t xwin_region(int64_t n, int K);
+bool block_pair_side(const BlockOp* B);
+// the padded layout costs at most 1.3x the unpadded passes (the single-GPU
+// default basis of the CG and of Lanczos)
+bool block_efficient(const BlockOp* B);
 
 }  // namespace gg

@@ -3,7 +3,10 @@
 // the snapshot is taken -- at the first lookup, at every gg_kron_create /
 // gg_cg_create (a handle's configuration is latched when it is made) and by
 // gg_knobs_reload -- so no launch path calls getenv.  Snapshots are never
-// freed: a pointer knob() returned stays valid after a reload.
+// freed (a pointer knob() returned stays valid after a reload), and a reload
+// that finds an environment it has seen before reuses that snapshot, so a
+// loop creating handles does not grow memory: one snapshot per distinct
+// GG_* environment.
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -21,7 +24,7 @@ namespace gg {
 namespace {
 typedef std::map<std::string, std::string> Snapshot;
 std::mutex g_mu;
-std::vector<std::unique_ptr<Snapshot>> g_all;   // every snapshot taken (kept alive)
+std::vector<std::unique_ptr<Snapshot>> g_all;   // every distinct snapshot (kept alive)
 const Snapshot* g_cur = nullptr;
 
 const Snapshot* take() {
@@ -31,6 +34,8 @@ const Snapshot* take() {
     const char* eq = strchr(*e, '=');
     if (eq) (*s)[std::string(*e, eq - *e)] = std::string(eq + 1);
   }
+  for (const auto& old : g_all)
+    if (*old == *s) return old.get();
   g_all.push_back(std::move(s));
   return g_all.back().get();
 }

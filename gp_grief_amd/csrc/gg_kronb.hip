@@ -62,7 +62,12 @@ constexpr int kBlkPairWaves = 4;   // waves per blk_pair_kernel workgroup (2 sla
 struct BlockOp {
   int d = 0;
   int64_t m[kBlkMaxD] = {}, h[kBlkMaxD] = {};
-  int64_t nb = 0, n = 0;          // block size, vector length (2^d nb)
+  // the layout's extent per axis: h, except the two innermost (the pair
+  // axes), padded to hp = 16 TF + 4 >= h (round 6: pair orders that are not
+  // 16 TF + 4 -- 64, 96, 128 ... -- run the same pair kernels on slabs whose
+  // rows / columns past h are zero in the vectors and in the factors)
+  int64_t e[kBlkMaxD] = {};
+  int64_t nb = 0, n = 0;          // block size (prod e), vector length (2^d nb)
   // A / B fragments of S (parity 0) and T (1) per axis: [KS][JT][64] doubles,
   // frag(s, t, l) = F[16 t + (l & 15)][4 s + (l >> 4)] for full tiles, the tail
   // tile (T4) F[16 (JT-1) + (l & 3)][4 s + (l >> 4)] (rows replicated over the
@@ -72,7 +77,6 @@ struct BlockOp {
   bool T4[kBlkMaxD] = {};
   int pTF = 0;   // pair axes: h = 16 pTF + 4
   int cus = 256;
-  int pair_abl = 0;   // diag ablation of the pair kernel's memory streams (GG_BLK_PAIR_ABL)
   // blk_pair_lds_kernel (TF 2..6; GG_BLK_PAIR_LDS=0: blk_pair_kernel) with
   // pair_spw slabs per workgroup (2 when a block holds an even slab count;
   // GG_BLK_PAIR_SPW=1 forces 1)
@@ -103,6 +107,7 @@ struct BlockOp {
 struct FoldGeom {
   int d;
   int64_t m[kBlkMaxD], h[kBlkMaxD], stride[kBlkMaxD];
+  int64_t hp;   // the slab's (padded) extent; positions with i or a >= h are zero
   int64_t nb;
   int64_t blk0, nblk;
 };
@@ -119,12 +124,21 @@ __global__ __launch_bounds__(256) void blk_fold_kernel(const double* __restrict_
     int64_t lo = 0, span[D];
     // t is the position in the block layout: the slab (outer axes, C order)
     // and, inside it, the k-step tiled (i, a) of the two innermost axes
-    const int64_t hs = g.h[D - 1];
+    const int64_t hs = g.hp;
     const int64_t q = t % (hs * hs);
     int64_t rem = t / (hs * hs);
     {
       const int64_t a4 = q / (4 * hs), r4 = q - a4 * 4 * hs;
       const int64_t i = r4 >> 2, a = 4 * a4 + (r4 & 3);
+      if (i >= g.h[D - 2] || a >= g.h[D - 1]) {
+        // padding: zero in every block (forward), no grid element (inverse)
+        if (!inverse)
+          for (int c = 0; c < C; ++c) {
+            const int64_t lb = (int64_t)c - g.blk0;
+            if (lb >= 0 && lb < g.nblk) y[lb * g.nb + t] = 0.0;
+          }
+        continue;
+      }
       lo = i * g.stride[D - 2] + a * g.stride[D - 1];
       span[D - 2] = (g.m[D - 2] - 1 - 2 * i) * g.stride[D - 2];   // low -> mirrored corner
       span[D - 1] = (g.m[D - 1] - 1 - 2 * a) * g.stride[D - 1];
@@ -277,7 +291,9 @@ __device__ __forceinline__ void st2g(double* p, double2 v) {
 // partial; the MFMA B operand is p_new; Y (the q buffer) is written over
 // q_old at the same positions after this wave has read them.  KIND 2: plain
 // plus the balanced x side job (x += c0 p0 + c1 p1 over half sc->xh of x),
-// one slice of it per strip.
+// one slice of it per strip.  KIND 4: the fused Lanczos step's prologue
+// (gg_lanczos_probe in the block basis): w = cy Y + cu u + cp u_prev formed
+// per element as the operand, stored over u_prev, |w|^2 partials.
 struct ModeArgs {
   const double* X;
   double* Y;
@@ -300,6 +316,11 @@ struct ModeArgs {
   const CgScalars* sc;
   double* rr_part;    // [grid] r.r, [pqo_stride + grid] p_new.q_old
   int64_t pqo_stride;
+  // Lanczos prologue (KIND 4): X holds u_prev, r the Lanczos vector u, q_old
+  // the previous matvec output Y; the operand is w = cy Y + cu u + cp u_prev
+  // (coef = [cy, cu, cp] on the device), stored over u_prev (p_out == X,
+  // element-wise in place), |w|^2 partials to rr_part
+  const double* coef;
   // side job (KIND 2): x += c0 p0 + c1 p1 over [soff, soff + sn) (half 0) or
   // [soff_h1, soff_h1 + sn_h1) (half 1); each strip slot takes sstep elements
   double* sx;
@@ -311,7 +332,7 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
   constexpr int W = kBlkModeWaves;
   constexpr int TF = T4 ? JT - 1 : JT;   // full 16-row tiles
   constexpr int kDepth = 8;              // k-steps in flight per wave
-  constexpr int NV = KIND == 1 ? 3 : 1;  // streams per element
+  constexpr int NV = (KIND == 1 || KIND == 4) ? 3 : 1;  // streams per element
   constexpr int kSD = 2;                 // side-job k-steps in flight
   extern __shared__ __attribute__((aligned(16))) double lds[];
   if (a.skip != nullptr && *a.skip) return;
@@ -378,6 +399,12 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
     alpha = a.sc->alpha;
     pqo_on = a.pqo_stride > 0 && !first;
   }
+  double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
+  if (KIND == 4) {
+    lz_cy = a.coef[0];
+    lz_cu = a.coef[1];
+    lz_cp = a.coef[2];
+  }
   // side job state
   double sc0 = 0.0, sc1 = 0.0;
   const double* sp0 = nullptr;
@@ -438,7 +465,7 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
       const int64_t ubr = in ? ub : base * 8;
       const uint32_t vo = in ? o_e : (uint32_t)(n16 * 8);
       ring[slot][0] = ldu(a.X, ubr, vo);
-      if (KIND == 1) {
+      if (KIND == 1 || KIND == 4) {
         ring[slot][1] = ldu(a.r, ubr, vo);
         ring[slot][2] = ldu(a.q_old, ubr, vo);
       }
@@ -512,6 +539,17 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
             }
             if (!(i < a.h)) xb = 0.0;
           }
+          if (KIND == 4) {
+            const bool ok = cs_valid && i < a.h;
+            const double uv = i < a.h ? ring[u][1] : 0.0;
+            const double yv = i < a.h ? ring[u][2] : 0.0;
+            xb = fma(lz_cp, xb, fma(lz_cu, uv, lz_cy * yv));   // lz_update_kernel's expression
+            if (ok) {
+              stu(a.p_out, (cs_base + (int64_t)4 * cs_s * a.inner) * 8, o_e, xb);
+              rr_acc = fma(xb, xb, rr_acc);
+            }
+            if (!(i < a.h)) xb = 0.0;
+          }
           const double* fs = lds + ((int64_t)cs_s * JT) * 64 + lane;
 #pragma unroll
           for (int t = 0; t < TF; ++t)
@@ -560,7 +598,7 @@ __global__ __launch_bounds__(64 * kBlkModeWaves, 1) void blk_mode_kernel(ModeArg
     }
     sg0 = sg1;
   }
-  if (KIND == 1) {
+  if (KIND == 1 || KIND == 4) {
     __shared__ double red[2 * kBlkModeWaves];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -608,7 +646,7 @@ constexpr int fast_waves() {
 
 template <int TF, int KIND_>
 __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_kernel(ModeArgs a) {
-  constexpr bool NT = KIND_ == 3;
+  constexpr bool NT = KIND_ == 3 || KIND_ == 4;   // KIND 4 (Lanczos): non-temporal too
   constexpr int KIND = KIND_ == 3 ? 1 : KIND_;
   constexpr int W = fast_waves<KIND>();
   constexpr int JT = TF + 1;
@@ -686,6 +724,12 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
     alpha = a.sc->pending != 0 ? a.sc->alpha : 0.0;   // not pending: r stays r
     pqo_on = a.pqo_stride > 0 && !first;
   }
+  double lz_cy = 0.0, lz_cu = 0.0, lz_cp = 0.0;
+  if (KIND == 4) {
+    lz_cy = a.coef[0];
+    lz_cu = a.coef[1];
+    lz_cp = a.coef[2];
+  }
   const bool pending = KIND == 1 && a.sc->pending != 0;
   double sc0 = 0.0, sc1 = 0.0;
   const double* sp0 = a.sx;
@@ -739,7 +783,7 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
       // k-step s of the load cursor's strip (s compile-time)
       const int64_t ub = l_base * 8 + (int64_t)s * rstep;
       ring[slot][0] = lduq<NT>(a.X, ub, o_e);
-      if (KIND == 1) {
+      if (KIND == 1 || KIND == 4) {
         ring[slot][1] = lduq<NT>(a.r, ub, o_e);
         ring[slot][2] = lduq<NT>(a.q_old, ub, o_e);
       }
@@ -796,6 +840,15 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
           stq_nt(cvalid, a.r, ub, o_e, r);
           stq_nt(cvalid, a.p_out, ub, o_e, xb);
         }
+        if (KIND == 4) {
+          const int64_t ub = (cbase + (int64_t)4 * s * a.inner) * 8;
+          xb = fma(lz_cp, xb, fma(lz_cu, ring[slot][1], lz_cy * ring[slot][2]));
+          const double rr = fma(xb, xb, rr_acc);
+          if (cvalid) rr_acc = rr;   // wave-uniform
+          // over u_prev (X) at the position this wave just read; a spare
+          // strip's (which re-read the last valid strip) to the trash slot
+          stq_nt(cvalid, a.p_out, ub, o_e, xb);
+        }
         const double* fs = reinterpret_cast<const double*>(lb + (s * JT) * 512);
 #pragma unroll
         for (int t = 0; t < TF; ++t)
@@ -832,7 +885,7 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
     }
     sg0 = sg1;
   }
-  if (KIND == 1) {
+  if (KIND == 1 || KIND == 4) {
     __shared__ double red[2 * W];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -897,10 +950,9 @@ struct PairArgs {
   const CgScalars* sc;
   double* sx;
   int64_t soff, sn, soff_h1, sn_h1, sstep;
-  int abl;             // diag only (GG_BLK_PAIR_ABL): 1 X from 16 slabs, 2 Z to 16 slabs
-                       // (blk_pair_kernel); 4 no GEMM 2 k-loop, 8 no GEMM 1 MFMAs;
-                       // 32 the x side job back in the second launch (A/B); 128 no
-                       // side job (timing only)
+  // x_defer mode 3 (SIDE bit 4): the armed region sc->sreg of length sreg_len
+  // (sn = the vector's length) gets x += sum_t sc->scoef[t] sc->sdir[t]
+  int64_t sreg_len;
 };
 
 // swizzle a double within 32-lane groups: lane (b4 b3 b2 b1 b0) reads lane
@@ -990,7 +1042,6 @@ __device__ __forceinline__ void pair_gemm2(const PairArgs& A, int64_t sbyte, con
     for (int s = 0; s < kPF; ++s) fr[s] = ldu(f2, fti + s * FS, o_f);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      if (A.abl & 4) break;   // diag: GEMM 2 without its k-loop
       const double f = fr[s % kPF];
       if (s + kPF < KS) fr[s % kPF] = ldu(f2, fti + (s + kPF) * FS, o_f);
 #pragma unroll
@@ -1062,8 +1113,8 @@ __device__ __forceinline__ void pair_slab(const PairArgs& A, int64_t slab, doubl
   const int par3 = (int)(blk & 1), par2 = (int)((blk >> 1) & 1);
   const double* f3 = par3 ? A.f3T : A.f3S;
   const double* f2 = par2 ? A.f2T : A.f2S;
-  const int64_t sbyte = ((A.abl & 2) ? slab % 16 : slab) * (int64_t)H * H * 8;
-  const int64_t xbyte = ((A.abl & 1) ? slab % 16 : slab) * (int64_t)H * H * 8;
+  const int64_t sbyte = slab * (int64_t)H * H * 8;
+  const int64_t xbyte = sbyte;
 
   // ---- GEMM 1: W = X F3^T (the role's columns)
   bd4 W[TF][NJ > 0 ? NJ : 1];
@@ -1324,10 +1375,6 @@ __device__ __forceinline__ void pair_slab_lds(const PairArgs& A, int64_t slab, i
 #pragma unroll
     for (int u = 0; u < NJ; ++u) fb[u] = *reinterpret_cast<const double*>(sb + o_f + (J0 + u) * 512);
     if (TJ) fb[NJ] = *reinterpret_cast<const double*>(sb + o_f + TF * 512);
-    if (A.abl & 8) {   // diag: GEMM 1 without its MFMAs
-      slot = (slot + 1) & (NS - 1);
-      continue;
-    }
 #pragma unroll
     for (int t = 0; t < TF; ++t)
 #pragma unroll
@@ -1427,7 +1474,23 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
   const double* sp1 = nullptr;
   double* sxo = nullptr;
   int64_t slen = 0;
-  if (SIDE & 1) {
+  // mode 3: the armed region, wcnt directions (wave-uniform)
+  double wcf[kXWinMax];
+  const double* wdir[kXWinMax];
+  int wcnt = 0;
+  if (SIDE & 4) {
+    if (A.sc->warm && !A.sc->done) {
+      const int64_t off = (int64_t)A.sc->sreg * A.sreg_len;
+      slen = max((int64_t)0, min(A.sn - off, A.sreg_len));
+      wcnt = A.sc->scnt;
+#pragma unroll
+      for (int t = 0; t < kXWinMax; ++t) {
+        wcf[t] = A.sc->scoef[t];
+        wdir[t] = A.sc->sdir[t] + off;
+      }
+      sxo = A.sx + off;
+    }
+  } else if (SIDE & 1) {
     const int xh = A.sc->xh;
     if (xh < 2 && !A.sc->done) {
       const int64_t off = xh ? A.soff_h1 : A.soff;
@@ -1468,6 +1531,48 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
       }
     }
   };
+  // mode 3: the wave's slice of the armed region, x += sum_t c_t p_t with every
+  // direction's loads of kWB batches in flight before the first sum (the
+  // direction count is wave-uniform: scalar branches; cg_x_flush3_kernel
+  // forms the same expression)
+  auto side_chunk_win = [&](int64_t slot) {
+    const int64_t q0 = slot * A.sstep;
+    const int64_t q1 = min(slen, q0 + A.sstep);
+    constexpr int kWB = 4;
+    for (int64_t e0 = q0 + 2 * lane; e0 < q1; e0 += kWB * 128) {
+      double2 xv[kWB], a[kXWinMax][kWB];
+#pragma unroll
+      for (int u = 0; u < kWB; ++u) {
+        const int64_t e = e0 + (int64_t)u * 128;
+        if (e + 1 < q1) xv[u] = ld2g(sxo + e);
+      }
+#pragma unroll
+      for (int t = 0; t < kXWinMax; ++t)
+        if (t < wcnt)
+#pragma unroll
+          for (int u = 0; u < kWB; ++u) {
+            const int64_t e = e0 + (int64_t)u * 128;
+            if (e + 1 < q1) a[t][u] = ld2g(wdir[t] + e);
+          }
+#pragma unroll
+      for (int u = 0; u < kWB; ++u) {
+        const int64_t e = e0 + (int64_t)u * 128;
+        if (e + 1 < q1) {
+          double2 s = {0.0, 0.0};
+#pragma unroll
+          for (int t = 0; t < kXWinMax; ++t)
+            if (t < wcnt) {
+              s.x += wcf[t] * a[t][u].x;
+              s.y += wcf[t] * a[t][u].y;
+            }
+          double2 o;
+          o.x = xv[u].x + s.x;
+          o.y = xv[u].y + s.y;
+          st2g(sxo + e, o);
+        }
+      }
+    }
+  };
   PairSlabSrc cur = src_at(0);
 #pragma unroll
   for (int j = 0; j + 1 < NS; ++j) issue(cur, min(j, R::KS - 1), j);   // stages 0 .. NS - 2
@@ -1484,8 +1589,9 @@ __global__ __launch_bounds__(128 * SPW, 2) void blk_pair_lds_kernel(PairArgs A) 
     else
       pair_slab_lds<TF, SPW, EPI, JA, TF - JA, false, (SIDE & 2) != 0>(A, slab, sl, cslot, it == 0, cur, nxt, nv,
                                                       ring, issue, pq, qq);
-    // diag 128: the side job skipped (timing only)
-    if ((SIDE & 1) && slen > 0 && !(A.abl & 128))
+    if ((SIDE & 4) && slen > 0)
+      side_chunk_win(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
+    else if ((SIDE & 1) && slen > 0)
       side_chunk(((int64_t)blockIdx.x + (int64_t)it * G) * R::NW + wave);
     cslot = (cslot + R::KS) % NS;
     cur = nxt;
@@ -1563,7 +1669,8 @@ static blk_mode_fn mode_fast_fn(int JT) {
 // h = 16 (JT - 1) + 4 exactly (KS = 4 JT - 3)
 static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast = false) {
   if (T4 && h == 16 * (JT - 1) + 4 && fast) {
-    const blk_mode_fn f = kind == 3   ? mode_fast_fn<3>(JT)
+    const blk_mode_fn f = kind == 4   ? mode_fast_fn<4>(JT)
+                          : kind == 3 ? mode_fast_fn<3>(JT)
                           : kind == 1 ? mode_fast_fn<1>(JT)
                           : kind == 2 ? mode_fast_fn<2>(JT)
                                       : mode_fast_fn<0>(JT);
@@ -1572,6 +1679,7 @@ static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast =
   // kind 3 (the non-temporal prologue) exists on the fast kernel only
   return (kind == 1 || kind == 3) ? mode_fn<1>(JT, T4)
          : kind == 2              ? mode_fn<2>(JT, T4)
+         : kind == 4              ? mode_fn<4>(JT, T4)
                                   : mode_fn<0>(JT, T4);
 }
 
@@ -1601,11 +1709,16 @@ static blk_pair_fn select_pair_lds(int TF, int spw) {
 
 // epi: the fused CG's epilogue; side: its x side job rides in the launch
 // (LDS kernel only; the CG epilogue always comes with it there); nt: that
-// launch's p loads and q stores non-temporal (SIDE bit 2)
+// launch's p loads and q stores non-temporal (SIDE bit 2); win: the side job
+// is x_defer mode 3's armed region (SIDE bit 4) instead of mode 2's half
 static blk_pair_fn select_pair(int TF, bool lds = false, int spw = 1, bool epi = false,
-                               bool side = false, bool nt = false) {
+                               bool side = false, bool nt = false, bool win = false) {
   if (lds) {
+    if (side && win) return nt ? select_pair_lds<1, 7>(TF, spw) : select_pair_lds<1, 5>(TF, spw);
     if (side) return nt ? select_pair_lds<1, 3>(TF, spw) : select_pair_lds<1, 1>(TF, spw);
+    // the fused Lanczos step's pair launch: its w loads / Y stores
+    // non-temporal as the CG's (SIDE bit 2 alone)
+    if (epi && nt) return select_pair_lds<1, 2>(TF, spw);
     return epi ? select_pair_lds<1, 0>(TF, spw) : select_pair_lds<0, 0>(TF, spw);
   }
   switch (TF) {
@@ -1633,7 +1746,7 @@ static int blk_cus() {
 static void blk_set_lds_limits(const BlockOp* B) {
   for (int k = 0; k + 2 < B->d; ++k) {
     const size_t bytes = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
-    for (int kind = 0; kind < 4; ++kind)
+    for (int kind = 0; kind < 5; ++kind)
       GG_HIP(hipFuncSetAttribute(
           reinterpret_cast<const void*>(
               select_mode(kind, B->JT[k], B->T4[k], (int)B->h[k], B->fast)),
@@ -1650,10 +1763,12 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     if (rows[k] != cols[k] || rows[k] % 2 != 0 || rows[k] < 2) return nullptr;
     if (rows[k] / 2 > 112) return nullptr;   // blk_mode_kernel: JT <= 7
   }
-  const int64_t hp = rows[d - 1] / 2;
-  if (rows[d - 2] != rows[d - 1] || (hp - 4) % 16 != 0) return nullptr;
-  const int TF = (int)((hp - 4) / 16);
+  // the pair axes: equal orders, half order h padded to hp = 16 TF + 4 >= h
+  const int64_t hpair = rows[d - 1] / 2;
+  if (rows[d - 2] != rows[d - 1]) return nullptr;
+  const int TF = (int)std::max<int64_t>(1, ceil_div(hpair - 4, 16));
   if (select_pair(TF) == nullptr) return nullptr;
+  const int64_t hp = 16 * (int64_t)TF + 4;
   // centrosymmetric factors only (the test of gg_kron.hip pack_fold)
   for (int k = 0; k < d; ++k) {
     const int64_t m = rows[k];
@@ -1673,7 +1788,8 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     for (int k = 0; k < d; ++k) {
       B->m[k] = rows[k];
       B->h[k] = rows[k] / 2;
-      B->nb *= B->h[k];
+      B->e[k] = k >= d - 2 ? hp : B->h[k];
+      B->nb *= B->e[k];
     }
     B->n = B->nb << d;
     B->pTF = TF;
@@ -1684,8 +1800,6 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
     B->pro_nt = !(ne && atoi(ne) == 0);
     const char* ee = gg::knob("GG_BLK_EPI_NT");      // A/B knob, read at creation only
     B->epi_nt = !(ee && atoi(ee) == 0);
-    const char* pe = gg::knob("GG_BLK_PAIR_ABL");   // diag ablation, read at creation only
-    B->pair_abl = pe ? atoi(pe) : 0;
     const char* le = gg::knob("GG_BLK_PAIR_LDS");   // A/B knob, read at creation only
     B->pair_lds = select_pair(TF, true) != nullptr && !(le && atoi(le) == 0);
     {
@@ -1704,14 +1818,16 @@ BlockOp* block_create(int d, const int64_t* rows, const int64_t* cols,
       int JT, KS;
       bool T4;
       if (k >= d - 2) {
+        // the pair kernel's shape (hp); fragments past h stay zero
         JT = TF + 1;
         T4 = true;
+        KS = 4 * TF + 1;
       } else {
         const int64_t tail = h % 16;
         T4 = tail != 0 && tail <= 4;
         JT = (int)ceil_div(h, 16);
+        KS = (int)ceil_div(h, 4);
       }
-      KS = (int)ceil_div(h, 4);
       B->JT[k] = JT;
       B->KS[k] = KS;
       B->T4[k] = T4;
@@ -1776,6 +1892,7 @@ void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, doub
   FoldGeom g{};
   g.d = B->d;
   g.nb = B->nb;
+  g.hp = B->e[B->d - 1];
   g.blk0 = blk0;
   g.nblk = nblk;
   int64_t st = 1;
@@ -1810,7 +1927,8 @@ void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, doub
 static int mode_waves(int kind, const BlockOp* B, int k) {
   const int JT = B->JT[k];
   const bool fast = B->T4[k] && B->h[k] == 16 * (JT - 1) + 4 && B->fast &&
-                    (kind == 3   ? mode_fast_fn<3>(JT)
+                    (kind == 4   ? mode_fast_fn<4>(JT)
+                     : kind == 3 ? mode_fast_fn<3>(JT)
                      : kind == 1 ? mode_fast_fn<1>(JT)
                      : kind == 2 ? mode_fast_fn<2>(JT)
                                  : mode_fast_fn<0>(JT)) != nullptr;
@@ -1822,7 +1940,7 @@ static int64_t mode_geometry(const BlockOp* B, int k, int W, ModeArgs& a, int* g
                              int64_t nblk = -1) {
   const int d = B->d;
   int64_t inner = 1, outer = 1;
-  for (int i = k + 1; i < d; ++i) inner *= B->h[i];
+  for (int i = k + 1; i < d; ++i) inner *= B->e[i];
   for (int i = 0; i < k; ++i) outer *= B->h[i];
   GG_REQUIRE(inner % 16 == 0, GG_ERR_VALUE, "block basis: inner extent not a multiple of 16");
   a.h = (int)B->h[k];
@@ -1854,7 +1972,7 @@ int64_t block_prologue_blocks(const BlockOp* B) {
 // blk_pair_lds_kernel one slab each, 4 per CU (28 KiB of LDS ring apiece at
 // h = 100), persistent
 static int pair_grid(const BlockOp* B, int64_t nblk = -1) {
-  const int64_t nslab = B->nb / (B->h[B->d - 1] * B->h[B->d - 2]) *
+  const int64_t nslab = B->nb / (B->e[B->d - 1] * B->e[B->d - 2]) *
                         (nblk < 0 ? ((int64_t)1 << B->d) : nblk);
   if (B->pair_lds)   // 4 slabs in flight per CU (the LDS ring's budget)
     return (int)std::min<int64_t>(nslab / B->pair_spw, (int64_t)B->cus * 4 / B->pair_spw);
@@ -1882,25 +2000,38 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   GG_REQUIRE(blk0 >= 0 && nblk >= 1 && blk0 + nblk <= ((int64_t)1 << d), GG_ERR_VALUE,
              "block range outside the 2^d blocks");
   if (cg == nullptr) cgp = 0;
-  GG_REQUIRE(cgp == 0 || cgp == 2, GG_ERR_VALUE, "block basis: plain or fused CG only");
-  GG_REQUIRE(cgp == 0 || d >= 3, GG_ERR_VALUE, "block basis CG: d >= 3");
+  GG_REQUIRE(cgp == 0 || cgp == 2 || cgp == 3, GG_ERR_VALUE,
+             "block basis: plain, fused CG or fused Lanczos only");
+  GG_REQUIRE(cgp == 0 || d >= 3, GG_ERR_VALUE, "block basis CG / Lanczos: d >= 3");
   GG_REQUIRE(x != y, GG_ERR_VALUE, "x and y must not alias");
   if (cgp == 2)
     GG_REQUIRE(cg->q_old == y && cg->p_out != nullptr && cg->p_out != x &&
                    cg->blk_q_out != nullptr && cg->blk_q_out != y,
                GG_ERR_VALUE, "block CG: buffer roles");
+  else if (cgp == 3)
+    // Lanczos: x = u_prev (w written over it), cg->r = u, y = the previous
+    // output (the chain runs in place on it), the pair launch writes blk_q_out
+    GG_REQUIRE(cg->q_old == y && cg->p_out == x && cg->r != nullptr && cg->r != x &&
+                   cg->r != y && cg->coef != nullptr && cg->blk_q_out != nullptr &&
+                   cg->blk_q_out != y && cg->blk_q_out != x && cg->blk_q_out != cg->r,
+               GG_ERR_VALUE, "block Lanczos: buffer roles");
   else if (d >= 3)
     GG_REQUIRE(work != nullptr && work != x && work != y, GG_ERR_VALUE,
                "block basis: scratch required");
   if (ev) GG_HIP(hipEventRecord(ev[0], stream));
   const double* src = x;
-  double* chain = cgp == 2 ? y : work;
+  double* chain = cgp >= 2 ? y : work;
   int pos = 0;
   // the fused CG's x side job: in the pair launch where the LDS pair kernel
   // runs (beside its MFMA-bound slab products), else in the second launch (a
   // streaming kernel after the first when d = 3)
-  const bool side = cgp == 2 && cg->sx != nullptr && cg->xdefer == 2;
-  const bool pair_side = side && B->pair_lds && !(B->pair_abl & 32);
+  const bool side = cgp == 2 && cg->sx != nullptr && (cg->xdefer == 2 || cg->xdefer == 3);
+  const bool pair_side = side && B->pair_lds;
+  // mode 3 (the window): in the pair launch only (gg_cg_start picks it where
+  // block_pair_side holds)
+  const bool win = side && cg->xdefer == 3;
+  GG_REQUIRE(!win || (pair_side && cg->xwin >= 2 && cg->xwin <= kXWinMax), GG_ERR_VALUE,
+             "block CG: the x window needs the LDS pair launch");
   // (a share of each x half on a concurrent stream beside the plain launch
   // measured slower: 20 % of it made the plain launch +0.76 ms and the pair
   // launch -0.55 ms, profiles/r05/za_conc)
@@ -1910,6 +2041,8 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     int kind = 0;
     if (cgp == 2 && k == 0)
       kind = B->pro_nt ? 3 : 1;
+    else if (cgp == 3 && k == 0)
+      kind = 4;
     else if (k == 1 && side && !pair_side)
       kind = 2;
     const int W = mode_waves(kind, B, k);
@@ -1925,6 +2058,14 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
       a.sc = cg->sc;
       a.rr_part = cg->rr_part;
       a.pqo_stride = cg->pqo_stride;
+      GG_REQUIRE(grid <= cg->rr_cap, GG_ERR_VALUE, "prologue partial array too short");
+      if (cg->pro_blocks != nullptr) *cg->pro_blocks = grid;
+    } else if (kind == 4) {
+      a.r = cg->r;
+      a.q_old = cg->q_old;
+      a.p_out = cg->p_out;
+      a.coef = cg->coef;
+      a.rr_part = cg->rr_part;
       GG_REQUIRE(grid <= cg->rr_cap, GG_ERR_VALUE, "prologue partial array too short");
       if (cg->pro_blocks != nullptr) *cg->pro_blocks = grid;
     } else if (kind == 2) {
@@ -1954,19 +2095,20 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
   // the pair launch
   PairArgs p{};
   p.X = src;
-  p.Y = cgp == 2 ? cg->blk_q_out : y;
+  p.Y = cgp >= 2 ? cg->blk_q_out : y;
   const int k3 = d - 1, k2 = d - 2;
   p.f3S = B->frag[k3][0];
   p.f3T = B->frag[k3][1];
   p.f2S = B->frag[k2][0];
   p.f2T = B->frag[k2][1];
-  p.spb = B->nb / (B->h[k3] * B->h[k2]);
+  p.spb = B->nb / (B->e[k3] * B->e[k2]);
   p.nslab = p.spb * nblk;
   p.blk0 = blk0;
   p.skip = skip;
-  p.abl = B->pair_abl;
   const int grid = pair_grid(B, nblk);
-  if (cgp == 2) {
+  if (cgp >= 2) {
+    // q = Z + shift p_new (CG) / Y = Z + shift w (Lanczos) with the p.q, q.q
+    // partials (Lanczos: u.Y for alpha)
     p.P = cg->p_out;
     p.shift = shift;
     p.partials = dot_partials;
@@ -1975,7 +2117,14 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     p.P = x;
     p.shift = shift;
   }
-  if (pair_side) {
+  if (pair_side && win) {
+    p.sc = cg->sc;
+    p.sx = cg->sx;
+    p.sn = cg->sn;
+    p.sreg_len = xwin_region(cg->sn, cg->xwin);
+    const int64_t slots = p.nslab / B->pair_spw * 2 * B->pair_spw;
+    p.sstep = 2 * ceil_div(std::max<int64_t>(p.sreg_len, 1), 2 * slots);
+  } else if (pair_side) {
     p.sc = cg->sc;
     p.sx = cg->sx;
     const int64_t sn = cg->sn;
@@ -1988,16 +2137,32 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     const int64_t slots = p.nslab / B->pair_spw * 2 * B->pair_spw;
     p.sstep = 2 * ceil_div(std::max<int64_t>(std::max(p.sn, p.sn_h1), 1), 2 * slots);
   }
+  // non-temporal epilogue streams: the CG's (with its side job) and the
+  // Lanczos step's (cgp 3); the plain / shifted matvec keeps normal ones
   hipLaunchKernelGGL(select_pair(B->pTF, B->pair_lds, B->pair_spw, p.P != nullptr, pair_side,
-                                 B->epi_nt),
+                                 B->epi_nt && (pair_side || cgp == 3), win),
                      dim3(grid), dim3(B->pair_lds ? 128 * B->pair_spw : 64 * kBlkPairWaves), 0,
                      stream, p);
   GG_LAUNCH_CHECK();
   if (ev) GG_HIP(hipEventRecord(ev[++pos], stream));
-  if (n_partials) *n_partials = (cgp == 2) ? grid : 0;
+  if (n_partials) *n_partials = (cgp >= 2) ? grid : 0;
 }
 
 // the x side job's half boundary in the block path (the closing flush uses it)
 int64_t block_side_half(int64_t n) { return 2 * ceil_div(n, (int64_t)4); }
+
+bool block_pair_side(const BlockOp* B) { return B != nullptr && B->pair_lds; }
+
+// the padded slabs cost (hp / h)^2 of every pass over the vector; up to 1.3x
+// (h = 48 / 64 / 50 .. -> 52 / 68 / 52: 1.17 / 1.13 / 1.08) the block basis's
+// 12-13 passes still beat the grid basis's 15, beyond it (h = 24 -> 36: 2.25x,
+// h = 32 -> 36: 1.27x is inside) one GPU keeps the grid basis by default; the
+// block-sharded CG takes it regardless (no exchange across ranks)
+bool block_efficient(const BlockOp* B) {
+  if (B == nullptr) return false;
+  const int d = B->d;
+  const double pad = (double)(B->e[d - 1] * B->e[d - 2]) / (double)(B->h[d - 1] * B->h[d - 2]);
+  return pad <= 1.3;
+}
 
 }  // namespace gg

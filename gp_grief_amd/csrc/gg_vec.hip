@@ -280,10 +280,81 @@ __global__ __launch_bounds__(kVecThreads) void cg_x_flush2_kernel(double* __rest
   }
 }
 
+// The CG prologue's stream pattern alone (gg_cg_calibrate): per element,
+// read p_old, r and q, write r, p_new and q -- the six passes of the fused
+// prologue launch over the same buffers, with its non-temporal mask (every
+// stream but the q write, the launch's output Y), values passed through
+// unchanged (r = r, p_new = p_old, q = q; the loaded values pass an opaque
+// asm so the compiler cannot drop a store of what was just loaded from the
+// same address).  No MFMA work: the launch's memory floor on this box.
+__global__ __launch_bounds__(256) void cg_stream_probe_kernel(double* __restrict__ r,
+                                                              const double* __restrict__ p,
+                                                              double* __restrict__ p2,
+                                                              double* __restrict__ q,
+                                                              int64_t n) {
+  typedef double v2 __attribute__((ext_vector_type(2)));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 2;
+  constexpr int kU = 2;
+  int64_t i = 2 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  for (; i + (kU - 1) * stride + 1 < n; i += kU * stride) {
+    v2 a[kU], b[kU], c[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      a[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p + i + u * stride));
+      b[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(r + i + u * stride));
+      c[u] = __builtin_nontemporal_load(reinterpret_cast<const v2*>(q + i + u * stride));
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) asm volatile("" : "+v"(a[u]), "+v"(b[u]), "+v"(c[u]));
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      __builtin_nontemporal_store(b[u], reinterpret_cast<v2*>(r + i + u * stride));
+      __builtin_nontemporal_store(a[u], reinterpret_cast<v2*>(p2 + i + u * stride));
+      *reinterpret_cast<v2*>(q + i + u * stride) = c[u];
+    }
+  }
+  for (; i < n; i += stride) {
+    p2[i] = p[i];
+    if (i + 1 < n) p2[i + 1] = p[i + 1];
+  }
+}
+
 __global__ void cg_x_flushed_kernel(CgScalars* sc) {
   sc->xpend = 0;
   sc->xh = 2;
   sc->xs = 0;
+}
+
+// x_defer mode 3: every region gets the steps it has not seen, [wa[r], wn)
+// (at most wk of them, all still in the ring) -- the side job's expression
+__global__ __launch_bounds__(kVecThreads) void cg_x_flush3_kernel(double* __restrict__ x,
+                                                                  int64_t n, int64_t R,
+                                                                  const CgScalars* __restrict__ sc) {
+  const int K = sc->wk, slots = K + 1, wn = sc->wn;
+  if (K <= 0) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int r = (int)(i / R);
+    double s = 0.0;
+    for (int t = sc->wa[r]; t < wn; ++t) s += sc->wc[t % slots] * sc->wp[t % slots][i];
+    x[i] = x[i] + s;
+  }
+}
+
+__global__ void cg_x_flushed3_kernel(CgScalars* sc) {
+  for (int r = 0; r < kXWinMax; ++r) sc->wa[r] = sc->wn;
+  sc->warm = 0;
+}
+
+// x_defer mode 3 at gg_cg_start: window K, nothing applied or armed
+__global__ void cg_xwin_init_kernel(CgScalars* sc, int K) {
+  sc->wk = K;
+  sc->wn = 0;
+  sc->wnext = 0;
+  sc->warm = 0;
+  sc->sreg = 0;
+  sc->scnt = 0;
+  for (int r = 0; r < kXWinMax; ++r) sc->wa[r] = 0;
 }
 
 // Fused recurrence, end of iteration j (after the last mode product):
@@ -335,6 +406,12 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
   __syncthreads();
   const double rr = block_sum(a3);
   if (threadIdx.x == 0) {
+    // mode 3: this iteration's pair launch applied the armed side job (it ran:
+    // done was 0 then, as it is now)
+    if (xmode == 3 && sc->warm) {
+      sc->wa[sc->sreg] = sc->wn;
+      sc->warm = 0;
+    }
     if (pend) {
       sc->rho_prev = sc->rho;
       sc->rho = rr;
@@ -366,7 +443,27 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     sc->beta = sc->repair ? 0.0 : rt / rho;
     sc->first = 0;
     sc->pending = 1;
-    if (p_new != nullptr && xmode == 2) {
+    if (p_new != nullptr && xmode == 3) {
+      // step wn = (alpha_j, p_j) into the ring, then arm the next region with
+      // every step it has not seen (wk at most: it was armed wk arms ago)
+      const int K = sc->wk, slots = K + 1;
+      const int j = sc->wn;
+      sc->wc[j % slots] = alpha;
+      sc->wp[j % slots] = p_new;
+      sc->wn = j + 1;
+      const int reg = sc->wnext;
+      sc->wnext = reg + 1 == K ? 0 : reg + 1;
+      const int a = sc->wa[reg];
+      const int cnt = sc->wn - a;
+      sc->sreg = reg;
+      sc->scnt = cnt;
+      for (int t = 0; t < kXWinMax; ++t) {
+        const int i = a + (t < cnt ? t : 0);
+        sc->scoef[t] = t < cnt ? sc->wc[i % slots] : 0.0;
+        sc->sdir[t] = sc->wp[i % slots];
+      }
+      sc->warm = cnt > 0 ? 1 : 0;
+    } else if (p_new != nullptr && xmode == 2) {
       if (sc->xh < 2) sc->xh += 1;   // this iteration's side job took a half
       if (!sc->xs) {
         sc->xs = 1;
@@ -456,6 +553,10 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->xpend = 0;
     sc->xh = 2;
     sc->xs = 0;
+    sc->wn = 0;
+    sc->wnext = 0;
+    sc->warm = 0;
+    for (int r = 0; r < kXWinMax; ++r) sc->wa[r] = 0;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -531,6 +632,41 @@ __global__ void lz_beta_kernel(double* __restrict__ lzs, double* __restrict__ be
   *beta = b;
   lzs[1] = lzs[0];
   lzs[0] = b > 0.0 ? 1.0 / b : 0.0;
+}
+
+// The block-basis Lanczos step's scalars (lanczos_block), after step j's
+// three launches: rr = |w_{j-1}|^2 (the prologue's partials; |u_0|^2 = 1 at
+// j = 0), dot = u_j.Y_j (the pair launch's p.q partials).  beta_{j-1} =
+// sqrt(rr), v_j = u_j / beta_{j-1} (sV), v_{j-1} = sP u_{j-1} (the previous
+// sV), alpha_j = sV^2 dot, and the next prologue's w_j = A v_j - alpha_j v_j -
+// beta_{j-1} v_{j-1} = cy Y_j + cu u_j + cp u_{j-1}.
+// lzs: [0] sV, [1] sP, [2] cy, [3] cu, [4] cp
+__global__ __launch_bounds__(1024) void lzb_step_kernel(const double* __restrict__ rr_part,
+                                                        int64_t nrr,
+                                                        const double* __restrict__ dot_part,
+                                                        int64_t ndot, double* __restrict__ lzs,
+                                                        double* __restrict__ alpha_out,
+                                                        double* __restrict__ beta_out,
+                                                        int first) {
+  double a0 = 0.0, a1 = 0.0;
+  for (int64_t i = threadIdx.x; i < nrr; i += blockDim.x) a0 += rr_part[i];
+  for (int64_t i = threadIdx.x; i < ndot; i += blockDim.x) a1 += dot_part[i];
+  const double rr = block_sum(a0);
+  __syncthreads();
+  const double dot = block_sum(a1);
+  if (threadIdx.x == 0) {
+    const double beta = sqrt(rr);
+    if (!first) *beta_out = beta;
+    const double sP = lzs[0];
+    const double sV = beta > 0.0 ? 1.0 / beta : 0.0;
+    const double alpha = sV * sV * dot;
+    *alpha_out = alpha;
+    lzs[0] = sV;
+    lzs[1] = sP;
+    lzs[2] = sV;
+    lzs[3] = -alpha * sV;
+    lzs[4] = first ? 0.0 : -beta * sP;
+  }
 }
 
 // A[i][j] *= w[i] (mode 0) or /= w[i] (mode 1); square (mode 2): A = A * A
@@ -666,6 +802,24 @@ static KronDiag make_diag(int d, const int64_t* m, int64_t* n_out) {
 
 // ------------------------------------------------------------------- CG state
 namespace gg {
+// RAII set of HIP events (timed Lanczos, calibration)
+struct EventSet {
+  std::vector<hipEvent_t> ev;
+  explicit EventSet(size_t n) {
+    ev.reserve(n);
+    for (size_t i = 0; i < n; ++i) {
+      hipEvent_t e;
+      GG_HIP(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+  }
+  ~EventSet() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  EventSet(const EventSet&) = delete;
+  EventSet& operator=(const EventSet&) = delete;
+};
+
 // a handle's scalar block: zeroed, with the cancellation threshold of the
 // knob snapshot (GG_CG_CANCEL_TOL, tests: forces the repair / restart paths)
 static void scalars_clear(CgScalars* sc) {
@@ -726,8 +880,73 @@ struct gg_cg {
   // cancelled beta (p = r) as a sharded rank does instead of repairing it --
   // the restart penalty measured on one GPU with everything else equal
   bool restart = false;
+  // x_defer mode 3 (window; block basis with the LDS pair launch): the window
+  // requested at create (GG_CG_XWIN, 0 = the balanced pairs of mode 2), the
+  // mode in effect for the current solve (gg_cg_start*), and the ring of
+  // xwin + 1 direction buffers (slots 0..3 are p, p2, p3, p4 as created; the
+  // rest lie past the scratch region) with the current direction at pcur
+  int xwin = 0;
+  int xmode = 0;
+  double* ring[gg::kXWinMax + 1] = {};
+  int pcur = 0;
+  double *q_c = nullptr, *q2_c = nullptr;   // q / q2 as created (swapped per iteration)
   int launches() const { return block ? gg::block_launches(blk) : gg::kron_d(K); }
+  int nring() const { return xmode == 3 ? xwin + 1 : 4; }
+  // the length of the recurrence's vectors: the grid's n, or the block
+  // layout's (padded pair axes: >= n) for a full handle in the block basis
+  // (a block-range handle's n is already its blocks' length)
+  int64_t nvec() const { return (block && rnblk < 0) ? gg::block_n(blk) : n; }
+  // every solve starts from the buffers as created (a block solve swaps q / q2
+  // and rotates the directions)
+  void reset_buffers() {
+    p = ring[0];
+    p2 = ring[1];
+    p3 = ring[2];
+    p4 = ring[3];
+    q = q_c;
+    q2 = q2_c;
+    pcur = 0;
+  }
+  // after an iteration's scalars: p_new (p2) becomes the current direction
+  void rotate_dirs() {
+    if (xmode == 3) {
+      const int ns = nring();
+      pcur = (pcur + 1) % ns;
+      p = ring[pcur];
+      p2 = ring[(pcur + 1) % ns];
+    } else if (xmode == 2) {
+      // (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2}): the
+      // active pair (at most p_{j-1}, p_{j-2} next iteration) stays alive
+      double* cur = p;
+      double* o2 = p3;
+      p = p2;
+      p2 = p4;
+      p3 = cur;
+      p4 = o2;
+    } else if (xmode == 1) {
+      // (cur, free, old) <- (free, old, cur): p_j becomes current, p_{j-1}
+      // is kept one more iteration for the deferred x update
+      double* old_ = p3;
+      p3 = p;
+      p = p2;
+      p2 = old_;
+    } else {
+      std::swap(p, p2);
+    }
+  }
 };
+
+namespace gg {
+// x_defer mode 3's window from the knob snapshot (GG_CG_XWIN; < 2: off)
+static int cg_xwin_knob() {
+  const char* e = knob("GG_CG_XWIN");
+  const int k = e ? atoi(e) : kXWinDefault;
+  return k < 2 ? 0 : std::min(k, kXWinMax);
+}
+// direction buffers beyond the four every handle has
+static int64_t cg_extra_dirs(int K) { return K >= 2 ? std::max(0, K + 1 - 4) : 0; }
+int64_t xwin_region(int64_t n, int K) { return 2 * ceil_div(n, 2 * (int64_t)K); }
+}  // namespace gg
 
 extern "C" {
 
@@ -847,6 +1066,23 @@ static int64_t cg_vec_pad() {
 static int64_t cg_vec_stride(int64_t n) { return (n + 31) / 32 * 32 + cg_vec_pad(); }
 constexpr int64_t kCgAlignSlack = 32;   // doubles: room to round the base up to 256 B
 
+// gg_cg_create's layout: r, p, q, p2, p3, p4, then the scratch region (the
+// matvec scratch, or xb and q2 in the block basis), then the window's extra
+// direction buffers; *extra_off = where those start (from the aligned base)
+static int64_t cg_layout_elems(const gg_kron* K, int64_t n, int64_t* extra_off = nullptr,
+                               int* xwin = nullptr, int64_t* vstride = nullptr) {
+  const gg::BlockOp* B = gg::kron_block(K);
+  // every vector holds the grid's n or the block layout's (padded) length
+  const int64_t vs = cg_vec_stride(B ? std::max(n, gg::block_n(B)) : n);
+  if (vstride) *vstride = vs;
+  const int64_t scratch = gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
+  const int64_t region = (std::max(scratch, B ? 2 * vs : 0) + 31) / 32 * 32;
+  const int w = (B && gg::block_pair_side(B)) ? gg::cg_xwin_knob() : 0;
+  if (extra_off) *extra_off = 6 * vs + region;
+  if (xwin) *xwin = w;
+  return kCgAlignSlack + 6 * vs + region + gg::cg_extra_dirs(w) * vs;
+}
+
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
@@ -855,9 +1091,8 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
     // r, p, q, p2, p3, p4 (x_defer) + the matvec scratch (+ the first mode
     // product's own output for an odd number of factors, MpFuse::first_dst);
     // the block basis (gg_kronb.hip) takes the scratch region for xb and q2
-    const int64_t scratch = gg::kron_work_elems(K, false) + (gg::kron_d(K) % 2 == 1 ? n : 0);
-    const int64_t blk = gg::kron_block(K) != nullptr ? 2 * cg_vec_stride(n) : 0;
-    *elems = kCgAlignSlack + 6 * cg_vec_stride(n) + std::max(scratch, blk);
+    // + the window's extra direction buffers (x_defer mode 3, block basis)
+    *elems = cg_layout_elems(K, n);
   });
 }
 
@@ -869,8 +1104,10 @@ int gg_cg_work_elems_blocks(const gg_kron* K, int64_t nblk, int64_t* elems) {
     GG_REQUIRE(nblk >= 1 && nblk <= ((int64_t)1 << gg::block_d(B)), GG_ERR_VALUE,
                "block count outside 1..2^d");
     gg::knobs_reload();   // the CG handle made next latches this snapshot
-    // r, p, q, p2, p3, p4 and q2 (the pair launch's q)
-    *elems = kCgAlignSlack + 7 * cg_vec_stride(nblk * gg::block_nb(B));
+    // r, p, q, p2, p3, p4 and q2 (the pair launch's q), then the window's
+    // extra direction buffers (x_defer mode 3)
+    const int w = gg::block_pair_side(B) ? gg::cg_xwin_knob() : 0;
+    *elems = kCgAlignSlack + (7 + gg::cg_extra_dirs(w)) * cg_vec_stride(nblk * gg::block_nb(B));
   });
 }
 
@@ -901,6 +1138,14 @@ int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shi
       cg->p3 = work_dev + 4 * vs;
       cg->p4 = work_dev + 5 * vs;
       cg->q2 = work_dev + 6 * vs;
+      cg->xwin = gg::block_pair_side(B) ? gg::cg_xwin_knob() : 0;
+      cg->ring[0] = cg->p;
+      cg->ring[1] = cg->p2;
+      cg->ring[2] = cg->p3;
+      cg->ring[3] = cg->p4;
+      for (int i = 0; i < gg::cg_extra_dirs(cg->xwin); ++i) cg->ring[4 + i] = work_dev + (7 + i) * vs;
+      cg->q_c = cg->q;
+      cg->q2_c = cg->q2;
       cg->blk = B;
       cg->basis = 1;
       cg->rblk0 = blk0;
@@ -936,7 +1181,8 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->K = K;
       cg->shift = shift;
       cg->n = nr;
-      const int64_t vs = cg_vec_stride(nr);
+      int64_t vs = 0;
+      cg_layout_elems(K, nr, nullptr, nullptr, &vs);
       GG_REQUIRE((reinterpret_cast<uintptr_t>(work_dev) & 7) == 0, GG_ERR_VALUE,
                  "the CG workspace must hold doubles (8-byte aligned)");
       work_dev = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(work_dev) + 255) &
@@ -950,11 +1196,25 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->mv_work = work_dev + 6 * vs;
       if (gg::kron_d(K) % 2 == 1) cg->first_dst = cg->mv_work + gg::kron_work_elems(K, false);
       cg->blk = gg::kron_block(K);
+      int64_t extra_off = 0;
+      int xwin = 0;
+      cg_layout_elems(K, nr, &extra_off, &xwin);
+      cg->ring[0] = cg->p;
+      cg->ring[1] = cg->p2;
+      cg->ring[2] = cg->p3;
+      cg->ring[3] = cg->p4;
+      cg->q_c = cg->q;
       if (cg->blk != nullptr) {
         cg->xb = work_dev + 6 * vs;
         cg->q2 = work_dev + 7 * vs;
+        cg->q2_c = cg->q2;
         const char* be = gg::knob("GG_CG_BASIS");   // read once per handle
-        if (be) cg->basis = atoi(be) != 0 ? 1 : 0;
+        // default: the block basis where its padding costs little
+        cg->basis = be ? (atoi(be) != 0 ? 1 : 0) : (gg::block_efficient(cg->blk) ? 1 : 0);
+        // the window only where the pair launch carries the side job
+        cg->xwin = gg::block_pair_side(cg->blk) ? xwin : 0;
+        for (int i = 0; i < gg::cg_extra_dirs(xwin); ++i)
+          cg->ring[4 + i] = work_dev + extra_off + i * vs;
       } else {
         cg->basis = 0;
       }
@@ -1047,11 +1307,17 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
     const int64_t n = cg->n;
     cg->block = cg->blk != nullptr && cg->basis != 0 && cg->fused && cg->fusion == 0 &&
                 cg->xdefer == 2 && cg->rq == 1 && gg::block_d(cg->blk) >= 3;
+    cg->xmode = (cg->fused && cg->fusion != 2) ? cg->xdefer : 0;
+    if (cg->block && cg->xwin >= 2) cg->xmode = 3;
+    cg->reset_buffers();
+    hipLaunchKernelGGL(gg::cg_xwin_init_kernel, dim3(1), dim3(1), 0, s, cg->sc,
+                       cg->xmode == 3 ? cg->xwin : 0);
+    GG_LAUNCH_CHECK();
     GG_HIP(hipMemsetAsync(x_dev, 0, n * sizeof(double), s));
     if (cg->block) {
       // r = P b (the fold, with its |P b|^2 partials), x_b = 0
       gg::block_fold(cg->blk, false, b_dev, cg->r, cg->partials, s);
-      GG_HIP(hipMemsetAsync(cg->xb, 0, n * sizeof(double), s));
+      GG_HIP(hipMemsetAsync(cg->xb, 0, cg->nvec() * sizeof(double), s));
       hipLaunchKernelGGL(gg::cg_init_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
                          gg::block_fold_partials(cg->blk), cg->sc, rtol, atol);
       GG_LAUNCH_CHECK();
@@ -1083,6 +1349,7 @@ int gg_cg_set_recurrence(gg_cg* cg, int fused) {
 int gg_cg_set_fusion(gg_cg* cg, int layout) {
   return gg::guard([&] {
     GG_REQUIRE(cg, GG_ERR_VALUE, "NULL handle");
+    GG_REQUIRE(cg->x == nullptr, GG_ERR_VALUE, "set the fusion layout before gg_cg_start");
     GG_REQUIRE(layout >= 0 && layout <= 2, GG_ERR_VALUE, "fusion layout must be 0, 1 or 2");
     GG_REQUIRE(layout == 0 || gg::kron_first_single_launch(cg->K), GG_ERR_VALUE,
                "fusion layouts 1 / 2 need the first factor within one launch (<= 256 rows)");
@@ -1110,6 +1377,51 @@ int gg_cg_get_xdefer(const gg_cg* cg, int* on) {
   return gg::guard([&] {
     GG_REQUIRE(cg && on, GG_ERR_VALUE, "NULL argument");
     *on = (cg->fused && cg->fusion != 2) ? cg->xdefer : 0;
+  });
+}
+
+int gg_cg_get_xwin(const gg_cg* cg, int* K) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && K, GG_ERR_VALUE, "NULL argument");
+    if (cg->x != nullptr) {
+      *K = cg->xmode == 3 ? cg->xwin : 0;
+    } else {
+      int b = 0;
+      gg_cg_get_basis(cg, &b);
+      *K = (b && cg->xwin >= 2) ? cg->xwin : 0;
+    }
+  });
+}
+
+int gg_cg_calibrate(gg_cg* cg, int reps, double* ms_host, int64_t* offsets_host,
+                    gg_stream stream) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && ms_host && reps >= 1, GG_ERR_VALUE, "bad argument");
+    GG_REQUIRE((reinterpret_cast<uintptr_t>(cg->p) & 15) == 0, GG_ERR_VALUE,
+               "the CG workspace is not 16-byte aligned");
+    hipStream_t s = gg::as_stream(stream);
+    int dev = 0, cus = 0;
+    GG_HIP(hipGetDevice(&dev));
+    GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    gg::EventSet ev(2);
+    // one untimed pass (first touch of p2 in this process), then reps timed
+    for (int it = 0; it <= reps; ++it) {
+      if (it == 1) GG_HIP(hipEventRecord(ev.ev[0], s));
+      hipLaunchKernelGGL(gg::cg_stream_probe_kernel, dim3((unsigned)std::max(cus, 1) * 8),
+                         dim3(256), 0, s, cg->r, cg->p, cg->p2, cg->q, cg->nvec());
+      GG_LAUNCH_CHECK();
+    }
+    GG_HIP(hipEventRecord(ev.ev[1], s));
+    GG_HIP(hipEventSynchronize(ev.ev[1]));
+    float ms = 0.f;
+    GG_HIP(hipEventElapsedTime(&ms, ev.ev[0], ev.ev[1]));
+    *ms_host = ms / reps;
+    if (offsets_host) {
+      // the buffers' addresses modulo 2 MiB (the allocator's large-page grain)
+      const double* b[4] = {cg->r, cg->p, cg->p2, cg->q};
+      for (int k = 0; k < 4; ++k)
+        offsets_host[k] = (int64_t)(reinterpret_cast<uintptr_t>(b[k]) & ((1u << 21) - 1));
+    }
   });
 }
 
@@ -1188,8 +1500,10 @@ int gg_cg_iterate(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
 int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
+    GG_REQUIRE(cg->rnblk < 0, GG_ERR_VALUE,
+               "a block-range handle (gg_cg_create_blocks) runs through gg_cg_iterate_partial");
     hipStream_t s = gg::as_stream(stream);
-    const int64_t n = cg->n;
+    const int64_t n = cg->nvec();
     const int nb = gg::vec_blocks(n);
     if (check_every <= 0) check_every = max_iters;
     for (int it = 0; it < max_iters; ++it) {
@@ -1205,8 +1519,8 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         ev = cg->events.data() + cg->events_used;
         cg->events_used = need;
       }
-      const bool xdefer = cg->fused && cg->xdefer != 0 && cg->fusion != 2;
-      const int xmode = xdefer ? cg->xdefer : 0;
+      const int xmode = cg->xmode;   // fixed at gg_cg_start
+      const bool xdefer = xmode != 0;
       if (cg->fused) {
         // repair (no-op unless the last beta cancelled): x += alpha p,
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
@@ -1235,6 +1549,7 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         fz.sp = cg->p;
         fz.sn = n;
         fz.xdefer = xmode;
+        fz.xwin = cg->xwin;
         fz.first_dst = cg->first_dst;
         // r.q: conjugacy identity (layout 0: the prologue adds p_new.q_old
         // partials, the epilogue skips its pass over r) or read in the epilogue
@@ -1260,25 +1575,7 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
                            xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
         GG_LAUNCH_CHECK();
         if (cg->block) std::swap(cg->q, cg->q2);
-        if (xmode == 2) {
-          // (cur, free, p_{j-2}, p_{j-3}) <- (free, p_{j-3}, cur, p_{j-2}): the
-          // active pair (at most p_{j-1}, p_{j-2} next iteration) stays alive
-          double* cur = cg->p;
-          double* o2 = cg->p3;
-          cg->p = cg->p2;
-          cg->p2 = cg->p4;
-          cg->p3 = cur;
-          cg->p4 = o2;
-        } else if (xdefer) {
-          // (cur, free, old) <- (free, old, cur): p_j becomes current, p_{j-1}
-          // is kept one more iteration for the deferred x update
-          double* old_ = cg->p3;
-          cg->p3 = cg->p;
-          cg->p = cg->p2;
-          cg->p2 = old_;
-        } else {
-          std::swap(cg->p, cg->p2);
-        }
+        cg->rotate_dirs();
       } else {
         gg::MpFuse fz;
         fz.r = cg->r;
@@ -1310,15 +1607,23 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
 int gg_cg_close(gg_cg* cg, gg_stream stream) {
   return gg::guard([&] {
     GG_REQUIRE(cg && cg->x, GG_ERR_VALUE, "CG not started");
+    GG_REQUIRE(cg->rnblk < 0, GG_ERR_VALUE,
+               "a block-range handle (gg_cg_create_blocks) closes through gg_cg_close_partial");
     hipStream_t s = gg::as_stream(stream);
-    const int64_t n = cg->n;
+    const int64_t n = cg->nvec();
     const int nb = gg::vec_blocks(n);
     if (cg->fused) {
-      const bool xdefer = cg->xdefer != 0 && cg->fusion != 2;
+      const bool xdefer = cg->xmode != 0;
       // closing update (no-op unless pending): x += alpha p, r -= alpha q,
       // rho = r.r, beta, iteration count -- the textbook state.  x_defer: the
       // deferred steps first (also after convergence), then r only
-      if (xdefer && cg->xdefer == 2) {
+      if (cg->xmode == 3) {
+        hipLaunchKernelGGL(gg::cg_x_flush3_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           cg->block ? cg->xb : cg->x, n, gg::xwin_region(n, cg->xwin), cg->sc);
+        GG_LAUNCH_CHECK();
+        hipLaunchKernelGGL(gg::cg_x_flushed3_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+        GG_LAUNCH_CHECK();
+      } else if (cg->xmode == 2) {
         hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                            cg->block ? cg->xb : cg->x, n,
                            cg->block ? gg::block_side_half(n) : gg::kron_side_half(cg->K, n),
@@ -1361,6 +1666,12 @@ int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* r
     // the block layout (gg_cg_create_blocks; b and x in that layout)
     cg->block = cg->rnblk > 0;
     cg->await_finish = false;
+    cg->xmode = cg->xdefer;
+    if (cg->block && cg->xwin >= 2) cg->xmode = 3;
+    cg->reset_buffers();
+    hipLaunchKernelGGL(gg::cg_xwin_init_kernel, dim3(1), dim3(1), 0, s, cg->sc,
+                       cg->xmode == 3 ? cg->xwin : 0);
+    GG_LAUNCH_CHECK();
     const int64_t n = cg->n;
     GG_HIP(hipMemcpyAsync(cg->r, b_dev, n * sizeof(double), hipMemcpyDeviceToDevice, s));
     GG_HIP(hipMemsetAsync(x_dev, 0, n * sizeof(double), s));
@@ -1404,7 +1715,7 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     }
     // no repair kernels: a cancelled beta (set to 0 by the scalars) restarts
     // the recurrence with p = r instead of a second all-reduce
-    const int xmode = cg->xdefer;
+    const int xmode = cg->xmode;
     gg::MpFuse fz;
     fz.r = cg->r;
     fz.q_old = cg->q;
@@ -1418,6 +1729,7 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     fz.sp = cg->p;
     fz.sn = n;
     fz.xdefer = xmode;
+    fz.xwin = cg->xwin;
     fz.first_dst = cg->first_dst;
     const bool rq_ident = cg->rq != 0;
     fz.er = rq_ident ? nullptr : cg->r;
@@ -1448,28 +1760,14 @@ int gg_cg_iterate_finish(gg_cg* cg, const double* red_dev, gg_stream stream) {
     GG_REQUIRE(cg && red_dev, GG_ERR_VALUE, "NULL argument");
     GG_REQUIRE(cg->await_finish, GG_ERR_VALUE, "gg_cg_iterate_partial first");
     hipStream_t s = gg::as_stream(stream);
-    const int xmode = cg->xdefer;
+    const int xmode = cg->xmode;
     const bool rq_ident = cg->rq != 0;
     // red = [rr, p.q_old | p.q, r.q, q.q]: one-element partial arrays
     hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, red_dev,
                        (int64_t)1, (int64_t)1, red_dev + 2, (int64_t)1, (int64_t)1, cg->sc,
                        xmode ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
     GG_LAUNCH_CHECK();
-    if (xmode == 2) {
-      double* cur = cg->p;
-      double* o2 = cg->p3;
-      cg->p = cg->p2;
-      cg->p2 = cg->p4;
-      cg->p3 = cur;
-      cg->p4 = o2;
-    } else if (xmode == 1) {
-      double* old_ = cg->p3;
-      cg->p3 = cg->p;
-      cg->p = cg->p2;
-      cg->p2 = old_;
-    } else {
-      std::swap(cg->p, cg->p2);
-    }
+    cg->rotate_dirs();
     cg->await_finish = false;
   });
 }
@@ -1481,24 +1779,30 @@ int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream) {
     hipStream_t s = gg::as_stream(stream);
     const int64_t n = cg->n;
     const int nb = gg::vec_blocks(n);
-    if (cg->xdefer == 2) {
+    if (cg->xmode == 3) {
+      hipLaunchKernelGGL(gg::cg_x_flush3_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
+                         gg::xwin_region(n, cg->xwin), cg->sc);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::cg_x_flushed3_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+      GG_LAUNCH_CHECK();
+    } else if (cg->xmode == 2) {
       hipLaunchKernelGGL(gg::cg_x_flush2_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
                          cg->block ? gg::block_side_half(n) : gg::kron_side_half(cg->K, n),
                          cg->sc);
       GG_LAUNCH_CHECK();
-    } else if (cg->xdefer == 1) {
+    } else if (cg->xmode == 1) {
       hipLaunchKernelGGL(gg::cg_x_flush_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s, cg->x, n,
                          cg->sc);
       GG_LAUNCH_CHECK();
     }
-    if (cg->xdefer) {
+    if (cg->xmode == 1 || cg->xmode == 2) {
       hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
       GG_LAUNCH_CHECK();
     }
     // the pending r update (x: the x_defer bookkeeping above, or here)
     GG_HIP(hipMemsetAsync(cg->partials, 0, nb * sizeof(double), s));
     hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                       cg->xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                       cg->xmode ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
                        cg->partials, 1);
     GG_LAUNCH_CHECK();
     gg::launch_reduce_to(cg->partials, nb, rr_dev, s);
@@ -1545,23 +1849,6 @@ int gg_cg_status(gg_cg* cg, int* iters, int* converged, double* resid_norm, doub
 
 namespace gg {
 
-// RAII set of HIP events (timed Lanczos)
-struct EventSet {
-  std::vector<hipEvent_t> ev;
-  explicit EventSet(size_t n) {
-    ev.reserve(n);
-    for (size_t i = 0; i < n; ++i) {
-      hipEvent_t e;
-      GG_HIP(hipEventCreate(&e));
-      ev.push_back(e);
-    }
-  }
-  ~EventSet() {
-    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-  }
-  EventSet(const EventSet&) = delete;
-  EventSet& operator=(const EventSet&) = delete;
-};
 
 // gg_lanczos_probe / gg_lanczos_probe_timed.  step_ms (steps entries, may be
 // null): HIP events on the stream at every step boundary -- the first after
@@ -1573,6 +1860,7 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
                           double* work_dev, double* alphas_host, double* betas_host,
                           int* steps_done, double* step_ms, double* launch_ms,
                           gg_stream stream);
+static bool lanczos_use_block(const gg_kron* K);
 
 }  // namespace gg
 
@@ -1584,6 +1872,15 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
   return gg::guard([&] {
     gg::lanczos_probe(K, shift, seed, probe, steps, work_dev, alphas_host, betas_host,
                       steps_done, nullptr, nullptr, stream);
+  });
+}
+
+int gg_lanczos_info(const gg_kron* K, int* block, int* launches) {
+  return gg::guard([&] {
+    GG_REQUIRE(K && block && launches, GG_ERR_VALUE, "NULL argument");
+    const bool b = gg::lanczos_use_block(K);
+    *block = b ? 1 : 0;
+    *launches = b ? gg::block_launches(gg::kron_block(K)) : gg::kron_d(K);
   });
 }
 
@@ -1602,6 +1899,127 @@ int gg_lanczos_probe_timed(const gg_kron* K, double shift, uint64_t seed, int pr
 
 namespace gg {
 
+// the block basis for the probe where the operator has one with d >= 3 (the
+// Lanczos tridiagonal is invariant under the orthogonal fold P: the probe z
+// becomes P z, the operator P K P^T); GG_LZ_BASIS=0 (snapshot) keeps the grid
+static bool lanczos_use_block(const gg_kron* K) {
+  const BlockOp* B = kron_block(K);
+  // unpadded layouts only: the probe's workspace is 4 n (the grid's n)
+  if (B == nullptr || block_d(B) < 3 || block_n(B) != kron_n(K)) return false;
+  const char* e = knob("GG_LZ_BASIS");
+  if (e) return atoi(e) != 0;
+  return block_efficient(B);
+}
+
+// The fused Lanczos step in the parity-block basis: d - 1 launches and 10
+// passes over N per step -- the first launch's prologue forms w_{j-1} = cy Y +
+// cu u + cp u_prev (KIND 4: read Y, u, u_prev, write w over u_prev and the
+// launch's output over Y), the plain launches 2 each, the pair launch reads
+// its slab and w and writes Y_j = (K + shift) w with the u.Y partials.  One
+// fold of the probe before, no unfold (only the tridiagonal leaves).
+static void lanczos_block(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
+                          double* work_dev, double* alphas_host, double* betas_host,
+                          int* steps_done, double* step_ms, double* launch_ms,
+                          gg_stream stream) {
+  hipStream_t s = gg::as_stream(stream);
+  const BlockOp* B = kron_block(K);
+  const int64_t n = block_n(B);
+  const int L = block_launches(B);
+  double* P = work_dev;          // u_prev; w is written over it
+  double* V = work_dev + n;      // u (v = sV u)
+  double* W = work_dev + 2 * n;  // Y of the previous step (the chain runs in place on it)
+  double* W2 = work_dev + 3 * n; // the pair launch's output
+  const int nb = vec_blocks(n);
+  const int64_t npart = std::max<int64_t>(block_partials_needed(B), kVecBlocks);
+  const int64_t nrr = std::max<int64_t>(block_prologue_blocks(B), 1);
+  // [alphas | betas | partials (3 x npart: p.q, r.q, q.q) | |w|^2 partials | lzs(8)]
+  double* scal = nullptr;
+  GG_HIP(hipMallocAsync(&scal, (2 * (size_t)steps + 3 * npart + nrr + 8) * sizeof(double), s));
+  double* alphas = scal;
+  double* betas = scal + steps;
+  double* parts = scal + 2 * steps;
+  double* rrparts = parts + 3 * npart;
+  double* lzs = rrparts + nrr;
+  // step 0's prologue copies u_0: w = 0 Y + 1 u + 0 u_prev (Y, u_prev zeroed)
+  const double init[5] = {1.0, 0.0, 0.0, 1.0, 0.0};
+  GG_HIP(hipMemcpyAsync(lzs, init, sizeof(init), hipMemcpyHostToDevice, s));
+  GG_HIP(hipMemsetAsync(P, 0, n * sizeof(double), s));
+  GG_HIP(hipMemsetAsync(W, 0, n * sizeof(double), s));
+  // the probe (grid layout, |z| = 1) into W2, folded into V
+  hipLaunchKernelGGL(probe_kernel, dim3(nb), dim3(kVecThreads), 0, s, probe_base(seed, probe),
+                     1.0 / std::sqrt((double)n), W2, n);
+  GG_LAUNCH_CHECK();
+  block_fold(B, false, W2, V, nullptr, s);
+  const bool timed = step_ms != nullptr;
+  EventSet sev(timed ? (size_t)steps + 1 : 0);
+  EventSet mev(timed && launch_ms ? (size_t)steps * (L + 1) : 0);
+  auto mp_ev = [&](int j) -> hipEvent_t* {
+    return mev.ev.empty() ? nullptr : mev.ev.data() + (size_t)j * (L + 1);
+  };
+  if (timed) GG_HIP(hipEventRecord(sev.ev[0], s));
+  for (int j = 0; j < steps; ++j) {
+    MpFuse lf;
+    lf.r = V;
+    lf.q_old = W;
+    lf.p_out = P;
+    lf.coef = lzs + 2;
+    lf.rr_part = rrparts;
+    lf.rr_cap = nrr;
+    int64_t pro_blocks = 0;
+    lf.pro_blocks = &pro_blocks;
+    lf.blk_q_out = W2;
+    lf.pstride = npart;
+    int64_t np = 0;
+    block_apply(B, P, W, shift, nullptr, parts, nullptr, s, &np, &lf, 3, mp_ev(j));
+    GG_REQUIRE(pro_blocks > 0 && pro_blocks <= nrr, GG_ERR_RUNTIME,
+               "Lanczos: no prologue launch recorded");
+    hipLaunchKernelGGL(lzb_step_kernel, dim3(1), dim3(1024), 0, s, rrparts, pro_blocks, parts, np,
+                       lzs, alphas + j, j > 0 ? betas + (j - 1) : betas, j == 0 ? 1 : 0);
+    GG_LAUNCH_CHECK();
+    std::swap(P, V);    // u_prev <- u_j's predecessor ... u <- w (= u_j)
+    std::swap(W, W2);   // Y_j becomes the next step's chain
+    if (timed && j + 1 < steps) GG_HIP(hipEventRecord(sev.ev[j + 1], s));
+  }
+  // beta_{steps-1} = |w_{steps-1}| (one streaming pass, in place of Y)
+  const int wide = ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(V) |
+                     reinterpret_cast<uintptr_t>(P)) & 15) == 0;
+  hipLaunchKernelGGL(lz_update_kernel, dim3(nb), dim3(kVecThreads), 0, s, W, V, P, n, lzs + 0,
+                     parts, wide);
+  GG_LAUNCH_CHECK();
+  launch_reduce_to(parts, nb, betas + (steps - 1), s);
+  hipLaunchKernelGGL(lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + (steps - 1));
+  GG_LAUNCH_CHECK();
+  if (timed) GG_HIP(hipEventRecord(sev.ev[steps], s));
+  GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipMemcpyAsync(betas_host, betas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
+  GG_HIP(hipFreeAsync(scal, s));
+  GG_HIP(hipStreamSynchronize(s));
+  if (timed) {
+    for (int j = 0; j < steps; ++j) {
+      float ms = 0.f;
+      GG_HIP(hipEventElapsedTime(&ms, sev.ev[j], sev.ev[j + 1]));
+      step_ms[j] = ms;
+    }
+    if (launch_ms) {
+      const int d = kron_d(K);
+      for (int k = 0; k < d; ++k) launch_ms[k] = 0.0;
+      for (int j = 0; j < steps; ++j)
+        for (int k = 0; k < L; ++k) {
+          float ms = 0.f;
+          GG_HIP(hipEventElapsedTime(&ms, mp_ev(j)[k], mp_ev(j)[k + 1]));
+          launch_ms[k] += ms;
+        }
+    }
+  }
+  int done = steps;
+  for (int j = 0; j < steps; ++j)
+    if (!(betas_host[j] > 1e-300)) {
+      done = j + 1;
+      break;
+    }
+  if (steps_done) *steps_done = done;
+}
+
 static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
                           double* work_dev, double* alphas_host, double* betas_host,
                           int* steps_done, double* step_ms, double* launch_ms,
@@ -1613,6 +2031,11 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
     gg_kron_shape(K, 0, &nr, &nc, &we);
     GG_REQUIRE(nr == nc, GG_ERR_VALUE, "Lanczos needs a square operator");
     GG_REQUIRE(we <= nr, GG_ERR_VALUE, "non-square factors are not supported here");
+    if (lanczos_use_block(K)) {
+      lanczos_block(K, shift, seed, probe, steps, work_dev, alphas_host, betas_host, steps_done,
+                    step_ms, launch_ms, stream);
+      return;
+    }
     hipStream_t s = gg::as_stream(stream);
     const int64_t n = nr;
     double* P = work_dev;        // u_prev (v_prev = sP u_prev)

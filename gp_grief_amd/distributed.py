@@ -833,7 +833,11 @@ def block_range(d, world, rank):
 def block_shard_ok(K, world):
     """world = 2^K <= 2^d and K (a KronMatrix) has a device parity-block
     basis with d >= 3 (every factor square, even-order, centrosymmetric; the
-    last two of equal order h in {20, 36, 100})."""
+    last two of equal order m = 2h with h = 16 TF + 4, TF in 1..6: m in {40,
+    72, 104, 136, 168, 200} -- include/gp_grief_amd.h gg_kron_block_info).
+    Decided on this rank alone: solve() takes the decomposition only when
+    every rank agrees (a rank whose device operator failed must not pick
+    another collective pattern than its peers)."""
     world = int(world)
     if world < 1 or world & (world - 1):
         return False
@@ -871,6 +875,9 @@ class BlockHipEngine(object):
                      "gg_cg_create_blocks")
         self.h = h
         self.shift = float(shift)
+        xw = ctypes.c_int()
+        native.check(L.gg_cg_get_xwin(self.h, ctypes.byref(xw)), "gg_cg_get_xwin")
+        self.xwin = xw.value   # x_defer mode 3's window on this rank (0: pairs)
         _, n, self.launches = self.dk.block_info()
         self.n = n
         self.n_local = n // (1 << self.d) * self.nblk
@@ -983,7 +990,12 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
     n = int(np.prod(m))
     maxiter = 10 * n if maxiter is None else int(maxiter)
     if decomposition == "auto":
-        decomposition = ("block" if engine is not None or block_shard_ok(K, world) else
+        # every rank takes the same decomposition: the block basis only where
+        # all ranks built it (parity_ok is host arithmetic on identical factors)
+        ok = engine is not None or block_shard_ok(K, world)
+        if world > 1:
+            ok = all(ex.all_gather_object(bool(ok)))
+        decomposition = ("block" if ok else
                          "parity" if parity_ok(F, world) else "transpose")
     if decomposition == "block":
         if engine is not None:
@@ -996,7 +1008,7 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
         xl, info = cg.solve(eng.fold(bg), rtol, atol, maxiter, check_every)
         x = eng.unfold(xl)
         ex.all_reduce(x)
-        it = cg.status()[0]
+        it, _, res, tol = cg.status()
         solve.last_cancels = cg.cancels()
     elif decomposition == "parity":
         bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
@@ -1007,7 +1019,7 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
         solve.last_cancels = cg.cancels()
         parts = ex.all_gather_object(dev.to_host(xl))
         x = dev.to_device(parity_unfold(parts, m))
-        it = cg.status()[0]
+        it, _, res, tol = cg.status()
     elif decomposition == "transpose":
         bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
                         dtype=np.float64).reshape(-1)
@@ -1017,10 +1029,13 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
                             maxiter, check_every)
         parts = ex.all_gather_object(dev.to_host(xl))
         x = dev.to_device(gather_global(parts, m))
-        it = cg.status()[0]
+        it, _, rho, tol = cg.status()
+        res = float(np.sqrt(max(rho, 0.0)))
         solve.last_cancels = None
     else:
         raise ValueError("decomposition must be 'auto', 'block', 'parity' or 'transpose'")
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    # the global residual norm and tolerance of the finished solve (linalg.cg.last)
+    solve.last_resid = (float(res), float(tol))
     return x, info, it, decomposition

@@ -166,6 +166,9 @@ class KronCG(object):
             native.check(L.gg_cg_set_basis(h, int(basis == "block")), "gg_cg_set_basis")
         native.check(L.gg_cg_get_basis(h, ctypes.byref(f)))
         self.basis = "block" if f.value else "grid"
+        # the block basis's x window (x_defer mode 3, GG_CG_XWIN; 0: not in effect)
+        native.check(L.gg_cg_get_xwin(h, ctypes.byref(f)))
+        self.xwin = f.value
         self.n = int(K.shape[0])
         self.x = None
 
@@ -204,6 +207,17 @@ class KronCG(object):
                                                ctypes.byref(res), ctypes.byref(tol),
                                                native.stream_ptr()))
         return it.value, bool(conv.value), res.value, tol.value
+
+    def calibrate(self, reps=5):
+        """The fused prologue's six streams alone over this handle's buffers
+        (gg_cg_calibrate; after start, before the iterations): (ms per pass,
+        [r, p_old, p_new, q addresses mod 2 MiB])."""
+        from . import native
+        ms = ctypes.c_double()
+        off = (ctypes.c_int64 * 4)()
+        native.check(native.lib().gg_cg_calibrate(self.h, int(reps), ctypes.byref(ms), off,
+                                                  native.stream_ptr()), "gg_cg_calibrate")
+        return ms.value, [int(v) for v in off]
 
     def cancels(self):
         """Cancelled betas since start (gg_cg_cancels; synchronising)."""
@@ -275,6 +289,12 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         check_every = 10 if n >= 1 << 20 else 50
     if comm is not None:
         from . import distributed
+        # the sharded solve runs its own recurrence (fused, layout 0, in the
+        # decomposition's basis): a non-default choice cannot be honoured there
+        if recurrence != "fused" or fusion not in (None, 0) or basis is not None:
+            raise ValueError("comm=: the sharded CG runs the fused recurrence (layout 0) in "
+                             "the decomposition's own basis; recurrence / fusion / basis "
+                             "cannot be chosen")
         x, info, it, how = distributed.solve(K, bd, shift, comm, rtol, atol, maxiter,
                                              check_every, decomposition)
         if callback is not None:
@@ -282,7 +302,8 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
                 callback()
         out = (x.reshape(tuple(b.shape)) if b.numel() == n else x) if was_dev else \
             dev.to_host(x).reshape(np.shape(b))
-        cg.last = CGResult(out, info, it, None, None)
+        res, tol = getattr(distributed.solve, "last_resid", (None, None))
+        cg.last = CGResult(out, info, it, res, tol)
         cg.last.decomposition = how
         return out, info
     solver = KronCG(K, shift, recurrence, fusion=fusion, basis=basis)
@@ -302,6 +323,17 @@ def cg(K, b, shift=0.0, rtol=1e-5, atol=0.0, maxiter=None, check_every=None, cal
         out = dev.to_host(x).reshape(np.shape(b))
     cg.last = CGResult(out, info, it, res, tol)
     return out, info
+
+
+def lanczos_info(K):
+    """(block, launches): whether gg_lanczos_probe runs the probe in the
+    operator's parity-block basis (round 6; GG_LZ_BASIS=0 keeps the grid
+    layout) and its launches per step."""
+    from . import native
+    b, L = ctypes.c_int(), ctypes.c_int()
+    native.check(native.lib().gg_lanczos_info(K._device().h, ctypes.byref(b), ctypes.byref(L)),
+                 "gg_lanczos_info")
+    return bool(b.value), L.value
 
 
 def lanczos_tridiag(K, shift, steps, seed=0, probe=0, work=None, timed=False):

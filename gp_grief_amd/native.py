@@ -81,6 +81,8 @@ SIGNATURES = {
     "gg_cg_get_fusion": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_xdefer": [_vp, ctypes.c_int],
     "gg_cg_get_xdefer": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_get_xwin": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_calibrate": [_vp, ctypes.c_int, _c_dp, _c_i64p, _vp],
     "gg_cg_set_rq": [_vp, ctypes.c_int],
     "gg_cg_get_rq": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_set_basis": [_vp, ctypes.c_int],
@@ -106,6 +108,7 @@ SIGNATURES = {
                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                _vp],
+    "gg_lanczos_info": [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)],
     "gg_probe_fill": [ctypes.c_uint64, ctypes.c_int, _c_dp, ctypes.c_int64, _vp],
     "gg_sym_eig_batched": [ctypes.c_int, _c_i64p, _c_dp, _c_dp, _c_dp, _c_dp, ctypes.c_int64,
                            ctypes.c_int, _vp],

@@ -77,9 +77,14 @@ class _DeviceKron(object):
                                                      ctypes.byref(l)))
         return bool(a.value), n.value, l.value
 
+    def block_n(self):
+        """The block layout's length: n, or more when the two innermost
+        (pair) axes are padded to 16 TF + 4 (round 6)."""
+        return self.block_info()[1]
+
     def block_fold(self, xd, inverse=False, out=None):
         """P x (inverse: P^T x) between the grid and the block layout."""
-        y = dev.empty(self.n_rows) if out is None else out
+        y = dev.empty(self.n_rows if inverse else self.block_n()) if out is None else out
         native.check(native.lib().gg_kron_block_fold(self.h, int(bool(inverse)),
                                                      native.dptr(xd), native.dptr(y),
                                                      native.stream_ptr()), "gg_kron_block_fold")
@@ -91,7 +96,7 @@ class _DeviceKron(object):
         (gg_kron_block_fold_range; summed over a sharded CG's ranks)."""
         _, n, _ = self.block_info()
         nl = n // (1 << len(self._keep)) * int(nblk)
-        y = dev.empty(n if inverse else nl) if out is None else out
+        y = dev.empty(self.n_rows if inverse else nl) if out is None else out
         native.check(native.lib().gg_kron_block_fold_range(
             self.h, int(bool(inverse)), native.dptr(xd), native.dptr(y), int(blk0), int(nblk),
             native.stream_ptr()), "gg_kron_block_fold_range")
@@ -109,12 +114,12 @@ class _DeviceKron(object):
 
     def _block_work(self):
         if "block" not in self._work:
-            self._work["block"] = dev.empty(self.n_rows)
+            self._work["block"] = dev.empty(self.block_n())
         return self._work["block"]
 
     def block_matvec(self, xd, shift=0.0, out=None):
         """(P K P^T + shift I) x in the block layout (gg_kron_block_matvec)."""
-        y = dev.empty(self.n_rows) if out is None else out
+        y = dev.empty(self.block_n()) if out is None else out
         native.check(native.lib().gg_kron_block_matvec(self.h, native.dptr(xd), native.dptr(y),
                                                        float(shift),
                                                        native.dptr(self._block_work()),

@@ -99,15 +99,22 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
  * A matvec there is d - 1 launches (the last two axes of a block share one
  * launch): the CG (gg_cg_*) runs in this basis by default when it exists
  * (gg_cg_set_basis), folding b at start and unfolding x at every close.
- * Existence: 2 <= d <= 6, h_{d-2} = h_{d-1} = 16 TF + 4, TF in 1..6 (m = 40,
- * 72, 104, 136, 168, 200), every h <= 112
- * (GG_KRON_BLOCK=0 at gg_kron_create disables it).  No reference counterpart:
- * an execution detail of kron_matrix.py:52-97.                              */
+ * Existence: 2 <= d <= 6, h_{d-2} = h_{d-1} <= 100, every h <= 112
+ * (GG_KRON_BLOCK=0 at gg_kron_create disables it).  The two innermost axes
+ * of the layout have extent hp = 16 TF + 4 >= h (TF in 1..6: the pair
+ * kernels' slab shapes); where h is not of that form (m = 64, 96, 128 ...,
+ * round 6) the positions past h are zero padding -- *n, the block layout's
+ * length, is then 2^d prod(h_k) (hp / h)^2 > the grid's n.  The CG and the
+ * Lanczos probe take the block basis by default on one GPU where (hp / h)^2
+ * <= 1.3 (unpadded only, for Lanczos); the block-sharded CG wherever it
+ * exists.  No reference counterpart: an execution detail of
+ * kron_matrix.py:52-97.                                                     */
 int gg_kron_block_info(const gg_kron* K, int* available, int64_t* n, int* launches);
-/* y = P x (inverse: x = P^T y, the unfold); x, y distinct n-vectors.        */
+/* y = P x (inverse: x = P^T y, the unfold); x, y distinct: the grid vector
+ * (the operator's n) and the block-layout vector (gg_kron_block_info's n).  */
 int gg_kron_block_fold(const gg_kron* K, int inverse, const double* x_dev, double* y_dev,
                        gg_stream stream);
-/* y = (P K P^T + shift I) x in the block layout; work_dev: n doubles (d >= 3).
+/* y = (P K P^T + shift I) x in the block layout; work_dev: n (the block layout's) doubles (d >= 3).
  * The operator of kron_matrix.py:52-97 in the parity-block basis.           */
 int gg_kron_block_matvec(const gg_kron* K, const double* x_dev, double* y_dev, double shift,
                          double* work_dev, gg_stream stream);
@@ -191,6 +198,25 @@ int gg_cg_get_fusion(const gg_cg* cg, int* layout);
  * set: before gg_cg_start; get: 1 when the deferral is in effect.         */
 int gg_cg_set_xdefer(gg_cg* cg, int on);
 int gg_cg_get_xdefer(const gg_cg* cg, int* on);
+/* The x window of the block-basis CG (x_defer mode 3; GG_CG_XWIN at
+ * gg_cg_work_elems / gg_cg_create, default 8, 0 = mode 2's balanced pairs):
+ * x is cut into K regions and each iteration's pair launch brings ONE region
+ * up to date with the (at most K) steps it has not seen, so x moves once per
+ * K iterations and each direction once -- (K + 2) / K passes per iteration
+ * instead of 2, with K + 1 direction buffers in work_dev.  Same iterates up to
+ * rounding.  *K: the window in effect (once started; before, what gg_cg_start
+ * will pick), 0 when x is updated otherwise.                              */
+int gg_cg_get_xwin(const gg_cg* cg, int* K);
+/* The box's memory floor for the fused CG prologue launch (bench.py, round
+ * 6): the prologue's six streams alone over the handle's own buffers -- read
+ * p_old, r, q; write r, p_new, q (values unchanged, the launch's
+ * non-temporal mask) -- one untimed and `reps` timed passes, HIP events on the
+ * stream (synchronising).  *ms_host: time per pass; offsets_host (4 entries,
+ * may be NULL): the addresses of r, p_old, p_new, q modulo 2 MiB.  Call after
+ * gg_cg_start and before the iterations (it overwrites p_new, which the first
+ * prologue writes anyway).                                                  */
+int gg_cg_calibrate(gg_cg* cg, int reps, double* ms_host, int64_t* offsets_host,
+                    gg_stream stream);
 /* Fused recurrence, layout 0: where r_j.q_j (for beta's |r - alpha q|^2
  * expansion) comes from.  1 (default; GG_CG_RQ=0 at gg_cg_create turns it
  * off): the conjugacy identity r_j.q_j = p_j.q_j - beta_j p_j.q_{j-1}, with
@@ -283,6 +309,14 @@ int gg_lanczos_probe_timed(const gg_kron* K, double shift, uint64_t seed, int pr
                            double* work_dev, double* alphas_host, double* betas_host,
                            int* steps_done, double* step_ms_host, double* launch_ms_host,
                            gg_stream stream);
+/* Where the probe runs (round 6): *block = 1 when the operator has a
+ * parity-block basis with d >= 3 (GG_LZ_BASIS=0 at gg_kron_create's snapshot
+ * keeps the grid layout) -- the probe is folded once (P z) and every step is
+ * the fused block step, d - 1 launches and 10 passes over N (the Lanczos
+ * tridiagonal of P K P^T from P z is that of K from z: P is orthogonal);
+ * *launches: the launches per step (the positions of launch_ms_host, the rest
+ * of its d entries 0).                                                       */
+int gg_lanczos_info(const gg_kron* K, int* block, int* launches);
 int gg_probe_fill(uint64_t seed, int probe, double* z_dev, int64_t n, gg_stream stream);
 
 /* --------------------------------------- per-factor symmetric eigensolver

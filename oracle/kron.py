@@ -306,17 +306,47 @@ def slab_tile(xb, hs, inverse=False):
     return out.reshape(-1)
 
 
-def block_fold(x, ms, inverse=False):
+def block_pad(h):
+    """The device's slab extent for pair axes of half order h (gg_kronb.hip
+    block_create, round 6): the smallest 16 TF + 4 >= h, TF >= 1 -- the pair
+    kernels' shape; the rows / columns past h are zero."""
+    h = int(h)
+    return 16 * max(1, -(-(h - 4) // 16)) + 4
+
+
+def block_extents(ms, pad=False):
+    """The block layout's per-axis extents: h_k = m_k / 2, the two innermost
+    padded to block_pad when pad (the device layout)."""
+    hs = [int(m) // 2 for m in ms]
+    if pad:
+        hs[-2], hs[-1] = block_pad(hs[-2]), block_pad(hs[-1])
+    return hs
+
+
+def block_fold(x, ms, inverse=False, pad=False):
     """P x for the orthogonal per-axis butterfly u_i = (x_i + x_{m-1-i}) / sqrt 2,
     v_i = (x_i - x_{m-1-i}) / sqrt 2 (i < m/2) on every axis (C order, factor 0
     slowest).  Block layout: parity pattern beta (bit d-1-k for axis k) slowest,
     then (i'_0 .. i'_{d-3}) C order, each slab (i'_{d-2}, i'_{d-1}) k-step tiled
-    (slab_tile).  inverse=True applies P^T (block -> grid).
+    (slab_tile).  inverse=True applies P^T (block -> grid).  pad: the two
+    innermost axes zero-padded to block_pad(h) (the device layout for pair
+    orders that are not 16 TF + 4; a no-op for those that are).
     """
     ms = [int(m) for m in ms]
     d = len(ms)
     hs = [m // 2 for m in ms]
+    es = block_extents(ms, pad)
     s = 1.0 / np.sqrt(2.0)
+    if pad and es != hs:
+        if not inverse:
+            nb = int(np.prod(hs))
+            y = slab_tile(block_fold(x, ms), hs, inverse=True)
+            out = np.zeros((2 ** d,) + tuple(es))
+            out[(slice(None),) + tuple(slice(0, h) for h in hs)] = y.reshape((2 ** d,) + tuple(hs))
+            return slab_tile(out.reshape(-1), es)
+        y = slab_tile(np.asarray(x, dtype=np.float64), es, inverse=True)
+        y = y.reshape((2 ** d,) + tuple(es))[(slice(None),) + tuple(slice(0, h) for h in hs)]
+        return block_fold(slab_tile(np.ascontiguousarray(y).reshape(-1), hs), ms, inverse=True)
     if not inverse:
         t = np.asarray(x, dtype=np.float64).reshape(ms)
         # per axis: [lo half ; reversed hi half] -> (even, odd) stacked on a new
@@ -355,12 +385,20 @@ def block_factors(F):
     return F[:h, :h] + Fr, F[:h, :h] - Fr
 
 
-def block_matvec(factors, xb):
+def block_matvec(factors, xb, pad=False):
     """(P K P^T) x_b in the block layout: block beta is the Kronecker product of
-    S_k (beta_k = 0) / T_k (beta_k = 1) (kron_matvec on each block)."""
+    S_k (beta_k = 0) / T_k (beta_k = 1) (kron_matvec on each block).  pad: the
+    device layout (block_fold's pad; the factors zero-padded alike)."""
     d = len(factors)
-    st = [block_factors(F) for F in factors]
-    hs = [np.shape(F)[0] // 2 for F in factors]
+    hs = block_extents([np.shape(F)[0] for F in factors], pad)
+    st = []
+    for F, e in zip(factors, hs):
+        S, T = block_factors(F)
+        if S.shape[0] != e:
+            Sp, Tp = np.zeros((e, e)), np.zeros((e, e))
+            Sp[:S.shape[0], :S.shape[0]], Tp[:S.shape[0], :S.shape[0]] = S, T
+            S, T = Sp, Tp
+        st.append((S, T))
     nb = int(np.prod(hs))
     xb = slab_tile(xb, hs, inverse=True)
     out = np.empty_like(xb)

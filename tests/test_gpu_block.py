@@ -81,7 +81,7 @@ def test_block_info(gg, ms):
 @pytest.mark.parametrize("ms,why", [
     ((9, 40, 40), "odd order"),
     ((8, 40, 72), "unequal pair orders"),
-    ((8, 48, 48), "no pair kernel for h = 24"),
+    ((8, 208, 208), "pair h = 104 > 100 (no 16 TF + 4 slab kernel)"),
     ((8, 240, 40, 40), "h > 112"),
 ])
 def test_block_unavailable(gg, ms, why):
@@ -290,3 +290,199 @@ def test_block_cg_state_textbook_after_close(gg):
     r = b - (oracle.kron_matvec(F, x) + shift * x)
     assert it == 30 and not conv
     assert abs(np.linalg.norm(r) - res) <= 1e-6 * np.linalg.norm(b)
+
+
+# ---- x_defer mode 3: the x window (gg_cg_get_xwin, GG_CG_XWIN) -------------
+@pytest.mark.parametrize("K", [0, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("ms,shift", [((6, 12, 72, 72), 0.05), ((8, 6, 104, 104), 0.1)])
+def test_block_cg_window_vs_oracle(gg, monkeypatch, K, ms, shift):
+    """Every window K (0: mode 2's balanced pairs) solves to the oracle CG's
+    answer: iterations within 2 %, x to 1e-8, true residual at the tolerance."""
+    monkeypatch.setenv("GG_CG_XWIN", str(K))
+    F = factors(ms, 4)
+    Km = gg.tensors.KronMatrix(F, sym=True)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(11).standard_normal((n, 1))
+    s = gg.linalg.KronCG(Km, shift)
+    assert s.basis == "block" and s.xwin == (K if K >= 2 else 0)
+    x, info = gg.linalg.cg(Km, b, shift=shift, rtol=1e-10, maxiter=20000)
+    it = gg.linalg.cg.last.iters
+    xs, _, its = oracle_cg(F, b[:, 0], shift, 1e-10, 20000)
+    assert info == 0
+    assert abs(it - its) <= max(2, 0.02 * its), (it, its)
+    assert rel(x, xs) < 1e-8
+    r = oracle.kron_matvec(F, x[:, 0]) + shift * x[:, 0] - b[:, 0]
+    assert np.linalg.norm(r) <= 1.5e-10 * np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("K", [4, 8])
+def test_block_cg_window_open_chain_bitwise(gg, monkeypatch, K):
+    """Open calls chain into one closed call bitwise with the window too (the
+    armed region and the ring of directions carry across calls)."""
+    monkeypatch.setenv("GG_CG_XWIN", str(K))
+    ms, shift = (6, 12, 72, 72), 0.05   # the LDS pair launch (h >= 36) carries the window
+    Km = gg.tensors.KronMatrix(factors(ms, 2), sym=True)
+    bd = dev(gg, np.random.default_rng(6).standard_normal(int(np.prod(ms))))
+    a = gg.linalg.KronCG(Km, shift)
+    assert a.xwin == K
+    a.start(bd, rtol=1e-14)
+    a.iterate(37)
+    xa = host(gg, a.x)
+    c = gg.linalg.KronCG(Km, shift)
+    c.start(bd, rtol=1e-14)
+    for k in (5, 11, 1, 20):
+        c.iterate(k, close=False)
+    c.close()
+    assert np.array_equal(host(gg, c.x), xa)
+    assert a.status()[0] == c.status()[0] == 37
+
+
+@pytest.mark.parametrize("K", [2, 3, 4, 6, 8])
+def test_block_cg_window_matches_pairs(gg, monkeypatch, K):
+    """x never feeds back into the recurrence (r, p, q and the scalars are the
+    same kernels whatever the x schedule), so a window K run and a mode-2
+    (pairs) run have bitwise the same residual history and x equal up to the
+    order of x's sums -- one 37-iteration call, and closed chunks of 1, 7, 3
+    and 26 iterations (every close flushes all regions; the recurrence then
+    continues), each chunk's x with the true residual |r_k| of its status."""
+    ms, shift = (8, 72, 72), 0.05
+    F = factors(ms, 3)
+    b = np.random.default_rng(7).standard_normal(int(np.prod(ms)))
+    runs = {}
+    for w in (str(K), "0"):
+        monkeypatch.setenv("GG_CG_XWIN", w)
+        Km = gg.tensors.KronMatrix(F, sym=True)
+        a = gg.linalg.KronCG(Km, shift)
+        assert a.xwin == (K if w != "0" else 0)
+        a.start(dev(gg, b), rtol=1e-14)
+        a.iterate(37)
+        c = gg.linalg.KronCG(Km, shift)
+        c.start(dev(gg, b), rtol=1e-14)
+        chunks = []
+        for k in (1, 7, 3, 26):
+            c.iterate(k)
+            it, conv, res, tol = c.status()
+            x = host(gg, c.x)
+            r = b - (oracle.kron_matvec(F, x) + shift * x)
+            assert abs(np.linalg.norm(r) - res) <= 1e-6 * np.linalg.norm(b), (w, k)
+            chunks.append((x, (it, conv, res)))
+        runs[w] = (host(gg, a.x), a.status(), chunks)
+    (xw, sw, cw), (xp, sp, cp) = runs[str(K)], runs["0"]
+    assert sw == sp and sw[0] == 37
+    assert rel(xw, xp) < 1e-11
+    for (x1, s1), (x2, s2) in zip(cw, cp):
+        assert s1 == s2
+        assert rel(x1, x2) < 1e-11
+
+
+def test_block_cg_window_converges_inside_first_window(gg, monkeypatch):
+    """A solve that converges before the ring has filled (fewer iterations
+    than the window) still returns the full x."""
+    monkeypatch.setenv("GG_CG_XWIN", "8")
+    ms, shift = (4, 8, 72, 72), 1e7   # (K + s I) ~ s I: a few iterations
+    F = factors(ms, 5)
+    Km = gg.tensors.KronMatrix(F, sym=True)
+    b = np.random.default_rng(8).standard_normal((int(np.prod(ms)), 1))
+    assert gg.linalg.KronCG(Km, shift).xwin == 8
+    x, info = gg.linalg.cg(Km, b, shift=shift, rtol=1e-8, maxiter=1000)
+    it = gg.linalg.cg.last.iters
+    xs, _, its = oracle_cg(F, b[:, 0], shift, 1e-8, 1000)
+    assert its < 8, its
+    assert info == 0 and it < 8 and abs(it - its) <= 1
+    assert rel(x, xs) < 1e-9
+
+
+# ---- the fused Lanczos step in the block basis (gg_lanczos_info) -----------
+@pytest.mark.parametrize("ms", [(40, 40, 40, 40), (72, 72, 72, 72), (8, 6, 104, 104),
+                                (12, 72, 72)])
+def test_block_lanczos_matches_grid_and_oracle(gg, monkeypatch, ms):
+    """The probe folded once and every step in the parity-block basis gives the
+    grid-basis tridiagonal (P is orthogonal: same Krylov space) to 1e-10 over
+    the first 12 steps, and the oracle's (oracle.lanczos_tridiag on the
+    reference operator kron_matrix.py:52-97 from the same probe) to 1e-8."""
+    F = factors(ms, 6)
+    n = int(np.prod(ms))
+    s = 0.03
+    out = {}
+    for basis in ("1", "0"):
+        monkeypatch.setenv("GG_LZ_BASIS", basis)
+        K = gg.tensors.KronMatrix(F, sym=True)
+        blk, L = gg.linalg.lanczos_info(K)
+        assert blk == (basis == "1") and L == (len(ms) - 1 if blk else len(ms))
+        out[basis] = gg.linalg.lanczos_tridiag(K, s, 20, seed=7, probe=2)
+    (ab, bb), (ag, bg) = out["1"], out["0"]
+    k = min(ab.size, ag.size, 12)
+    np.testing.assert_allclose(ab[:k], ag[:k], rtol=1e-10)
+    np.testing.assert_allclose(bb[:k - 1], bg[:k - 1], rtol=1e-10)
+    zp = oracle.cg.probe_signs(7, 2, n)
+    ao, bo = oracle.lanczos_tridiag(lambda v: oracle.kron_matvec(F, v) + s * v, zp, 20)
+    np.testing.assert_allclose(ab[:k], ao[:k], rtol=1e-8)
+    np.testing.assert_allclose(bb[:k - 1], bo[:k - 1], rtol=1e-7)
+
+
+def test_block_lanczos_timed_and_slq(gg):
+    """The timed probe (bench.py's Lanczos leg) runs the same steps: identical
+    tridiagonal, a time per step and per launch (d - 1 positions, the d-th
+    entry 0); SLQ in the block basis against the exact shifted log det."""
+    ms = (8, 12, 72, 72)
+    F = factors(ms, 7)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    assert gg.linalg.lanczos_info(K) == (True, 3)
+    a0, b0 = gg.linalg.lanczos_tridiag(K, 0.05, 12, seed=3, probe=1)
+    a1, b1, step_ms, launch_ms = gg.linalg.lanczos_tridiag(K, 0.05, 12, seed=3, probe=1,
+                                                           timed=True)
+    assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
+    assert len(step_ms) == 12 and all(t > 0 for t in step_ms)
+    assert all(t > 0 for t in launch_ms[:3]) and launch_ms[3] == 0.0
+    Q, lam = oracle.factor_eigh(F)
+    exact = float(np.sum(np.log(oracle.kron_expand(lam) + 0.05)))
+    est, _ = gg.linalg.slq_logdet(K, 0.05, probes=8, steps=60, seed=1)
+    assert abs(est - exact) < 0.02 * abs(exact), (est, exact)
+
+
+# ---- padded pair axes (round 6): h not of the form 16 TF + 4 --------------
+# the layout pads the two innermost axes to hp = 16 TF + 4 >= h (zeros in the
+# vectors and the factors), so 64^d / 96^d / 128^d grids (h = 32 / 48 / 64)
+# take the block basis; (hp / h)^2 <= 1.3 keeps it the CG's default on one GPU
+PADDED = [((6, 64, 64), True), ((4, 96, 96), True), ((2, 8, 128, 128), True),
+          ((4, 6, 100, 100), True), ((8, 48, 48), False), ((12, 32, 32), False),
+          ((10, 64, 64), True)]
+
+
+@pytest.mark.parametrize("ms,efficient", PADDED)
+def test_block_padded_info_fold_matvec(gg, ms, efficient):
+    F = factors(ms)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    dk = K._device()
+    ok, nb, L = dk.block_info()
+    es = oracle.kron.block_extents(ms, pad=True)
+    assert ok and L == len(ms) - 1 and nb == int(np.prod(es)) << len(ms)
+    n = int(np.prod(ms))
+    x = np.random.default_rng(12).standard_normal(n)
+    xb = host(gg, dk.block_fold(dev(gg, x)))
+    assert rel(xb, oracle.kron.block_fold(x, ms, pad=True)) < 1e-15
+    assert rel(host(gg, dk.block_fold(dev(gg, xb), inverse=True)), x) < 1e-15
+    for shift in (0.0, 0.05):
+        yb = host(gg, dk.block_matvec(dev(gg, xb), shift=shift))
+        assert rel(yb, oracle.kron.block_matvec(F, xb, pad=True) + shift * xb) < 1e-13
+        y = oracle.kron.block_fold(yb, ms, inverse=True, pad=True)
+        assert rel(y, oracle.kron_matvec(F, x) + shift * x) < 1e-13
+        # the padding (exact zeros of the folded random vector) stays zero
+        assert np.all(yb[oracle.kron.block_fold(x, ms, pad=True) == 0.0] == 0.0)
+    assert gg.linalg.KronCG(K, 0.05).basis == ("block" if efficient else "grid")
+
+
+@pytest.mark.parametrize("ms,shift", [((6, 64, 64), 0.05), ((4, 8, 96, 96), 0.1),
+                                      ((8, 48, 48), 0.05)])
+def test_block_padded_cg_vs_oracle(gg, ms, shift):
+    """The CG in the padded block basis (forced where the default keeps the
+    grid) against the oracle CG: iterations within 2 %, x to 1e-8."""
+    F = factors(ms, 8)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    b = np.random.default_rng(13).standard_normal((int(np.prod(ms)), 1))
+    x, info = gg.linalg.cg(K, b, shift=shift, rtol=1e-10, maxiter=20000, basis="block")
+    it = gg.linalg.cg.last.iters
+    xs, _, its = oracle_cg(F, b[:, 0], shift, 1e-10, 20000)
+    assert info == 0
+    assert abs(it - its) <= max(2, 0.02 * its), (it, its)
+    assert rel(x, xs) < 1e-8

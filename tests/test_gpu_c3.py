@@ -114,6 +114,28 @@ def test_c3_cg_true_vs_recursive_residual(op, rhs, recurrence):
     del s
 
 
+def test_c3_block_cg_250_iterations(op, rhs):
+    """The default path (block basis, x window) over 250 iterations at full
+    size, closed every 50 (each close flushes every x region and unfolds x):
+    at each close the true residual b - (K + s I) x agrees with the
+    recurrence's |r_k| -- the window's bookkeeping and the pair launch's x
+    side job hold over many iterations, not just 20."""
+    import gp_grief_amd as gg
+    s = gg.linalg.KronCG(op, S2)
+    assert s.basis == "block" and s.xwin >= 2
+    s.start(rhs, rtol=0.0, atol=0.0)
+    bn = float(rhs.norm())
+    for k in range(5):
+        s.iterate(50, check_every=0)
+        it, conv, res, tol = s.status()
+        assert it == 50 * (k + 1) and not conv
+        true = op.matvec_device(s.x, shift=S2)
+        true -= rhs
+        assert abs(float(true.norm()) - res) < 1e-9 * bn, (it, float(true.norm()), res)
+        del true
+    del s
+
+
 def test_c3_slq_logdet_within_1pct(op):
     import gp_grief_amd as gg
     Q, T = op.schur()

@@ -1,7 +1,10 @@
 """HBM traffic per launch of the block-basis fused CG (gg_kronb.hip) from two
 rocprofv3 PMC passes, as tools/pmc_traffic.py does for the grid basis.
 
-usage: python tools/pmc_block.py RD_DIR WR_DIR OUT_JSON
+usage: python tools/pmc_block.py RD_DIR WR_DIR OUT_JSON [XWIN]
+
+XWIN: the x window the runs took (gg_cg_get_xwin; default GG_CG_XWIN or the
+library default 8; 0 = mode 2's balanced pairs).
 
 Counters (separate --pmc runs of `bench.py --steps 4 --warmup 2 --matvec 0
 --lanczos 0 --grief off --cpu-baseline off`, kernel trace only, per
@@ -37,6 +40,8 @@ def dispatches(d):
 
 def main():
     rd_dir, wr_dir, out = sys.argv[1:4]
+    xwin = int(sys.argv[4]) if len(sys.argv) > 4 else int(os.environ.get("GG_CG_XWIN", "8"))
+    xwin = xwin if xwin >= 2 else 0
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     rd, names = dispatches(rd_dir)
@@ -46,7 +51,7 @@ def main():
     iters = [ids[i:i + L] for i in range(0, len(ids) - L + 1, L)]
     last2 = iters[-2:]
     n = 200 ** 4
-    passes = [float(v) for v in bench.block_launch_passes(d)]
+    passes = [float(v) for v in bench.block_launch_passes(d, xwin)]
     per_pos = []
     for k in range(L):
         dids = [it[k] for it in last2]
@@ -61,7 +66,7 @@ def main():
         per_pos.append(pp)
     tot = sum(pp["traffic_bytes"] for pp in per_pos)
     res = {
-        "block_basis": True, "recurrence": "fused", "fusion_layout": 0, "x_deferred": 2,
+        "block_basis": True, "recurrence": "fused", "fusion_layout": 0, "x_deferred": 2, "x_window": xwin,
         "rq_identity": 1, "fold_mask": 0,
         "source_sha256": bench.kernel_source_hash(),
         "sources": bench.KERNEL_SOURCES,
