@@ -812,7 +812,7 @@ def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_ma
 
 
 PMC_JSON = os.path.join("profiles", "r04", "pmc_mode_product.json")
-PMC_JSON_BLOCK = os.path.join("profiles", "r05", "pmc_block.json")
+PMC_JSON_BLOCK = os.path.join("profiles", "r06", "pmc_block.json")
 # the sources that decide the CG launches' HBM traffic
 KERNEL_SOURCES = ["gp_grief_amd/csrc/gg_kron.hip", "gp_grief_amd/csrc/gg_kron_fold.hip",
                   "gp_grief_amd/csrc/gg_mp.h", "gp_grief_amd/csrc/gg_internal.h",

@@ -257,8 +257,8 @@ int64_t block_side_half(int64_t n);
 // shorter) and whether the operator's pair launch can carry that side job
 int64_t xwin_region(int64_t n, int K);
 bool block_pair_side(const BlockOp* B);
-// the padded layout costs at most 1.3x the unpadded passes (the single-GPU
-// default basis of the CG and of Lanczos)
+// the layout is unpadded (the single-GPU default basis of the CG and of
+// Lanczos: padded slabs measured slower than the grid basis)
 bool block_efficient(const BlockOp* B);
 
 }  // namespace gg

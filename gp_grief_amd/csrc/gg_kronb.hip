@@ -2153,16 +2153,18 @@ int64_t block_side_half(int64_t n) { return 2 * ceil_div(n, (int64_t)4); }
 
 bool block_pair_side(const BlockOp* B) { return B != nullptr && B->pair_lds; }
 
-// the padded slabs cost (hp / h)^2 of every pass over the vector; up to 1.3x
-// (h = 48 / 64 / 50 .. -> 52 / 68 / 52: 1.17 / 1.13 / 1.08) the block basis's
-// 12-13 passes still beat the grid basis's 15, beyond it (h = 24 -> 36: 2.25x,
-// h = 32 -> 36: 1.27x is inside) one GPU keeps the grid basis by default; the
-// block-sharded CG takes it regardless (no exchange across ranks)
+// the padded slabs cost (hp / h)^2 of every pass over the vector: measured at
+// d = 4 (profiles/r06/d_prof/block_vs_grid.jsonl), the padded block basis
+// loses to the grid basis on one GPU even at 1.13x -- CG iteration 64^4
+// 0.51 vs 0.43 ms, 96^4 2.19 vs 2.02, 128^4 6.64 vs 6.56 -- where the unpadded
+// orders win (136^4 7.33 vs 8.25 ms, 200^4 33.3 vs 38); so one GPU takes the
+// block basis by default only unpadded, and the block-sharded CG wherever it
+// exists (no exchange across ranks; the alternatives fold on the host or
+// exchange twice per matvec)
 bool block_efficient(const BlockOp* B) {
   if (B == nullptr) return false;
   const int d = B->d;
-  const double pad = (double)(B->e[d - 1] * B->e[d - 2]) / (double)(B->h[d - 1] * B->h[d - 2]);
-  return pad <= 1.3;
+  return B->e[d - 1] == B->h[d - 1] && B->e[d - 2] == B->h[d - 2];
 }
 
 }  // namespace gg

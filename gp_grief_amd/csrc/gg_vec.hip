@@ -9,6 +9,8 @@
 #include <cmath>
 #include <vector>
 
+#include <map>
+
 #include "gg_internal.h"
 
 namespace gg {
@@ -1083,6 +1085,12 @@ static int64_t cg_layout_elems(const gg_kron* K, int64_t n, int64_t* extra_off =
   return kCgAlignSlack + 6 * vs + region + gg::cg_extra_dirs(w) * vs;
 }
 
+// the workspace each thread's last gg_cg_work_elems sized per operator: a
+// gg_cg_create whose layout (read from the snapshot current then) needs more
+// -- another handle's creation re-took the GG_* snapshot with, say, a wider
+// window in between -- is refused instead of overrunning the caller's buffer
+static thread_local std::map<const gg_kron*, int64_t> t_cg_sized;
+
 int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
   return gg::guard([&] {
     GG_REQUIRE(K && elems, GG_ERR_VALUE, "NULL argument");
@@ -1093,6 +1101,7 @@ int gg_cg_work_elems(const gg_kron* K, int64_t* elems) {
     // the block basis (gg_kronb.hip) takes the scratch region for xb and q2
     // + the window's extra direction buffers (x_defer mode 3, block basis)
     *elems = cg_layout_elems(K, n);
+    t_cg_sized[K] = *elems;
   });
 }
 
@@ -1182,7 +1191,12 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       cg->shift = shift;
       cg->n = nr;
       int64_t vs = 0;
-      cg_layout_elems(K, nr, nullptr, nullptr, &vs);
+      const int64_t need = cg_layout_elems(K, nr, nullptr, nullptr, &vs);
+      const auto sized = t_cg_sized.find(K);
+      GG_REQUIRE(sized == t_cg_sized.end() || need <= sized->second, GG_ERR_VALUE,
+                 "the CG workspace was sized (gg_cg_work_elems) under another GG_* snapshot: "
+                 "call gg_cg_work_elems again before gg_cg_create");
+      if (sized != t_cg_sized.end()) t_cg_sized.erase(sized);   // one check per sizing
       GG_REQUIRE((reinterpret_cast<uintptr_t>(work_dev) & 7) == 0, GG_ERR_VALUE,
                  "the CG workspace must hold doubles (8-byte aligned)");
       work_dev = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(work_dev) + 255) &

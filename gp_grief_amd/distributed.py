@@ -601,6 +601,35 @@ def _parity_transform(X, K, inverse=False):
     return X
 
 
+def device_parity_fold(x, m, world, rank, inverse=False, out=None):
+    """gg_parity_fold on the device: the grid vector -> this rank's block in
+    the even / odd basis of factors 0..K-1 (the layout of parity_fold's
+    entries); inverse: the block -> its contribution to the grid vector
+    (summed over the ranks by an all-reduce, as parity_unfold's result)."""
+    m = [int(v) for v in m]
+    n = int(np.prod(m))
+    y = dev.empty(n if inverse else n // int(world)) if out is None else out
+    native.check(native.lib().gg_parity_fold(len(m), native.i64_array(m), int(world), int(rank),
+                                             int(bool(inverse)), native.dptr(x), native.dptr(y),
+                                             native.stream_ptr()), "gg_parity_fold")
+    return y
+
+
+def device_shard0_fold(x, m, world, rank, inverse=False, out=None):
+    """gg_shard0_fold on the device: this rank's factor-0 row block of the
+    grid vector (the scatter_global layout); inverse: written back into the
+    grid vector `out` (zeroed here when not given: this rank's contribution)."""
+    m = [int(v) for v in m]
+    n = int(np.prod(m))
+    if out is None:
+        out = dev.zeros(n) if inverse else dev.empty(n // int(world))
+    native.check(native.lib().gg_shard0_fold(len(m), native.i64_array(m), int(world), int(rank),
+                                             int(bool(inverse)), native.dptr(x),
+                                             native.dptr(out), native.stream_ptr()),
+                 "gg_shard0_fold")
+    return out
+
+
 def parity_fold(vec, m, world):
     """Host: the global vector (C order over factors of sizes m) -> every
     rank's local block in the even / odd basis (flattened, C order over the
@@ -1011,24 +1040,24 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
         it, _, res, tol = cg.status()
         solve.last_cancels = cg.cancels()
     elif decomposition == "parity":
-        bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
-                        dtype=np.float64).reshape(-1)
+        # device fold of the rank's block, device unfold of its contribution,
+        # one all-reduce of the grid vector (round 6: no host arrays)
+        bd = dev.to_device(b).reshape(-1)
         cg = ParityShardCG(F, world, rank, ex, shift)
-        bl = dev.to_device(parity_fold(bh, m, world)[rank])
+        bl = device_parity_fold(bd, m, world, rank)
         xl, info = cg.solve(bl, rtol, atol, maxiter, check_every)
         solve.last_cancels = cg.cancels()
-        parts = ex.all_gather_object(dev.to_host(xl))
-        x = dev.to_device(parity_unfold(parts, m))
+        x = device_parity_fold(xl, m, world, rank, inverse=True)
+        ex.all_reduce(x)
         it, _, res, tol = cg.status()
     elif decomposition == "transpose":
-        bh = np.asarray(dev.to_host(b) if dev.is_device_array(b) else b,
-                        dtype=np.float64).reshape(-1)
+        bd = dev.to_device(b).reshape(-1)
         eng = HipEngine(F, world, rank)
         cg = DistKronCG(eng, ex, shift)
-        xl, info = cg.solve(dev.to_device(scatter_global(bh, m, world, rank)), rtol, atol,
-                            maxiter, check_every)
-        parts = ex.all_gather_object(dev.to_host(xl))
-        x = dev.to_device(gather_global(parts, m))
+        xl, info = cg.solve(device_shard0_fold(bd, m, world, rank), rtol, atol, maxiter,
+                            check_every)
+        x = device_shard0_fold(xl, m, world, rank, inverse=True)
+        ex.all_reduce(x)
         it, _, rho, tol = cg.status()
         res = float(np.sqrt(max(rho, 0.0)))
         solve.last_cancels = None

@@ -89,6 +89,10 @@ SIGNATURES = {
     "gg_cg_get_basis": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_launches": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_start_partial": [_vp, _c_dp, _c_dp, _c_dp, _vp],
+    "gg_parity_fold": [ctypes.c_int, _c_i64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp,
+                       _c_dp, _vp],
+    "gg_shard0_fold": [ctypes.c_int, _c_i64p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dp,
+                       _c_dp, _vp],
     "gg_cg_start_finish": [_vp, _c_dp, ctypes.c_double, ctypes.c_double, _vp],
     "gg_cg_iterate_partial": [_vp, _c_dp, _vp],
     "gg_cg_iterate_finish": [_vp, _c_dp, _vp],

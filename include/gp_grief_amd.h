@@ -105,9 +105,9 @@ int gg_kron_matvec_timed(const gg_kron* K, int transpose, const double* x_dev, d
  * kernels' slab shapes); where h is not of that form (m = 64, 96, 128 ...,
  * round 6) the positions past h are zero padding -- *n, the block layout's
  * length, is then 2^d prod(h_k) (hp / h)^2 > the grid's n.  The CG and the
- * Lanczos probe take the block basis by default on one GPU where (hp / h)^2
- * <= 1.3 (unpadded only, for Lanczos); the block-sharded CG wherever it
- * exists.  No reference counterpart: an execution detail of
+ * Lanczos probe take the block basis by default on one GPU where it is
+ * unpadded (padded slabs measured slower than the grid basis there); the
+ * block-sharded CG wherever it exists (no exchange between ranks).  No reference counterpart: an execution detail of
  * kron_matrix.py:52-97.                                                     */
 int gg_kron_block_info(const gg_kron* K, int* available, int64_t* n, int* launches);
 /* y = P x (inverse: x = P^T y, the unfold); x, y distinct: the grid vector
@@ -279,6 +279,23 @@ int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* r
 int gg_cg_work_elems_blocks(const gg_kron* K, int64_t nblk, int64_t* elems);
 int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shift,
                         double* work_dev, gg_cg** out);
+/* The other decompositions' once-per-solve fold / unfold on the device
+ * (round 6; gp_grief_amd/distributed.py solve, which before folded on the
+ * host and gathered host arrays through object collectives).
+ * gg_parity_fold -- world = 2^K ranks, factors 0..K-1 of even order: forward
+ * in = the grid vector (C order over m), out = rank's block in the even / odd
+ * basis of axes 0..K-1, C order over (m_K .. m_{d-1}, h_0 .. h_{K-1}) (the
+ * local factor order of distributed.parity_local_factors); inverse in = that
+ * block, out = its contribution P^T to EVERY grid element (summed over the
+ * ranks by the caller's all-reduce).
+ * gg_shard0_fold -- factor 0's row blocks (the transpose decomposition;
+ * layout (m_1 .. m_{d-1}, a), a = i_0 - rank m_0 / world fastest): forward
+ * out = the rank's elements of the grid vector in; inverse writes them back
+ * into the grid vector out (its other elements untouched).                */
+int gg_parity_fold(int d, const int64_t* m, int world, int rank, int inverse,
+                   const double* in_dev, double* out_dev, gg_stream stream);
+int gg_shard0_fold(int d, const int64_t* m, int world, int rank, int inverse,
+                   const double* in_dev, double* out_dev, gg_stream stream);
 int gg_cg_start_finish(gg_cg* cg, const double* rr_dev, double rtol, double atol,
                        gg_stream stream);
 int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream);

@@ -443,10 +443,11 @@ def test_block_lanczos_timed_and_slq(gg):
 # ---- padded pair axes (round 6): h not of the form 16 TF + 4 --------------
 # the layout pads the two innermost axes to hp = 16 TF + 4 >= h (zeros in the
 # vectors and the factors), so 64^d / 96^d / 128^d grids (h = 32 / 48 / 64)
-# take the block basis; (hp / h)^2 <= 1.3 keeps it the CG's default on one GPU
-PADDED = [((6, 64, 64), True), ((4, 96, 96), True), ((2, 8, 128, 128), True),
-          ((4, 6, 100, 100), True), ((8, 48, 48), False), ((12, 32, 32), False),
-          ((10, 64, 64), True)]
+# have the block basis (the block-sharded CG, no exchange); one GPU keeps the
+# grid basis by default there (measured faster, gg_kronb.hip block_efficient)
+PADDED = [((6, 64, 64), False), ((4, 96, 96), False), ((2, 8, 128, 128), False),
+          ((4, 6, 100, 100), False), ((8, 48, 48), False), ((12, 32, 32), False),
+          ((10, 64, 64), False), ((6, 72, 72), True)]
 
 
 @pytest.mark.parametrize("ms,efficient", PADDED)
@@ -486,3 +487,28 @@ def test_block_padded_cg_vs_oracle(gg, ms, shift):
     assert info == 0
     assert abs(it - its) <= max(2, 0.02 * its), (it, its)
     assert rel(x, xs) < 1e-8
+
+
+def test_cg_create_refuses_workspace_sized_under_another_snapshot(gg, monkeypatch):
+    """gg_cg_create reads its layout from the current GG_* snapshot: a
+    workspace gg_cg_work_elems sized under a smaller window is refused (a
+    clean GG_ERR_VALUE instead of buffers past its end)."""
+    import ctypes
+    from gp_grief_amd import native
+    monkeypatch.setenv("GG_CG_XWIN", "2")
+    K = gg.tensors.KronMatrix(factors((6, 12, 72, 72)), sym=True)
+    dk = K._device()
+    L = native.lib()
+    we = ctypes.c_int64()
+    native.check(L.gg_cg_work_elems(dk.h, ctypes.byref(we)))
+    work = gg.device.empty(we.value)
+    monkeypatch.setenv("GG_CG_XWIN", "8")
+    native.check(L.gg_knobs_reload())
+    h = ctypes.c_void_p()
+    st = L.gg_cg_create(dk.h, 0.05, native.dptr(work), ctypes.byref(h))
+    assert st == -1 and not h.value
+    # sized again under the current snapshot: accepted
+    native.check(L.gg_cg_work_elems(dk.h, ctypes.byref(we)))
+    work = gg.device.empty(we.value)
+    native.check(L.gg_cg_create(dk.h, 0.05, native.dptr(work), ctypes.byref(h)))
+    native.check(L.gg_cg_destroy(h))

@@ -544,3 +544,85 @@ def test_block_sharded_cg_processes(gpu, tmp_path):
         assert str(r["how"]) == "block" and int(r["info"]) == 0
         assert abs(int(r["iters"]) - it) <= max(2, 0.02 * it)
         assert np.linalg.norm(r["x"] - xs) / np.linalg.norm(xs) < 1e-8
+
+
+@pytest.mark.parametrize("m,world", [((10, 12, 9), 2), ((8, 6, 12, 5), 4), ((6, 4, 8), 8)])
+def test_device_parity_and_shard0_folds_vs_host(gpu, m, world):
+    """gg_parity_fold / gg_shard0_fold (round 6: the parity and transpose
+    decompositions' fold / unfold on the device) against the host
+    restatements parity_fold / parity_unfold and scatter_global /
+    gather_global, every rank; the unfold contributions sum to the vector."""
+    import gp_grief_amd as gg
+    from gp_grief_amd import distributed as D
+    n = int(np.prod(m))
+    x = np.random.default_rng(31).standard_normal(n)
+    xd = gg.device.to_device(x)
+    host = D.parity_fold(x, m, world)
+    acc = np.zeros(n)
+    for g in range(world):
+        loc = gg.device.to_host(D.device_parity_fold(xd, m, world, g))
+        assert np.allclose(loc, host[g], rtol=0, atol=1e-14)
+        acc += gg.device.to_host(D.device_parity_fold(gg.device.to_device(loc), m, world, g,
+                                                      inverse=True))
+    assert np.allclose(acc, x, rtol=0, atol=1e-13)
+    if m[0] % world == 0:
+        acc = np.zeros(n)
+        for g in range(world):
+            loc = gg.device.to_host(D.device_shard0_fold(xd, m, world, g))
+            assert np.array_equal(loc, D.scatter_global(x, m, world, g))
+            acc += gg.device.to_host(D.device_shard0_fold(gg.device.to_device(loc), m, world, g,
+                                                          inverse=True))
+        assert np.array_equal(acc, x)
+
+
+def _fallback_worker(rank, world, port, out_dir, how):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from dist_helpers import bind_device
+    bind_device(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import gp_grief_amd as gg
+    from gp_grief_amd.distributed import block_shard_ok
+    ms, F = _fallback_problem(how)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    assert not block_shard_ok(K, world)
+    y = np.random.default_rng(25).standard_normal(int(np.prod(ms)))
+    x, info = gg.linalg.cg(K, y, shift=0.05, rtol=1e-10, comm=True)
+    np.savez(os.path.join(out_dir, "rank%d.npz" % rank), x=x, info=info,
+             iters=gg.linalg.cg.last.iters, how=gg.linalg.cg.last.decomposition)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _fallback_problem(how):
+    """A grid where the block decomposition does not exist: an odd order
+    (parity sharding on the even factor 0), or factor 0 not centrosymmetric
+    (the transpose decomposition)."""
+    ms = (10, 12, 9) if how == "parity" else (10, 8, 12)
+    F = reference_factors_ms(ms)
+    if how == "transpose":
+        F[0] = F[0] + np.diag(np.linspace(0.0, 0.2, ms[0]))   # breaks J F J = F
+    return ms, F
+
+
+@pytest.mark.parametrize("how", ["parity", "transpose"])
+def test_fallback_decompositions_processes(gpu, tmp_path, how):
+    """linalg.cg(comm=True) over two gloo processes on a grid without the
+    block basis: the 'auto' decomposition falls back to parity / transpose
+    sharding, whose fold and unfold now run on the device (one all-reduce of
+    the grid vector instead of gathered host arrays) -- x against the oracle."""
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.start_processes(_fallback_worker, args=(2, port, str(tmp_path), how), nprocs=2,
+                       join=True, start_method="spawn")
+    res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(2)]
+    ms, F = _fallback_problem(how)
+    y = np.random.default_rng(25).standard_normal(int(np.prod(ms)))
+    xs, _, it = oracle.cg_solve(lambda v: oracle.kron_matvec(F, v) + 0.05 * v, y, rtol=1e-10)
+    for r in res:
+        assert str(r["how"]) == how and int(r["info"]) == 0
+        assert abs(int(r["iters"]) - it) <= max(2, 0.02 * it)
+        assert np.linalg.norm(r["x"] - xs) / np.linalg.norm(xs) < 1e-8

@@ -37,7 +37,8 @@ def main():
     K = gg.tensors.KronMatrix(F, sym=True)
     dk = K._device()
     ok, n, L = dk.block_info()
-    out = {"m": m, "d": d, "block": ok, "launches": L}
+    out = {"m": m, "d": d, "block": ok, "launches": L, "block_n": n, "grid_n": m ** d,
+           "padding": n / float(m ** d) if ok else None}
     if not a.no_matvec and ok:
         x = torch.randn(n, dtype=torch.float64, device="cuda")
         y = torch.empty_like(x)
@@ -48,17 +49,18 @@ def main():
         out["block_launch_ms"] = [v / a.reps for v in lm]
         if not a.no_grid:
             # plain grid-basis matvec for comparison
-            y2 = torch.empty_like(x)
-            lm2, tot2 = dk.matvec_timed(x, y2, a.reps)
+            xg = torch.randn(m ** d, dtype=torch.float64, device="cuda")   # grid layout
+            y2 = torch.empty_like(xg)
+            lm2, tot2 = dk.matvec_timed(xg, y2, a.reps)
             out["grid_matvec_ms"] = tot2 / a.reps
             out["grid_launch_ms"] = [v / a.reps for v in lm2]
-            del y2
+            del y2, xg
         del x, y
         dk.release_work()
         torch.cuda.empty_cache()
     bases = [] if a.no_cg else (["block"] if ok else []) + (["grid"] if a.grid_cg or not ok else [])
     for basis in bases:
-        b = torch.randn(n, dtype=torch.float64, device="cuda")
+        b = torch.randn(m ** d, dtype=torch.float64, device="cuda")   # the grid's N
         s = gg.linalg.KronCG(K, 0.01, basis=basis)
         s.start(b, rtol=1e-14)
         s.iterate(3, close=False)
