@@ -566,6 +566,7 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
                    "cg_basis": "block",
                    "blocks_per_rank": (1 << d) // world,
                    "cg_x_window": int(getattr(eng, "xwin", 0)),
+                   "cg_r_derived": bool(getattr(eng, "rderive", False)),
                    "n_per_rank": nl,
                    "launches_per_iteration": d - 1,
                    "timed_region": "exactly `steps` fused CG iterations continuing the "
@@ -595,7 +596,8 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
         # the dominant kernel of a rank (its blocks are whole blocks: the
         # single-GPU block roofline with n -> N / G)
         roof, extra = roofline_report(per_pos, nl, m, d, "fused", ms_per_step, block=True,
-                                      xwin=int(getattr(eng, "xwin", 0)))
+                                      xwin=int(getattr(eng, "xwin", 0)),
+                                      rderive=bool(getattr(eng, "rderive", False)))
         roof["scope"] = "per rank: the rank's dominant launch on its N / G elements " \
                         "(max over ranks of the per-launch %s means)" \
                         % ("HIP-event" if on_gpu else "host-timer (CPU rehearsal engine)")
@@ -674,7 +676,7 @@ def launch_passes(d, recurrence, fusion=0, xdefer=False, rq=False):
     return passes
 
 
-def block_launch_passes(d, xwin=0):
+def block_launch_passes(d, xwin=0, rderive=False):
     """Passes over N of each launch of the fused CG iteration in the
     parity-block basis (gg_kronb.hip block_apply; d - 1 launches): the first
     (axis 0, in place) carries the prologue -- p_old (its MFMA operand), r and
@@ -683,9 +685,11 @@ def block_launch_passes(d, xwin=0):
     and carries the x side job: xwin = 0, mode 2's balanced pairs (half of x
     per iteration: x, p_{j-2}, p_{j-1} read, x written = 2 passes); xwin = K,
     mode 3's window (one of K regions of x read and written, its K pending
-    directions read = (K + 2) / K passes); the ones between are plain."""
+    directions read = (K + 2) / K passes); the ones between are plain.
+    rderive (round 6): the prologue keeps no r -- it reads p_{j-2} in place of
+    r and stores no r, one pass fewer."""
     passes = [2.0] * (d - 1)
-    passes[0] += 4.0
+    passes[0] += 3.0 if rderive else 4.0
     passes[-1] += 1.0 + ((xwin + 2.0) / xwin if xwin >= 2 else 2.0)
     return passes
 
@@ -731,14 +735,14 @@ def dominant_group(per_pos, kinds):
 
 
 def roofline_report(per_pos, n, m, d, recurrence, ms_per_step, fusion=0, fold_mask=0,
-                    xdefer=False, rq=False, block=False, xwin=0):
+                    xdefer=False, rq=False, block=False, xwin=0, rderive=False):
     """fold_mask bit k: mode product k runs on the centrosymmetric split
     (gg_kron_fold_mask), executing n m MFMA FLOP instead of the dense 2 n m;
     the roofline prices the work the kernel actually does.  block: the CG runs
     in the parity-block basis (d - 1 launches)."""
     if block:
         flops = block_launch_flops(n, m, d)
-        passes = block_launch_passes(d, xwin)
+        passes = block_launch_passes(d, xwin, rderive)
         kinds = block_launch_kernels(d)
     else:
         flops = [(1.0 if (fold_mask >> k) & 1 else 2.0) * n * m for k in range(d)]
@@ -830,7 +834,7 @@ def kernel_source_hash():
 
 
 def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True, rq=False,
-                block=False, xwin=0):
+                block=False, xwin=0, rderive=False):
     """HBM bytes per launch of the dominant kernel (averaged over its launch
     positions) from the committed PMC passes (tools/pmc_traffic.py) -- only
     when they were taken on this workload, recurrence, fusion layout and fold
@@ -851,6 +855,8 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
         return None, "PMC passes taken with another fold state"
     if int(rec.get("x_deferred", 0)) != int(xdefer) or int(rec.get("x_window", 0)) != int(xwin):
         return None, "PMC passes taken with another x-update schedule"
+    if bool(rec.get("r_derived", False)) != bool(rderive):
+        return None, "PMC passes taken with another r source"
     if int(rec.get("rq_identity", 0)) != int(rq):
         return None, "PMC passes taken with another r.q source"
     if rec.get("source_sha256") != kernel_source_hash():
@@ -1290,11 +1296,11 @@ def main():
     block = solver.basis == "block"
     roof, extra = roofline_report(per_pos, n, m, d, solver.recurrence, ms_per_step,
                                   solver.fusion, fold_mask, solver.xdefer, solver.rq, block,
-                                  solver.xwin)
+                                  solver.xwin, solver.rderive)
     # the block basis has no per-factor fold state (tools/pmc_block.py records 0)
     traffic, src = pmc_traffic(m, d, roof["positions"], solver.recurrence, solver.fusion or 0,
                                0 if block else fold_mask, solver.xdefer, solver.rq, block,
-                               solver.xwin)
+                               solver.xwin, solver.rderive)
     roof["traffic"], roof["traffic_source"] = traffic, src
     result = {
         "metric": METRIC,
@@ -1316,6 +1322,7 @@ def main():
                    "cg_fusion_layout": solver.fusion,
                    "cg_x_deferred": solver.xdefer,
                    "cg_x_window": solver.xwin,
+                   "cg_r_derived": solver.rderive,
                    "cg_rq_identity": solver.rq,
                    "cg_basis": solver.basis,
                    "launches_per_iteration": solver.launches(),

@@ -117,6 +117,12 @@ struct CgScalars {
   int sreg, scnt;
   double scoef[kXWinMax];
   const double* sdir[kXWinMax];
+  // derived r (block-basis CG with the window, round 6): the prologue does
+  // not keep r; r_{j-1} = p_{j-1} - beta_p p_{j-2} from the two directions
+  // the window's ring holds (beta_p: the beta that formed the current
+  // direction) unless rstored -- r is in its buffer (start, repair, close)
+  double beta_p;
+  int rstored;
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is
@@ -183,6 +189,10 @@ struct MpFuse {
   // block-basis CG (gg_kronb.hip): the pair launch's output q (the chain runs
   // in place on q_old, the last launch cannot)
   double* blk_q_out = nullptr;
+  // derived r (CgScalars::rstored): the prologue reads p_{j-2} (pprev) in
+  // place of r unless sc->rstored, and never stores r (KIND 5)
+  bool rderive = false;
+  const double* pprev = nullptr;
 };
 
 // Output address map of a mode product (see gg_kron.hip epilogue):
@@ -260,5 +270,8 @@ bool block_pair_side(const BlockOp* B);
 // the layout is unpadded (the single-GPU default basis of the CG and of
 // Lanczos: padded slabs measured slower than the grid basis)
 bool block_efficient(const BlockOp* B);
+// the CG prologue can run with derived r (the fast kernel's KIND 5 exists for
+// axis 0 and the non-temporal prologue is on)
+bool block_rderive_ok(const BlockOp* B);
 
 }  // namespace gg

@@ -316,6 +316,10 @@ struct ModeArgs {
   const CgScalars* sc;
   double* rr_part;    // [grid] r.r, [pqo_stride + grid] p_new.q_old
   int64_t pqo_stride;
+  // derived r (KIND 5, the CG prologue of KIND 3 without r in memory): r_{j-1}
+  // = X - sc->beta_p pprev (X = p_{j-1}, pprev = p_{j-2}) unless sc->rstored
+  // (then read from r); r is never stored
+  const double* pprev;
   // Lanczos prologue (KIND 4): X holds u_prev, r the Lanczos vector u, q_old
   // the previous matvec output Y; the operand is w = cy Y + cu u + cp u_prev
   // (coef = [cy, cu, cp] on the device), stored over u_prev (p_out == X,
@@ -646,8 +650,9 @@ constexpr int fast_waves() {
 
 template <int TF, int KIND_>
 __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_kernel(ModeArgs a) {
-  constexpr bool NT = KIND_ == 3 || KIND_ == 4;   // KIND 4 (Lanczos): non-temporal too
-  constexpr int KIND = KIND_ == 3 ? 1 : KIND_;
+  constexpr bool NT = KIND_ >= 3;   // KIND 4 (Lanczos), 5 (derived r): non-temporal too
+  constexpr bool RDER = KIND_ == 5;
+  constexpr int KIND = (KIND_ == 3 || KIND_ == 5) ? 1 : KIND_;
   constexpr int W = fast_waves<KIND>();
   constexpr int JT = TF + 1;
   constexpr int KS = 4 * TF + 1;
@@ -731,6 +736,10 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
     lz_cp = a.coef[2];
   }
   const bool pending = KIND == 1 && a.sc->pending != 0;
+  // derived r: the second stream is r (stored) or p_{j-2}
+  const bool rst = !RDER || a.sc->rstored != 0;
+  const double bprev = RDER ? a.sc->beta_p : 0.0;
+  const double* rsrc = (KIND == 1 && !rst) ? a.pprev : a.r;
   double sc0 = 0.0, sc1 = 0.0;
   const double* sp0 = a.sx;
   const double* sp1 = a.sx;
@@ -784,7 +793,7 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
       const int64_t ub = l_base * 8 + (int64_t)s * rstep;
       ring[slot][0] = lduq<NT>(a.X, ub, o_e);
       if (KIND == 1 || KIND == 4) {
-        ring[slot][1] = lduq<NT>(a.r, ub, o_e);
+        ring[slot][1] = lduq<NT>(KIND == 1 ? rsrc : a.r, ub, o_e);
         ring[slot][2] = lduq<NT>(a.q_old, ub, o_e);
       }
       if (KIND == 2) {
@@ -825,7 +834,9 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
         // h = 16 TF + 4: every row 4 s + kq of the strip is inside h
         double xb = ring[slot][0];
         if (KIND == 1) {
-          double r = ring[slot][1];
+          // derived: r_{j-1} = p_{j-1} - beta_p p_{j-2} (a select, not a
+          // multiply: the stored r needs no p_{j-1})
+          double r = rst ? ring[slot][1] : fma(-bprev, ring[slot][1], xb);
           const double q = ring[slot][2];
           const int64_t ub = (cbase + (int64_t)4 * s * a.inner) * 8;
           r = r - alpha * q;
@@ -837,7 +848,8 @@ __global__ __launch_bounds__(64 * fast_waves<KIND_>(), 1) void blk_mode_fast_ker
             if (pqo_on) pqo_acc = pqo;
           }
           // stores unconditional: a spare strip's go to the trash slot
-          stq_nt(cvalid, a.r, ub, o_e, r);
+          // (derived r: no r store -- 5 passes instead of 6)
+          if (!RDER) stq_nt(cvalid, a.r, ub, o_e, r);
           stq_nt(cvalid, a.p_out, ub, o_e, xb);
         }
         if (KIND == 4) {
@@ -1669,7 +1681,8 @@ static blk_mode_fn mode_fast_fn(int JT) {
 // h = 16 (JT - 1) + 4 exactly (KS = 4 JT - 3)
 static blk_mode_fn select_mode(int kind, int JT, bool T4, int h = 0, bool fast = false) {
   if (T4 && h == 16 * (JT - 1) + 4 && fast) {
-    const blk_mode_fn f = kind == 4   ? mode_fast_fn<4>(JT)
+    const blk_mode_fn f = kind == 5   ? mode_fast_fn<5>(JT)
+                          : kind == 4 ? mode_fast_fn<4>(JT)
                           : kind == 3 ? mode_fast_fn<3>(JT)
                           : kind == 1 ? mode_fast_fn<1>(JT)
                           : kind == 2 ? mode_fast_fn<2>(JT)
@@ -1746,7 +1759,7 @@ static int blk_cus() {
 static void blk_set_lds_limits(const BlockOp* B) {
   for (int k = 0; k + 2 < B->d; ++k) {
     const size_t bytes = (size_t)B->KS[k] * B->JT[k] * 64 * sizeof(double);
-    for (int kind = 0; kind < 5; ++kind)
+    for (int kind = 0; kind < 6; ++kind)
       GG_HIP(hipFuncSetAttribute(
           reinterpret_cast<const void*>(
               select_mode(kind, B->JT[k], B->T4[k], (int)B->h[k], B->fast)),
@@ -1927,7 +1940,8 @@ void block_fold(const BlockOp* B, bool inverse, const double* x, double* y, doub
 static int mode_waves(int kind, const BlockOp* B, int k) {
   const int JT = B->JT[k];
   const bool fast = B->T4[k] && B->h[k] == 16 * (JT - 1) + 4 && B->fast &&
-                    (kind == 4   ? mode_fast_fn<4>(JT)
+                    (kind == 5   ? mode_fast_fn<5>(JT)
+                     : kind == 4 ? mode_fast_fn<4>(JT)
                      : kind == 3 ? mode_fast_fn<3>(JT)
                      : kind == 1 ? mode_fast_fn<1>(JT)
                      : kind == 2 ? mode_fast_fn<2>(JT)
@@ -2040,7 +2054,7 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     int grid = 0;
     int kind = 0;
     if (cgp == 2 && k == 0)
-      kind = B->pro_nt ? 3 : 1;
+      kind = cg->rderive ? 5 : B->pro_nt ? 3 : 1;
     else if (cgp == 3 && k == 0)
       kind = 4;
     else if (k == 1 && side && !pair_side)
@@ -2051,8 +2065,11 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
     a.X = src;
     a.Y = chain;
     a.skip = skip;
-    if (kind == 1 || kind == 3) {
+    if (kind == 1 || kind == 3 || kind == 5) {
       a.r = cg->r;
+      a.pprev = cg->pprev;
+      GG_REQUIRE(kind != 5 || cg->pprev != nullptr, GG_ERR_VALUE,
+                 "block CG: derived r needs p_{j-2}");
       a.q_old = cg->q_old;
       a.p_out = cg->p_out;
       a.sc = cg->sc;
@@ -2152,6 +2169,12 @@ void block_apply(const BlockOp* B, const double* x, double* y, double shift, dou
 int64_t block_side_half(int64_t n) { return 2 * ceil_div(n, (int64_t)4); }
 
 bool block_pair_side(const BlockOp* B) { return B != nullptr && B->pair_lds; }
+
+bool block_rderive_ok(const BlockOp* B) {
+  if (B == nullptr || B->d < 3 || !B->pro_nt) return false;
+  const int JT = B->JT[0];
+  return B->T4[0] && B->h[0] == 16 * (JT - 1) + 4 && B->fast && mode_fast_fn<5>(JT) != nullptr;
+}
 
 // the padded slabs cost (hp / h)^2 of every pass over the vector: measured at
 // d = 4 (profiles/r06/d_prof/block_vs_grid.jsonl), the padded block basis

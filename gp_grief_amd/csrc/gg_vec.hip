@@ -189,9 +189,39 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
     sc->first = 0;
     sc->pending = 0;
     sc->repair = 0;
+    sc->rstored = 1;   // r is in its buffer (the update just wrote it)
     if (!(sqrt(s) >= sc->tol)) sc->done = 1;  // also stops on NaN
   }
 }
+
+// derived r (CgScalars::rstored): write the current r into its buffer --
+// r = (rstored ? r : p - beta_p p_prev) (- alpha q when pending) -- with its
+// r.r partials.  mode 2: only when the recurrence asked for a repair (before
+// the prologue); mode 1: the close (whenever r is not stored or an update is
+// pending).  cg_rho_kernel / cg_r_stored_kernel then mark it stored.
+__global__ __launch_bounds__(kVecThreads) void cg_r_materialize_kernel(
+    double* __restrict__ r, const double* __restrict__ p, const double* __restrict__ pprev,
+    const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
+    double* __restrict__ partials, int mode) {
+  if (sc->done && sc->rstored) return;
+  if (mode == 2 && (sc->done || !sc->repair || !sc->pending)) return;
+  if (mode == 1 && sc->rstored && !sc->pending) return;
+  const bool st = sc->rstored != 0;
+  const double bp = sc->beta_p;
+  const double a = sc->pending ? sc->alpha : 0.0;
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double rv = st ? r[i] : fma(-bp, pprev[i], p[i]);
+    if (a != 0.0) rv -= a * q[i];
+    r[i] = rv;
+    acc = fma(rv, rv, acc);
+  }
+  const double s = block_sum(acc);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ void cg_r_stored_kernel(CgScalars* sc) { sc->rstored = 1; }
 
 // x_defer: fold the deferred steps into x, x += sum_{i < xpend} xc[i] xp[i]
 // (also after convergence: x lags r by up to two steps)
@@ -384,7 +414,7 @@ __global__ void cg_xwin_init_kernel(CgScalars* sc, int K) {
 __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     const double* __restrict__ rr_part, int64_t nrr, int64_t rr_stride,
     const double* __restrict__ mv_part, int64_t nmv, int64_t pstride, CgScalars* sc,
-    const double* p_new, int xmode, int rq_ident) {
+    const double* p_new, int xmode, int rq_ident, int rder) {
   if (sc->done) return;
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   for (int64_t i = threadIdx.x; i < nmv; i += blockDim.x) {
@@ -413,6 +443,12 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     if (xmode == 3 && sc->warm) {
       sc->wa[sc->sreg] = sc->wn;
       sc->warm = 0;
+    }
+    // derived r: this iteration's prologue formed p_j with sc->beta; when an
+    // update was pending it computed r_j without storing it
+    if (rder) {
+      sc->beta_p = sc->beta;
+      if (pend) sc->rstored = 0;
     }
     if (pend) {
       sc->rho_prev = sc->rho;
@@ -559,6 +595,8 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     sc->wnext = 0;
     sc->warm = 0;
     for (int r = 0; r < kXWinMax; ++r) sc->wa[r] = 0;
+    sc->beta_p = 0.0;
+    sc->rstored = 1;   // r = b (or P b) is in its buffer
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -892,6 +930,16 @@ struct gg_cg {
   double* ring[gg::kXWinMax + 1] = {};
   int pcur = 0;
   double *q_c = nullptr, *q2_c = nullptr;   // q / q2 as created (swapped per iteration)
+  // derived r (CgScalars::rstored; with the window in the block basis): the
+  // prologue keeps no r -- 5 passes instead of 6.  rder_ok: the knob
+  // (GG_CG_RDERIVE, default on) latched at create; rder: in effect this solve
+  bool rder_ok = true;
+  bool rder = false;
+  // the direction before the current one (p_{j-2} for iteration j's prologue)
+  double* pprev_buf() const {
+    const int ns = nring();
+    return ring[(pcur + ns - 1) % ns];
+  }
   int launches() const { return block ? gg::block_launches(blk) : gg::kron_d(K); }
   int nring() const { return xmode == 3 ? xwin + 1 : 4; }
   // the length of the recurrence's vectors: the grid's n, or the block
@@ -1160,6 +1208,8 @@ int gg_cg_create_blocks(const gg_kron* K, int64_t blk0, int64_t nblk, double shi
       cg->rblk0 = blk0;
       cg->rnblk = nblk;
       cg->fused = true;   // layout 0, x_defer 2, rq 1: the block path's only form
+      const char* rde = gg::knob("GG_CG_RDERIVE");  // A/B: 0 keeps r in memory
+      cg->rder_ok = !(rde && atoi(rde) == 0);
       cg->mv_partials = gg::block_partials_needed(B);
       GG_HIP(hipMalloc(&cg->partials,
                        std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials) * sizeof(double)));
@@ -1238,6 +1288,8 @@ int gg_cg_create(const gg_kron* K, double shift, double* work_dev, gg_cg** out) 
       if (rqe) cg->rq = std::min(2, std::max(0, atoi(rqe)));   // 2: diagnostic
       const char* rse = gg::knob("GG_CG_RESTART");  // A/B: restart instead of repair
       cg->restart = rse && atoi(rse) == 1;
+      const char* rde = gg::knob("GG_CG_RDERIVE");  // A/B: 0 keeps r in memory
+      cg->rder_ok = !(rde && atoi(rde) == 0);
       cg->mv_partials = gg::kron_partials_needed(K, false);
       if (cg->blk) cg->mv_partials = std::max(cg->mv_partials, gg::block_partials_needed(cg->blk));
       const int64_t np = std::max<int64_t>(gg::kVecBlocks, 3 * cg->mv_partials);
@@ -1323,6 +1375,7 @@ int gg_cg_start(gg_cg* cg, const double* b_dev, double* x_dev, double rtol, doub
                 cg->xdefer == 2 && cg->rq == 1 && gg::block_d(cg->blk) >= 3;
     cg->xmode = (cg->fused && cg->fusion != 2) ? cg->xdefer : 0;
     if (cg->block && cg->xwin >= 2) cg->xmode = 3;
+    cg->rder = cg->xmode == 3 && cg->rder_ok && gg::block_rderive_ok(cg->blk);
     cg->reset_buffers();
     hipLaunchKernelGGL(gg::cg_xwin_init_kernel, dim3(1), dim3(1), 0, s, cg->sc,
                        cg->xmode == 3 ? cg->xwin : 0);
@@ -1403,6 +1456,19 @@ int gg_cg_get_xwin(const gg_cg* cg, int* K) {
       int b = 0;
       gg_cg_get_basis(cg, &b);
       *K = (b && cg->xwin >= 2) ? cg->xwin : 0;
+    }
+  });
+}
+
+int gg_cg_get_rderive(const gg_cg* cg, int* on) {
+  return gg::guard([&] {
+    GG_REQUIRE(cg && on, GG_ERR_VALUE, "NULL argument");
+    if (cg->x != nullptr) {
+      *on = cg->rder ? 1 : 0;
+    } else {
+      int K = 0;
+      gg_cg_get_xwin(cg, &K);
+      *on = (K >= 2 && cg->rder_ok && gg::block_rderive_ok(cg->blk)) ? 1 : 0;
     }
   });
 }
@@ -1540,9 +1606,14 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         // r -= alpha q, rho = r.r, textbook beta; the prologue then sees no
         // pending update (x_defer: r only, x keeps its deferred steps)
         if (!cg->restart) {
-          hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                             xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
-                             cg->partials, 2);
+          if (cg->rder)   // r derived from the directions (not stored)
+            hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0,
+                               s, cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials,
+                               2);
+          else
+            hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                               xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                               cg->partials, 2);
           GG_LAUNCH_CHECK();
           hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
                              (int64_t)nb, cg->sc, 2);
@@ -1564,6 +1635,8 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         fz.sn = n;
         fz.xdefer = xmode;
         fz.xwin = cg->xwin;
+        fz.rderive = cg->rder;
+        fz.pprev = cg->rder ? cg->pprev_buf() : nullptr;
         fz.first_dst = cg->first_dst;
         // r.q: conjugacy identity (layout 0: the prologue adds p_new.q_old
         // partials, the epilogue skips its pass over r) or read in the epilogue
@@ -1586,7 +1659,8 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, cg->rr_part,
                            pro_blocks, cg->rr_count, cg->partials, nparts, cg->mv_partials,
                            cg->sc,
-                           xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
+                           xdefer ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0,
+                           cg->rder ? 1 : 0);
         GG_LAUNCH_CHECK();
         if (cg->block) std::swap(cg->q, cg->q2);
         cg->rotate_dirs();
@@ -1652,13 +1726,21 @@ int gg_cg_close(gg_cg* cg, gg_stream stream) {
         hipLaunchKernelGGL(gg::cg_x_flushed_kernel, dim3(1), dim3(1), 0, s, cg->sc);
         GG_LAUNCH_CHECK();
       }
-      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                         xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc, cg->partials,
-                         1);
+      if (cg->rder)   // r from the directions (- alpha q when pending) into its buffer
+        hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials, 1);
+      else
+        hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                           xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                           cg->partials, 1);
       GG_LAUNCH_CHECK();
       hipLaunchKernelGGL(gg::cg_rho_kernel, dim3(1), dim3(1024), 0, s, cg->partials,
                          (int64_t)nb, cg->sc, 1);
       GG_LAUNCH_CHECK();
+      if (cg->rder) {
+        hipLaunchKernelGGL(gg::cg_r_stored_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+        GG_LAUNCH_CHECK();
+      }
     }
     // the block basis: the caller's x = P^T x_b
     if (cg->block) gg::block_fold(cg->blk, true, cg->xb, cg->x, nullptr, s);
@@ -1682,6 +1764,7 @@ int gg_cg_start_partial(gg_cg* cg, const double* b_dev, double* x_dev, double* r
     cg->await_finish = false;
     cg->xmode = cg->xdefer;
     if (cg->block && cg->xwin >= 2) cg->xmode = 3;
+    cg->rder = cg->xmode == 3 && cg->rder_ok && gg::block_rderive_ok(cg->blk);
     cg->reset_buffers();
     hipLaunchKernelGGL(gg::cg_xwin_init_kernel, dim3(1), dim3(1), 0, s, cg->sc,
                        cg->xmode == 3 ? cg->xwin : 0);
@@ -1744,6 +1827,8 @@ int gg_cg_iterate_partial(gg_cg* cg, double* red_dev, gg_stream stream) {
     fz.sn = n;
     fz.xdefer = xmode;
     fz.xwin = cg->xwin;
+    fz.rderive = cg->rder;
+    fz.pprev = cg->rder ? cg->pprev_buf() : nullptr;
     fz.first_dst = cg->first_dst;
     const bool rq_ident = cg->rq != 0;
     fz.er = rq_ident ? nullptr : cg->r;
@@ -1779,7 +1864,8 @@ int gg_cg_iterate_finish(gg_cg* cg, const double* red_dev, gg_stream stream) {
     // red = [rr, p.q_old | p.q, r.q, q.q]: one-element partial arrays
     hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, s, red_dev,
                        (int64_t)1, (int64_t)1, red_dev + 2, (int64_t)1, (int64_t)1, cg->sc,
-                       xmode ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0);
+                       xmode ? (const double*)cg->p2 : nullptr, xmode, rq_ident ? 1 : 0,
+                       cg->rder ? 1 : 0);
     GG_LAUNCH_CHECK();
     cg->rotate_dirs();
     cg->await_finish = false;
@@ -1815,9 +1901,16 @@ int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream) {
     }
     // the pending r update (x: the x_defer bookkeeping above, or here)
     GG_HIP(hipMemsetAsync(cg->partials, 0, nb * sizeof(double), s));
-    hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                       cg->xmode ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
-                       cg->partials, 1);
+    if (cg->rder) {
+      hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                         cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials, 1);
+      GG_LAUNCH_CHECK();
+      hipLaunchKernelGGL(gg::cg_r_stored_kernel, dim3(1), dim3(1), 0, s, cg->sc);
+    } else {
+      hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
+                         cg->xmode ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
+                         cg->partials, 1);
+    }
     GG_LAUNCH_CHECK();
     gg::launch_reduce_to(cg->partials, nb, rr_dev, s);
   });
@@ -2522,7 +2615,7 @@ int gg_cgs_fused_scalars(gg_cgs* c, const double* red_dev, const double* p_new_d
     // with one-element partial arrays (rr stride 1, matvec stride 1)
     hipLaunchKernelGGL(gg::cg_fused_scalars_kernel, dim3(1), dim3(1024), 0, gg::as_stream(stream),
                        red_dev, (int64_t)1, (int64_t)1, red_dev + 2, (int64_t)1, (int64_t)1,
-                       c->sc, p_new_dev, 2, 1);
+                       c->sc, p_new_dev, 2, 1, 0);
     GG_LAUNCH_CHECK();
   });
 }

@@ -907,6 +907,8 @@ class BlockHipEngine(object):
         xw = ctypes.c_int()
         native.check(L.gg_cg_get_xwin(self.h, ctypes.byref(xw)), "gg_cg_get_xwin")
         self.xwin = xw.value   # x_defer mode 3's window on this rank (0: pairs)
+        native.check(L.gg_cg_get_rderive(self.h, ctypes.byref(xw)), "gg_cg_get_rderive")
+        self.rderive = bool(xw.value)   # no r in memory on this rank
         _, n, self.launches = self.dk.block_info()
         self.n = n
         self.n_local = n // (1 << self.d) * self.nblk

@@ -169,6 +169,9 @@ class KronCG(object):
         # the block basis's x window (x_defer mode 3, GG_CG_XWIN; 0: not in effect)
         native.check(L.gg_cg_get_xwin(h, ctypes.byref(f)))
         self.xwin = f.value
+        # r derived from the window's directions (no r in memory; GG_CG_RDERIVE)
+        native.check(L.gg_cg_get_rderive(h, ctypes.byref(f)))
+        self.rderive = bool(f.value)
         self.n = int(K.shape[0])
         self.x = None
 

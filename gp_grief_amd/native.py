@@ -82,6 +82,7 @@ SIGNATURES = {
     "gg_cg_set_xdefer": [_vp, ctypes.c_int],
     "gg_cg_get_xdefer": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_get_xwin": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "gg_cg_get_rderive": [_vp, ctypes.POINTER(ctypes.c_int)],
     "gg_cg_calibrate": [_vp, ctypes.c_int, _c_dp, _c_i64p, _vp],
     "gg_cg_set_rq": [_vp, ctypes.c_int],
     "gg_cg_get_rq": [_vp, ctypes.POINTER(ctypes.c_int)],

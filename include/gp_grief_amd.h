@@ -207,6 +207,14 @@ int gg_cg_get_xdefer(const gg_cg* cg, int* on);
  * rounding.  *K: the window in effect (once started; before, what gg_cg_start
  * will pick), 0 when x is updated otherwise.                              */
 int gg_cg_get_xwin(const gg_cg* cg, int* K);
+/* With the window in the block basis the CG keeps no r in memory (round 6,
+ * GG_CG_RDERIVE=0 at create keeps it): the prologue takes r_{j-1} = p_{j-1} -
+ * beta_{j-1} p_{j-2} from the two directions the window's ring holds, so it
+ * reads p_{j-2} instead of r and stores no r -- 5 passes instead of 6; r is
+ * materialised by a repair and by every close (the textbook state).  Same
+ * iterates up to rounding.  *on: 1 when in effect (or, before start, when
+ * gg_cg_start will choose it).                                             */
+int gg_cg_get_rderive(const gg_cg* cg, int* on);
 /* The box's memory floor for the fused CG prologue launch (bench.py, round
  * 6): the prologue's six streams alone over the handle's own buffers -- read
  * p_old, r, q; write r, p_new, q (values unchanged, the launch's

@@ -349,6 +349,7 @@ def test_block_cg_window_matches_pairs(gg, monkeypatch, K):
     F = factors(ms, 3)
     b = np.random.default_rng(7).standard_normal(int(np.prod(ms)))
     runs = {}
+    monkeypatch.setenv("GG_CG_RDERIVE", "0")   # the same r recurrence in both
     for w in (str(K), "0"):
         monkeypatch.setenv("GG_CG_XWIN", w)
         Km = gg.tensors.KronMatrix(F, sym=True)
@@ -512,3 +513,58 @@ def test_cg_create_refuses_workspace_sized_under_another_snapshot(gg, monkeypatc
     work = gg.device.empty(we.value)
     native.check(L.gg_cg_create(dk.h, 0.05, native.dptr(work), ctypes.byref(h)))
     native.check(L.gg_cg_destroy(h))
+
+
+# ---- derived r (gg_cg_get_rderive): no r in memory with the window ---------
+@pytest.mark.parametrize("ms,shift", [((6, 12, 72, 72), 0.05), ((8, 6, 104, 104), 0.1),
+                                      ((40, 72, 72), 0.2)])
+def test_block_cg_rderive_vs_stored_and_oracle(gg, monkeypatch, ms, shift):
+    """The prologue taking r_{j-1} = p_{j-1} - beta_{j-1} p_{j-2} (5 passes)
+    solves to the oracle CG's answer, within 2 % of its iterations, like the
+    stored-r recurrence (GG_CG_RDERIVE=0); over 37 open iterations + close the
+    two agree to rounding and the closed r is the true residual."""
+    F = factors(ms, 9)
+    n = int(np.prod(ms))
+    b = np.random.default_rng(14).standard_normal(n)
+    xs, _, its = oracle_cg(F, b, shift, 1e-10, 20000)
+    out = {}
+    for rd in ("1", "0"):
+        monkeypatch.setenv("GG_CG_RDERIVE", rd)
+        K = gg.tensors.KronMatrix(F, sym=True)
+        s = gg.linalg.KronCG(K, shift)
+        assert s.rderive == (rd == "1") and s.xwin == 8
+        x, info = gg.linalg.cg(K, b.reshape(-1, 1), shift=shift, rtol=1e-10, maxiter=20000)
+        it = gg.linalg.cg.last.iters
+        assert info == 0 and abs(it - its) <= max(2, 0.02 * its), (rd, it, its)
+        assert rel(x, xs) < 1e-8
+        s.start(dev(gg, b), rtol=1e-14)
+        for k in (5, 11, 21):
+            s.iterate(k, close=False)
+        s.close()
+        itc, conv, res, tol = s.status()
+        xc = host(gg, s.x)
+        r = b - (oracle.kron_matvec(F, xc) + shift * xc)
+        assert itc == 37 and abs(np.linalg.norm(r) - res) <= 1e-8 * np.linalg.norm(b)
+        out[rd] = (xc, res)
+    assert rel(out["1"][0], out["0"][0]) < 1e-9
+    assert abs(out["1"][1] - out["0"][1]) <= 1e-9 * np.linalg.norm(b)
+
+
+def test_block_cg_rderive_repairs(gg, monkeypatch):
+    """Forced cancellations (GG_CG_CANCEL_TOL = 0.3 counts beta < 0.3 as
+    cancelled) exercise the repair with derived r: it materialises r_j from
+    the directions, takes the true r.r, and the solve still lands on the
+    oracle's x."""
+    monkeypatch.setenv("GG_CG_CANCEL_TOL", "0.3")
+    ms, shift = (6, 12, 72, 72), 0.05
+    F = factors(ms, 10)
+    K = gg.tensors.KronMatrix(F, sym=True)
+    s = gg.linalg.KronCG(K, shift)
+    assert s.rderive
+    b = np.random.default_rng(15).standard_normal(int(np.prod(ms)))
+    s.start(dev(gg, b), rtol=1e-10)
+    s.iterate(20000, check_every=25)
+    it, conv, res, tol = s.status()
+    assert conv and s.cancels() > 0
+    xs, _, its = oracle_cg(F, b, shift, 1e-10, 20000)
+    assert rel(host(gg, s.x), xs) < 1e-8

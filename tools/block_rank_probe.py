@@ -73,11 +73,11 @@ def main():
             launch = [v / max(nm, 1) for v in per]
             ms_it = ev[2].elapsed_time(ev[3]) / a.steps
             flops = bench.block_launch_flops(nl, m, d)
-            passes = bench.block_launch_passes(d, eng.xwin)
+            passes = bench.block_launch_passes(d, eng.xwin, eng.rderive)
             dom = max(range(len(launch)), key=lambda i: launch[i])
             rec = {
                 "G": G, "rank": g, "blocks": [eng.blk0, eng.nblk], "n_local": nl,
-                "x_window": eng.xwin, "iterations": it,
+                "x_window": eng.xwin, "r_derived": eng.rderive, "iterations": it,
                 "ms_per_iteration": ms_it, "launch_ms": launch,
                 "launch_ms_source": "HIP events the library records around each launch "
                                     "(gg_cg_profile) over %d iterations" % a.steps,

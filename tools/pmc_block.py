@@ -1,7 +1,7 @@
 """HBM traffic per launch of the block-basis fused CG (gg_kronb.hip) from two
 rocprofv3 PMC passes, as tools/pmc_traffic.py does for the grid basis.
 
-usage: python tools/pmc_block.py RD_DIR WR_DIR OUT_JSON [XWIN]
+usage: python tools/pmc_block.py RD_DIR WR_DIR OUT_JSON [XWIN [RDERIVE]]
 
 XWIN: the x window the runs took (gg_cg_get_xwin; default GG_CG_XWIN or the
 library default 8; 0 = mode 2's balanced pairs).
@@ -42,6 +42,8 @@ def main():
     rd_dir, wr_dir, out = sys.argv[1:4]
     xwin = int(sys.argv[4]) if len(sys.argv) > 4 else int(os.environ.get("GG_CG_XWIN", "8"))
     xwin = xwin if xwin >= 2 else 0
+    rder = bool(int(sys.argv[5])) if len(sys.argv) > 5 else \
+        (xwin >= 2 and os.environ.get("GG_CG_RDERIVE", "1") != "0")
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     rd, names = dispatches(rd_dir)
@@ -51,7 +53,7 @@ def main():
     iters = [ids[i:i + L] for i in range(0, len(ids) - L + 1, L)]
     last2 = iters[-2:]
     n = 200 ** 4
-    passes = [float(v) for v in bench.block_launch_passes(d, xwin)]
+    passes = [float(v) for v in bench.block_launch_passes(d, xwin, rder)]
     per_pos = []
     for k in range(L):
         dids = [it[k] for it in last2]
@@ -66,7 +68,7 @@ def main():
         per_pos.append(pp)
     tot = sum(pp["traffic_bytes"] for pp in per_pos)
     res = {
-        "block_basis": True, "recurrence": "fused", "fusion_layout": 0, "x_deferred": 2, "x_window": xwin,
+        "block_basis": True, "recurrence": "fused", "fusion_layout": 0, "x_deferred": 2, "x_window": xwin, "r_derived": rder,
         "rq_identity": 1, "fold_mask": 0,
         "source_sha256": bench.kernel_source_hash(),
         "sources": bench.KERNEL_SOURCES,
