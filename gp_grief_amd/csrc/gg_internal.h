@@ -123,6 +123,11 @@ struct CgScalars {
   // direction) unless rstored -- r is in its buffer (start, repair, close)
   double beta_p;
   int rstored;
+  // the last two directions the recurrence formed (recorded by the scalars
+  // of every iteration that ran: the host keeps rotating its buffers through
+  // the skipped iterations after convergence, these do not move)
+  const double* rp_cur;
+  const double* rp_prev;
 };
 
 // Fusions carried by one mode-product launch (gg_kron.hip).  Every pointer is

@@ -199,15 +199,17 @@ __global__ __launch_bounds__(1024) void cg_rho_kernel(const double* __restrict__
 // r.r partials.  mode 2: only when the recurrence asked for a repair (before
 // the prologue); mode 1: the close (whenever r is not stored or an update is
 // pending).  cg_rho_kernel / cg_r_stored_kernel then mark it stored.
+// The directions are the ones the scalars recorded (sc->rp_cur, rp_prev).
 __global__ __launch_bounds__(kVecThreads) void cg_r_materialize_kernel(
-    double* __restrict__ r, const double* __restrict__ p, const double* __restrict__ pprev,
-    const double* __restrict__ q, int64_t n, const CgScalars* __restrict__ sc,
-    double* __restrict__ partials, int mode) {
+    double* __restrict__ r, const double* __restrict__ q, int64_t n,
+    const CgScalars* __restrict__ sc, double* __restrict__ partials, int mode) {
   if (sc->done && sc->rstored) return;
   if (mode == 2 && (sc->done || !sc->repair || !sc->pending)) return;
   if (mode == 1 && sc->rstored && !sc->pending) return;
   const bool st = sc->rstored != 0;
   const double bp = sc->beta_p;
+  const double* __restrict__ p = sc->rp_cur;
+  const double* __restrict__ pprev = sc->rp_prev;
   const double a = sc->pending ? sc->alpha : 0.0;
   double acc = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -449,6 +451,8 @@ __global__ __launch_bounds__(1024) void cg_fused_scalars_kernel(
     if (rder) {
       sc->beta_p = sc->beta;
       if (pend) sc->rstored = 0;
+      sc->rp_prev = sc->rp_cur;
+      sc->rp_cur = p_new;
     }
     if (pend) {
       sc->rho_prev = sc->rho;
@@ -597,6 +601,7 @@ __global__ void cg_init_kernel(const double* __restrict__ partials, int64_t coun
     for (int r = 0; r < kXWinMax; ++r) sc->wa[r] = 0;
     sc->beta_p = 0.0;
     sc->rstored = 1;   // r = b (or P b) is in its buffer
+    sc->rp_cur = sc->rp_prev = nullptr;
     sc->done = (s == 0.0 || !(sqrt(s) >= sc->tol)) ? 1 : 0;
   }
 }
@@ -1608,8 +1613,7 @@ int gg_cg_iterate_open(gg_cg* cg, int max_iters, int check_every, gg_stream stre
         if (!cg->restart) {
           if (cg->rder)   // r derived from the directions (not stored)
             hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0,
-                               s, cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials,
-                               2);
+                               s, cg->r, cg->q, n, cg->sc, cg->partials, 2);
           else
             hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                                xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
@@ -1728,7 +1732,7 @@ int gg_cg_close(gg_cg* cg, gg_stream stream) {
       }
       if (cg->rder)   // r from the directions (- alpha q when pending) into its buffer
         hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                           cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials, 1);
+                           cg->r, cg->q, n, cg->sc, cg->partials, 1);
       else
         hipLaunchKernelGGL(gg::cg_xr_update_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
                            xdefer ? nullptr : cg->x, cg->r, cg->p, cg->q, n, cg->sc,
@@ -1903,7 +1907,7 @@ int gg_cg_close_partial(gg_cg* cg, double* rr_dev, gg_stream stream) {
     GG_HIP(hipMemsetAsync(cg->partials, 0, nb * sizeof(double), s));
     if (cg->rder) {
       hipLaunchKernelGGL(gg::cg_r_materialize_kernel, dim3(nb), dim3(gg::kVecThreads), 0, s,
-                         cg->r, cg->p, cg->pprev_buf(), cg->q, n, cg->sc, cg->partials, 1);
+                         cg->r, cg->q, n, cg->sc, cg->partials, 1);
       GG_LAUNCH_CHECK();
       hipLaunchKernelGGL(gg::cg_r_stored_kernel, dim3(1), dim3(1), 0, s, cg->sc);
     } else {

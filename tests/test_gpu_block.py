@@ -517,7 +517,7 @@ def test_cg_create_refuses_workspace_sized_under_another_snapshot(gg, monkeypatc
 
 # ---- derived r (gg_cg_get_rderive): no r in memory with the window ---------
 # (derived r needs the fast prologue kernel on axis 0: an order 16 TF + 4 >= 40)
-@pytest.mark.parametrize("ms,shift", [((40, 6, 72, 72), 0.05), ((104, 4, 104, 104), 0.1),
+@pytest.mark.parametrize("ms,shift", [((40, 6, 72, 72), 0.05), ((104, 2, 72, 72), 0.1),
                                       ((40, 72, 72), 0.2)])
 def test_block_cg_rderive_vs_stored_and_oracle(gg, monkeypatch, ms, shift):
     """The prologue taking r_{j-1} = p_{j-1} - beta_{j-1} p_{j-2} (5 passes)
