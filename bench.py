@@ -1337,13 +1337,19 @@ def main():
     result.update(extra)
     # the box: the prologue's streams alone on these
     # buffers -- the launch's memory floor here -- beside the launch itself
-    cal_bytes = 6.0 * 8.0 * n
+    rd = bool(getattr(solver, "rderive", False))
+    cal_bytes = (5.0 if rd else 6.0) * 8.0 * n
     result["prologue_calibration_gbs"] = cal_bytes / (cal_ms * 1e-3) / 1e9
     result["prologue_calibration"] = {
         "ms": cal_ms, "bytes": cal_bytes,
-        "pattern": "read p_old, r, q; write r, p_new, q (the fused prologue's six streams, "
-                   "its non-temporal mask, no MFMA work; gg_cg_calibrate, 5 passes)",
-        "buffer_offsets_mod_2MiB": dict(zip(["r", "p_old", "p_new", "q"], cal_off)),
+        "pattern": ("read p_old, p_{j-2}, q; write p_new, q (the derived-r prologue's five "
+                    "streams" if rd else
+                    "read p_old, r, q; write r, p_new, q (the fused prologue's six streams") +
+                   ", its non-temporal mask, no MFMA work; gg_cg_calibrate: a plain "
+                   "grid-stride stream kernel, 2 untimed + 5 timed passes -- a reference "
+                   "rate for this box, not a bound)",
+        "buffer_offsets_mod_2MiB": dict(zip(["r" if not rd else "p_{j-2}", "p_old", "p_new",
+                                             "q"], cal_off)),
         "buffers_256B_aligned": all(v % 256 == 0 for v in cal_off),
         "prologue_launch_ms": per_pos[0],
         "prologue_launch_vs_streams": per_pos[0] / cal_ms}

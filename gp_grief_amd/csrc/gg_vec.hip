@@ -317,10 +317,13 @@ __global__ __launch_bounds__(kVecThreads) void cg_x_flush2_kernel(double* __rest
 // The CG prologue's stream pattern alone (gg_cg_calibrate): per element,
 // read p_old, r and q, write r, p_new and q -- the six passes of the fused
 // prologue launch over the same buffers, with its non-temporal mask (every
-// stream but the q write, the launch's output Y), values passed through
-// unchanged (r = r, p_new = p_old, q = q; the loaded values pass an opaque
-// asm so the compiler cannot drop a store of what was just loaded from the
-// same address).  No MFMA work: the launch's memory floor on this box.
+// stream but the q write, the launch's output Y); with derived r (RD) the
+// five of that prologue: read p_old, p_{j-2} (in r's place) and q, write
+// p_new and q.  Values pass through unchanged (r = r, p_new = p_old, q = q;
+// the loaded values pass an opaque asm so the compiler cannot drop a store of
+// what was just loaded from the same address).  No MFMA work: the launch's
+// streams alone on this box.
+template <bool RD>
 __global__ __launch_bounds__(256) void cg_stream_probe_kernel(double* __restrict__ r,
                                                               const double* __restrict__ p,
                                                               double* __restrict__ p2,
@@ -342,7 +345,12 @@ __global__ __launch_bounds__(256) void cg_stream_probe_kernel(double* __restrict
     for (int u = 0; u < kU; ++u) asm volatile("" : "+v"(a[u]), "+v"(b[u]), "+v"(c[u]));
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      __builtin_nontemporal_store(b[u], reinterpret_cast<v2*>(r + i + u * stride));
+      if (RD) {
+        // keep the p_{j-2} stream's loads live without changing p_new
+        asm volatile("" : : "v"(b[u]));
+      } else {
+        __builtin_nontemporal_store(b[u], reinterpret_cast<v2*>(r + i + u * stride));
+      }
       __builtin_nontemporal_store(a[u], reinterpret_cast<v2*>(p2 + i + u * stride));
       *reinterpret_cast<v2*>(q + i + u * stride) = c[u];
     }
@@ -1489,11 +1497,21 @@ int gg_cg_calibrate(gg_cg* cg, int reps, double* ms_host, int64_t* offsets_host,
     GG_HIP(hipGetDevice(&dev));
     GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     gg::EventSet ev(2);
-    // one untimed pass (first touch of p2 in this process), then reps timed
-    for (int it = 0; it <= reps; ++it) {
-      if (it == 1) GG_HIP(hipEventRecord(ev.ev[0], s));
-      hipLaunchKernelGGL(gg::cg_stream_probe_kernel, dim3((unsigned)std::max(cus, 1) * 8),
-                         dim3(256), 0, s, cg->r, cg->p, cg->p2, cg->q, cg->nvec());
+    // the prologue this solve runs: derived r reads p_{j-2} in r's place
+    // (a direction slot the first iterations overwrite anyway)
+    const bool rd = cg->rder;
+    double* second = rd ? cg->ring[(cg->pcur + 2) % cg->nring()] : cg->r;
+    // two untimed passes (first touch in this process), then reps timed
+    for (int it = 0; it < reps + 2; ++it) {
+      if (it == 2) GG_HIP(hipEventRecord(ev.ev[0], s));
+      if (rd)
+        hipLaunchKernelGGL(gg::cg_stream_probe_kernel<true>,
+                           dim3((unsigned)std::max(cus, 1) * 8), dim3(256), 0, s, second, cg->p,
+                           cg->p2, cg->q, cg->nvec());
+      else
+        hipLaunchKernelGGL(gg::cg_stream_probe_kernel<false>,
+                           dim3((unsigned)std::max(cus, 1) * 8), dim3(256), 0, s, second, cg->p,
+                           cg->p2, cg->q, cg->nvec());
       GG_LAUNCH_CHECK();
     }
     GG_HIP(hipEventRecord(ev.ev[1], s));
@@ -1503,7 +1521,7 @@ int gg_cg_calibrate(gg_cg* cg, int reps, double* ms_host, int64_t* offsets_host,
     *ms_host = ms / reps;
     if (offsets_host) {
       // the buffers' addresses modulo 2 MiB (the allocator's large-page grain)
-      const double* b[4] = {cg->r, cg->p, cg->p2, cg->q};
+      const double* b[4] = {second, cg->p, cg->p2, cg->q};
       for (int k = 0; k < 4; ++k)
         offsets_host[k] = (int64_t)(reinterpret_cast<uintptr_t>(b[k]) & ((1u << 21) - 1));
     }

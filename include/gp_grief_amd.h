@@ -215,14 +215,16 @@ int gg_cg_get_xwin(const gg_cg* cg, int* K);
  * iterates up to rounding.  *on: 1 when in effect (or, before start, when
  * gg_cg_start will choose it).                                             */
 int gg_cg_get_rderive(const gg_cg* cg, int* on);
-/* The box's memory floor for the fused CG prologue launch (bench.py, round
- * 6): the prologue's six streams alone over the handle's own buffers -- read
- * p_old, r, q; write r, p_new, q (values unchanged, the launch's
- * non-temporal mask) -- one untimed and `reps` timed passes, HIP events on the
- * stream (synchronising).  *ms_host: time per pass; offsets_host (4 entries,
- * may be NULL): the addresses of r, p_old, p_new, q modulo 2 MiB.  Call after
- * gg_cg_start and before the iterations (it overwrites p_new, which the first
- * prologue writes anyway).                                                  */
+/* A reference stream rate for the fused CG prologue launch on this box
+ * (bench.py, round 6): the prologue's streams alone over the handle's own
+ * buffers -- read p_old, r, q, write r, p_new, q (six passes); with derived r
+ * read p_old, p_{j-2}, q, write p_new, q (five) -- values unchanged, the
+ * launch's non-temporal mask, a plain grid-stride kernel: two untimed and
+ * `reps` timed passes, HIP events on the stream (synchronising).  *ms_host:
+ * time per pass; offsets_host (4 entries, may be NULL): the addresses of the
+ * second stream (r or p_{j-2}), p_old, p_new, q modulo 2 MiB.  Call after
+ * gg_cg_start and before the iterations (it overwrites p_new and the slot
+ * p_{j-2} will take, which the first prologues write anyway).              */
 int gg_cg_calibrate(gg_cg* cg, int reps, double* ms_host, int64_t* offsets_host,
                     gg_stream stream);
 /* Fused recurrence, layout 0: where r_j.q_j (for beta's |r - alpha q|^2
