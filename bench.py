@@ -845,7 +845,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
     if (m, d) != (200, 4):
         return None, "no PMC passes for this workload"
     if not os.path.exists(path):
-        return None, "no PMC passes committed (%s)" % PMC_JSON
+        return None, "no PMC passes committed (%s)" % (PMC_JSON_BLOCK if block else PMC_JSON)
     rec = json.load(open(path))
     if bool(rec.get("block_basis", False)) != bool(block):
         return None, "PMC passes taken in another CG basis"
