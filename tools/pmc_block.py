@@ -6,8 +6,9 @@ usage: python tools/pmc_block.py RD_DIR WR_DIR OUT_JSON [XWIN [RDERIVE]]
 XWIN: the x window the runs took (gg_cg_get_xwin; default GG_CG_XWIN or the
 library default 8; 0 = mode 2's balanced pairs).
 
-Counters (separate --pmc runs of `bench.py --steps 4 --warmup 2 --matvec 0
---lanczos 0 --grief off --cpu-baseline off`, kernel trace only, per
+Counters (separate --pmc runs of `bench.py --steps 2 --warmup 10 --matvec 0
+--lanczos 0 --grief off --cpu-baseline off` -- 12 iterations, so the last two
+carry the full x window; PMC_BENCH_STEPS overrides the label --, kernel trace only, per
 MI355X_MICROARCH.md): reads TCC_EA0_RDREQ_{32B,64B,128B}_sum, writes
 TCC_EA0_WRREQ_64B_sum; bytes = request counts x request sizes.  The launches
 of one iteration are the three blk_* kernels (prologue, plain mode product,
@@ -77,10 +78,11 @@ def main():
                         "per_position_ratio": [pp["ratio"] for pp in per_pos]},
         "per_position": per_pos,
         "method": "separate rocprofv3 --pmc passes (reads by request size / writes), kernel "
-                  "trace only, bench.py --steps 4 --warmup 2 at 200^4 (block basis); bytes = "
+                  "trace only, bench.py %s at 200^4 (block basis); bytes = "
                   "request counts x request sizes, averaged over the last two iterations; "
                   "checked per launch against its algorithmic passes (%s x 12.8 GB)"
-                  % " / ".join("%g" % v for v in passes),
+                  % (os.environ.get("PMC_BENCH_STEPS", "--steps 2 --warmup 10"),
+                     " / ".join("%g" % v for v in passes)),
     }
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_position"}))
