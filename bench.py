@@ -488,7 +488,7 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
     eng = Engine(K, world, rank, s)
     ex = TorchExchange()
     sync = torch.cuda.synchronize if on_gpu else (lambda: None)
-    fold_ms = unfold_ms = xred_ms = None
+    fold_ms = unfold_ms = xred_ms = xgat_ms = unfold_all_ms = None
     if on_gpu:
         yg = grid_rhs_device(m, d, torch, dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -540,6 +540,25 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
             xred_ms = e0.elapsed_time(e1)
         del xg
         torch.cuda.empty_cache()
+        # the default way back (distributed.block_solution): an all-gather of
+        # the N / G shares, then the whole unfold on every rank (under gloo the
+        # shares are not gathered through the host: the unfold is timed on the
+        # rank's own share repeated, the same bytes)
+        if backend == "nccl":
+            e0.record()
+            xa = ex.all_gather(cg.x)
+            e1.record()
+            sync()
+            xgat_ms = e0.elapsed_time(e1)
+        else:
+            xa = torch.cat([cg.x] * world)
+        e0.record()
+        xg = eng.unfold_all(xa)
+        e1.record()
+        sync()
+        unfold_all_ms = e0.elapsed_time(e1)
+        del xa, xg
+        torch.cuda.empty_cache()
     nl = n // world
     bf = backend_fields(backend, world, torch, on_gpu)
     ms_per_step = 1e3 * dt / a.steps
@@ -585,7 +604,7 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
     if ph:
         keys = sorted(ph)
         v = torch.tensor([ph[k] / a.steps for k in keys] + [x / max(nm, 1) for x in per] +
-                         [fold_ms or 0.0, unfold_ms or 0.0],
+                         [fold_ms or 0.0, unfold_ms or 0.0, unfold_all_ms or 0.0],
                          dtype=torch.float64, device=dev)
         _all_reduce(dist, v, dist.ReduceOp.MAX)
         vals = [float(u) for u in v.tolist()]
@@ -608,11 +627,18 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
         ar = phases.get("allreduce", 0.0)
         res_["allreduce"] = {"ms_per_iteration": ar, "share_of_iteration": ar / ms_per_step,
                              "doubles_per_iteration": 5, "collectives": bf["collectives"]}
-        res_["fold_ms"] = vals[-2] if on_gpu else None
-        res_["unfold_ms"] = vals[-1] if on_gpu else None
+        res_["fold_ms"] = vals[-3] if on_gpu else None
+        res_["unfold_ms"] = vals[-2] if on_gpu else None
         res_["fold_unfold_bytes_per_rank"] = 8.0 * (n + nl)
+        # the solution's two ways back, once per solve (rank 0's events; the
+        # unfolds max over ranks): "reduce" = unfold_ms + solution_allreduce_ms,
+        # "gather" (distributed.solve's default) = solution_allgather_ms +
+        # unfold_all_ms
+        res_["unfold_all_ms"] = vals[-1] if on_gpu else None
         if xred_ms is not None:
             res_["solution_allreduce_ms"] = xred_ms
+        if xgat_ms is not None:
+            res_["solution_allgather_ms"] = xgat_ms
     return res_
 
 

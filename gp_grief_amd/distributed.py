@@ -34,6 +34,7 @@ GPU).  The exchange is injected: `TorchExchange` (RCCL / gloo collectives) in
 production; the tests also drive the same orchestration with virtual ranks.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -108,6 +109,19 @@ class TorchExchange(object):
         out = [None] * self.dist.get_world_size(self.group)
         self.dist.all_gather_object(out, obj, group=self.group)
         return out
+
+    def all_gather(self, t):
+        """The ranks' equal-length 1-D tensors concatenated in rank order (one
+        RCCL all-gather into a device tensor; under gloo through host copies)."""
+        world = self.dist.get_world_size(self.group)
+        if self.backend == "nccl":
+            out = self.torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+            self.dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
+            return out
+        h = t.detach().cpu().contiguous()
+        parts = [self.torch.empty_like(h) for _ in range(world)]
+        self.dist.all_gather(parts, h, group=self.group)
+        return self.torch.cat(parts).to(t.device)
 
     def size(self):
         return self.dist.get_world_size(self.group)
@@ -931,6 +945,11 @@ class BlockHipEngine(object):
         the ranks is the solution)."""
         return self.dk.block_fold_range(x_local, self.blk0, self.nblk, inverse=True, out=out)
 
+    def unfold_all(self, x_blocks, out=None):
+        """P^T x of the whole block vector (every rank's blocks in rank
+        order, as an all-gather leaves them): the solution on the grid."""
+        return self.dk.block_fold_range(x_blocks, 0, 1 << self.d, inverse=True, out=out)
+
     def apply(self, x, y):
         self.dk.block_matvec_range(x, self.blk0, self.nblk, out=y)
 
@@ -1001,6 +1020,24 @@ def comm_exchange(comm):
     return ex, ex.size(), ex.rank()
 
 
+def block_solution(eng, ex, xl):
+    """The grid solution on every rank from the ranks' block shares.  Default
+    (GG_DIST_SOLUTION=gather): one all-gather of the N / G shares (each rank
+    receives (G - 1) N / G doubles) and the whole unfold on every rank;
+    "reduce": each rank unfolds its own blocks into a zero grid vector (every
+    element: each grid point mixes all 2^d blocks) and one all-reduce of N
+    doubles sums them (a ring moves 2 (G - 1) N / G per rank).  Exchanges or
+    engines without all_gather / unfold_all take the all-reduce."""
+    how = os.environ.get("GG_DIST_SOLUTION", "gather")
+    if how not in ("gather", "reduce"):
+        raise ValueError("GG_DIST_SOLUTION must be 'gather' or 'reduce'")
+    if how == "gather" and hasattr(ex, "all_gather") and hasattr(eng, "unfold_all"):
+        return eng.unfold_all(ex.all_gather(xl))
+    x = eng.unfold(xl)
+    ex.all_reduce(x)
+    return x
+
+
 def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_every=20,
           decomposition="auto", engine=None):
     """CG on (K + shift I) x = b across the ranks of `comm` (every rank passes
@@ -1037,8 +1074,7 @@ def solve(K, b, shift=0.0, comm=True, rtol=1e-5, atol=0.0, maxiter=None, check_e
             bg = dev.to_device(b).reshape(-1)
         cg = ParityShardCG(F, world, rank, ex, shift, engine=eng)
         xl, info = cg.solve(eng.fold(bg), rtol, atol, maxiter, check_every)
-        x = eng.unfold(xl)
-        ex.all_reduce(x)
+        x = block_solution(eng, ex, xl)
         it, _, res, tol = cg.status()
         solve.last_cancels = cg.cancels()
     elif decomposition == "parity":

@@ -234,6 +234,14 @@ class ThreadExchange(object):
         self.bar.wait()
         return out
 
+    def all_gather(self, t):
+        g = self.local.rank
+        self.slots[g] = t.clone()
+        self.bar.wait()
+        out = torch.cat(list(self.slots))
+        self.bar.wait()
+        return out
+
     def all_reduce(self, t):
         g = self.local.rank
         self.slots[g] = t.clone()
@@ -458,3 +466,8 @@ class BlockNumpyEngine(ParityNumpyEngine):
         full = np.zeros(self.nb << self.d)
         full[self.blk0 * self.nb:(self.blk0 + self.nblk) * self.nb] = np.asarray(xl)
         return torch.from_numpy(oracle.kron.block_fold(full, self.ms, inverse=True))
+
+    def unfold_all(self, xall):
+        """P^T of the whole block vector (the ranks' shares in rank order)."""
+        return torch.from_numpy(oracle.kron.block_fold(np.asarray(xall, dtype=np.float64),
+                                                       self.ms, inverse=True))

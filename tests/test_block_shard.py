@@ -49,6 +49,24 @@ def test_rank_blocks_are_the_parity_blocks(world):
                 assert (b >> (d - 1 - k)) & 1 == (g >> (K - 1 - k)) & 1
 
 
+def test_block_engine_unfold_all_equals_sum_of_rank_unfolds():
+    """The all-gather route: the whole unfold of the concatenated shares is
+    the sum of the ranks' own unfolds (the all-reduce route), bit for bit up
+    to the order of the sum."""
+    from dist_helpers import BlockNumpyEngine, reference_factors
+    from gp_grief_amd.tensors import KronMatrix
+    ms, world = (6, 8, 10), 4
+    F = [reference_factors(m, 1)[0] for m in ms]
+    Kh = KronMatrix(F, sym=True)
+    b = np.random.default_rng(5).standard_normal(int(np.prod(ms)))
+    engs = [BlockNumpyEngine(Kh, world, g, 0.1) for g in range(world)]
+    shares = [e.fold(b) for e in engs]
+    via_gather = engs[0].unfold_all(torch.cat(shares)).numpy()
+    via_reduce = sum(e.unfold(x).numpy() for e, x in zip(engs, shares))
+    assert np.linalg.norm(via_gather - via_reduce) < 1e-14 * np.linalg.norm(b)
+    assert np.linalg.norm(via_gather - b) < 1e-13 * np.linalg.norm(b)
+
+
 def test_block_engine_fold_unfold_sum_over_ranks():
     """The ranks' unfold contributions sum to P^T of the whole block vector,
     and their folds tile P b."""
@@ -77,11 +95,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, ms, shift, out_dir):
+def _worker(rank, world, port, ms, shift, out_dir, solution="gather"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      GG_DIST_SOLUTION=solution)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from dist_helpers import BlockNumpyEngine, reference_factors
     from gp_grief_amd.distributed import TorchExchange, solve
@@ -97,17 +116,23 @@ def _worker(rank, world, port, ms, shift, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,ms", [(2, (8, 6, 10)), (4, (6, 8, 8, 6)), (8, (6, 6, 8))])
-def test_block_sharded_solve_gloo(tmp_path, world, ms):
+@pytest.mark.parametrize("world,ms,solution", [(2, (8, 6, 10), "gather"),
+                                               (2, (8, 6, 10), "reduce"),
+                                               (4, (6, 8, 8, 6), "gather"),
+                                               (8, (6, 6, 8), "gather"),
+                                               (8, (6, 6, 8), "reduce")])
+def test_block_sharded_solve_gloo(tmp_path, world, ms, solution):
     """distributed.solve over gloo processes: every rank gets the whole x,
     equal to the oracle CG's on the reference operator (x to 1e-8, iteration
     counts within 2 %; the sharded fused recurrence restarts a cancelled
-    beta instead of repairing it)."""
+    beta instead of repairing it).  The solution comes back by an all-gather
+    of the block shares + the whole unfold (default) or by each rank's
+    unfold summed in an all-reduce (GG_DIST_SOLUTION=reduce)."""
     from dist_helpers import reference_factors
     shift = 0.05
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, ms, shift, str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, ms, shift, str(tmp_path), solution),
+                       nprocs=world, join=True, start_method="spawn")
     res = [np.load(os.path.join(tmp_path, "rank%d.npz" % g)) for g in range(world)]
     F = [reference_factors(m, 1)[0] for m in ms]
     b = np.random.default_rng(11).standard_normal(int(np.prod(ms)))

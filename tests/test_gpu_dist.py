@@ -323,19 +323,24 @@ def reference_factors_ms(ms):
             for k, x in enumerate(g)]
 
 
-@pytest.mark.parametrize("world,ms,shift", [(2, (6, 12, 40, 40), 0.05), (4, (6, 12, 40, 40), 0.05),
-                                            (8, (40, 40, 40, 40), 0.5), (16, (6, 12, 40, 40), 0.05),
-                                            (4, (8, 72, 72), 0.2), (2, (40, 8, 72, 72), 0.1)])
-def test_block_sharded_cg_virtual_ranks(gpu, world, ms, shift):
+@pytest.mark.parametrize("world,ms,shift,solution", [
+    (2, (6, 12, 40, 40), 0.05, "gather"), (4, (6, 12, 40, 40), 0.05, "gather"),
+    (8, (40, 40, 40, 40), 0.5, "gather"), (16, (6, 12, 40, 40), 0.05, "gather"),
+    (4, (8, 72, 72), 0.2, "gather"), (2, (40, 8, 72, 72), 0.1, "gather"),
+    (4, (8, 72, 72), 0.2, "reduce"), (8, (40, 40, 40, 40), 0.5, "reduce")])
+def test_block_sharded_cg_virtual_ranks(gpu, monkeypatch, world, ms, shift, solution):
     """distributed.solve, block decomposition: each virtual rank (a thread)
     runs the block kernels on its 2^d / G blocks (gg_cg_create_blocks,
-    gg_cg_*_partial / _finish), folds b on the device and contributes its
-    unfold to the all-reduced x.  Every rank's x equals the oracle CG's (1e-8),
+    gg_cg_*_partial / _finish), folds b on the device and gets x back by an
+    all-gather of the shares + the whole device unfold (default) or by its
+    own unfold summed in an all-reduce (GG_DIST_SOLUTION=reduce).  Every
+    rank's x equals the oracle CG's (1e-8),
     the iteration count the oracle's and the single-GPU block CG's within 2 %
     (the restart vs repair of a cancelled beta, and the summation order:
     test_restart_penalty_single_gpu separates the two)."""
     import gp_grief_amd as gg
     from gp_grief_amd.distributed import solve
+    monkeypatch.setenv("GG_DIST_SOLUTION", solution)
     F = reference_factors_ms(ms)
     K = gg.tensors.KronMatrix(F, sym=True)
     n = int(np.prod(ms))
