@@ -541,24 +541,24 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
         del xg
         torch.cuda.empty_cache()
         # the default way back (distributed.block_solution): an all-gather of
-        # the N / G shares, then the whole unfold on every rank (under gloo the
-        # shares are not gathered through the host: the unfold is timed on the
-        # rank's own share repeated, the same bytes)
+        # the N / G shares, then the whole unfold on every rank.  Timed with
+        # RCCL only: in the one-card rehearsal the ranks' two more grid-sized
+        # buffers push the card's shared HBM past its size and the driver
+        # evicts buffers to host memory (the unfold then ran 1.5 s against
+        # 13.5 ms alone, tools/fold_probe.py)
         if backend == "nccl":
             e0.record()
             xa = ex.all_gather(cg.x)
             e1.record()
             sync()
             xgat_ms = e0.elapsed_time(e1)
-        else:
-            xa = torch.cat([cg.x] * world)
-        e0.record()
-        xg = eng.unfold_all(xa)
-        e1.record()
-        sync()
-        unfold_all_ms = e0.elapsed_time(e1)
-        del xa, xg
-        torch.cuda.empty_cache()
+            e0.record()
+            xg = eng.unfold_all(xa)
+            e1.record()
+            sync()
+            unfold_all_ms = e0.elapsed_time(e1)
+            del xa, xg
+            torch.cuda.empty_cache()
     nl = n // world
     bf = backend_fields(backend, world, torch, on_gpu)
     ms_per_step = 1e3 * dt / a.steps
@@ -634,7 +634,7 @@ def run_block(a, world, rank, torch, dev, dist, on_gpu, K, F, backend="nccl"):
         # unfolds max over ranks): "reduce" = unfold_ms + solution_allreduce_ms,
         # "gather" (distributed.solve's default) = solution_allgather_ms +
         # unfold_all_ms
-        res_["unfold_all_ms"] = vals[-1] if on_gpu else None
+        res_["unfold_all_ms"] = vals[-1] if unfold_all_ms is not None else None
         if xred_ms is not None:
             res_["solution_allreduce_ms"] = xred_ms
         if xgat_ms is not None:
