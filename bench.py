@@ -1033,8 +1033,10 @@ def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
     anything is timed; the library records HIP events at every step boundary on
     the stream it launches on (gg_lanczos_probe_timed: after the probe is drawn,
     before the tridiagonal is copied back) and around every mode product, so
-    ms_per_step is the mean of the per-step event times.  bracket_ms (events
-    around the whole call, workspace already resident) is reported beside it."""
+    ms_per_step is the mean of the per-step event times; the closing pass
+    after the last step (beta_{k-1}: one streaming pass, once per probe) is
+    closing_ms.  bracket_ms (events around the whole call, workspace already
+    resident) is reported beside them."""
     from gp_grief_amd import device as gdev
     from gp_grief_amd import linalg
     t0 = time.perf_counter()
@@ -1047,6 +1049,7 @@ def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
     e0.record()
     a, b, step_ms, launch_ms = linalg.lanczos_tridiag(K, s, steps, seed=0, probe=0, work=work,
                                                       timed=True)
+    closing = linalg.lanczos_tridiag.closing_ms
     e1.record()
     torch.cuda.synchronize()
     bracket = e0.elapsed_time(e1)
@@ -1061,7 +1064,11 @@ def time_lanczos(K, s, steps, torch, n, m, d, fold_mask):
            "steady_ms_per_step": steady, "first_step_ms": st[0],
            "step_ms_min": float(np.min(st)), "step_ms_max": float(np.max(st)),
            "ms_source": "mean of per-step HIP events the library records on its stream "
-                        "(gg_lanczos_probe_timed); workspace allocated before timing",
+                        "(gg_lanczos_probe_timed); workspace allocated before timing; the "
+                        "once-per-probe closing pass (the last beta's streaming pass after "
+                        "the last step) is closing_ms, as the CG leg's closing update",
+           "closing_ms": closing,
+           "probe_ms": float(np.sum(st)) + (closing or 0.0),
            "basis": "block" if block else "grid", "launches_per_step": L,
            "mode_product_ms_by_position": [t / steps for t in launch_ms[:L]],
            "bracket_ms": bracket, "bracket_ms_per_step": bracket / max(k, 1),

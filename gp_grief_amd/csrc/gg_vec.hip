@@ -2080,7 +2080,8 @@ static void lanczos_block(const gg_kron* K, double shift, uint64_t seed, int pro
   GG_LAUNCH_CHECK();
   block_fold(B, false, W2, V, nullptr, s);
   const bool timed = step_ms != nullptr;
-  EventSet sev(timed ? (size_t)steps + 1 : 0);
+  // step boundaries, then the closing pass's end (ev[steps] -> ev[steps + 1])
+  EventSet sev(timed ? (size_t)steps + 2 : 0);
   EventSet mev(timed && launch_ms ? (size_t)steps * (L + 1) : 0);
   auto mp_ev = [&](int j) -> hipEvent_t* {
     return mev.ev.empty() ? nullptr : mev.ev.data() + (size_t)j * (L + 1);
@@ -2109,7 +2110,9 @@ static void lanczos_block(const gg_kron* K, double shift, uint64_t seed, int pro
     std::swap(W, W2);   // Y_j becomes the next step's chain
     if (timed && j + 1 < steps) GG_HIP(hipEventRecord(sev.ev[j + 1], s));
   }
-  // beta_{steps-1} = |w_{steps-1}| (one streaming pass, in place of Y)
+  // the closing pass, once per probe: beta_{steps-1} = |w_{steps-1}| (one
+  // streaming pass, in place of Y; T_k itself needs beta_0 .. beta_{k-2})
+  if (timed) GG_HIP(hipEventRecord(sev.ev[steps], s));
   const int wide = ((reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(V) |
                      reinterpret_cast<uintptr_t>(P)) & 15) == 0;
   hipLaunchKernelGGL(lz_update_kernel, dim3(nb), dim3(kVecThreads), 0, s, W, V, P, n, lzs + 0,
@@ -2118,7 +2121,7 @@ static void lanczos_block(const gg_kron* K, double shift, uint64_t seed, int pro
   launch_reduce_to(parts, nb, betas + (steps - 1), s);
   hipLaunchKernelGGL(lz_beta_kernel, dim3(1), dim3(1), 0, s, lzs, betas + (steps - 1));
   GG_LAUNCH_CHECK();
-  if (timed) GG_HIP(hipEventRecord(sev.ev[steps], s));
+  if (timed) GG_HIP(hipEventRecord(sev.ev[steps + 1], s));
   GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
   GG_HIP(hipMemcpyAsync(betas_host, betas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
   GG_HIP(hipFreeAsync(scal, s));
@@ -2138,6 +2141,9 @@ static void lanczos_block(const gg_kron* K, double shift, uint64_t seed, int pro
           GG_HIP(hipEventElapsedTime(&ms, mp_ev(j)[k], mp_ev(j)[k + 1]));
           launch_ms[k] += ms;
         }
+      float ms = 0.f;
+      GG_HIP(hipEventElapsedTime(&ms, sev.ev[steps], sev.ev[steps + 1]));
+      launch_ms[d] = ms;
     }
   }
   int done = steps;
@@ -2193,7 +2199,9 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
     GG_LAUNCH_CHECK();
     const int d = gg::kron_d(K);
     const bool timed = step_ms != nullptr;
-    gg::EventSet sev(timed ? (size_t)steps + 1 : 0);
+    // step boundaries, then the closing pass's end (ev[steps] -> ev[steps + 1];
+    // with the update fused, the last step's update pass is the closing one)
+    gg::EventSet sev(timed ? (size_t)steps + 2 : 0);
     gg::EventSet mev(timed && launch_ms ? (size_t)steps * (d + 1) : 0);
     auto mp_ev = [&](int j) -> hipEvent_t* {
       return mev.ev.empty() ? nullptr : mev.ev.data() + (size_t)j * (d + 1);
@@ -2244,7 +2252,9 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
       hipLaunchKernelGGL(gg::lz_coef_kernel, dim3(1), dim3(1), 0, s, lzs, dot, alphas + j,
                          beta_prev);
       GG_LAUNCH_CHECK();
+      const bool closing = fuse && j + 1 == steps;
       if (!fuse || j + 1 == steps) {
+        if (timed && closing) GG_HIP(hipEventRecord(sev.ev[steps], s));
         update_beta(j);
         if (j + 1 < steps) {
           // rotate: u_prev <- u, u <- w, the old u_prev buffer takes the next matvec
@@ -2254,8 +2264,9 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
           W = oldP;
         }
       }
-      if (timed) GG_HIP(hipEventRecord(sev.ev[j + 1], s));
+      if (timed && !closing) GG_HIP(hipEventRecord(sev.ev[j + 1], s));
     }
+    if (timed) GG_HIP(hipEventRecord(sev.ev[steps + 1], s));
     GG_HIP(hipMemcpyAsync(alphas_host, alphas, steps * sizeof(double), hipMemcpyDeviceToHost,
                           s));
     GG_HIP(hipMemcpyAsync(betas_host, betas, steps * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -2275,6 +2286,9 @@ static void lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int pro
             GG_HIP(hipEventElapsedTime(&ms, mp_ev(j)[k], mp_ev(j)[k + 1]));
             launch_ms[k] += ms;
           }
+        float ms = 0.f;
+        GG_HIP(hipEventElapsedTime(&ms, sev.ev[steps], sev.ev[steps + 1]));
+        launch_ms[d] = ms;
       }
     }
     int done = steps;

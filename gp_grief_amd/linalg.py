@@ -345,7 +345,9 @@ def lanczos_tridiag(K, shift, steps, seed=0, probe=0, work=None, timed=False):
     work: optional device workspace of >= 4 N elements (allocated here
     otherwise).  timed=True also returns the per-step HIP-event times (ms, one
     per step run) and the summed time of each mode-product position
-    (gg_lanczos_probe_timed): (alphas, betas, step_ms, launch_ms)."""
+    (gg_lanczos_probe_timed): (alphas, betas, step_ms, launch_ms); the
+    once-per-probe closing pass (the last beta's streaming pass, after the
+    last step) is left in lanczos_tridiag.closing_ms."""
     from . import device as dev
     from . import native
     dk = K._device()
@@ -360,7 +362,7 @@ def lanczos_tridiag(K, shift, steps, seed=0, probe=0, work=None, timed=False):
     if timed:
         d = len(dk._keep)
         sm = (ctypes.c_double * steps)()
-        lm = (ctypes.c_double * d)()
+        lm = (ctypes.c_double * (d + 1))()
         native.check(native.lib().gg_lanczos_probe_timed(
             dk.h, float(shift), int(seed), int(probe), int(steps), native.dptr(work), a, b,
             ctypes.byref(done), sm, lm, native.stream_ptr()), "gg_lanczos_probe_timed")
@@ -372,8 +374,12 @@ def lanczos_tridiag(K, shift, steps, seed=0, probe=0, work=None, timed=False):
     k = done.value
     out = np.array(a[:k]), np.array(b[:max(k - 1, 0)])
     if timed:
+        lanczos_tridiag.closing_ms = lm[d]
         return out + ([sm[j] for j in range(steps)], [lm[i] for i in range(d)])
     return out
+
+
+lanczos_tridiag.closing_ms = None
 
 
 def slq_logdet(K, shift, probes=8, steps=30, seed=0):

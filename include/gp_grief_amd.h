@@ -329,9 +329,13 @@ int gg_lanczos_probe(const gg_kron* K, double shift, uint64_t seed, int probe, i
                      int* steps_done, gg_stream stream);
 /* The same with live per-step timing: step_ms_host[j] (steps entries) is the
  * HIP-event time of step j on the stream (the first event after the probe is
- * drawn, the last before alphas / betas are copied back); launch_ms_host
- * (d entries, may be NULL) the summed time of each mode-product position over
- * the steps.  No reference counterpart (SLQ is absent from the reference).  */
+ * drawn); launch_ms_host (d + 1 entries, may be NULL) the summed time of each
+ * mode-product position over the steps (d - 1 positions in the parity-block
+ * basis, the rest 0), then the closing pass's time: once per probe, after
+ * the last step, the streaming pass that forms beta_{steps-1} (T_k itself
+ * needs beta_0 .. beta_{k-2}; with the update fused into the next step's
+ * first launch, the last step has no next step to carry it).  No reference
+ * counterpart (SLQ is absent from the reference).  */
 int gg_lanczos_probe_timed(const gg_kron* K, double shift, uint64_t seed, int probe, int steps,
                            double* work_dev, double* alphas_host, double* betas_host,
                            int* steps_done, double* step_ms_host, double* launch_ms_host,

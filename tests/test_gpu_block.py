@@ -435,6 +435,8 @@ def test_block_lanczos_timed_and_slq(gg):
     assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
     assert len(step_ms) == 12 and all(t > 0 for t in step_ms)
     assert all(t > 0 for t in launch_ms[:3]) and launch_ms[3] == 0.0
+    # the closing pass (beta_{k-1}) is timed apart from the 12 steps
+    assert gg.linalg.lanczos_tridiag.closing_ms > 0
     Q, lam = oracle.factor_eigh(F)
     exact = float(np.sum(np.log(oracle.kron_expand(lam) + 0.05)))
     est, _ = gg.linalg.slq_logdet(K, 0.05, probes=8, steps=60, seed=1)

@@ -357,6 +357,10 @@ def test_lanczos_timed_matches_untimed(gg, fold_small, ms):
     assert np.array_equal(a0, a1) and np.array_equal(b0, b1)
     assert len(step_ms) == 12 and all(t > 0 for t in step_ms)
     assert len(launch_ms) == len(ms) and all(t > 0 for t in launch_ms)
+    # the closing pass (the last beta) is timed apart from the steps: a pass
+    # of its own with the update fused (even d), none otherwise
+    cl = gg.linalg.lanczos_tridiag.closing_ms
+    assert cl is not None and (cl > 0 if len(ms) % 2 == 0 else cl >= 0)
 
 
 def test_matvec_timed_matches_matvec(gg, fold_small):
