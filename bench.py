@@ -886,7 +886,7 @@ def pmc_traffic(m, d, positions, recurrence, fusion=0, fold_mask=0, xdefer=True,
     if int(rec.get("rq_identity", 0)) != int(rq):
         return None, "PMC passes taken with another r.q source"
     if rec.get("source_sha256") != kernel_source_hash():
-        return None, "stale: the kernel sources changed since the PMC passes (%s)" % PMC_JSON
+        return None, "stale: the kernel sources changed since the PMC passes (%s)" % (PMC_JSON_BLOCK if block else PMC_JSON)
     if not rec.get("calibrated_on_own_pattern"):
         return None, "PMC bytes did not match the algorithmic bytes of every launch"
     per = {pp["position"]: pp["traffic_bytes"] for pp in rec.get("per_position", [])}
