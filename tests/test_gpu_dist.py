@@ -327,7 +327,11 @@ def reference_factors_ms(ms):
     (2, (6, 12, 40, 40), 0.05, "gather"), (4, (6, 12, 40, 40), 0.05, "gather"),
     (8, (40, 40, 40, 40), 0.5, "gather"), (16, (6, 12, 40, 40), 0.05, "gather"),
     (4, (8, 72, 72), 0.2, "gather"), (2, (40, 8, 72, 72), 0.1, "gather"),
-    (4, (8, 72, 72), 0.2, "reduce"), (8, (40, 40, 40, 40), 0.5, "reduce")])
+    (4, (8, 72, 72), 0.2, "reduce"), (8, (40, 40, 40, 40), 0.5, "reduce"),
+    # padded pair axes (h = 32 / 24 in slabs of 36 / 36): the shares and the
+    # whole block vector carry the zero padding through both routes
+    (2, (6, 64, 64), 0.05, "gather"), (4, (4, 8, 48, 48), 0.1, "gather"),
+    (4, (4, 8, 48, 48), 0.1, "reduce")])
 def test_block_sharded_cg_virtual_ranks(gpu, monkeypatch, world, ms, shift, solution):
     """distributed.solve, block decomposition: each virtual rank (a thread)
     runs the block kernels on its 2^d / G blocks (gg_cg_create_blocks,
