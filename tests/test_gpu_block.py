@@ -51,7 +51,7 @@ def host(gg, xd):
     return gg.device.to_host(xd).reshape(-1)
 
 
-# shapes: d = 2 .. 5; the pair orders 40 / 72 / 200 (h = 20 / 36 / 100) and
+# shapes: d = 2 .. 6; the pair orders 40 / 72 / 200 (h = 20 / 36 / 100) and
 # leading orders with h = 1..100 (full tiles, 4-row tails, padded tiles)
 SHAPES = [
     (200, 200),
@@ -68,6 +68,7 @@ SHAPES = [
     (4, 136, 136),
     (2, 168, 168),
     (104, 8, 136, 136),   # a fast mode kernel of order 104 (axis 0): JT 4
+    (2, 4, 2, 6, 40, 40),  # d = 6: four mode launches before the pair
 ]
 
 
@@ -224,7 +225,7 @@ def oracle_cg(F, b, shift, rtol, maxiter):
                                       ((4, 8, 72, 72), 0.2), ((8, 6, 8, 40, 40), 0.1),
                                       ((40, 40, 40, 40), 0.5), ((40, 72, 72), 0.2),
                                       ((6, 104, 104), 0.1), ((4, 6, 136, 136), 0.1),
-                                      ((8, 6, 168, 168), 0.2)])
+                                      ((8, 6, 168, 168), 0.2), ((2, 4, 2, 6, 40, 40), 0.1)])
 def test_block_cg_vs_oracle(gg, ms, shift):
     F = factors(ms)
     K = gg.tensors.KronMatrix(F, sym=True)
