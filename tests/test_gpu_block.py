@@ -396,7 +396,7 @@ def test_block_cg_window_converges_inside_first_window(gg, monkeypatch):
 
 # ---- the fused Lanczos step in the block basis (gg_lanczos_info) -----------
 @pytest.mark.parametrize("ms", [(40, 40, 40, 40), (72, 72, 72, 72), (8, 6, 104, 104),
-                                (12, 72, 72)])
+                                (12, 72, 72), (4, 6, 8, 40, 40), (2, 4, 2, 6, 40, 40)])
 def test_block_lanczos_matches_grid_and_oracle(gg, monkeypatch, ms):
     """The probe folded once and every step in the parity-block basis gives the
     grid-basis tridiagonal (P is orthogonal: same Krylov space) to 1e-10 over
